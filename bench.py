@@ -1,0 +1,191 @@
+#!/usr/bin/env python
+"""Headline benchmark: GPT-NeoX-20B, ZeRO-3, bf16, synthetic data, random-init weights.
+
+Metric (BASELINE.json): tokens/sec for the whole node at N = 1/2/4/8 MI355X (weak scaling:
+the per-GPU micro-batch and gradient-accumulation are fixed as N grows).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Each step is a full training step through the framework: forward + backward of every
+micro-batch (activation recompute on), ZeRO-3 all-gathers / reduce-scatters over RCCL,
+global-norm clipping, fused Adam on the fp32 master, bf16 parameter refresh.  With a
+single GPU the 20B model's optimizer state does not fit in 288 GB next to the moments, so
+the fp32 master is offloaded to pinned host memory (ZeRO-Offload, master-only mode) and
+streamed through the step; with N >= 2 everything stays in HBM.
+
+Rank 0 prints ONE JSON line.  `vs_baseline` divides by the only DeeperSpeed-derived
+number BASELINE.md gives for this model/metric (410 tokens/s per GPU: the reference's best
+published ZeRO-3 efficiency of 49 TFLOPS/GPU applied to 20B at 6N FLOPs/token), times N.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REF_TOKENS_PER_GPU = 410.0  # BASELINE.md "North-star planning targets (derived)"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--model", type=str, default="gpt-neox-20b")
+    p.add_argument("--micro-batch", type=int, default=None)
+    p.add_argument("--grad-accum", type=int, default=None)
+    p.add_argument("--seq", type=int, default=2048)
+    p.add_argument("--zero", type=int, default=3)
+    p.add_argument("--offload", type=str, default="auto", choices=["auto", "none", "master", "all"])
+    p.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (0 = off)")
+    p.add_argument("--local_rank", type=int, default=None)
+    return p.parse_args()
+
+
+def log(msg):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        # single-process launch with --gpus 1 (or a mismatch): trust the launcher's world
+        if world == 1 and args.gpus != 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("DSA_SKIP_MODEL_BROADCAST", "1")  # identical seeded init on every rank
+
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
+    from deeperspeed_amd.ops import native
+
+    ds.init_distributed(dist_backend="nccl")
+    rank = dist.get_rank()
+    local = int(os.environ["LOCAL_RANK"])
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    native.hip_ops()  # fail loudly if the HIP extension is missing
+
+    cfg = get_config(args.model, max_seq_len=args.seq, checkpoint_activations=True)
+    big = cfg.num_params() > 5e9
+    mb = args.micro_batch or (4 if big else 8)
+    ga = args.grad_accum or (4 if big else 2)
+    offload = args.offload
+    if offload == "auto":
+        # 16 B/param of model state: keep everything in HBM when it fits with activations
+        per_gpu = cfg.num_params() * 16 / world
+        offload = "master" if per_gpu > 200e9 else "none"
+    zcfg = {"stage": args.zero, "overlap_comm": True, "reduce_bucket_size": int(2e8),
+            "stage3_prefetch_bucket_size": int(5e8), "stage3_param_persistence_threshold": int(1e6),
+            "stage3_unit_max_numel": int(2e8)}
+    if offload != "none":
+        zcfg["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": offload}
+    conf = {
+        "train_micro_batch_size_per_gpu": mb,
+        "gradient_accumulation_steps": ga,
+        "optimizer": {"type": "Adam", "params": {"lr": 1e-4, "betas": [0.9, 0.95], "eps": 1e-8,
+                                                  "weight_decay": 0.01}},
+        "fp16": {"enabled": True, "type": "bfloat16"},
+        "fp32_allreduce": False,
+        "gradient_clipping": 1.0,
+        "zero_optimization": zcfg,
+        "steps_per_print": 1000000,
+        "wall_clock_breakdown": False,
+    }
+    log(f"model={args.model} params={cfg.num_params() / 1e9:.2f}B world={world} mb={mb} ga={ga} seq={args.seq} "
+        f"zero={args.zero} offload={offload}")
+    t0 = time.time()
+    torch.manual_seed(1234)
+    model = GPTNeoX(cfg, device=dev, dtype=torch.bfloat16)
+    log(f"model built in {time.time() - t0:.1f}s, mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    del model
+    log(f"engine ready in {time.time() - t0:.1f}s, mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321 + rank)
+    batches = [torch.randint(0, cfg.vocab_size, (mb, args.seq), device=dev, generator=g) for _ in range(ga)]
+
+    def train_step():
+        loss = None
+        for i in range(ga):
+            loss = engine(batches[i], labels=batches[i])
+            engine.backward(loss)
+            engine.step()
+        return loss
+
+    for i in range(args.warmup):
+        ts = time.time()
+        loss = train_step()
+        torch.cuda.synchronize()
+        log(f"warmup {i} loss={float(loss):.4f} {time.time() - ts:.2f}s "
+            f"peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+
+    dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.time()
+    for i in range(args.steps):
+        loss = train_step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.time() - t_start
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if args.profile_steps > 0:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(args.profile_steps):
+                train_step()
+            torch.cuda.synchronize()
+        if rank == 0:
+            os.makedirs("gpurun_out", exist_ok=True)
+            with open("gpurun_out/torch_profile.txt", "w") as f:
+                f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+
+    global_batch = mb * ga * world
+    tokens = global_batch * args.seq * args.steps
+    tps = tokens / elapsed
+    flops_tok = cfg.flops_per_token(args.seq, recompute=True)
+    ms_step = elapsed / args.steps * 1000.0
+    out = {
+        "metric": "tokens/sec (node) GPT-NeoX-20B ZeRO-3" if args.model == "gpt-neox-20b" else f"tokens/sec {args.model}",
+        "value": round(tps, 2),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(tps / (REF_TOKENS_PER_GPU * world), 3),
+        "dtype": "bf16",
+        "data": "synthetic random tokens, random-init weights",
+        "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq,
+                   "parallelism": f"zero{args.zero}-dp{world}", "micro_batch": mb, "grad_accum": ga,
+                   "offload": offload, "activation_checkpointing": True,
+                   "params_per_gpu": round(cfg.num_params() / world / 1e9, 3),
+                   "model_tflops_per_gpu": round(tps * flops_tok / world / 1e12, 1),
+                   "final_loss": round(float(loss), 4),
+                   "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N), BASELINE.md derived target"},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,226 @@
+"""GPT-NeoX family (flagship model of the framework).
+
+Architecture as trained with DeeperSpeed by GPT-NeoX: pre-LayerNorm blocks with *parallel*
+attention + MLP residual (`x + attn(ln1(x)) + mlp(ln2(x))`), partial rotary position
+embedding (rotary_pct of each head), GeLU MLP of width 4h, untied input/output
+embeddings, final LayerNorm.  Presets include GPT-NeoX-20B (the north-star config of
+BASELINE.json), 1.3B and GPT-3-6.7B-shaped models.
+
+Hot ops run on the framework's HIP kernels (LayerNorm, bias+GeLU, fused rotary/QKV split,
+fused attention softmax or flash attention); GEMMs use hipBLASLt through torch.
+Layers are plain modules so the same blocks serve `DeepSpeedEngine` (ZeRO-1/2/3) and the
+pipeline engine (`to_pipeline()` builds a PipelineModule of LayerSpecs).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, asdict
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import native
+from ..ops.attention import attention, rotary_split
+from ..runtime.activation_checkpointing import checkpointing as ds_ckpt
+
+
+@dataclass
+class GPTNeoXConfig:
+    vocab_size: int = 50432
+    hidden_size: int = 6144
+    num_layers: int = 44
+    num_heads: int = 64
+    intermediate_size: Optional[int] = None
+    rotary_pct: float = 0.25
+    rotary_base: float = 10000.0
+    max_seq_len: int = 2048
+    layernorm_eps: float = 1e-5
+    use_parallel_residual: bool = True
+    gelu_approximate: bool = False
+    checkpoint_activations: bool = True
+    init_std: float = 0.02
+    hidden_dropout: float = 0.0
+    attention_dropout: float = 0.0
+
+    def __post_init__(self):
+        if self.intermediate_size is None:
+            self.intermediate_size = 4 * self.hidden_size
+        assert self.hidden_size % self.num_heads == 0
+        rot = int(self.head_dim * self.rotary_pct)
+        self.rotary_dim = rot - rot % 2
+
+    @property
+    def head_dim(self):
+        return self.hidden_size // self.num_heads
+
+    def num_params(self, include_embeddings=True):
+        h, i, L, V = self.hidden_size, self.intermediate_size, self.num_layers, self.vocab_size
+        per_layer = 3 * h * h + 3 * h + h * h + h + 2 * h * i + i + h + 4 * h
+        n = L * per_layer + 2 * h
+        if include_embeddings:
+            n += 2 * V * h
+        return n
+
+    def flops_per_token(self, seq_len=None, recompute=True):
+        """Model FLOPs per trained token (fwd+bwd[+recompute]) incl. attention."""
+        s = seq_len or self.max_seq_len
+        n = self.num_params(include_embeddings=False) + self.vocab_size * self.hidden_size  # output proj GEMM
+        attn = 2 * self.num_layers * s * self.hidden_size  # QK^T + PV per token (causal halves, x2 fwd terms)
+        mult = 8 if recompute else 6
+        return mult * n + (mult // 2) * attn
+
+
+PRESETS = {
+    "gpt-neox-20b": dict(vocab_size=50432, hidden_size=6144, num_layers=44, num_heads=64, rotary_pct=0.25),
+    "gpt-neox-1.3b": dict(vocab_size=50304, hidden_size=2048, num_layers=24, num_heads=16, rotary_pct=0.25),
+    "gpt-neox-125m": dict(vocab_size=50304, hidden_size=768, num_layers=12, num_heads=12, rotary_pct=0.25),
+    "gpt3-6.7b": dict(vocab_size=50304, hidden_size=4096, num_layers=32, num_heads=32, rotary_pct=1.0),
+    "tiny": dict(vocab_size=512, hidden_size=128, num_layers=2, num_heads=4, rotary_pct=0.25, max_seq_len=64),
+}
+
+
+def get_config(name: str, **overrides) -> GPTNeoXConfig:
+    d = dict(PRESETS[name])
+    d.update(overrides)
+    return GPTNeoXConfig(**d)
+
+
+class NeoXAttention(nn.Module):
+    def __init__(self, cfg: GPTNeoXConfig, device=None, dtype=None):
+        super().__init__()
+        h = cfg.hidden_size
+        self.cfg = cfg
+        self.query_key_value = nn.Linear(h, 3 * h, device=device, dtype=dtype)
+        self.dense = nn.Linear(h, h, device=device, dtype=dtype)
+
+    def forward(self, x):
+        cfg = self.cfg
+        B, S, H = x.shape
+        qkv = F.linear(x, self.query_key_value.weight, self.query_key_value.bias)
+        q, k, v = rotary_split(qkv, cfg.num_heads, cfg.head_dim, cfg.rotary_dim, cfg.rotary_base,
+                               qscale=1.0 / math.sqrt(cfg.head_dim))
+        ctx = attention(q, k, v, causal=True, softmax_scale=1.0, dropout_p=cfg.attention_dropout,
+                        training=self.training)
+        ctx = ctx.transpose(1, 2).reshape(B, S, H)
+        return F.linear(ctx, self.dense.weight, self.dense.bias)
+
+
+class NeoXMLP(nn.Module):
+    def __init__(self, cfg: GPTNeoXConfig, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        self.dense_h_to_4h = nn.Linear(cfg.hidden_size, cfg.intermediate_size, device=device, dtype=dtype)
+        self.dense_4h_to_h = nn.Linear(cfg.intermediate_size, cfg.hidden_size, device=device, dtype=dtype)
+
+    def forward(self, x):
+        h = F.linear(x, self.dense_h_to_4h.weight)  # bias fused into the GeLU kernel
+        h = native.bias_gelu(h, self.dense_h_to_4h.bias, self.cfg.gelu_approximate)
+        return F.linear(h, self.dense_4h_to_h.weight, self.dense_4h_to_h.bias)
+
+
+class NeoXTransformerLayer(nn.Module):
+    """One GPT-NeoX block. Class name matches DeeperSpeed's `layers_to_hook` pattern."""
+
+    def __init__(self, cfg: GPTNeoXConfig, layer_number: int = 0, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        self.layer_number = layer_number
+        self.input_layernorm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
+        self.post_attention_layernorm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device,
+                                                              dtype=dtype)
+        self.attention = NeoXAttention(cfg, device, dtype)
+        self.mlp = NeoXMLP(cfg, device, dtype)
+
+    def _block(self, x):
+        a = self.attention(self.input_layernorm(x))
+        if self.cfg.use_parallel_residual:
+            m = self.mlp(self.post_attention_layernorm(x))
+            return x + a + m
+        x = x + a
+        return x + self.mlp(self.post_attention_layernorm(x))
+
+    def forward(self, x):
+        if self.cfg.checkpoint_activations and self.training and torch.is_grad_enabled():
+            return ds_ckpt.checkpoint(self._block, x)
+        return self._block(x)
+
+
+class GPTNeoX(nn.Module):
+    """Causal LM; `forward(input_ids, labels=None)` returns logits or the mean token loss."""
+
+    def __init__(self, cfg: GPTNeoXConfig, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        self.embed_in = nn.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
+        self.layers = nn.ModuleList([NeoXTransformerLayer(cfg, i, device, dtype) for i in range(cfg.num_layers)])
+        self.final_layer_norm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
+        self.embed_out = nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        std = self.cfg.init_std
+        out_std = std / math.sqrt(2.0 * max(1, self.cfg.num_layers))
+        for name, p in self.named_parameters():
+            if p.dim() >= 2:
+                p.normal_(0.0, out_std if name.endswith("dense.weight") or name.endswith("4h_to_h.weight") else std)
+            elif "layernorm" in name or "layer_norm" in name:
+                p.fill_(1.0 if name.endswith("weight") else 0.0)
+            else:
+                p.zero_()
+
+    def forward(self, input_ids, labels=None):
+        x = self.embed_in(input_ids)
+        for layer in self.layers:
+            x = layer(x)
+        x = self.final_layer_norm(x)
+        logits = F.linear(x, self.embed_out.weight)
+        if labels is None:
+            return logits
+        return lm_loss(logits, labels)
+
+
+def lm_loss(logits, labels):
+    return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.reshape(-1))
+
+
+# -------------------------------------------------------------------------- pipeline form
+class _EmbedPipe(nn.Module):
+    def __init__(self, cfg, device=None, dtype=None):
+        super().__init__()
+        self.embed_in = nn.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
+        nn.init.normal_(self.embed_in.weight, 0.0, cfg.init_std)
+
+    def forward(self, input_ids):
+        return self.embed_in(input_ids)
+
+
+class _LayerPipe(NeoXTransformerLayer):
+    pass
+
+
+class _FinalPipe(nn.Module):
+    def __init__(self, cfg, device=None, dtype=None):
+        super().__init__()
+        self.final_layer_norm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
+        self.embed_out = nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
+        nn.init.normal_(self.embed_out.weight, 0.0, cfg.init_std)
+
+    def forward(self, x):
+        return F.linear(self.final_layer_norm(x), self.embed_out.weight)
+
+
+def to_pipeline(cfg: GPTNeoXConfig, num_stages: int, topology=None, partition_method="type:NeoXTransformerLayer",
+                activation_checkpoint_interval=0, **kw):
+    """GPT-NeoX as a PipelineModule (embedding, N blocks, final norm + head)."""
+    from ..runtime.pipe.module import LayerSpec, PipelineModule
+    specs = [LayerSpec(_EmbedPipe, cfg)]
+    for i in range(cfg.num_layers):
+        specs.append(LayerSpec(NeoXTransformerLayer, cfg, i))
+    specs.append(LayerSpec(_FinalPipe, cfg))
+    return PipelineModule(layers=specs, num_stages=num_stages if topology is None else None, topology=topology,
+                          loss_fn=lm_loss, partition_method=partition_method,
+                          activation_checkpoint_interval=activation_checkpoint_interval, **kw)

@@ -1,0 +1,243 @@
+"""In-tree native build system for deeperspeed_amd (replaces the reference's op_builder).
+
+Reference parity: ``op_builder/builder.py:81-256`` (``OpBuilder.load/jit_load``) and the
+``DS_BUILD_*`` switches of ``setup.py:73-134``.  Design here is MI355X-only:
+
+* HIP sources are compiled directly with ``hipcc --offload-arch=gfx950`` (no hipify, no CUDA
+  sources, no dual code paths).  Device translation units include no torch headers, so
+  they compile in seconds; one binding unit links them into a torch extension.
+* Host-only C++ (CPU Adam with AVX-512 dispatch, async NVMe I/O, flatten) builds with g++.
+* Every artefact is written IN-TREE next to this file (``_hip_ops*.so``, ``_cpu_ops*.so``)
+  so it travels with the repository snapshot to the GPU box.
+* Builds are content-hashed: an object is rebuilt only when its source, a shared header or
+  the flags change.  ``build_all()`` compiles everything in parallel.
+"""
+
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import hashlib
+import importlib
+import importlib.util
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+import threading
+from typing import Dict, List, Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(_HERE, "csrc")
+BUILD_DIR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "build", "ops")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+_lock = threading.Lock()
+_loaded: Dict[str, object] = {}
+
+
+def _torch_paths():
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, "include"), os.path.join(tdir, "include", "torch", "csrc", "api", "include")]
+    return tdir, inc, os.path.join(tdir, "lib"), bool(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def _ext_specs() -> Dict[str, dict]:
+    return {
+        "_hip_ops": dict(
+            kind="hip",
+            sources=[os.path.join(CSRC, "bindings.cpp")] + sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))),
+            headers=sorted(glob.glob(os.path.join(CSRC, "include", "*.h"))),
+        ),
+        "_cpu_ops": dict(
+            kind="cpu",
+            sources=sorted(glob.glob(os.path.join(CSRC, "cpu", "*.cpp"))),
+            headers=sorted(glob.glob(os.path.join(CSRC, "cpu", "*.h"))),
+        ),
+    }
+
+
+def _hash(paths: List[str], extra: str) -> str:
+    h = hashlib.sha1(extra.encode())
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _so_path(name: str) -> str:
+    return os.path.join(_HERE, name + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _compile_cmd(kind: str, name: str, src: str, obj: str) -> List[str]:
+    tdir, tinc, _, abi = _torch_paths()
+    pyinc = sysconfig.get_paths()["include"]
+    common = ["-O3", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={int(abi)}", f"-DTORCH_EXTENSION_NAME={name}",
+              "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-unused-result", "-Wno-deprecated-declarations"]
+    is_binding = src.endswith(".cpp")
+    if kind == "hip" and not is_binding:
+        cmd = [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + common
+        cmd += ["-c", src, "-o", obj]
+        return cmd
+    # host-only C++: AVX-512 paths are compiled per-function via target attributes and
+    # selected at run time (cpu_adam.cpp), so the baseline stays portable.
+    cmd = ["g++", "-fopenmp", "-mavx2", "-mfma", "-mf16c"] + common
+    cmd += [f"-I{p}" for p in tinc] + [f"-I{pyinc}", f"-I{CSRC}", f"-I{os.path.join(ROCM, 'include')}",
+                                      "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1"]
+    cmd += ["-c", src, "-o", obj]
+    return cmd
+
+
+def _link_cmd(kind: str, objs: List[str], out: str) -> List[str]:
+    _, _, tlib, _ = _torch_paths()
+    libs = [f"-L{tlib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python"]
+    if kind == "hip":
+        return [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + \
+            ["-o", out] + libs + ["-lc10_hip", "-ltorch_hip", f"-Wl,-rpath,{tlib}"]
+    return ["g++", "-shared", "-fPIC", "-fopenmp"] + objs + ["-o", out] + libs + \
+        [f"-L{os.path.join(ROCM, 'lib')}", "-lamdhip64", f"-Wl,-rpath,{tlib}", "-lpthread"]
+
+
+def _run(cmd: List[str]):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("native build failed:\n$ " + " ".join(cmd) + "\n" + r.stdout[-8000:])
+    return r.stdout
+
+
+def build(name: str, jobs: Optional[int] = None, verbose: bool = False) -> str:
+    """Build extension `name` in-tree; returns the .so path."""
+    spec = _ext_specs()[name]
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    kind = spec["kind"]
+    if kind == "hip" and not os.path.exists(os.path.join(ROCM, "bin", "hipcc")):
+        raise RuntimeError("hipcc not found; cannot build HIP extension " + name)
+    objs, todo = [], []
+    for src in spec["sources"]:
+        probe = _compile_cmd(kind, name, src, "X.o")
+        h = _hash([src] + spec["headers"], " ".join(probe))
+        obj = os.path.join(BUILD_DIR, f"{os.path.basename(src)}.{h}.o")
+        objs.append(obj)
+        if not os.path.exists(obj):
+            todo.append(_compile_cmd(kind, name, src, obj))
+    jobs = jobs or int(os.environ.get("MAX_JOBS", min(8, os.cpu_count() or 4)))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
+            for out in ex.map(_run, todo):
+                if verbose and out.strip():
+                    print(out)
+    out = _so_path(name)
+    stamp = out + ".hash"
+    link_h = _hash([], "|".join(objs))
+    if not os.path.exists(out) or not os.path.exists(stamp) or open(stamp).read() != link_h:
+        tmp = out + ".tmp"
+        _run(_link_cmd(kind, objs, tmp))
+        os.replace(tmp, out)
+        with open(stamp, "w") as f:
+            f.write(link_h)
+    return out
+
+
+def build_all(verbose: bool = False) -> List[str]:
+    outs = []
+    for name in _ext_specs():
+        if name == "_cpu_ops" and not _ext_specs()[name]["sources"]:
+            continue
+        outs.append(build(name, verbose=verbose))
+    return outs
+
+
+def is_built(name: str) -> bool:
+    return os.path.exists(_so_path(name))
+
+
+def load(name: str):
+    """Import an in-tree extension, building it first when missing or stale.
+
+    Raises loudly when the extension cannot be built or imported: the GPU hot path must
+    never silently fall back to eager PyTorch.
+    """
+    with _lock:
+        if name in _loaded:
+            return _loaded[name]
+        import torch  # noqa: F401  (load libtorch / libamdhip64 first)
+        if os.environ.get("DSA_SKIP_BUILD", "0") != "1":
+            try:
+                build(name)
+            except RuntimeError:
+                if not is_built(name):
+                    raise
+        spec = importlib.util.spec_from_file_location(f"deeperspeed_amd.ops.{name}", _so_path(name))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        sys.modules[f"deeperspeed_amd.ops.{name}"] = mod
+        _loaded[name] = mod
+        return mod
+
+
+class OpBuilder:
+    """Reference-style builder facade (``op_builder/builder.py:81``): ``XBuilder().load()``."""
+    NAME = "_hip_ops"
+    BUILD_VAR = "DS_BUILD_OPS"
+
+    def __init__(self, name: Optional[str] = None):
+        self.name = name or self.NAME
+
+    def absolute_name(self):
+        return f"deeperspeed_amd.ops.{self.NAME}"
+
+    def is_compatible(self) -> bool:
+        if self.NAME == "_cpu_ops":
+            return shutil.which("g++") is not None
+        return os.path.exists(os.path.join(ROCM, "bin", "hipcc"))
+
+    def load(self, verbose: bool = False):
+        return load(self.NAME)
+
+    def jit_load(self, verbose: bool = False):
+        return load(self.NAME)
+
+
+class FusedAdamBuilder(OpBuilder):
+    NAME = "_hip_ops"
+
+
+class FusedLambBuilder(OpBuilder):
+    NAME = "_hip_ops"
+
+
+class TransformerBuilder(OpBuilder):
+    NAME = "_hip_ops"
+
+
+class StochasticTransformerBuilder(OpBuilder):
+    NAME = "_hip_ops"
+
+
+class SparseAttnBuilder(OpBuilder):
+    NAME = "_hip_ops"
+
+
+class CPUAdamBuilder(OpBuilder):
+    NAME = "_cpu_ops"
+
+
+class AsyncIOBuilder(OpBuilder):
+    NAME = "_cpu_ops"
+
+
+class UtilsBuilder(OpBuilder):
+    NAME = "_cpu_ops"
+
+
+ALL_OPS = {b.__name__: b for b in (FusedAdamBuilder, FusedLambBuilder, TransformerBuilder,
+                                    StochasticTransformerBuilder, SparseAttnBuilder, CPUAdamBuilder,
+                                    AsyncIOBuilder, UtilsBuilder)}
+
+if __name__ == "__main__":
+    for p in build_all(verbose=True):
+        print("built", p)

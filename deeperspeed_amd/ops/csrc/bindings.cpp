@@ -1,0 +1,305 @@
+// PyTorch bindings for the deeperspeed_amd HIP kernels (module `_hip_ops`).
+//
+// Thin layer: validates shapes/dtypes on the host (a wrong shape never reaches
+// a kernel), allocates outputs with the caching allocator and launches on the
+// current HIP stream. All device code lives in kernels/*.hip.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include <optional>
+#include <vector>
+
+#include "include/launchers.h"
+
+namespace {
+
+using at::Tensor;
+using OptT = std::optional<Tensor>;
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+inline int dcode(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return dsa::kCodeF32;
+    case at::kBFloat16: return dsa::kCodeBF16;
+    case at::kHalf: return dsa::kCodeF16;
+    default: TORCH_CHECK(false, "deeperspeed_amd kernels support fp32/bf16/fp16, got ", t.scalar_type());
+  }
+  return -1;
+}
+
+inline void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// ----------------------------------------------------------------------------- optim
+void adam_flat(Tensor w, Tensor g, Tensor m, Tensor v, OptT out, double lr, double beta1, double beta2, double eps,
+               double wd, double bc1, double bc2, double grad_scale, bool adamw) {
+  check_dev(w, "w"); check_dev(g, "g"); check_dev(m, "exp_avg"); check_dev(v, "exp_avg_sq");
+  const int64_t n = w.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam_flat: size mismatch");
+  TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat, "adam states must be fp32");
+  TORCH_CHECK(aligned16(w.data_ptr()) && aligned16(m.data_ptr()) && aligned16(v.data_ptr()),
+              "adam_flat: w/m/v must be 16-byte aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(g.data_ptr()) & (g.element_size() * 4 - 1)) == 0,
+              "adam_flat: grad must be aligned to 4 elements");
+  void* optr = nullptr;
+  int ot = dsa::kCodeBF16;
+  if (out.has_value()) {
+    check_dev(*out, "out");
+    TORCH_CHECK(out->numel() == n, "adam_flat: out size mismatch");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(out->data_ptr()) & (out->element_size() * 4 - 1)) == 0,
+                "adam_flat: out must be aligned to 4 elements");
+    optr = out->data_ptr();
+    ot = dcode(*out);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  dsa::AdamArgs a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2,
+                  (float)grad_scale, adamw ? 1 : 0};
+  dsa::launch_adam_flat(w.data_ptr(), dcode(w), g.data_ptr(), dcode(g), m.data_ptr<float>(), v.data_ptr<float>(),
+                        optr, ot, n, a, cur_stream());
+}
+
+// meta: device int64 table built by ops/adam.py (see optim.hip adam_multi_kernel)
+void adam_multi(Tensor meta, int64_t T, int64_t total_chunks, int64_t chunk, int64_t wt, int64_t gt, int64_t ot,
+                double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2,
+                double grad_scale, bool adamw) {
+  check_dev(meta, "meta");
+  TORCH_CHECK(meta.scalar_type() == at::kLong && meta.numel() == 7 * T + 1, "adam_multi: bad meta table");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(meta.device());
+  dsa::AdamArgs a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2,
+                  (float)grad_scale, adamw ? 1 : 0};
+  dsa::launch_adam_multi(meta.data_ptr<int64_t>(), (int)T, total_chunks, chunk, (int)wt, (int)gt, (int)ot, a,
+                         cur_stream());
+}
+
+// out[0] += sum(x^2) in fp32. workspace >= 1024 floats.
+void sumsq_accum(Tensor x, Tensor workspace, Tensor out) {
+  check_dev(x, "x");
+  TORCH_CHECK(workspace.numel() >= 1024 && workspace.scalar_type() == at::kFloat, "sumsq: workspace");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "sumsq: out must be fp32");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0, "sumsq: x must be 16-byte aligned");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  dsa::launch_sumsq_accum(x.data_ptr(), dcode(x), x.numel(), workspace.data_ptr<float>(), out.data_ptr<float>(),
+                          cur_stream());
+}
+
+void scale_copy(Tensor x, Tensor y, OptT scale_t, double scale) {
+  check_dev(x, "x"); check_dev(y, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "scale_copy: size mismatch");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & (x.element_size() * 4 - 1)) == 0 &&
+                  (reinterpret_cast<uintptr_t>(y.data_ptr()) & (y.element_size() * 4 - 1)) == 0,
+              "scale_copy: tensors must be aligned to 4 elements");
+  const float* sp = nullptr;
+  if (scale_t.has_value()) {
+    TORCH_CHECK(scale_t->scalar_type() == at::kFloat && scale_t->is_cuda(), "scale tensor must be fp32 GPU");
+    sp = scale_t->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  dsa::launch_scale_copy(x.data_ptr(), dcode(x), y.data_ptr(), dcode(y), x.numel(), sp, (float)scale,
+                         cur_stream());
+}
+
+void lamb(Tensor w, Tensor g, Tensor m, Tensor v, Tensor upd, OptT out, double lr, double beta1, double beta2,
+          double eps, double wd, double bc1, double bc2, double grad_scale, double max_coeff, double min_coeff,
+          bool adamw, Tensor workspace, Tensor coeff_out) {
+  check_dev(w, "w"); check_dev(g, "g"); check_dev(m, "m"); check_dev(v, "v"); check_dev(upd, "upd");
+  const int64_t n = w.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && upd.numel() == n, "lamb: size mismatch");
+  TORCH_CHECK(workspace.numel() >= 2048 && coeff_out.numel() >= 1, "lamb: workspace");
+  void* optr = nullptr;
+  int ot = dsa::kCodeBF16;
+  if (out.has_value()) { optr = out->data_ptr(); ot = dcode(*out); TORCH_CHECK(out->numel() == n); }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
+  dsa::LambArgs a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2,
+                  (float)grad_scale, (float)max_coeff, (float)min_coeff, adamw ? 1 : 0};
+  dsa::launch_lamb(w.data_ptr(), dcode(w), g.data_ptr(), dcode(g), m.data_ptr<float>(), v.data_ptr<float>(),
+                   upd.data_ptr<float>(), optr, ot, n, a, workspace.data_ptr<float>(), coeff_out.data_ptr<float>(),
+                   cur_stream());
+}
+
+// ----------------------------------------------------------------------------- layer norm
+// Returns (y, mean, rstd, sum) where sum = x + res (+bias) when res is given (else undefined).
+std::vector<Tensor> ln_fwd(Tensor x, Tensor gamma, OptT beta, double eps, OptT res, OptT bias) {
+  check_dev(x, "x"); check_dev(gamma, "gamma");
+  const int64_t H = x.size(-1);
+  const int64_t rows = x.numel() / H;
+  const int dt = dcode(x);
+  TORCH_CHECK(gamma.numel() == H && gamma.scalar_type() == x.scalar_type(), "ln_fwd: gamma must match x");
+  TORCH_CHECK(H % (dt == dsa::kCodeF32 ? 4 : 8) == 0, "ln_fwd: hidden must be a multiple of 16 bytes");
+  TORCH_CHECK(H <= dsa::ln_max_hidden(dt), "ln_fwd: hidden too large");
+  if (beta.has_value()) TORCH_CHECK(beta->numel() == H && beta->scalar_type() == x.scalar_type(), "ln_fwd: beta");
+  Tensor sum;
+  if (res.has_value()) {
+    check_dev(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(), "ln_fwd: res mismatch");
+    sum = at::empty_like(x);
+    if (bias.has_value()) TORCH_CHECK(bias->numel() == H && bias->scalar_type() == x.scalar_type());
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty_like(x);
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({rows}, f32), rstd = at::empty({rows}, f32);
+  dsa::launch_ln_fwd(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr,
+                     (res.has_value() && bias.has_value()) ? bias->data_ptr() : nullptr,
+                     res.has_value() ? sum.data_ptr() : nullptr, gamma.data_ptr(),
+                     beta.has_value() ? beta->data_ptr() : nullptr, y.data_ptr(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), rows, (int)H, (float)eps, dt, cur_stream());
+  return {y, mean, rstd, sum};
+}
+
+// Returns (dx, dgamma, dbeta)
+std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, bool has_beta, OptT dres) {
+  check_dev(dy, "dy"); check_dev(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "ln_bwd: dy/x mismatch");
+  const int64_t H = x.size(-1);
+  const int64_t rows = x.numel() / H;
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "ln_bwd: stats size");
+  if (dres.has_value()) TORCH_CHECK(dres->sizes() == x.sizes() && dres->is_contiguous(), "ln_bwd: dres");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor dx = at::empty_like(x);
+  Tensor dgamma = at::empty_like(gamma);
+  Tensor dbeta = has_beta ? at::empty_like(gamma) : Tensor();
+  const int grid = dsa::ln_bwd_grid(rows);
+  Tensor partial = at::empty({2 * (int64_t)grid * H}, x.options().dtype(at::kFloat));
+  dsa::launch_ln_bwd(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                     dres.has_value() ? dres->data_ptr() : nullptr, dx.data_ptr(), dgamma.data_ptr(),
+                     has_beta ? dbeta.data_ptr() : nullptr, partial.data_ptr<float>(), rows, (int)H, dcode(x),
+                     cur_stream());
+  return {dx, dgamma, dbeta};
+}
+
+// ----------------------------------------------------------------------------- bias + gelu
+Tensor bias_gelu_fwd(Tensor x, OptT b, bool approx) {
+  check_dev(x, "x");
+  const int64_t C = x.size(-1);
+  const int dt = dcode(x);
+  TORCH_CHECK(C % (dt == dsa::kCodeF32 ? 4 : 8) == 0, "bias_gelu: last dim must be a multiple of 16 bytes");
+  if (b.has_value()) TORCH_CHECK(b->numel() == C && b->scalar_type() == x.scalar_type(), "bias_gelu: bias");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty_like(x);
+  dsa::launch_bias_gelu_fwd(x.data_ptr(), b.has_value() ? b->data_ptr() : nullptr, y.data_ptr(), x.numel() / C,
+                            (int)C, approx ? 1 : 0, dt, cur_stream());
+  return y;
+}
+
+// Returns (dx, dbias)
+std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, OptT b, bool approx) {
+  check_dev(dy, "dy"); check_dev(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "bias_gelu_bwd: mismatch");
+  const int64_t C = x.size(-1);
+  const int64_t rows = x.numel() / C;
+  const int dt = dcode(x);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor dx = at::empty_like(x);
+  Tensor db, partial;
+  if (b.has_value()) {
+    db = at::empty_like(*b);
+    partial = at::empty({(int64_t)dsa::bias_gelu_row_chunks(rows, (int)C, dt) * C}, x.options().dtype(at::kFloat));
+  }
+  dsa::launch_bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), b.has_value() ? b->data_ptr() : nullptr, dx.data_ptr(),
+                            b.has_value() ? db.data_ptr() : nullptr,
+                            b.has_value() ? partial.data_ptr<float>() : nullptr, rows, (int)C, approx ? 1 : 0, dt,
+                            cur_stream());
+  return {dx, db};
+}
+
+// Sum over all leading dims -> [C]
+Tensor colsum(Tensor x) {
+  check_dev(x, "x");
+  const int64_t C = x.size(-1);
+  const int64_t rows = x.numel() / C;
+  const int dt = dcode(x);
+  TORCH_CHECK(C % (dt == dsa::kCodeF32 ? 4 : 8) == 0, "colsum: last dim must be a multiple of 16 bytes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor out = at::empty({C}, x.options());
+  Tensor partial =
+      at::empty({(int64_t)dsa::bias_gelu_row_chunks(rows, (int)C, dt) * C}, x.options().dtype(at::kFloat));
+  dsa::launch_colsum(x.data_ptr(), out.data_ptr(), partial.data_ptr<float>(), rows, (int)C, 0, dt, cur_stream());
+  return out;
+}
+
+// ----------------------------------------------------------------------------- attention elementwise
+// qkv [B,S,NH*3*HD] (NeoX per-head q|k|v) -> q,k,v [B,NH,S,HD]; cs [S, ROT/2, 2] fp32
+std::vector<Tensor> rotary_split_fwd(Tensor qkv, Tensor cs, int64_t NH, int64_t HD, int64_t ROT, double qscale) {
+  check_dev(qkv, "qkv"); check_dev(cs, "cos_sin");
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == NH * 3 * HD, "rotary_split: qkv must be [B,S,NH*3*HD]");
+  TORCH_CHECK(HD % 8 == 0 && ROT % 2 == 0 && ROT <= HD, "rotary_split: HD % 8 == 0, ROT even and <= HD");
+  TORCH_CHECK(qkv.scalar_type() != at::kFloat, "rotary_split: 16-bit inputs only");
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  TORCH_CHECK(cs.scalar_type() == at::kFloat && cs.numel() >= S * (ROT / 2) * 2, "rotary_split: cos/sin table");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  auto opts = qkv.options();
+  Tensor q = at::empty({B, NH, S, HD}, opts), k = at::empty({B, NH, S, HD}, opts), v = at::empty({B, NH, S, HD}, opts);
+  dsa::launch_rotary_split_fwd(qkv.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cs.data_ptr<float>(),
+                               (int)B, (int)S, (int)NH, (int)HD, (int)ROT, (float)qscale, dcode(qkv), cur_stream());
+  return {q, k, v};
+}
+
+Tensor rotary_split_bwd(Tensor dq, Tensor dk, Tensor dv, Tensor cs, int64_t ROT, double qscale) {
+  check_dev(dq, "dq"); check_dev(dk, "dk"); check_dev(dv, "dv");
+  TORCH_CHECK(dq.dim() == 4 && dq.sizes() == dk.sizes() && dq.sizes() == dv.sizes(), "rotary_split_bwd: shapes");
+  const int64_t B = dq.size(0), NH = dq.size(1), S = dq.size(2), HD = dq.size(3);
+  TORCH_CHECK(HD % 8 == 0, "rotary_split_bwd: HD % 8");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dq.device());
+  Tensor dqkv = at::empty({B, S, NH * 3 * HD}, dq.options());
+  dsa::launch_rotary_split_bwd(dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dqkv.data_ptr(), cs.data_ptr<float>(),
+                               (int)B, (int)S, (int)NH, (int)HD, (int)ROT, (float)qscale, dcode(dq), cur_stream());
+  return dqkv;
+}
+
+// scores [..., Sq, C] -> probs. mask: optional additive [Bm, 1|.., Sq, C] broadcast over heads.
+Tensor softmax_fwd(Tensor x, OptT mask, double scale, bool causal, int64_t heads) {
+  check_dev(x, "scores");
+  TORCH_CHECK(x.scalar_type() != at::kFloat, "softmax: 16-bit inputs only");
+  const int64_t C = x.size(-1), Sq = x.size(-2);
+  const int64_t R = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= dsa::softmax_max_cols(), "softmax: key length must be a multiple of 8 and <= ",
+              dsa::softmax_max_cols());
+  if (mask.has_value()) {
+    check_dev(*mask, "mask");
+    TORCH_CHECK(mask->scalar_type() == x.scalar_type() && mask->size(-1) == C && mask->size(-2) == Sq,
+                "softmax: mask must be [B,1,Sq,C] in the score dtype");
+    TORCH_CHECK(mask->numel() / (Sq * C) * heads * Sq * C == x.numel(), "softmax: mask batch mismatch");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty_like(x);
+  dsa::launch_softmax_fwd(x.data_ptr(), y.data_ptr(), mask.has_value() ? mask->data_ptr() : nullptr, R, (int)C,
+                          (int)Sq, (int)heads, (float)scale, causal ? 1 : 0, dcode(x), cur_stream());
+  return y;
+}
+
+Tensor softmax_bwd(Tensor dy, Tensor y, double scale) {
+  check_dev(dy, "dy"); check_dev(y, "y");
+  TORCH_CHECK(dy.sizes() == y.sizes() && dy.scalar_type() == y.scalar_type(), "softmax_bwd: mismatch");
+  const int64_t C = y.size(-1);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
+  Tensor dx = at::empty_like(y);
+  dsa::launch_softmax_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), y.numel() / C, (int)C, (float)scale, dcode(y),
+                          cur_stream());
+  return dx;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("rotary_split_fwd", &rotary_split_fwd);
+  m.def("rotary_split_bwd", &rotary_split_bwd);
+  m.def("softmax_fwd", &softmax_fwd);
+  m.def("softmax_bwd", &softmax_bwd);
+  m.doc() = "deeperspeed_amd CDNA4 (gfx950) HIP kernels";
+  m.def("adam_flat", &adam_flat);
+  m.def("adam_multi", &adam_multi);
+  m.def("sumsq_accum", &sumsq_accum);
+  m.def("scale_copy", &scale_copy);
+  m.def("lamb", &lamb);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("bias_gelu_fwd", &bias_gelu_fwd);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("colsum", &colsum);
+}

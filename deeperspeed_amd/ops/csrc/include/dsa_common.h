@@ -1,0 +1,202 @@
+// Shared device helpers for the deeperspeed_amd CDNA4 (gfx950) kernels.
+//
+// Design rules (MI355X): wave = 64 lanes, block sizes are multiples of 64,
+// bf16/fp16 memory traffic is always vectorised to 16 bytes per lane, math is
+// done in fp32, reductions use wave64 shuffles then one LDS hop.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+namespace dsa {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------------------
+// dtype tags. The host side passes an integer code; kernels are templated.
+// ---------------------------------------------------------------------------
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+struct bf16_t { uint16_t x; };
+struct f16_t { uint16_t x; };
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// Round-to-nearest-even; a plain cast lowers to v_cvt_pk_bf16_f32 on gfx950
+// and keeps NaNs NaN.
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t v) {
+  __half h = *reinterpret_cast<__half*>(&v);
+  return __half2float(h);
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  __half h = __float2half(f);
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+
+template <typename T> struct Conv;
+template <> struct Conv<float> {
+  __device__ __forceinline__ static float load(const float* p, int64_t i) { return p[i]; }
+  __device__ __forceinline__ static void store(float* p, int64_t i, float v) { p[i] = v; }
+};
+template <> struct Conv<bf16_t> {
+  __device__ __forceinline__ static float load(const bf16_t* p, int64_t i) {
+    return bf16_to_f32(p[i].x);
+  }
+  __device__ __forceinline__ static void store(bf16_t* p, int64_t i, float v) {
+    p[i].x = f32_to_bf16(v);
+  }
+};
+template <> struct Conv<f16_t> {
+  __device__ __forceinline__ static float load(const f16_t* p, int64_t i) {
+    return f16_to_f32(p[i].x);
+  }
+  __device__ __forceinline__ static void store(f16_t* p, int64_t i, float v) {
+    p[i].x = f32_to_f16(v);
+  }
+};
+
+// 16-byte vector load/store of N elements of T converted to/from fp32.
+// N * sizeof(T) must be 16 (8 x 16-bit, or 4 x fp32).
+template <typename T> struct Vec16;
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  __device__ __forceinline__ static void load(const float* p, float (&o)[4]) {
+    float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&o)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+};
+
+template <typename T16, float (*TO)(uint16_t), uint16_t (*FROM)(float)>
+struct Vec16Half {
+  static constexpr int N = 8;
+  __device__ __forceinline__ static void load(const T16* p, float (&o)[8]) {
+    uint4 v = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = TO((uint16_t)(w[i] & 0xffff));
+      o[2 * i + 1] = TO((uint16_t)(w[i] >> 16));
+    }
+  }
+  __device__ __forceinline__ static void store(T16* p, const float (&o)[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = (uint32_t)FROM(o[2 * i]) | ((uint32_t)FROM(o[2 * i + 1]) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <> struct Vec16<bf16_t> : Vec16Half<bf16_t, bf16_to_f32, f32_to_bf16> {};
+template <> struct Vec16<f16_t> : Vec16Half<f16_t, f16_to_f32, f32_to_f16> {};
+
+// Generic N-element (N = 4 or 8) vector IO for mixed-dtype elementwise kernels:
+// loads N contiguous elements as fp32 irrespective of storage type.
+template <typename T, int N>
+__device__ __forceinline__ void load_n(const T* p, float (&o)[N]) {
+  if constexpr (Vec16<T>::N == N) {
+    Vec16<T>::load(p, o);
+  } else if constexpr (Vec16<T>::N * 2 == N) {
+    float a[N / 2], b[N / 2];
+    Vec16<T>::load(p, a);
+    Vec16<T>::load(p + N / 2, b);
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) { o[i] = a[i]; o[i + N / 2] = b[i]; }
+  } else {  // 8-byte half load for 16-bit types with N == 4
+    static_assert(N == 4, "unsupported vector width");
+    uint2 v = *reinterpret_cast<const uint2*>(p);
+    float t[8];
+    uint32_t w[2] = {v.x, v.y};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      t[2 * i] = Conv<T>::load(reinterpret_cast<const T*>(&w[i]), 0);
+      t[2 * i + 1] = Conv<T>::load(reinterpret_cast<const T*>(&w[i]), 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = t[i];
+  }
+}
+template <typename T, int N>
+__device__ __forceinline__ void store_n(T* p, const float (&o)[N]) {
+  if constexpr (Vec16<T>::N == N) {
+    Vec16<T>::store(p, o);
+  } else if constexpr (Vec16<T>::N * 2 == N) {
+    float a[N / 2], b[N / 2];
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) { a[i] = o[i]; b[i] = o[i + N / 2]; }
+    Vec16<T>::store(p, a);
+    Vec16<T>::store(p + N / 2, b);
+  } else {
+    static_assert(N == 4, "unsupported vector width");
+    uint32_t w[2];
+    T* t = reinterpret_cast<T*>(w);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Conv<T>::store(t, i, o[i]);
+    *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wave64 / block reductions
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Sum over the whole block (blockDim.x a multiple of 64, <= 1024). `red` must
+// hold >= 16 floats of LDS. Result is broadcast to every thread.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();  // protect `red` reuse across consecutive calls
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += red[i];
+  return r;
+}
+// Two sums at once (one LDS round trip).
+__device__ __forceinline__ void block_sum2(float& a, float& b, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  __syncthreads();
+  if (lane == 0) { red[wid] = a; red[16 + wid] = b; }
+  __syncthreads();
+  float ra = 0.f, rb = 0.f;
+  for (int i = 0; i < nw; ++i) { ra += red[i]; rb += red[16 + i]; }
+  a = ra; b = rb;
+}
+
+// Bijective XCD-aware remap of a flat block id (cdna_hip_programming T1): blocks
+// dealt round-robin over the 8 XCDs are renumbered so that each XCD receives
+// a contiguous range of logical tiles (neighbouring tiles share its L2).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  constexpr int NX = 8;
+  if (nwg < NX) return orig;
+  const int q = nwg / NX, r = nwg % NX;
+  const int xcd = orig % NX, idx = orig / NX;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace dsa
+
+#define DSA_CHECK_LAUNCH() (void)hipGetLastError()

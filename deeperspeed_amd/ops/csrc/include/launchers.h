@@ -1,0 +1,64 @@
+// Host-side launcher declarations shared by the .hip translation units and the
+// torch binding unit. Kernels never include torch headers (keeps device compiles
+// fast); bindings never include kernel code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dsa {
+
+enum DTypeCode : int { kCodeF32 = 0, kCodeBF16 = 1, kCodeF16 = 2 };
+
+struct AdamArgs {
+  float lr, beta1, beta2, eps, weight_decay;
+  float bc1, bc2;
+  float grad_scale;
+  int adamw;
+};
+
+struct LambArgs {
+  float lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale;
+  float max_coeff, min_coeff;
+  int adamw;
+};
+
+// optim.hip
+void launch_adam_flat(void* w, int wt, const void* g, int gt, float* m, float* v, void* out, int ot, int64_t n,
+                      AdamArgs a, hipStream_t s);
+void launch_adam_multi(const int64_t* meta, int T, int64_t total_chunks, int64_t chunk, int wt, int gt, int ot,
+                       AdamArgs a, hipStream_t s);
+void launch_sumsq_accum(const void* x, int xt, int64_t n, float* workspace, float* out, hipStream_t s);
+void launch_scale_copy(const void* x, int xt, void* y, int yt, int64_t n, const float* scale_ptr, float scale,
+                       hipStream_t s);
+void launch_lamb(void* w, int wt, const void* g, int gt, float* m, float* v, float* upd, void* out, int ot,
+                 int64_t n, LambArgs a, float* workspace, float* coeff_out, hipStream_t s);
+
+// norm_act.hip
+int ln_max_hidden(int dt);
+int ln_bwd_grid(int64_t rows);
+void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_out, const void* gamma,
+                   const void* beta, void* y, float* mean, float* rstd, int64_t rows, int H, float eps, int dt,
+                   hipStream_t s);
+void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
+                   const void* dres, void* dx, void* dgamma, void* dbeta, float* partial, int64_t rows, int H,
+                   int dt, hipStream_t s);
+void launch_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, int C, int approx, int dt,
+                          hipStream_t s);
+int bias_gelu_row_chunks(int64_t rows, int C, int dt);
+void launch_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, void* db, float* partial,
+                          int64_t rows, int C, int approx, int dt, hipStream_t s);
+void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C, int accum, int dt,
+                   hipStream_t s);
+
+// attn_elem.hip
+void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const float* cs, int B, int S, int NH,
+                             int HD, int ROT, float qscale, int dt, hipStream_t s);
+void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, void* dqkv, const float* cs, int B,
+                             int S, int NH, int HD, int ROT, float qscale, int dt, hipStream_t s);
+int softmax_max_cols();
+void launch_softmax_fwd(const void* x, void* y, const void* mask, int64_t R, int C, int Sq, int heads, float scale,
+                        int causal, int dt, hipStream_t s);
+void launch_softmax_bwd(const void* dy, const void* y, void* dx, int64_t R, int C, float scale, int dt,
+                        hipStream_t s);
+
+}  // namespace dsa

@@ -1,0 +1,279 @@
+// Attention-side memory-bound kernels for CDNA4:
+//  * rotary_split: fused QKV layout transform + rotary embedding + query pre-scaling
+//    (GPT-NeoX layout [B,S,heads,3*hd] -> q,k,v each [B,heads,S,hd]); and its backward.
+//    Reference analogues: bias_add_transform_0213 / transform4d_0213
+//    (csrc/transformer/transform_kernels.cu:161-560), extended with NeoX partial rotary.
+//  * scaled masked softmax fwd/bwd over score rows (reference attn_softmax /
+//    softmax_backward_kernel, csrc/transformer/softmax_kernels.cu:9-580) with causal,
+//    additive-mask and key-padding variants; rows held in registers, one 256-thread
+//    block per row, wave64 reductions (the reference is warp32 and capped at S<8192).
+#include "../include/dsa_common.h"
+#include "../include/launchers.h"
+
+namespace dsa {
+
+// --------------------------------------------------------------------------------------
+// rotary_split forward. One thread per 8-element vector of the [B,S,heads,3*hd] input.
+// cs: [S, rot/2] float2 table (cos, sin) for positions 0..S-1 (+ pos_offset).
+// --------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) rotary_split_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ q,
+                                                               T* __restrict__ k, T* __restrict__ v,
+                                                               const float2* __restrict__ cs, int B, int S,
+                                                               int NH, int HD, int ROT, float qscale) {
+  const int vec_per_item = 3 * HD / 8;
+  const int64_t total = (int64_t)B * S * NH * vec_per_item;
+  const int half = ROT / 2;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int vi = (int)(t % vec_per_item);
+    const int64_t item = t / vec_per_item;  // (b, s, h)
+    const int h = (int)(item % NH);
+    const int s = (int)((item / NH) % S);
+    const int b = (int)(item / ((int64_t)NH * S));
+    const int e0 = vi * 8;                // element within 3*hd
+    const int which = e0 / HD;            // 0=q 1=k 2=v
+    const int d0 = e0 - which * HD;       // element within hd (vector never straddles: HD % 8 == 0)
+    const T* src = qkv + item * 3 * HD;
+    float x[8];
+    Vec16<T>::load(src + e0, x);
+    if (which < 2 && d0 < ROT) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = d0 + j;
+        if (d < ROT) {
+          const int i = d < half ? d : d - half;
+          const float2 c = cs[(int64_t)s * half + i];
+          const int pd = d < half ? d + half : d - half;
+          const float partner = Conv<T>::load(src, which * HD + pd);
+          o[j] = d < half ? x[j] * c.x - partner * c.y : x[j] * c.x + partner * c.y;
+        } else {
+          o[j] = x[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = o[j];
+    }
+    if (which == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] *= qscale;
+    }
+    T* dst = which == 0 ? q : (which == 1 ? k : v);
+    const int64_t off = (((int64_t)b * NH + h) * S + s) * HD + d0;
+    Vec16<T>::store(dst + off, x);
+  }
+}
+
+// backward: dq,dk,dv [B,heads,S,hd] -> dqkv [B,S,heads,3*hd] (inverse rotation, q scale)
+template <typename T>
+__global__ void __launch_bounds__(256) rotary_split_bwd_kernel(const T* __restrict__ dq, const T* __restrict__ dk,
+                                                               const T* __restrict__ dv, T* __restrict__ dqkv,
+                                                               const float2* __restrict__ cs, int B, int S,
+                                                               int NH, int HD, int ROT, float qscale) {
+  const int vec_per_item = 3 * HD / 8;
+  const int64_t total = (int64_t)B * S * NH * vec_per_item;
+  const int half = ROT / 2;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int vi = (int)(t % vec_per_item);
+    const int64_t item = t / vec_per_item;
+    const int h = (int)(item % NH);
+    const int s = (int)((item / NH) % S);
+    const int b = (int)(item / ((int64_t)NH * S));
+    const int e0 = vi * 8;
+    const int which = e0 / HD;
+    const int d0 = e0 - which * HD;
+    const T* src = which == 0 ? dq : (which == 1 ? dk : dv);
+    const int64_t off = (((int64_t)b * NH + h) * S + s) * HD;
+    float g[8];
+    Vec16<T>::load(src + off + d0, g);
+    const float sc = which == 0 ? qscale : 1.f;
+    if (which < 2 && d0 < ROT) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = d0 + j;
+        if (d < ROT) {
+          const int i = d < half ? d : d - half;
+          const float2 c = cs[(int64_t)s * half + i];
+          const int pd = d < half ? d + half : d - half;
+          const float gp = Conv<T>::load(src + off, pd);
+          // y1 = x1 c - x2 s ; y2 = x2 c + x1 s  =>  dx1 = dy1 c + dy2 s ; dx2 = dy2 c - dy1 s
+          o[j] = d < half ? g[j] * c.x + gp * c.y : g[j] * c.x - gp * c.y;
+        } else {
+          o[j] = g[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = o[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] *= sc;
+    Vec16<T>::store(dqkv + item * 3 * HD + e0, g);
+  }
+}
+
+// --------------------------------------------------------------------------------------
+// Softmax over rows of scores [R, C] with row r belonging to query position
+// q = r % Sq (causal: keys > q + (C - Sq) masked). Optional additive mask [Bm, Sq, C]
+// broadcast over heads (mask row = (r / (heads*Sq)) * Sq + q when mask_batch > 0).
+// y = softmax(scale * x + mask). Rows processed one per 256-thread block.
+// --------------------------------------------------------------------------------------
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) softmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                          const T* __restrict__ mask, int64_t R, int C, int Sq,
+                                                          int heads, float scale, int causal) {
+  __shared__ float red[32];
+  constexpr int VN = 8;
+  const int64_t r = blockIdx.x;
+  const int q = (int)(r % Sq);
+  const int limit = causal ? q + (C - Sq) + 1 : C;  // valid keys [0, limit)
+  const T* xr = x + r * C;
+  const T* mr = nullptr;
+  if (mask) {
+    const int64_t bidx = r / ((int64_t)heads * Sq);
+    mr = mask + (bidx * Sq + q) * (int64_t)C;
+  }
+  float vals[NV][VN];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kk = 0; kk < NV; ++kk) {
+    const int c0 = (threadIdx.x + kk * 256) * VN;
+    if (c0 < C) {
+      Vec16<T>::load(xr + c0, vals[kk]);
+      float mv[VN];
+      if (mr) Vec16<T>::load(mr + c0, mv);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) {
+        float s = vals[kk][j] * scale + (mr ? mv[j] : 0.f);
+        if (c0 + j >= limit) s = -INFINITY;
+        vals[kk][j] = s;
+        mx = fmaxf(mx, s);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) vals[kk][j] = -INFINITY;
+    }
+  }
+  // block max
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < NV; ++kk)
+#pragma unroll
+    for (int j = 0; j < VN; ++j) {
+      const float e = (vals[kk][j] == -INFINITY || mx == -INFINITY) ? 0.f : __expf(vals[kk][j] - mx);
+      vals[kk][j] = e;
+      sum += e;
+    }
+  sum = block_sum(sum, red);
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;
+#pragma unroll
+  for (int kk = 0; kk < NV; ++kk) {
+    const int c0 = (threadIdx.x + kk * 256) * VN;
+    if (c0 < C) {
+      float o[VN];
+#pragma unroll
+      for (int j = 0; j < VN; ++j) o[j] = vals[kk][j] * inv;
+      Vec16<T>::store(y + r * C + c0, o);
+    }
+  }
+}
+
+// dx = scale * y * (dy - sum(dy*y))
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) softmax_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                          T* __restrict__ dx, int64_t R, int C, float scale) {
+  __shared__ float red[32];
+  constexpr int VN = 8;
+  const int64_t r = blockIdx.x;
+  float yv[NV][VN], gv[NV][VN];
+  float dot = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < NV; ++kk) {
+    const int c0 = (threadIdx.x + kk * 256) * VN;
+    if (c0 < C) {
+      Vec16<T>::load(y + r * C + c0, yv[kk]);
+      Vec16<T>::load(dy + r * C + c0, gv[kk]);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) dot = fmaf(yv[kk][j], gv[kk][j], dot);
+    }
+  }
+  dot = block_sum(dot, red);
+#pragma unroll
+  for (int kk = 0; kk < NV; ++kk) {
+    const int c0 = (threadIdx.x + kk * 256) * VN;
+    if (c0 < C) {
+      float o[VN];
+#pragma unroll
+      for (int j = 0; j < VN; ++j) o[j] = scale * yv[kk][j] * (gv[kk][j] - dot);
+      Vec16<T>::store(dx + r * C + c0, o);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------
+#define DSA_DISPATCH_16(code, T, ...)                      \
+  switch (code) {                                          \
+    case kBF16: { using T = bf16_t; __VA_ARGS__; } break;  \
+    case kF16: { using T = f16_t; __VA_ARGS__; } break;    \
+    default: break;                                        \
+  }
+
+#define DSA_DISPATCH_SNV(nv, NV, ...)                                \
+  switch (nv) {                                                      \
+    case 1: { constexpr int NV = 1; __VA_ARGS__; } break;            \
+    case 2: { constexpr int NV = 2; __VA_ARGS__; } break;            \
+    case 3: case 4: { constexpr int NV = 4; __VA_ARGS__; } break;    \
+    case 5: case 6: case 7: case 8: { constexpr int NV = 8; __VA_ARGS__; } break; \
+    default: { constexpr int NV = 16; __VA_ARGS__; } break;          \
+  }
+
+static int elem_grid(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  if (g > 16384) g = 16384;
+  return (int)(g < 1 ? 1 : g);
+}
+
+void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const float* cs, int B, int S, int NH,
+                             int HD, int ROT, float qscale, int dt, hipStream_t s) {
+  const int64_t work = (int64_t)B * S * NH * 3 * HD / 8;
+  DSA_DISPATCH_16(dt, T,
+    hipLaunchKernelGGL((rotary_split_fwd_kernel<T>), dim3(elem_grid(work)), dim3(256), 0, s, (const T*)qkv, (T*)q,
+                       (T*)k, (T*)v, (const float2*)cs, B, S, NH, HD, ROT, qscale));
+}
+
+void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, void* dqkv, const float* cs, int B,
+                             int S, int NH, int HD, int ROT, float qscale, int dt, hipStream_t s) {
+  const int64_t work = (int64_t)B * S * NH * 3 * HD / 8;
+  DSA_DISPATCH_16(dt, T,
+    hipLaunchKernelGGL((rotary_split_bwd_kernel<T>), dim3(elem_grid(work)), dim3(256), 0, s, (const T*)dq,
+                       (const T*)dk, (const T*)dv, (T*)dqkv, (const float2*)cs, B, S, NH, HD, ROT, qscale));
+}
+
+int softmax_max_cols() { return 16 * 256 * 8; }
+
+void launch_softmax_fwd(const void* x, void* y, const void* mask, int64_t R, int C, int Sq, int heads, float scale,
+                        int causal, int dt, hipStream_t s) {
+  if (R <= 0) return;
+  const int nv = (C / 8 + 255) / 256;
+  DSA_DISPATCH_16(dt, T, DSA_DISPATCH_SNV(nv, NV,
+    hipLaunchKernelGGL((softmax_fwd_kernel<T, NV>), dim3((unsigned)R), dim3(256), 0, s, (const T*)x, (T*)y,
+                       (const T*)mask, R, C, Sq, heads, scale, causal)));
+}
+
+void launch_softmax_bwd(const void* dy, const void* y, void* dx, int64_t R, int C, float scale, int dt,
+                        hipStream_t s) {
+  if (R <= 0) return;
+  const int nv = (C / 8 + 255) / 256;
+  DSA_DISPATCH_16(dt, T, DSA_DISPATCH_SNV(nv, NV,
+    hipLaunchKernelGGL((softmax_bwd_kernel<T, NV>), dim3((unsigned)R), dim3(256), 0, s, (const T*)dy,
+                       (const T*)y, (T*)dx, R, C, scale)));
+}
+
+}  // namespace dsa

@@ -1,0 +1,386 @@
+// LayerNorm / bias-GeLU / bias-residual-dropout kernels for CDNA4.
+//
+// Parity targets: csrc/transformer/normalize_kernels.cu (fused_bias_residual_layer_norm,
+// LayerNormBackward1/2), csrc/transformer/gelu_kernels.cu (fused_bias_gelu, d_gelu_func),
+// csrc/transformer/general_kernels.cu (column_sum_reduce).
+// MI355X design: one 256-thread block (4 waves) per row with the whole row held in
+// registers (16-byte vector loads), fp32 statistics, wave64 shuffles + one LDS hop;
+// weight/bias gradients are produced as per-block column partials in the same pass
+// and folded by a tiny column-reduce kernel (no atomics, deterministic).
+#include "../include/dsa_common.h"
+#include "../include/launchers.h"
+
+namespace dsa {
+
+constexpr int LN_THREADS = 256;
+constexpr int LN_MAXV = 8;  // up to 8 16-byte vectors per thread: H <= 16384 (bf16), 8192 (fp32)
+
+// ---------------------------------------------------------------------------
+// LayerNorm forward: y = (x - mean) * rstd * gamma + beta
+// optional: x_out = x + residual (+ bias) is formed first and stored (pre-LN
+// residual fusion); when `res` is null the input is used as-is.
+// ---------------------------------------------------------------------------
+template <typename T, int NV>
+__global__ void __launch_bounds__(LN_THREADS) ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                            const T* __restrict__ bias, T* __restrict__ sum_out,
+                                                            const T* __restrict__ gamma, const T* __restrict__ beta,
+                                                            T* __restrict__ y, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out, int H, float eps) {
+  __shared__ float red[32];
+  constexpr int VN = Vec16<T>::N;
+  const int nvec = H / VN;
+  const int64_t row = blockIdx.x;
+  const T* xr = x + row * H;
+  float vals[NV][VN];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int vi = threadIdx.x + k * LN_THREADS;
+    if (vi < nvec) {
+      Vec16<T>::load(xr + vi * VN, vals[k]);
+      if (res) {
+        float r[VN];
+        Vec16<T>::load(res + row * H + vi * VN, r);
+#pragma unroll
+        for (int j = 0; j < VN; ++j) vals[k][j] += r[j];
+        if (bias) {
+          float b[VN];
+          Vec16<T>::load(bias + vi * VN, b);
+#pragma unroll
+          for (int j = 0; j < VN; ++j) vals[k][j] += b[j];
+        }
+        if (sum_out) Vec16<T>::store(sum_out + row * H + vi * VN, vals[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < VN; ++j) s += vals[k][j];
+    }
+  }
+  const float mean = block_sum(s, red) / H;
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int vi = threadIdx.x + k * LN_THREADS;
+    if (vi < nvec) {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) { float d = vals[k][j] - mean; ss = fmaf(d, d, ss); }
+    }
+  }
+  const float var = block_sum(ss, red) / H;
+  const float rstd = rsqrtf(var + eps);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int vi = threadIdx.x + k * LN_THREADS;
+    if (vi < nvec) {
+      float gm[VN], bt[VN], o[VN];
+      Vec16<T>::load(gamma + vi * VN, gm);
+      if (beta) Vec16<T>::load(beta + vi * VN, bt);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) o[j] = (vals[k][j] - mean) * rstd * gm[j] + (beta ? bt[j] : 0.f);
+      Vec16<T>::store(y + row * H + vi * VN, o);
+    }
+  }
+  if (threadIdx.x == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm backward. Each block walks rows blockIdx.x, blockIdx.x + gridDim.x, ...
+// computes dx per row and accumulates dgamma/dbeta column partials in registers,
+// written once per block into partial[blockIdx.x][H] (and [gridDim + blockIdx.x][H]).
+// dres (optional): gradient flowing through a residual branch, added into dx.
+// ---------------------------------------------------------------------------
+template <typename T, int NV>
+__global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const T* __restrict__ gamma,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd,
+                                                            const T* __restrict__ dres, T* __restrict__ dx,
+                                                            float* __restrict__ partial, int64_t rows, int H) {
+  __shared__ float red[32];
+  constexpr int VN = Vec16<T>::N;
+  const int nvec = H / VN;
+  float dg[NV][VN], db[NV][VN], gm[NV][VN];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int vi = threadIdx.x + k * LN_THREADS;
+#pragma unroll
+    for (int j = 0; j < VN; ++j) { dg[k][j] = 0.f; db[k][j] = 0.f; gm[k][j] = 0.f; }
+    if (vi < nvec) Vec16<T>::load(gamma + vi * VN, gm[k]);
+  }
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NV][VN], g[NV][VN];
+    float a = 0.f, b = 0.f;  // sum(dxhat), sum(dxhat * xhat)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int vi = threadIdx.x + k * LN_THREADS;
+      if (vi < nvec) {
+        Vec16<T>::load(x + row * H + vi * VN, xh[k]);
+        Vec16<T>::load(dy + row * H + vi * VN, g[k]);
+#pragma unroll
+        for (int j = 0; j < VN; ++j) {
+          xh[k][j] = (xh[k][j] - mu) * rs;
+          dg[k][j] = fmaf(g[k][j], xh[k][j], dg[k][j]);
+          db[k][j] += g[k][j];
+          const float dxh = g[k][j] * gm[k][j];
+          a += dxh;
+          b = fmaf(dxh, xh[k][j], b);
+        }
+      }
+    }
+    block_sum2(a, b, red);
+    a /= H; b /= H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int vi = threadIdx.x + k * LN_THREADS;
+      if (vi < nvec) {
+        float o[VN];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) o[j] = rs * (g[k][j] * gm[k][j] - a - xh[k][j] * b);
+        if (dres) {
+          float r[VN];
+          Vec16<T>::load(dres + row * H + vi * VN, r);
+#pragma unroll
+          for (int j = 0; j < VN; ++j) o[j] += r[j];
+        }
+        Vec16<T>::store(dx + row * H + vi * VN, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int vi = threadIdx.x + k * LN_THREADS;
+    if (vi < nvec) {
+      float* pg = partial + (int64_t)blockIdx.x * H + vi * VN;
+      float* pb = partial + (int64_t)(gridDim.x + blockIdx.x) * H + vi * VN;
+#pragma unroll
+      for (int j = 0; j < VN; j += 4) {
+        *reinterpret_cast<float4*>(pg + j) = make_float4(dg[k][j], dg[k][j + 1], dg[k][j + 2], dg[k][j + 3]);
+        *reinterpret_cast<float4*>(pb + j) = make_float4(db[k][j], db[k][j + 1], db[k][j + 2], db[k][j + 3]);
+      }
+    }
+  }
+}
+
+// out[c] = sum_r partial[r][c] over R rows, C columns; written in dtype T
+// (optionally accumulated into existing out when `accum`).
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ partial, int R, int C,
+                                                     T* __restrict__ out, int accum) {
+  // 64 columns x 4 row-groups per block; lanes own columns -> coalesced reads.
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (c < C)
+    for (int r = rg; r < R; r += 4) acc += partial[(int64_t)r * C + c];
+  red[rg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (accum) v += Conv<T>::load(out, c);
+    Conv<T>::store(out, c, v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bias + GeLU (exact erf or tanh approximation)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float gelu_f(float x, bool approx) {
+  if (approx) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  }
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+__device__ __forceinline__ float dgelu_f(float x, bool approx) {
+  if (approx) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    const float u = k0 * (x + k1 * x * x * x);
+    const float t = tanhf(u);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+  }
+  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict__ x, const T* __restrict__ b,
+                                                            T* __restrict__ y, int64_t n, int C, int approx) {
+  constexpr int VN = Vec16<T>::N;
+  const int64_t nvec = n / VN;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    float v[VN], bb[VN];
+    Vec16<T>::load(x + i * VN, v);
+    const int c0 = (int)((i * VN) % C);
+    if (b) Vec16<T>::load(b + c0, bb);
+#pragma unroll
+    for (int j = 0; j < VN; ++j) v[j] = gelu_f(v[j] + (b ? bb[j] : 0.f), approx);
+    Vec16<T>::store(y + i * VN, v);
+  }
+}
+
+// dx = dy * gelu'(x + b); per-block column partials of dx for the bias gradient.
+// grid: (ceil(C / (256*VN)), row_chunks); each thread owns VN consecutive columns.
+template <typename T>
+__global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const T* __restrict__ b, T* __restrict__ dx,
+                                                            float* __restrict__ partial, int64_t rows, int C,
+                                                            int approx) {
+  constexpr int VN = Vec16<T>::N;
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * VN;
+  if (c0 >= C) return;
+  const int64_t chunk = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = blockIdx.y * chunk;
+  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float bb[VN], acc[VN];
+#pragma unroll
+  for (int j = 0; j < VN; ++j) acc[j] = 0.f;
+  if (b) Vec16<T>::load(b + c0, bb);
+  for (int64_t r = r0; r < r1; ++r) {
+    float xv[VN], g[VN];
+    Vec16<T>::load(x + r * C + c0, xv);
+    Vec16<T>::load(dy + r * C + c0, g);
+#pragma unroll
+    for (int j = 0; j < VN; ++j) {
+      g[j] *= dgelu_f(xv[j] + (b ? bb[j] : 0.f), approx);
+      acc[j] += g[j];
+    }
+    Vec16<T>::store(dx + r * C + c0, g);
+  }
+  if (partial) {
+    float* p = partial + (int64_t)blockIdx.y * C + c0;
+#pragma unroll
+    for (int j = 0; j < VN; j += 4) *reinterpret_cast<float4*>(p + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------
+#define DSA_DISPATCH_T2(code, T, ...)                     \
+  switch (code) {                                          \
+    case kF32: { using T = float; __VA_ARGS__; } break;    \
+    case kBF16: { using T = bf16_t; __VA_ARGS__; } break;  \
+    case kF16: { using T = f16_t; __VA_ARGS__; } break;    \
+    default: break;                                        \
+  }
+
+#define DSA_DISPATCH_NV(nv, NV, ...)                                \
+  switch (nv) {                                                      \
+    case 1: { constexpr int NV = 1; __VA_ARGS__; } break;            \
+    case 2: { constexpr int NV = 2; __VA_ARGS__; } break;            \
+    case 3: { constexpr int NV = 3; __VA_ARGS__; } break;            \
+    case 4: { constexpr int NV = 4; __VA_ARGS__; } break;            \
+    case 5: case 6: { constexpr int NV = 6; __VA_ARGS__; } break;    \
+    default: { constexpr int NV = 8; __VA_ARGS__; } break;           \
+  }
+
+int ln_max_hidden(int dt) { return LN_THREADS * LN_MAXV * (dt == kF32 ? 4 : 8); }
+
+void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_out, const void* gamma,
+                   const void* beta, void* y, float* mean, float* rstd, int64_t rows, int H, float eps, int dt,
+                   hipStream_t s) {
+  if (rows <= 0) return;
+  const int nv = (H / (dt == kF32 ? 4 : 8) + LN_THREADS - 1) / LN_THREADS;
+  DSA_DISPATCH_T2(dt, T, DSA_DISPATCH_NV(nv, NV,
+    hipLaunchKernelGGL((ln_fwd_kernel<T, NV>), dim3((unsigned)rows), dim3(LN_THREADS), 0, s,
+                       (const T*)x, (const T*)res, (const T*)bias, (T*)sum_out, (const T*)gamma,
+                       (const T*)beta, (T*)y, mean, rstd, H, eps)));
+}
+
+int ln_bwd_grid(int64_t rows) { return (int)(rows < 512 ? rows : 512); }
+
+// partial workspace: 2 * ln_bwd_grid(rows) * H floats
+void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
+                   const void* dres, void* dx, void* dgamma, void* dbeta, float* partial, int64_t rows, int H,
+                   int dt, hipStream_t s) {
+  if (rows <= 0) return;
+  const int grid = ln_bwd_grid(rows);
+  const int nv = (H / (dt == kF32 ? 4 : 8) + LN_THREADS - 1) / LN_THREADS;
+  DSA_DISPATCH_T2(dt, T,
+    DSA_DISPATCH_NV(nv, NV, hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(grid), dim3(LN_THREADS), 0, s,
+                       (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
+                       partial, rows, H));
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, s, partial, grid, H,
+                       (T*)dgamma, 0);
+    if (dbeta) hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, s,
+                                  partial + (int64_t)grid * H, grid, H, (T*)dbeta, 0));
+}
+
+void launch_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, int C, int approx, int dt,
+                          hipStream_t s) {
+  const int64_t n = rows * C;
+  if (n <= 0) return;
+  const int vn = dt == kF32 ? 4 : 8;
+  int64_t g = (n / vn + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  DSA_DISPATCH_T2(dt, T,
+    hipLaunchKernelGGL((bias_gelu_fwd_kernel<T>), dim3((unsigned)g), dim3(256), 0, s,
+                       (const T*)x, (const T*)b, (T*)y, n, C, approx));
+}
+
+int bias_gelu_row_chunks(int64_t rows, int C, int dt) {
+  const int vn = dt == kF32 ? 4 : 8;
+  const int cblocks = (C / vn + 255) / 256;
+  // aim for ~2048 blocks total, each walking >= 16 rows
+  int64_t rc = 2048 / (cblocks > 0 ? cblocks : 1);
+  if (rc > rows / 16) rc = rows / 16;
+  if (rc < 1) rc = 1;
+  return (int)rc;
+}
+
+// partial workspace: bias_gelu_row_chunks(rows, C) * C floats (when db != null)
+void launch_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, void* db, float* partial,
+                          int64_t rows, int C, int approx, int dt, hipStream_t s) {
+  if (rows <= 0) return;
+  const int vn = dt == kF32 ? 4 : 8;
+  const int cblocks = (C / vn + 255) / 256;
+  const int rc = bias_gelu_row_chunks(rows, C, dt);
+  DSA_DISPATCH_T2(dt, T,
+    hipLaunchKernelGGL((bias_gelu_bwd_kernel<T>), dim3(cblocks, rc), dim3(256), 0, s,
+                       (const T*)dy, (const T*)x, (const T*)b, (T*)dx, db ? partial : nullptr, rows, C, approx);
+    if (db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 63) / 64), dim3(256), 0, s, partial, rc, C,
+                               (T*)db, 0));
+}
+
+// Column sum of a [rows, C] tensor into out[C] (bias gradients of plain linears).
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const T* __restrict__ x, float* __restrict__ partial,
+                                                             int64_t rows, int C) {
+  constexpr int VN = Vec16<T>::N;
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * VN;
+  if (c0 >= C) return;
+  const int64_t chunk = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = blockIdx.y * chunk;
+  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float acc[VN];
+#pragma unroll
+  for (int j = 0; j < VN; ++j) acc[j] = 0.f;
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[VN];
+    Vec16<T>::load(x + r * C + c0, v);
+#pragma unroll
+    for (int j = 0; j < VN; ++j) acc[j] += v[j];
+  }
+  float* p = partial + (int64_t)blockIdx.y * C + c0;
+#pragma unroll
+  for (int j = 0; j < VN; j += 4) *reinterpret_cast<float4*>(p + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+}
+
+void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C, int accum, int dt,
+                   hipStream_t s) {
+  if (rows <= 0) return;
+  const int vn = dt == kF32 ? 4 : 8;
+  const int cblocks = (C / vn + 255) / 256;
+  const int rc = bias_gelu_row_chunks(rows, C, dt);
+  DSA_DISPATCH_T2(dt, T,
+    hipLaunchKernelGGL((colsum_partial_kernel<T>), dim3(cblocks, rc), dim3(256), 0, s, (const T*)x, partial,
+                       rows, C);
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 63) / 64), dim3(256), 0, s, partial, rc, C, (T*)out,
+                       accum));
+}
+
+}  // namespace dsa

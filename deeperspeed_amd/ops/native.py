@@ -1,0 +1,241 @@
+"""Python entry points for the native (HIP / C++) kernels.
+
+Every GPU hot op in the framework goes through this module.  On a GPU tensor the HIP
+extension is mandatory: if it cannot be built or imported the call raises (no silent
+eager fallback).  CPU tensors (unit tests on the CPU-only CI host) use a PyTorch reference
+implementation of the same math; that path is never taken for tensors on the MI355X.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import builder
+
+_hip = None
+
+
+def hip_ops():
+    """The `_hip_ops` extension module (built in-tree on first use)."""
+    global _hip
+    if _hip is None:
+        _hip = builder.load("_hip_ops")
+    return _hip
+
+
+def on_gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# --------------------------------------------------------------------------- LayerNorm
+def _ln_ref(x, gamma, beta, eps):
+    xf = x.float()
+    mean = xf.mean(-1, keepdim=True)
+    var = (xf - mean).pow(2).mean(-1, keepdim=True)
+    rstd = torch.rsqrt(var + eps)
+    y = (xf - mean) * rstd * gamma.float()
+    if beta is not None:
+        y = y + beta.float()
+    return y.to(x.dtype), mean.reshape(-1), rstd.reshape(-1)
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        x = x.contiguous()
+        if x.is_cuda:
+            y, mean, rstd, _ = hip_ops().ln_fwd(x, gamma, beta, eps, None, None)
+        else:
+            y, mean, rstd = _ln_ref(x, gamma, beta, eps)
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.has_beta = beta is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        if x.is_cuda:
+            dx, dg, db = hip_ops().ln_bwd(dy, x, gamma, mean, rstd, ctx.has_beta, None)
+        else:
+            H = x.shape[-1]
+            xf = x.float().reshape(-1, H)
+            g = dy.float().reshape(-1, H)
+            xh = (xf - mean[:, None]) * rstd[:, None]
+            dxh = g * gamma.float()
+            dx = rstd[:, None] * (dxh - dxh.mean(-1, keepdim=True) - xh * (dxh * xh).mean(-1, keepdim=True))
+            dx = dx.reshape(x.shape).to(x.dtype)
+            dg = (g * xh).sum(0).to(gamma.dtype)
+            db = g.sum(0).to(gamma.dtype) if ctx.has_beta else None
+        return dx, dg, (db if ctx.has_beta else None), None
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float = 1e-5):
+    return _LayerNormFn.apply(x, weight, bias, eps)
+
+
+class FusedLayerNorm(torch.nn.Module):
+    """LayerNorm on the HIP kernel (wave64 row reductions, fp32 statistics)."""
+
+    def __init__(self, hidden: int, eps: float = 1e-5, elementwise_affine: bool = True, dtype=None, device=None):
+        super().__init__()
+        self.normalized_shape = (hidden,)
+        self.eps = eps
+        self.weight = torch.nn.Parameter(torch.ones(hidden, dtype=dtype, device=device))
+        self.bias = torch.nn.Parameter(torch.zeros(hidden, dtype=dtype, device=device))
+
+    def forward(self, x):
+        return layer_norm(x, self.weight, self.bias, self.eps)
+
+    def extra_repr(self):
+        return f"{self.normalized_shape[0]}, eps={self.eps}"
+
+
+# --------------------------------------------------------------------------- bias + GeLU
+def _gelu_ref(x, approx):
+    return torch.nn.functional.gelu(x, approximate="tanh" if approx else "none")
+
+
+class _BiasGeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, approx):
+        x = x.contiguous()
+        if x.is_cuda:
+            y = hip_ops().bias_gelu_fwd(x, bias, approx)
+        else:
+            y = _gelu_ref((x.float() + (bias.float() if bias is not None else 0)), approx).to(x.dtype)
+        ctx.save_for_backward(x, bias)
+        ctx.approx = approx
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, bias = ctx.saved_tensors
+        dy = dy.contiguous()
+        if x.is_cuda:
+            dx, db = hip_ops().bias_gelu_bwd(dy, x, bias, ctx.approx)
+        else:
+            with torch.enable_grad():
+                xi = (x.float() + (bias.float() if bias is not None else 0)).detach().requires_grad_(True)
+                y = _gelu_ref(xi, ctx.approx)
+                (g,) = torch.autograd.grad(y, xi, dy.float())
+            dx = g.to(x.dtype)
+            db = g.reshape(-1, g.shape[-1]).sum(0).to(bias.dtype) if bias is not None else None
+        return dx, (db if ctx.has_bias else None), None
+
+
+def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False):
+    return _BiasGeluFn.apply(x, bias, approximate)
+
+
+# --------------------------------------------------------------------------- reductions
+_WS = {}
+
+
+def _workspace(device, n=2048):
+    key = (device, n)
+    ws = _WS.get(key)
+    if ws is None:
+        ws = torch.empty(n, dtype=torch.float32, device=device)
+        _WS[key] = ws
+    return ws
+
+
+def sumsq_accumulate(x: torch.Tensor, out: torch.Tensor):
+    """out[0] += sum(x.float()**2) without a host sync (HIP on GPU)."""
+    if x.numel() == 0:
+        return out
+    if x.is_cuda:
+        if x.data_ptr() % 16 != 0 or not x.is_contiguous():
+            out.add_(x.float().pow(2).sum())
+        else:
+            hip_ops().sumsq_accum(x, _workspace(x.device), out)
+    else:
+        out.add_(x.float().pow(2).sum())
+    return out
+
+
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    if x.is_cuda:
+        return hip_ops().colsum(x.contiguous())
+    return x.reshape(-1, x.shape[-1]).float().sum(0).to(x.dtype)
+
+
+# --------------------------------------------------------------------------- Adam
+def adam_flat_(w, g, m, v, out, lr, beta1, beta2, eps, weight_decay, step, bias_correction, grad_scale, adamw):
+    """In-place Adam/AdamW on flat tensors.  `w` is the fp32 master (or the param itself),
+    `out` an optional low-precision model copy refreshed in the same pass."""
+    bc1 = 1.0 - beta1 ** step if bias_correction else 1.0
+    bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
+    if w.is_cuda:
+        hip_ops().adam_flat(w, g, m, v, out, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale, adamw)
+        return
+    # CPU reference (tests on CPU CI): identical math in fp32
+    gf = g.float() * grad_scale
+    wf = w.float()
+    if not adamw and weight_decay != 0:
+        gf = gf + weight_decay * wf
+    m.mul_(beta1).add_(gf, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(gf, gf, value=1 - beta2)
+    upd = (m / bc1) / ((v / bc2).sqrt() + eps)
+    if adamw and weight_decay != 0:
+        upd = upd + weight_decay * wf
+    wf = wf - lr * upd
+    w.copy_(wf)
+    if out is not None:
+        out.copy_(wf)
+
+
+def scale_copy_(x: torch.Tensor, y: torch.Tensor, scale: float = 1.0, scale_tensor: Optional[torch.Tensor] = None):
+    if x.is_cuda and x.data_ptr() % (x.element_size() * 4) == 0 and y.data_ptr() % (y.element_size() * 4) == 0:
+        hip_ops().scale_copy(x, y, scale_tensor, scale)
+    else:
+        s = scale if scale_tensor is None else scale * scale_tensor.float()
+        y.copy_(x.float() * s)
+    return y
+
+
+# --------------------------------------------------------------------------- flash attention
+def has_flash_attention(q: torch.Tensor) -> bool:
+    """True when the fused MFMA attention kernel supports this problem."""
+    if not q.is_cuda or q.dtype not in (torch.bfloat16, torch.float16):
+        return False
+    mod = hip_ops()
+    return hasattr(mod, "flash_attn_fwd") and q.shape[-1] in (64, 96, 128)
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        o, lse = hip_ops().flash_attn_fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = hip_ops().flash_attn_bwd(do.contiguous(), q, k, v, o, lse, ctx.causal, ctx.scale)
+        return dq, dk, dv, None, None
+
+
+def flash_attention(q, k, v, causal=True, scale=1.0):
+    return _FlashAttnFn.apply(q, k, v, causal, scale)
+
+
+# --------------------------------------------------------------------------- flatten
+def _cpu_flatten():
+    """(flatten, unflatten) pair: native C++ ops when built, torch._utils otherwise."""
+    try:
+        mod = builder.load("_cpu_ops")
+        if hasattr(mod, "flatten"):
+            return mod.flatten, mod.unflatten
+    except Exception:
+        pass
+    from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+    return _flatten_dense_tensors, _unflatten_dense_tensors

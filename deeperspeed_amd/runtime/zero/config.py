@@ -1,0 +1,104 @@
+"""`zero_optimization` config section.
+
+Reference parity: deepspeed/runtime/zero/config.py:1-177, zero/constants.py:37-116,
+zero/offload_config.py, zero/offload_constants.py (same keys, defaults and deprecated
+aliases: legacy boolean form, `cpu_offload*`, `allgather_size`).
+"""
+
+from ..config_utils import DeepSpeedConfigObject
+
+ZERO_OPTIMIZATION = "zero_optimization"
+ZERO_OPTIMIZATION_DISABLED = 0
+ZERO_OPTIMIZATION_OPTIMIZER_STATES = 1
+ZERO_OPTIMIZATION_GRADIENTS = 2
+ZERO_OPTIMIZATION_WEIGHTS = 3
+MAX_STAGE_ZERO_OPTIMIZATION = ZERO_OPTIMIZATION_WEIGHTS
+
+OFFLOAD_CPU_DEVICE = "cpu"
+OFFLOAD_NVME_DEVICE = "nvme"
+
+# (key, default) for scalar fields; attribute name == key unless mapped below
+_SCALARS = {
+    "stage": 0,
+    "allgather_partitions": True,
+    "reduce_scatter": False,  # DeeperSpeed default (zero/constants.py:55)
+    "overlap_comm": None,  # resolved per stage below
+    "contiguous_gradients": False,
+    "reduce_bucket_size": int(5e8),
+    "allgather_bucket_size": int(5e8),
+    "load_from_fp32_weights": True,
+    "elastic_checkpoint": True,
+    "cpu_offload": False,
+    "cpu_offload_params": False,
+    "cpu_offload_use_pin_memory": False,
+    "sub_group_size": int(1e12),
+    "stage3_max_live_parameters": int(1e9),
+    "stage3_max_reuse_distance": int(1e9),
+    "stage3_prefetch_bucket_size": int(5e7),
+    "stage3_param_persistence_threshold": int(1e5),
+    "stage3_gather_fp16_weights_on_model_save": False,
+    # MI355X extension: run grad reduction in the model dtype even when the
+    # global fp32_allreduce default applies (kept off by default for parity).
+    "round_robin_gradients": False,
+}
+
+_OFFLOAD_PARAM_DEFAULTS = dict(device=None, nvme_path=None, buffer_count=5, buffer_size=int(1e8),
+                               max_in_cpu=int(1e9), pin_memory=False)
+_OFFLOAD_OPT_DEFAULTS = dict(device=None, nvme_path=None, buffer_count=4, pin_memory=False, pipeline_read=False,
+                             pipeline_write=False, fast_init=False,
+                             # MI355X extension: "all" = fp32 master + Adam moments on host (reference
+                             # ZeRO-Offload); "master" = only the fp32 master on host, moments stay in HBM
+                             # and the step streams the master through pinned buffers.
+                             states="all")
+
+
+class OffloadConfig(dict):
+    """dict with attribute access (offload_param / offload_optimizer sections)."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+
+def _parse_offload(d, defaults):
+    if d is None:
+        return None
+    out = OffloadConfig(defaults)
+    out.update(d)
+    if out.get("device") in (None, "none"):
+        return None
+    assert out["device"] in (OFFLOAD_CPU_DEVICE, OFFLOAD_NVME_DEVICE), f"bad offload device {out['device']}"
+    if out["device"] == OFFLOAD_NVME_DEVICE:
+        assert out.get("nvme_path"), "nvme offload requires nvme_path"
+    return out
+
+
+class DeepSpeedZeroConfig(DeepSpeedConfigObject):
+    def __init__(self, param_dict):
+        zd = param_dict.get(ZERO_OPTIMIZATION, {})
+        if isinstance(zd, bool):  # legacy `"zero_optimization": true` -> stage 1
+            zd = {"stage": ZERO_OPTIMIZATION_OPTIMIZER_STATES if zd else 0}
+        elif isinstance(zd, int):
+            zd = {"stage": zd}
+        self._raw = dict(zd)
+        for k, v in _SCALARS.items():
+            setattr(self, k, zd.get(k, v))
+        if "allgather_size" in zd:  # deprecated alias
+            self.allgather_bucket_size = zd["allgather_size"]
+        if self.overlap_comm is None:
+            self.overlap_comm = self.stage == ZERO_OPTIMIZATION_WEIGHTS
+        self.stage = int(self.stage)
+        self.reduce_bucket_size = int(self.reduce_bucket_size)
+        self.allgather_bucket_size = int(self.allgather_bucket_size)
+        self.offload_param = _parse_offload(zd.get("offload_param"), _OFFLOAD_PARAM_DEFAULTS)
+        self.offload_optimizer = _parse_offload(zd.get("offload_optimizer"), _OFFLOAD_OPT_DEFAULTS)
+        # deprecated booleans map onto the new sections
+        if self.cpu_offload and self.offload_optimizer is None:
+            self.offload_optimizer = OffloadConfig(_OFFLOAD_OPT_DEFAULTS)
+            self.offload_optimizer.update(device=OFFLOAD_CPU_DEVICE, pin_memory=self.cpu_offload_use_pin_memory)
+        if self.cpu_offload_params and self.offload_param is None:
+            self.offload_param = OffloadConfig(_OFFLOAD_PARAM_DEFAULTS)
+            self.offload_param.update(device=OFFLOAD_CPU_DEVICE, pin_memory=self.cpu_offload_use_pin_memory)
+        assert 0 <= self.stage <= MAX_STAGE_ZERO_OPTIMIZATION, f"ZeRO stage must be 0..3, got {self.stage}"

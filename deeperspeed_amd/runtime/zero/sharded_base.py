@@ -1,0 +1,453 @@
+"""Shared machinery of the flat-arena ZeRO optimizers (stages 0-3).
+
+Reference parity (behaviour, not structure): loss scaling + overflow skip + grad-norm
+clipping + inner step + fp16/bf16 copy-back of FP16_Optimizer (fp16/fused_optimizer.py:242-330)
+and of the ZeRO wrappers (stage2.py:1366-1596, stage3.py:2742-2940); ZeRO checkpoint
+state (stage2.py:1720-1880, stage3.py:3046-3160) including elastic re-partitioning when
+the data-parallel world size changes; ZeRO-Offload of optimizer state (stage2.py:750-911).
+
+MI355X design:
+* Per group: one contiguous fp32 master shard, one contiguous gradient shard, Adam moments
+  as flat tensors.  The step is one fused HIP launch per bucket chunk that reads the
+  reduced gradient, updates master + moments and writes the bf16 model shard in the same
+  pass (grad unscale and clip coefficient folded into a single scalar).
+* Overflow + global grad norm come from one device-side sum-of-squares per shard plus a
+  single all-reduce, then ONE host sync per step (reference: one per tensor).
+* Offload ("cpu"): `states="all"` keeps master+moments in pinned host memory and steps with
+  the native AVX-512 CPU Adam; `states="master"` (MI355X extension for 288 GB HBM) keeps
+  the moments in HBM and streams the fp32 master through pinned staging buffers with
+  H2D / kernel / D2H overlapped on separate HIP streams.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ...ops import native
+from ...ops.adam.fused_adam import FusedAdam
+from ...utils.logging import logger
+from ..fp16.loss_scaler import DynamicLossScaler, LossScaler
+from .layout import FlatGroup, layout_signature, params_to_shard, shards_to_params
+
+OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
+
+
+def _is_mp_param(p):
+    return bool(getattr(p, "model_parallel", False) or getattr(p, "tensor_model_parallel", False))
+
+
+def _dist_ready():
+    return dist.is_available() and dist.is_initialized()
+
+
+class ShardedOptimizerBase:
+    """Not an nn optimizer itself: wraps a client/basic torch optimizer (`init_optimizer`)."""
+
+    def __init__(self, init_optimizer, dp_process_group=None, mpu=None, clip_grad=0.0, static_loss_scale=1.0,
+                 dynamic_loss_scale=False, dynamic_loss_args=None, fp32_reduce=False, gradient_predivide_factor=1.0,
+                 gradient_accumulation_steps=1, offload_optimizer=None, timers=None, verbose=False):
+        self.optimizer = init_optimizer
+        self.dp_group = dp_process_group
+        self.mpu = mpu
+        self.clip_grad = float(clip_grad or 0.0)
+        self.fp32_reduce = bool(fp32_reduce)
+        self.gradient_predivide_factor = float(gradient_predivide_factor or 1.0)
+        self.gradient_accumulation_steps = int(gradient_accumulation_steps)
+        self.timers = timers
+        self.verbose = verbose
+        self.dp_world = dist.get_world_size(dp_process_group) if _dist_ready() else 1
+        self.dp_rank = dist.get_rank(dp_process_group) if _dist_ready() else 0
+        self.mp_world = mpu.get_model_parallel_world_size() if mpu is not None else 1
+        self.mp_rank = mpu.get_model_parallel_rank() if mpu is not None else 0
+        if dynamic_loss_scale:
+            self.loss_scaler = DynamicLossScaler(**(dynamic_loss_args or {}))
+            self.dynamic_loss_scale = True
+        else:
+            self.loss_scaler = LossScaler(scale=static_loss_scale)
+            self.dynamic_loss_scale = False
+        self.overflow = False
+        self.offload = offload_optimizer
+        self.offload_states = (offload_optimizer or {}).get("states", "all") if offload_optimizer else None
+        self.fused = isinstance(init_optimizer, FusedAdam) or getattr(init_optimizer, "supports_flat_update", False)
+        self.groups: List[FlatGroup] = []
+        self.is_gradient_accumulation_boundary = True
+        self._global_grad_norm = 0.0
+        self._norm_buf = None
+        self.device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+            else torch.device("cpu")
+        self._copy_streams = None
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    @property
+    def loss_scale(self):
+        return self.loss_scaler.loss_scale
+
+    @property
+    def cur_scale(self):
+        return self.loss_scaler.loss_scale
+
+    def _get_loss_scale(self):
+        return self.loss_scaler.loss_scale
+
+    def _set_loss_scale(self, v):
+        self.loss_scaler.cur_scale = v
+
+    def get_global_grad_norm(self):
+        return self._global_grad_norm
+
+    # ------------------------------------------------------------------ setup helpers
+    def _split_groups(self):
+        """Split each inner param group into (dtype, model-parallel) flat groups."""
+        from .layout import split_param_group
+        out = []
+        for gi, pg in enumerate(self.optimizer.param_groups):
+            for si, (dt, mp, plist) in enumerate(split_param_group(pg["params"], _is_mp_param)):
+                out.append(FlatGroup(group_index=gi, sub_index=si, dtype=dt, model_parallel=mp, params=plist))
+        return out
+
+    def _alloc_master_and_state(self, init_shard_fn):
+        """Create master shards from `init_shard_fn(group) -> fp32 tensor [S]` on the
+        right device, rebind inner optimizer param groups to the masters."""
+        host = self.offload is not None and self.offload.get("device") in ("cpu", "nvme")
+        pin = bool(self.offload and self.offload.get("pin_memory", True)) and torch.cuda.is_available()
+        for g in self.groups:
+            m = init_shard_fn(g).float()
+            if host:
+                hm = torch.empty(g.shard_numel, dtype=torch.float32, pin_memory=pin)
+                hm.copy_(m)
+                m = hm
+            g.master = m
+            g.master.requires_grad_(False)
+        # rebind optimizer groups: params -> masters of their flat groups
+        for gi, pg in enumerate(self.optimizer.param_groups):
+            pg["params"] = [g.master for g in self.groups if g.group_index == gi]
+        self.optimizer.state.clear()
+        # moments: allocated up-front so memory is visible and offload placement is explicit
+        if self.fused or self.offload is not None:
+            for g in self.groups:
+                st = self.optimizer.state[g.master]
+                st["step"] = 0
+                on_host = host and self.offload_states == "all"
+                kw = dict(dtype=torch.float32, pin_memory=on_host and pin)
+                if on_host:
+                    st["exp_avg"] = torch.zeros(g.shard_numel, **kw)
+                    st["exp_avg_sq"] = torch.zeros(g.shard_numel, **kw)
+                else:
+                    st["exp_avg"] = torch.zeros(g.shard_numel, dtype=torch.float32, device=self.device)
+                    st["exp_avg_sq"] = torch.zeros(g.shard_numel, dtype=torch.float32, device=self.device)
+
+    def _inner_group(self, g: FlatGroup):
+        return self.optimizer.param_groups[g.group_index]
+
+    # ------------------------------------------------------------------ norm / overflow
+    def _shard_grads_for_norm(self):
+        """Yield (tensor, include) pairs whose sum of squares forms this rank's share."""
+        for g in self.groups:
+            if g.shard_grad is None:
+                continue
+            # replicated (non model-parallel) params are counted on mp rank 0 only
+            include = g.model_parallel or self.mp_rank == 0
+            yield g.shard_grad, include
+
+    def _grads_are_sharded(self):
+        return True
+
+    def _compute_norm_sq(self) -> torch.Tensor:
+        if self._norm_buf is None:
+            self._norm_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+        buf = self._norm_buf
+        buf.zero_()
+        for t, include in self._shard_grads_for_norm():
+            if include:
+                native.sumsq_accumulate(t, buf)
+        if _dist_ready():
+            if self._grads_are_sharded() and self.dp_world > 1:
+                dist.all_reduce(buf, group=self.dp_group)
+            if self.mp_world > 1:
+                dist.all_reduce(buf, group=self.mpu.get_model_parallel_group())
+        return buf
+
+    def _grad_divisor(self):
+        """Total factor the summed gradients must be divided by (loss scale * averaging)."""
+        return self.loss_scale * self._avg_divisor()
+
+    def _avg_divisor(self):
+        return float(self.dp_world) / self._prescaled_by()
+
+    def _prescaled_by(self):
+        return 1.0
+
+    # ------------------------------------------------------------------ step
+    def _unscale_and_clip_coef(self, total_sq: float):
+        div = self._grad_divisor()
+        norm = math.sqrt(total_sq) / div if total_sq >= 0 else float("nan")
+        self._global_grad_norm = norm
+        coef = 1.0
+        if self.clip_grad > 0 and norm > self.clip_grad:
+            coef = self.clip_grad / (norm + 1e-6)
+        return coef / div, norm
+
+    def _check_overflow_and_scale(self):
+        total = float(self._compute_norm_sq().item())  # the one host sync per step
+        overflow = not math.isfinite(total)
+        self.overflow = overflow
+        if self.dynamic_loss_scale or overflow:
+            prev = self.loss_scale
+            self.loss_scaler.update_scale(overflow)
+            if overflow:
+                logger.info(f"[deepspeed] OVERFLOW! Skipping step. Attempted loss scale: {prev}, reducing to "
+                            f"{self.loss_scale}")
+        return overflow, total
+
+    def step(self, closure=None):
+        if self.timers is not None:
+            self.timers("optimizer_step").start()
+        overflow, total = self._check_overflow_and_scale()
+        if overflow:
+            self.zero_grad()
+            if self.timers is not None:
+                self.timers("optimizer_step").stop()
+            return
+        grad_scale, _ = self._unscale_and_clip_coef(total)
+        self._inner_step(grad_scale)
+        self._post_step()
+        self.zero_grad()
+        if self.timers is not None:
+            self.timers("optimizer_step").stop()
+
+    def _bucket_out(self, g: FlatGroup, b):
+        """Low-precision destination (view) of bucket b's shard chunk after the update."""
+        return g.shard_param[b.shard_offset: b.shard_offset + b.chunk]
+
+    def _after_bucket_update(self, g: FlatGroup, b):
+        pass
+
+    def _post_step(self):
+        pass
+
+    def _inner_step(self, grad_scale: float):
+        if self.offload is not None:
+            return self._offload_step(grad_scale)
+        if self.fused:
+            for g in self.groups:
+                st = self.optimizer.state_for(g.master) if isinstance(self.optimizer, FusedAdam) else \
+                    self.optimizer.state[g.master]
+                st["step"] = st.get("step", 0) + 1
+            for g in self.groups:
+                grp = self._inner_group(g)
+                for b in g.buckets:
+                    lo, hi = b.shard_offset, b.shard_offset + b.chunk
+                    out = self._bucket_out(g, b)
+                    self.optimizer.update_flat(grp, g.master, g.master, g.shard_grad, out=out, grad_scale=grad_scale,
+                                               lo=lo, hi=hi)
+                    self._after_bucket_update(g, b)
+            return
+        # generic torch optimizer over the fp32 master shards
+        for g in self.groups:
+            gr = g.shard_grad.float() if g.shard_grad.dtype != torch.float32 else g.shard_grad.clone()
+            gr.mul_(grad_scale)
+            g.master.grad = gr
+        self.optimizer.step()
+        for g in self.groups:
+            g.master.grad = None
+            for b in g.buckets:
+                out = self._bucket_out(g, b)
+                if out is not None and out.data_ptr() != g.master.data_ptr():
+                    native.scale_copy_(g.master[b.shard_offset: b.shard_offset + b.chunk], out)
+                self._after_bucket_update(g, b)
+
+    # ------------------------------------------------------------------ offload step
+    def _streams(self):
+        if self._copy_streams is None and torch.cuda.is_available():
+            self._copy_streams = (torch.cuda.Stream(), torch.cuda.Stream())
+        return self._copy_streams
+
+    def _offload_step(self, grad_scale: float):
+        grp_steps = {}
+        for g in self.groups:
+            st = self.optimizer.state[g.master]
+            st["step"] = st.get("step", 0) + 1
+            grp_steps[id(g)] = st["step"]
+        if self.offload_states == "master" and torch.cuda.is_available():
+            return self._offload_master_step(grad_scale, grp_steps)
+        return self._offload_all_step(grad_scale, grp_steps)
+
+    def _offload_master_step(self, grad_scale, grp_steps):
+        """fp32 master in pinned host memory, moments + grads in HBM.  Pipeline per piece:
+        H2D master (stream A) -> fused Adam (compute) -> D2H master (stream B)."""
+        h2d, d2h = self._streams()
+        cur = torch.cuda.current_stream()
+        nbuf = 3
+        piece = min(OFFLOAD_SUBCHUNK, max(b.chunk for g in self.groups for b in g.buckets))
+        stages = [torch.empty(piece, dtype=torch.float32, device=self.device) for _ in range(nbuf)]
+        free_ev = [None] * nbuf
+        k = 0
+        for g in self.groups:
+            grp = self._inner_group(g)
+            st = self.optimizer.state[g.master]
+            for b in g.buckets:
+                out_full = self._bucket_out(g, b)
+                for s in range(0, b.chunk, piece):
+                    e = min(s + piece, b.chunk)
+                    lo, hi, n = b.shard_offset + s, b.shard_offset + e, e - s
+                    i = k % nbuf
+                    k += 1
+                    buf = stages[i][:n]
+                    with torch.cuda.stream(h2d):
+                        if free_ev[i] is not None:
+                            h2d.wait_event(free_ev[i])
+                        buf.copy_(g.master[lo:hi], non_blocking=True)
+                        ev_in = torch.cuda.Event()
+                        ev_in.record(h2d)
+                    cur.wait_event(ev_in)
+                    b1, b2 = grp["betas"]
+                    native.adam_flat_(buf, g.shard_grad[lo:hi], st["exp_avg"][lo:hi], st["exp_avg_sq"][lo:hi],
+                                      out_full[s:e] if out_full is not None else None, grp["lr"], b1, b2, grp["eps"],
+                                      grp["weight_decay"], grp_steps[id(g)], grp.get("bias_correction", True),
+                                      grad_scale, bool(getattr(self.optimizer, "adam_w_mode", True)))
+                    ev_done = torch.cuda.Event()
+                    ev_done.record(cur)
+                    with torch.cuda.stream(d2h):
+                        d2h.wait_event(ev_done)
+                        g.master[lo:hi].copy_(buf, non_blocking=True)
+                        ev_free = torch.cuda.Event()
+                        ev_free.record(d2h)
+                    free_ev[i] = ev_free
+                self._after_bucket_update(g, b)
+        # host master must be final before the next step reads it (and before checkpoints)
+        d2h.synchronize()
+        del stages
+
+    def _offload_all_step(self, grad_scale, grp_steps):
+        """Reference ZeRO-Offload: master + moments on host, native CPU Adam."""
+        from ...ops.adam.cpu_adam import cpu_adam_update_flat
+        for g in self.groups:
+            grp = self._inner_group(g)
+            st = self.optimizer.state[g.master]
+            for b in g.buckets:
+                lo, hi = b.shard_offset, b.shard_offset + b.chunk
+                grad_host = g.shard_grad[lo:hi].to("cpu", dtype=torch.float32, non_blocking=False)
+                out = self._bucket_out(g, b)
+                cpu_adam_update_flat(g.master[lo:hi], grad_host, st["exp_avg"][lo:hi], st["exp_avg_sq"][lo:hi], grp,
+                                     grp_steps[id(g)], grad_scale, bool(getattr(self.optimizer, "adam_w_mode", True)),
+                                     out_device=out)
+                self._after_bucket_update(g, b)
+
+    # ------------------------------------------------------------------ grads
+    def zero_grad(self, set_to_none=True):
+        for g in self.groups:
+            if g.shard_grad is not None:
+                g.shard_grad.zero_()
+
+    # ------------------------------------------------------------------ checkpoint
+    def _zero_stage(self):
+        return 0
+
+    def state_dict(self):
+        base = self.optimizer.state_dict()
+        # move state tensors to cpu (checkpoint files are host tensors)
+        for k, v in base.get("state", {}).items():
+            for kk, vv in list(v.items()):
+                if torch.is_tensor(vv):
+                    v[kk] = vv.detach().cpu()
+        sd = {
+            "loss_scaler": self.loss_scaler.state_dict(),
+            "dynamic_loss_scale": self.dynamic_loss_scale,
+            "overflow": self.overflow,
+            "base_optimizer_state": base,
+            "zero_stage": self._zero_stage(),
+            "partition_count": self.dp_world,
+            "layout": layout_signature(self.groups),
+            "fp32_groups_key": self._fp32_key(),
+            self._fp32_key(): [g.master.detach().cpu() for g in self.groups],
+        }
+        return sd
+
+    def _fp32_key(self):
+        return "single_partition_of_fp32_groups"
+
+    def load_state_dict(self, state_dict_list, load_optimizer_states=True, load_from_fp32_weights=True):
+        if isinstance(state_dict_list, dict):
+            state_dict_list = [state_dict_list]
+        sd0 = state_dict_list[0]
+        if "loss_scaler" in sd0 and isinstance(sd0["loss_scaler"], dict):
+            self.loss_scaler.load_state_dict(sd0["loss_scaler"])
+        self.dynamic_loss_scale = sd0.get("dynamic_loss_scale", self.dynamic_loss_scale)
+        self.overflow = sd0.get("overflow", False)
+        key = sd0.get("fp32_groups_key", self._fp32_key())
+        same_layout = (len(state_dict_list) == self.dp_world and sd0.get("layout") == layout_signature(self.groups))
+        if same_layout:
+            mine = state_dict_list[self.dp_rank]
+            masters = mine[key]
+            moments = mine["base_optimizer_state"]
+        else:
+            masters, moments = self._elastic_merge(state_dict_list, key)
+        if load_from_fp32_weights:
+            for g, m in zip(self.groups, masters):
+                g.master.copy_(m.to(g.master.device))
+            self._refresh_params_from_master()
+        if load_optimizer_states:
+            self._load_moments(moments)
+
+    def _elastic_merge(self, sds, key):
+        """Re-partition masters and moments saved under a different DP world size."""
+        masters, moments_state = [], {}
+        sig_list = sds[0]["layout"]
+        old_base = [sd["base_optimizer_state"] for sd in sds]
+        for gi, g in enumerate(self.groups):
+            sig = sig_list[gi]
+            full = shards_to_params([sd[key][gi] for sd in sds], sig)
+            masters.append(params_to_shard(full, g, self.dp_rank, torch.float32))
+            st_new = {}
+            for name in ("exp_avg", "exp_avg_sq"):
+                olds = [ob["state"].get(gi, {}).get(name) for ob in old_base]
+                if all(o is not None for o in olds):
+                    st_new[name] = params_to_shard(shards_to_params(olds, sig), g, self.dp_rank, torch.float32)
+            step = old_base[0]["state"].get(gi, {}).get("step", 0)
+            st_new["step"] = step
+            moments_state[gi] = st_new
+        return masters, {"state": moments_state, "param_groups": old_base[0]["param_groups"]}
+
+    def _load_moments(self, base_sd):
+        # param groups hyper-params (lr etc.) restored; state tensors copied in place
+        saved_groups = base_sd.get("param_groups", [])
+        for pg, spg in zip(self.optimizer.param_groups, saved_groups):
+            for k, v in spg.items():
+                if k != "params":
+                    pg[k] = v
+        states = base_sd.get("state", {})
+        for gi, g in enumerate(self.groups):
+            s = states.get(gi)
+            if s is None:
+                continue
+            st = self.optimizer.state[g.master]
+            for k, v in s.items():
+                if torch.is_tensor(v) and k in st and torch.is_tensor(st[k]) and st[k].numel() == v.numel():
+                    st[k].copy_(v.to(st[k].device))
+                elif torch.is_tensor(v):
+                    st[k] = v.to(g.master.device if not (self.offload and self.offload_states == "all")
+                                 else "cpu").clone()
+                else:
+                    st[k] = v
+
+    def _refresh_params_from_master(self):
+        """Copy master -> low-precision shard/params after a fp32 restore."""
+        for g in self.groups:
+            for b in g.buckets:
+                out = self._bucket_out(g, b)
+                if out is not None and out.data_ptr() != g.master.data_ptr():
+                    out.copy_(g.master[b.shard_offset: b.shard_offset + b.chunk].to(out.device))
+                self._after_bucket_update(g, b)
+        self._post_step()

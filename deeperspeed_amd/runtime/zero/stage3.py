@@ -1,0 +1,498 @@
+"""ZeRO stage 3: parameter + gradient + optimizer-state partitioning.
+
+Reference parity (behaviour): deepspeed/runtime/zero/stage3.py (module pre/post forward and
+backward hooks, trace-driven prefetch bounded by `stage3_prefetch_bucket_size`, persistent
+small parameters below `stage3_param_persistence_threshold`, per-bucket gradient
+reduce-scatter during backward, sub-group steps, ZeRO-Offload / Infinity of optimizer
+state) and partition_parameters.py (`ds_shape`, `ds_numel`, status, external params).
+
+MI355X design:
+* Parameters are grouped into *units* (a module subtree of at most
+  `stage3_unit_max_numel` elements, else its direct params); each (unit, param group) is
+  ONE flat bucket.  Gathering a unit = one `all_gather_into_tensor` per bucket straight
+  into a fresh flat buffer whose slices become the parameters' storage; releasing drops
+  the buffer back to the caching allocator.  Gradient reduction = one
+  `reduce_scatter_tensor` per bucket as soon as the unit's backward completes.
+* Collectives are asynchronous on RCCL's stream; compute waits with stream-level
+  `work.wait()` only right before the unit is used (no device-wide synchronize).
+* Prefetch follows the forward/backward unit order recorded on the first step.
+* With a data-parallel world of 1 the shard IS the full parameter: parameters are bound
+  to views of the shard permanently and gradients accumulate in place into the shard
+  gradient (no gather, no copy) -- this is what makes the single-GPU 20B path fit in HBM.
+"""
+
+from __future__ import annotations
+
+import functools
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ...utils.logging import logger
+from .layout import ALIGN, FlatGroup, build_unit_buckets
+from .sharded_base import ShardedOptimizerBase, _dist_ready
+
+
+class ZeroParamStatus:
+    AVAILABLE = 1
+    NOT_AVAILABLE = 2
+    INFLIGHT = 3
+
+
+class ZeroParamType:
+    NORMAL = 1
+    PARTITIONED = 2
+    REMOTE = 3
+
+
+_EMPTY: Dict = {}
+
+
+def _empty_like(dtype, device):
+    key = (dtype, device)
+    t = _EMPTY.get(key)
+    if t is None:
+        t = torch.empty(0, dtype=dtype, device=device)
+        _EMPTY[key] = t
+    return t
+
+
+def _in_backward():
+    return torch._C._current_graph_task_id() != -1
+
+
+class ZeroUnit:
+    def __init__(self, uid, module, params):
+        self.uid = uid
+        self.module = module
+        self.params = list(params)
+        self.buckets = []  # (FlatGroup, Bucket)
+        self.status = ZeroParamStatus.NOT_AVAILABLE
+        self.works = []
+        self.fulls = []
+        self.numel = sum(p.numel() for p in self.params)
+        self.persistent = False
+        self.active = 0
+        self.in_backward = False
+        self.grad_fulls = []
+        self.bw_expected = 0
+        self.bw_ready = 0
+        self.reduced = False
+        self.external = []  # units whose params this module also uses (register_external_parameter)
+
+    def __repr__(self):
+        return f"ZeroUnit({self.uid}, {type(self.module).__name__}, numel={self.numel})"
+
+
+class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
+    def __init__(self, module, init_optimizer, dp_process_group=None, mpu=None, clip_grad=0.0,
+                 static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None,
+                 prefetch_bucket_size=int(5e7), max_live_parameters=int(1e9), max_reuse_distance=int(1e9),
+                 param_persistence_threshold=int(1e5), unit_max_numel=int(2e8), fp32_reduce=False,
+                 gradient_predivide_factor=1.0, gradient_accumulation_steps=1, offload_optimizer=None,
+                 offload_param=None, timers=None, overlap_comm=True, sub_group_size=int(1e12), verbose=False):
+        super().__init__(init_optimizer, dp_process_group=dp_process_group, mpu=mpu, clip_grad=clip_grad,
+                         static_loss_scale=static_loss_scale, dynamic_loss_scale=dynamic_loss_scale,
+                         dynamic_loss_args=dynamic_loss_args, fp32_reduce=fp32_reduce,
+                         gradient_predivide_factor=gradient_predivide_factor,
+                         gradient_accumulation_steps=gradient_accumulation_steps,
+                         offload_optimizer=offload_optimizer, timers=timers, verbose=verbose)
+        self.module = module
+        self.stage = 3
+        self.prefetch_bucket_size = int(prefetch_bucket_size)
+        self.max_live_parameters = int(max_live_parameters)
+        self.max_reuse_distance = int(max_reuse_distance)
+        self.persistence_threshold = int(param_persistence_threshold)
+        self.unit_max_numel = int(unit_max_numel)
+        self.offload_param = offload_param
+        self.single = self.dp_world == 1
+        self._pending = []
+        self._fwd_trace: List[int] = []
+        self._bwd_trace: List[int] = []
+        self._trace_frozen = False
+        self._fwd_pos = 0
+        self._bwd_pos = 0
+        self._units: List[ZeroUnit] = []
+        self._unit_of_param: Dict[int, ZeroUnit] = {}
+        self._assign_units(module)
+        self.groups = self._split_groups()
+        for g in self.groups:
+            build_unit_buckets(g, self.dp_world, lambda p: self._unit_of_param[id(p)])
+            for b in g.buckets:
+                b.unit.buckets.append((g, b))
+        self._build_shards()
+        self._alloc_master_and_state(lambda g: g.shard_param.float())
+        self._register_hooks()
+        if verbose or True:
+            n = sum(u.numel for u in self._units)
+            logger.info(f"ZeRO-3: {len(self._units)} units, {n / 1e9:.3f}B params, dp_world={self.dp_world}, "
+                        f"persistent units={sum(u.persistent for u in self._units)}")
+
+    # ------------------------------------------------------------------ units
+    def _assign_units(self, root):
+        seen = set()
+
+        def subtree_params(m):
+            return [p for p in m.parameters() if id(p) not in seen]
+
+        def make(m, params):
+            params = [p for p in params if id(p) not in seen]
+            if not params:
+                return
+            u = ZeroUnit(len(self._units), m, params)
+            for p in params:
+                seen.add(id(p))
+                self._unit_of_param[id(p)] = u
+            self._units.append(u)
+            m._zero_unit = u
+
+        def visit(m):
+            sub = subtree_params(m)
+            if not sub:
+                return
+            n = sum(p.numel() for p in sub)
+            kids = [c for c in m.children() if any(True for _ in c.parameters())]
+            if n <= self.unit_max_numel or not kids:
+                make(m, sub)
+                return
+            for c in m.children():
+                visit(c)
+            make(m, list(m.parameters(recurse=False)))
+
+        visit(root)
+        for u in self._units:
+            u.persistent = u.numel <= self.persistence_threshold and not self.single
+            for p in u.params:
+                p.ds_numel = p.numel()
+                p.ds_shape = p.shape
+                p.ds_id = id(p)
+                p.ds_unit = u
+                p.ds_status = ZeroParamStatus.AVAILABLE
+
+    def _build_shards(self):
+        """Create per-group bf16 shards from the (currently full) parameters, then free them."""
+        r = self.dp_rank
+        for g in self.groups:
+            dev = g.params[0].device if g.params[0].is_cuda else self.device
+            g.shard_param = torch.zeros(g.shard_numel, dtype=g.dtype, device=dev)
+            for b in g.buckets:
+                for i, p in enumerate(b.params):
+                    ov = b.chunk_overlap(r, i)
+                    if ov is None:
+                        continue
+                    p0, c0, ln = ov
+                    src = p.data.reshape(-1)
+                    if src.numel() == 0 and hasattr(p, "ds_tensor"):
+                        raise RuntimeError("zero.Init partitioned params must be adopted via GatheredParameters")
+                    g.shard_param[b.shard_offset + c0: b.shard_offset + c0 + ln].copy_(src[p0: p0 + ln])
+            gdt = self._grad_dtype(g)
+            g.shard_grad = torch.zeros(g.shard_numel, dtype=gdt, device=dev)
+        # release full parameters / bind permanently (single rank)
+        for u in self._units:
+            for g, b in u.buckets:
+                for i, p in enumerate(b.params):
+                    if self.single:
+                        off = b.shard_offset + b.offsets[i]
+                        p.data = g.shard_param[off: off + b.numels[i]].view(p.ds_shape)
+                        p.grad = g.shard_grad[off: off + b.numels[i]].view(p.ds_shape)
+                    else:
+                        p.data = _empty_like(g.dtype, g.shard_param.device)
+            u.status = ZeroParamStatus.AVAILABLE if self.single else ZeroParamStatus.NOT_AVAILABLE
+        if not self.single:
+            for u in self._units:
+                if u.persistent:
+                    self._fetch(u)
+                    self._wait(u)
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+
+    def _grad_dtype(self, g):
+        if self.single:
+            return g.dtype  # accumulate in place (p.grad views need the param dtype)
+        if self.fp32_reduce or self.gradient_accumulation_steps > 1 or g.dtype == torch.float32:
+            return torch.float32
+        return g.dtype
+
+    # ------------------------------------------------------------------ gather / release
+    def _fetch(self, u: ZeroUnit):
+        if u.status != ZeroParamStatus.NOT_AVAILABLE:
+            return
+        u.works, u.fulls = [], []
+        for g, b in u.buckets:
+            full = torch.empty(b.numel, dtype=g.dtype, device=g.shard_param.device)
+            chunk = g.shard_param[b.shard_offset: b.shard_offset + b.chunk]
+            if _dist_ready() and self.dp_world > 1:
+                u.works.append(dist.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True))
+            else:
+                full.copy_(chunk)
+            u.fulls.append(full)
+            for i, p in enumerate(b.params):
+                p.data = full[b.offsets[i]: b.offsets[i] + b.numels[i]].view(p.ds_shape)
+                p.ds_status = ZeroParamStatus.INFLIGHT
+        u.status = ZeroParamStatus.INFLIGHT
+
+    def _wait(self, u: ZeroUnit):
+        if u.status == ZeroParamStatus.INFLIGHT:
+            for w in u.works:
+                w.wait()
+            u.works = []
+            u.status = ZeroParamStatus.AVAILABLE
+            for p in u.params:
+                p.ds_status = ZeroParamStatus.AVAILABLE
+
+    def _release(self, u: ZeroUnit, force=False):
+        if self.single or u.status == ZeroParamStatus.NOT_AVAILABLE:
+            return
+        if u.persistent and not force:
+            return
+        if u.status == ZeroParamStatus.INFLIGHT:
+            self._wait(u)
+        for g, b in u.buckets:
+            e = _empty_like(g.dtype, g.shard_param.device)
+            for p in b.params:
+                p.data = e
+                p.ds_status = ZeroParamStatus.NOT_AVAILABLE
+        u.fulls = []
+        u.status = ZeroParamStatus.NOT_AVAILABLE
+
+    def gather_units(self, units):
+        for u in units:
+            self._fetch(u)
+        for u in units:
+            self._wait(u)
+
+    def release_units(self, units, force=False):
+        for u in units:
+            self._release(u, force=force)
+
+    def unit_of(self, p) -> Optional[ZeroUnit]:
+        return self._unit_of_param.get(id(p))
+
+    # ------------------------------------------------------------------ hooks
+    def _register_hooks(self):
+        self._handles = []
+        if self.single:
+            return  # parameters are permanently materialised; grads land in place
+        root = self.module
+        self._handles.append(root.register_forward_pre_hook(self._root_pre_forward))
+        for u in self._units:
+            m = u.module
+            self._handles.append(m.register_forward_pre_hook(functools.partial(self._pre_forward, u)))
+            self._handles.append(m.register_forward_hook(functools.partial(self._post_forward, u)))
+            for p in u.params:
+                if p.requires_grad:
+                    self._handles.append(p.register_post_accumulate_grad_hook(self._grad_ready))
+
+    def _root_pre_forward(self, module, inputs):
+        if not _in_backward():
+            self._fwd_pos = 0
+
+    def _prefetch(self, trace, pos):
+        if not self._trace_frozen or pos < 0:
+            return
+        budget = self.prefetch_bucket_size
+        k = pos + 1
+        while k < len(trace) and budget > 0:
+            u = self._units[trace[k]]
+            if u.status == ZeroParamStatus.NOT_AVAILABLE:
+                self._fetch(u)
+                budget -= u.numel
+            k += 1
+
+    def _pre_forward(self, u: ZeroUnit, module, inputs):
+        u.active += 1
+        if not _in_backward():
+            if not self._trace_frozen:
+                self._fwd_trace.append(u.uid)
+            elif self._fwd_pos < len(self._fwd_trace) and self._fwd_trace[self._fwd_pos] == u.uid:
+                self._prefetch(self._fwd_trace, self._fwd_pos)
+            self._fwd_pos += 1
+        self._fetch(u)
+        for x in u.external:
+            self._fetch(x)
+        self._wait(u)
+        for x in u.external:
+            self._wait(x)
+
+    def _post_forward(self, u: ZeroUnit, module, inputs, output):
+        u.active -= 1
+        if torch.is_grad_enabled():
+            self._register_bw_hooks(u, output)
+        if u.active == 0 and not _in_backward():
+            self._release(u)
+            for x in u.external:
+                if x.active == 0:
+                    self._release(x)
+        return None
+
+    def _register_bw_hooks(self, u, output):
+        def visit(o):
+            if torch.is_tensor(o):
+                if o.requires_grad and o.grad_fn is not None:
+                    o.register_hook(functools.partial(self._pre_backward_hook, u))
+            elif isinstance(o, (list, tuple)):
+                for x in o:
+                    visit(x)
+            elif isinstance(o, dict):
+                for x in o.values():
+                    visit(x)
+        visit(output)
+
+    def _pre_backward_hook(self, u, grad):
+        self._pre_backward(u)
+        return None
+
+    def _pre_backward(self, u: ZeroUnit):
+        if u.in_backward or u.reduced:
+            return
+        if not self._trace_frozen:
+            self._bwd_trace.append(u.uid)
+        elif self._bwd_pos < len(self._bwd_trace) and self._bwd_trace[self._bwd_pos] == u.uid:
+            self._prefetch(self._bwd_trace, self._bwd_pos)
+        self._bwd_pos += 1
+        self._fetch(u)
+        self._wait(u)
+        u.in_backward = True
+        u.grad_fulls = []
+        u.bw_expected = sum(1 for p in u.params if p.requires_grad)
+        u.bw_ready = 0
+        for g, b in u.buckets:
+            gf = torch.zeros(b.numel, dtype=g.dtype, device=g.shard_param.device)
+            u.grad_fulls.append(gf)
+            for i, p in enumerate(b.params):
+                if p.requires_grad:
+                    p.grad = gf[b.offsets[i]: b.offsets[i] + b.numels[i]].view(p.ds_shape)
+
+    def _grad_ready(self, p):
+        u = self._unit_of_param[id(p)]
+        if not u.in_backward:
+            # grad produced without the output hook firing (e.g. params used outside the
+            # unit's forward): materialise the unit's grad buffers now and fold it in
+            g_now = p.grad
+            p.grad = None
+            self._pre_backward(u)
+            if g_now is not None:
+                p.grad.add_(g_now)
+        u.bw_ready += 1
+        if u.bw_ready >= u.bw_expected:
+            self._reduce_unit(u)
+
+    def _reduce_unit(self, u: ZeroUnit):
+        if u.reduced:
+            return
+        u.reduced = True
+        u.in_backward = False
+        accumulate_needed = True
+        for (g, b), gf in zip(u.buckets, u.grad_fulls):
+            for p in b.params:
+                p.grad = None
+            src = gf
+            if g.dtype == torch.float16:
+                src.mul_(1.0 / self.dp_world)
+            if self.fp32_reduce and src.dtype != torch.float32:
+                src = src.float()
+            out_slice = g.shard_grad[b.shard_offset: b.shard_offset + b.chunk]
+            direct = (out_slice.dtype == src.dtype) and self.gradient_accumulation_steps == 1 and \
+                not self._grads_nonzero
+            out = out_slice if direct else torch.empty(b.chunk, dtype=src.dtype, device=src.device)
+            work = dist.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True)
+            if direct:
+                self._pending.append((work, None))
+            else:
+                self._pending.append((work, functools.partial(_accum, out_slice, out)))
+        u.grad_fulls = []
+        if u.active == 0:
+            self._release(u)
+
+    _grads_nonzero = False
+
+    def reduce_epilogue(self):
+        if self.single:
+            return
+        for u in self._units:
+            if u.in_backward and not u.reduced:
+                self._reduce_unit(u)
+        for work, fin in self._pending:
+            if work is not None:
+                work.wait()
+            if fin is not None:
+                fin()
+        self._pending = []
+        for u in self._units:
+            u.reduced = False
+            u.in_backward = False
+            if u.active == 0:
+                self._release(u)
+        self._grads_nonzero = True
+        if not self._trace_frozen and self._fwd_trace:
+            self._trace_frozen = True
+        self._bwd_pos = 0
+
+    overlapping_partition_gradients_reduce_epilogue = reduce_epilogue
+
+    # ------------------------------------------------------------------ step
+    def backward(self, loss, retain_graph=False):
+        self._bwd_pos = 0
+        self.loss_scaler.backward(loss.float(), retain_graph=retain_graph)
+
+    def _prescaled_by(self):
+        return float(self.dp_world) if (self.groups and self.groups[0].dtype == torch.float16) else 1.0
+
+    def _after_bucket_update(self, g, b):
+        pass
+
+    def _post_step(self):
+        if self.single:
+            return
+        for u in self._units:
+            if u.persistent:
+                self._release(u, force=True)
+                self._fetch(u)
+        for u in self._units:
+            if u.persistent:
+                self._wait(u)
+
+    def zero_grad(self, set_to_none=True):
+        for g in self.groups:
+            g.shard_grad.zero_()
+        self._grads_nonzero = False
+
+    def _zero_stage(self):
+        return 3
+
+    def _fp32_key(self):
+        return "fp32_flat_groups"
+
+    # ------------------------------------------------------------------ model state helpers
+    def register_external_parameter(self, module, param):
+        owner = self.unit_of(param)
+        mu = getattr(module, "_zero_unit", None)
+        if owner is None or mu is None or owner is mu:
+            return
+        if owner not in mu.external:
+            mu.external.append(owner)
+
+    def gathered_state_dict(self, module, prefix=""):
+        """Full (consolidated) low-precision state dict; every rank participates."""
+        out = {}
+        for name, p in module.named_parameters(prefix=prefix.rstrip(".")):
+            u = self.unit_of(p)
+            if u is not None:
+                was = u.status
+                self.gather_units([u])
+                out[name] = p.data.detach().clone().cpu()
+                if was == ZeroParamStatus.NOT_AVAILABLE:
+                    self._release(u)
+            else:
+                out[name] = p.detach().cpu()
+        for name, bfr in module.named_buffers(prefix=prefix.rstrip(".")):
+            out[name] = bfr.detach().cpu()
+        return out
+
+
+def _accum(dst, src):
+    dst.add_(src.to(dst.dtype))
+
+
+FP16_DeepSpeedZeroOptimizer_Stage3 = DeepSpeedZeroOptimizer_Stage3

@@ -1,0 +1,155 @@
+"""Numerics of the HIP kernels vs plain PyTorch fp32 references (run on MI355X)."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    return torch.device("cuda", 0)
+
+
+def test_extension_is_native():
+    from deeperspeed_amd.ops import native
+    mod = native.hip_ops()
+    assert mod.__file__.endswith(".so")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H", [64, 768, 2048, 6144])
+def test_layernorm_fwd_bwd(dtype, H):
+    from deeperspeed_amd.ops.native import layer_norm
+    torch.manual_seed(0)
+    x = torch.randn(37, 5, H, device=_dev(), dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=_dev())).to(dtype).requires_grad_(True)
+    b = (0.1 * torch.randn(H, device=_dev())).to(dtype).requires_grad_(True)
+    y = layer_norm(x, w, b, 1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    br = b.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, 1e-5)
+    yr.backward(dy.float())
+    tol = 2e-2 if dtype != torch.float32 else 1e-4
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 5, rtol=tol)
+    gtol = tol * 10 if dtype != torch.float32 else 1e-3
+    assert torch.allclose(w.grad.float(), wr.grad, atol=gtol * 10, rtol=gtol)
+    assert torch.allclose(b.grad.float(), br.grad, atol=gtol * 10, rtol=gtol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("approx", [False, True])
+def test_bias_gelu(dtype, approx):
+    from deeperspeed_amd.ops.native import bias_gelu
+    torch.manual_seed(1)
+    C = 4096
+    x = torch.randn(300, C, device=_dev(), dtype=dtype, requires_grad=True)
+    b = torch.randn(C, device=_dev(), dtype=dtype, requires_grad=True)
+    y = bias_gelu(x, b, approx)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    br = b.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.gelu(xr + br, approximate="tanh" if approx else "none")
+    yr.backward(dy.float())
+    tol = 2e-2 if dtype != torch.float32 else 1e-5
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol)
+    assert torch.allclose(b.grad.float(), br.grad, atol=0.5 if dtype != torch.float32 else 1e-3, rtol=2e-2)
+
+
+@pytest.mark.parametrize("pdtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("adamw", [False, True])
+def test_adam_flat_matches_torch(pdtype, adamw):
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(2)
+    n = 100003  # odd size exercises the tail path
+    master = torch.randn(n, device=_dev())
+    ref = master.clone().requires_grad_(True)
+    m = torch.zeros(n, device=_dev())
+    v = torch.zeros(n, device=_dev())
+    out = torch.empty(n, device=_dev(), dtype=pdtype)
+    cls = torch.optim.AdamW if adamw else torch.optim.Adam
+    opt = cls([ref], lr=1e-2, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 4):
+        g = torch.randn(n, device=_dev()).to(pdtype)
+        ref.grad = g.float().clone()
+        opt.step()
+        native.adam_flat_(master, g, m, v, out, 1e-2, 0.9, 0.999, 1e-8, 0.1, step, True, 1.0, adamw)
+    gtol = 1e-5
+    assert torch.allclose(master, ref.detach(), atol=gtol, rtol=gtol)
+    assert torch.allclose(out.float(), ref.detach(), atol=2e-2, rtol=1e-2)
+
+
+def test_sumsq_and_colsum():
+    from deeperspeed_amd.ops import native
+    x = torch.randn(1 << 20, device=_dev(), dtype=torch.bfloat16)
+    out = torch.zeros(1, device=_dev())
+    native.sumsq_accumulate(x, out)
+    native.sumsq_accumulate(x, out)
+    ref = 2 * x.float().pow(2).sum()
+    assert torch.allclose(out[0], ref, rtol=1e-4)
+    y = torch.randn(513, 1024, device=_dev(), dtype=torch.bfloat16)
+    assert torch.allclose(native.colsum(y).float(), y.float().sum(0), atol=0.2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("hd,rot", [(96, 24), (128, 32), (64, 64)])
+def test_rotary_split_matches_reference(hd, rot):
+    from deeperspeed_amd.ops import attention as A
+    torch.manual_seed(3)
+    B, S, NH = 2, 40, 4
+    qkv = torch.randn(B, S, NH * 3 * hd, device=_dev(), dtype=torch.bfloat16, requires_grad=True)
+    q, k, v = A.rotary_split(qkv, NH, hd, rot, qscale=0.5)
+    g = [torch.randn_like(t) for t in (q, k, v)]
+    torch.autograd.backward([q, k, v], g)
+    x = qkv.detach().cpu().float().requires_grad_(True)
+    qr, kr, vr = A.rotary_split(x, NH, hd, rot, qscale=0.5)
+    torch.autograd.backward([qr, kr, vr], [t.cpu().float() for t in g])
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        assert torch.allclose(a.float().cpu(), b, atol=3e-2, rtol=2e-2)
+    assert torch.allclose(qkv.grad.float().cpu(), x.grad, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("S", [64, 200, 2048])
+def test_masked_softmax(causal, S):
+    from deeperspeed_amd.ops.attention import masked_softmax
+    torch.manual_seed(4)
+    C = (S + 7) // 8 * 8
+    x = torch.randn(3, 5, S, C, device=_dev(), dtype=torch.bfloat16, requires_grad=True)
+    y = masked_softmax(x, None, 0.7, causal, 5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    s = xr * 0.7
+    if causal:
+        m = torch.ones(S, C, dtype=torch.bool, device=_dev()).triu(C - S + 1)
+        s = s.masked_fill(m, float("-inf"))
+    yr = torch.softmax(s, -1)
+    yr.backward(dy.float())
+    assert torch.allclose(y.float(), yr, atol=1e-2, rtol=2e-2)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=2e-2, rtol=5e-2)
+
+
+def test_attention_matches_sdpa_math():
+    from deeperspeed_amd.ops.attention import attention
+    torch.manual_seed(5)
+    B, NH, S, HD = 2, 4, 256, 96
+    q = torch.randn(B, NH, S, HD, device=_dev(), dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn_like(q, requires_grad=True)
+    v = torch.randn_like(q, requires_grad=True)
+    scale = HD ** -0.5
+    o = attention(q, k, v, causal=True, softmax_scale=scale)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    s = (qr @ kr.transpose(-1, -2)) * scale
+    s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=_dev()).triu(1), float("-inf"))
+    orf = torch.softmax(s, -1) @ vr
+    orf.backward(do.float())
+    assert torch.allclose(o.float(), orf, atol=3e-2, rtol=3e-2)
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        assert torch.allclose(a.grad.float(), b.grad, atol=6e-2, rtol=6e-2)
