@@ -271,15 +271,17 @@ class PartitionedTensor:
     def full(self, device=None):
         device = self.orig_device if device is None else device
         n = int(np.prod(self.full_size()))
-        flat = torch.zeros([n], dtype=self.local_data.dtype, device=device)
-        bufs = [flat.narrow(0, self.partition[i], self.partition[i + 1] - self.partition[i])
-                for i in range(self.num_parts)]
-        bufs[self.rank].copy_(self.local_data)
-        sizes = {b.numel() for b in bufs}
-        if len(sizes) == 1:
-            dist.all_gather_into_tensor(flat, bufs[self.rank].clone(), group=self.group)
+        sizes = [self.partition[i + 1] - self.partition[i] for i in range(self.num_parts)]
+        width = max(sizes)
+        # collectives need equal-sized pieces: gather padded parts, then compact
+        padded = torch.zeros(width * self.num_parts, dtype=self.local_data.dtype, device=device)
+        mine = torch.zeros(width, dtype=self.local_data.dtype, device=device)
+        mine[: sizes[self.rank]].copy_(self.local_data)
+        dist.all_gather_into_tensor(padded, mine, group=self.group)
+        if all(s == width for s in sizes):
+            flat = padded[:n]
         else:
-            dist.all_gather(bufs, bufs[self.rank].clone(), group=self.group)
+            flat = torch.cat([padded[i * width: i * width + sizes[i]] for i in range(self.num_parts)])
         return flat.view(self.full_size()).clone().detach()
 
     def to_meta(self):

@@ -387,9 +387,12 @@ class ShardedOptimizerBase:
         self.dynamic_loss_scale = sd0.get("dynamic_loss_scale", self.dynamic_loss_scale)
         self.overflow = sd0.get("overflow", False)
         key = sd0.get("fp32_groups_key", self._fp32_key())
-        same_layout = (len(state_dict_list) == self.dp_world and sd0.get("layout") == layout_signature(self.groups))
+        lw, lr = self._layout_world_rank()
+        if sd0.get("zero_stage", 0) == 0:
+            state_dict_list = state_dict_list[:1]  # unsharded: every rank saved the same full state
+        same_layout = (len(state_dict_list) == lw and sd0.get("layout") == layout_signature(self.groups))
         if same_layout:
-            mine = state_dict_list[self.dp_rank]
+            mine = state_dict_list[lr]
             masters = mine[key]
             moments = mine["base_optimizer_state"]
         else:
@@ -401,20 +404,25 @@ class ShardedOptimizerBase:
         if load_optimizer_states:
             self._load_moments(moments)
 
+    def _layout_world_rank(self):
+        """(world, rank) of the shard layout (unsharded stage 0 uses a world of 1)."""
+        return self.dp_world, self.dp_rank
+
     def _elastic_merge(self, sds, key):
         """Re-partition masters and moments saved under a different DP world size."""
+        _, my_rank = self._layout_world_rank()
         masters, moments_state = [], {}
         sig_list = sds[0]["layout"]
         old_base = [sd["base_optimizer_state"] for sd in sds]
         for gi, g in enumerate(self.groups):
             sig = sig_list[gi]
             full = shards_to_params([sd[key][gi] for sd in sds], sig)
-            masters.append(params_to_shard(full, g, self.dp_rank, torch.float32))
+            masters.append(params_to_shard(full, g, my_rank, torch.float32))
             st_new = {}
             for name in ("exp_avg", "exp_avg_sq"):
                 olds = [ob["state"].get(gi, {}).get(name) for ob in old_base]
                 if all(o is not None for o in olds):
-                    st_new[name] = params_to_shard(shards_to_params(olds, sig), g, self.dp_rank, torch.float32)
+                    st_new[name] = params_to_shard(shards_to_params(olds, sig), g, my_rank, torch.float32)
             step = old_base[0]["state"].get(gi, {}).get("step", 0)
             st_new["step"] = step
             moments_state[gi] = st_new

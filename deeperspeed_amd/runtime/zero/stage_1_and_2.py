@@ -320,6 +320,9 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
     def _zero_stage(self):
         return self.stage
 
+    def _layout_world_rank(self):
+        return (self.dp_world, self.dp_rank) if self.sharded else (1, 0)
+
     def _fp32_key(self):
         return "single_partition_of_fp32_groups" if self.sharded else "fp32_groups_flat"
 
