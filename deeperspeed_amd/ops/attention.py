@@ -13,6 +13,7 @@ CPU tensors use PyTorch reference math (unit tests on CPU CI).
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -130,9 +131,14 @@ def masked_softmax(scores, mask=None, scale: float = 1.0, causal: bool = False, 
 
 
 def attention(q, k, v, causal: bool = True, mask=None, softmax_scale: float = 1.0, dropout_p: float = 0.0,
-              training: bool = False):
-    """q,k,v [B,NH,S,HD] -> [B,NH,S,HD].  q is expected pre-scaled when softmax_scale == 1."""
-    if q.is_cuda and dropout_p == 0.0 and mask is None and native.has_flash_attention(q):
+              training: bool = False, use_flash=None):
+    """q,k,v [B,NH,S,HD] -> [B,NH,S,HD].  q is expected pre-scaled when softmax_scale == 1.
+    The fused kernel is used for self-attention without mask/dropout unless `use_flash` is
+    False or DSA_FLASH_ATTN=0."""
+    if use_flash is None:
+        use_flash = os.environ.get("DSA_FLASH_ATTN", "1") != "0"
+    if (use_flash and q.is_cuda and dropout_p == 0.0 and mask is None and q.shape == k.shape == v.shape
+            and native.has_flash_attention(q)):
         return native.flash_attention(q, k, v, causal, softmax_scale)
     B, NH, S, HD = q.shape
     scores = torch.matmul(q, k.transpose(-1, -2))

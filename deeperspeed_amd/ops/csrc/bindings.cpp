@@ -284,9 +284,47 @@ Tensor softmax_bwd(Tensor dy, Tensor y, double scale) {
   return dx;
 }
 
+// Fused attention. q,k,v [B, H, S, D] contiguous 16-bit -> (o [B,H,S,D], lse [B,H,S] fp32)
+std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale) {
+  check_dev(q, "q"); check_dev(k, "k"); check_dev(v, "v");
+  TORCH_CHECK(q.dim() == 4 && q.sizes() == k.sizes() && q.sizes() == v.sizes(), "flash_attn: q/k/v shape mismatch");
+  TORCH_CHECK(q.scalar_type() != at::kFloat && q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(),
+              "flash_attn: 16-bit q/k/v of one dtype");
+  TORCH_CHECK(q.is_contiguous() && k.is_contiguous() && v.is_contiguous(), "flash_attn: contiguous inputs");
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
+  TORCH_CHECK(dsa::flash_supported((int)D), "flash_attn: head dim must be 64, 96 or 128");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  Tensor o = at::empty_like(q);
+  Tensor lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  dsa::launch_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)(B * H),
+                        (int)S, (int)D, causal, (float)scale, dcode(q), cur_stream());
+  return {o, lse};
+}
+
+std::vector<Tensor> flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal,
+                                   double scale) {
+  for (auto* t : {&dout, &q, &k, &v, &o}) {
+    check_dev(*t, "flash_attn_bwd");
+    TORCH_CHECK(t->sizes() == q.sizes() && t->scalar_type() == q.scalar_type() && t->is_contiguous(),
+                "flash_attn_bwd: operands must match q");
+  }
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == q.numel() / q.size(3),
+              "flash_attn_bwd: lse");
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  Tensor dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  Tensor delta = at::empty_like(lse);
+  dsa::launch_flash_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                        delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)(B * H), (int)S,
+                        (int)D, causal, (float)scale, dcode(q), cur_stream());
+  return {dq, dk, dv};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("rotary_split_fwd", &rotary_split_fwd);
   m.def("rotary_split_bwd", &rotary_split_bwd);
   m.def("softmax_fwd", &softmax_fwd);

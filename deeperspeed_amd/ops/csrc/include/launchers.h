@@ -61,4 +61,12 @@ void launch_softmax_fwd(const void* x, void* y, const void* mask, int64_t R, int
 void launch_softmax_bwd(const void* dy, const void* y, void* dx, int64_t R, int C, float scale, int dt,
                         hipStream_t s);
 
+// flash_attn.hip: q,k,v,o [BH, S, D] (D in 64/96/128), lse/delta [BH, S] fp32
+bool flash_supported(int D);
+void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
+                      bool causal, float scale, int dt, hipStream_t s);
+void launch_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
+                      float* delta, void* dq, void* dk, void* dv, int BH, int S, int D, bool causal, float scale,
+                      int dt, hipStream_t s);
+
 }  // namespace dsa

@@ -153,3 +153,50 @@ def test_attention_matches_sdpa_math():
     assert torch.allclose(o.float(), orf, atol=3e-2, rtol=3e-2)
     for a, b in ((q, qr), (k, kr), (v, vr)):
         assert torch.allclose(a.grad.float(), b.grad, atol=6e-2, rtol=6e-2)
+
+
+def _attn_ref(q, k, v, causal, scale):
+    s = (q.float() @ k.float().transpose(-1, -2)) * scale
+    if causal:
+        S = q.shape[-2]
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+    return torch.softmax(s, -1) @ v.float()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("D", [64, 96, 128])
+@pytest.mark.parametrize("S,causal", [(128, True), (200, True), (96, False), (333, False)])
+def test_flash_attention_fwd_bwd(dtype, D, S, causal):
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(0)
+    B, H = 2, 3
+    scale = D ** -0.5
+    q = torch.randn(B, H, S, D, device=_dev(), dtype=dtype, requires_grad=True)
+    k = torch.randn(B, H, S, D, device=_dev(), dtype=dtype, requires_grad=True)
+    v = torch.randn(B, H, S, D, device=_dev(), dtype=dtype, requires_grad=True)
+    assert native.has_flash_attention(q)
+    o = native.flash_attention(q, k, v, causal, scale)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, causal, scale)
+    ref.backward(do.float())
+    tol = 2e-2 if dtype == torch.bfloat16 else 5e-3
+    torch.testing.assert_close(o.float(), ref, atol=tol, rtol=tol)
+    for got, want in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        err = (got.float() - want).abs().max().item()
+        assert err <= 4 * tol * max(1.0, want.abs().max().item()), err
+
+
+def test_flash_attention_lse_and_large_logits():
+    """Large score magnitudes exercise the online-softmax rescale path."""
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(1)
+    q = (8 * torch.randn(1, 2, 256, 128, device=_dev())).to(torch.bfloat16)
+    k = torch.randn(1, 2, 256, 128, device=_dev()).to(torch.bfloat16)
+    v = torch.randn(1, 2, 256, 128, device=_dev()).to(torch.bfloat16)
+    o, lse = native.hip_ops().flash_attn_fwd(q.contiguous(), k.contiguous(), v.contiguous(), True, 0.125)
+    s = (q.float() @ k.float().transpose(-1, -2)) * 0.125
+    s = s.masked_fill(torch.ones(256, 256, dtype=torch.bool, device=_dev()).triu(1), float("-inf"))
+    torch.testing.assert_close(lse, torch.logsumexp(s, -1), atol=2e-2, rtol=1e-3)
+    torch.testing.assert_close(o.float(), torch.softmax(s, -1) @ v.float(), atol=3e-2, rtol=3e-2)
