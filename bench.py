@@ -41,10 +41,34 @@ def parse():
     p.add_argument("--grad-accum", type=int, default=None)
     p.add_argument("--seq", type=int, default=2048)
     p.add_argument("--zero", type=int, default=3)
-    p.add_argument("--offload", type=str, default="auto", choices=["auto", "none", "master", "all"])
+    p.add_argument("--offload", type=str, default="auto", choices=["auto", "none", "compact", "master", "all"])
+    p.add_argument("--ckpt", type=str, default="auto", choices=["auto", "on", "off"],
+                   help="activation checkpointing; auto = off when activations fit in HBM next to the shards")
+    p.add_argument("--layers", type=int, default=None, help="override depth (memory experiments only)")
     p.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (0 = off)")
     p.add_argument("--local_rank", type=int, default=None)
     return p.parse_args()
+
+
+def plan_memory(cfg, mb, seq, world, offload, ckpt):
+    """Bytes of HBM one rank needs: ZeRO-3 model states + activations + transient buffers.
+
+    States per parameter: bf16 weight shard 2 B + bf16 grad shard 2 B + fp32 moments 8 B
+    + fp32 master 4 B (2 B int16 residual with compact_master, 0 B when offloaded).
+    Calibrated on MI355X: 20B, N=1, compact, recompute on -> planned 279 GiB, measured peak
+    274.7 GiB.  Activations per layer with the fused attention
+    kernel (no S x S scores), measured on MI355X: ~36 * s * b * h bytes in bf16 without
+    recompute, one s*b*h layer input with it.  Transients: two gathered ZeRO-3 units, the
+    logits (fp32 for the loss) and allocator slack."""
+    p = cfg.num_params()
+    per_param = {"none": 16, "compact": 14, "master": 12, "all": 4}[offload]
+    states = p * per_param / world
+    sbh = seq * mb * cfg.hidden_size
+    act_layer = 2 * sbh if ckpt else 36 * sbh
+    acts = cfg.num_layers * act_layer + (36 * sbh if ckpt else 0)
+    logits = seq * mb * cfg.vocab_size * 4  # bf16 logits + bf16 grad (fused HIP cross-entropy)
+    transient = 2 * 2 * 2e8 * 2 + logits + 2 * 2**30
+    return states + acts + transient
 
 
 def log(msg):
@@ -77,19 +101,29 @@ def main():
     dev = torch.device("cuda", local)
     native.hip_ops()  # fail loudly if the HIP extension is missing
 
-    cfg = get_config(args.model, max_seq_len=args.seq, checkpoint_activations=True)
+    over = {"num_layers": args.layers} if args.layers else {}
+    cfg = get_config(args.model, max_seq_len=args.seq, checkpoint_activations=True, **over)
     big = cfg.num_params() > 5e9
     mb = args.micro_batch or (4 if big else 8)
     ga = args.grad_accum or (4 if big else 2)
+    hbm = torch.cuda.get_device_properties(local).total_memory
+    budget = 0.97 * hbm
+    # model-state layout: everything in HBM (16 B/param) > compact fp32 master (14 B/param)
+    # > fp32 master offloaded to host (12 B/param in HBM); then recompute only if needed
     offload = args.offload
     if offload == "auto":
-        # 16 B/param of model state: keep everything in HBM when it fits with activations
-        per_gpu = cfg.num_params() * 16 / world
-        offload = "master" if per_gpu > 200e9 else "none"
+        offload = next((o for o in ("none", "compact", "master")
+                        if plan_memory(cfg, mb, args.seq, world, o, True) < budget), "master")
+    ckpt = args.ckpt
+    if ckpt == "auto":
+        ckpt = "off" if plan_memory(cfg, mb, args.seq, world, offload, False) < budget else "on"
+    cfg.checkpoint_activations = ckpt == "on"
     zcfg = {"stage": args.zero, "overlap_comm": True, "reduce_bucket_size": int(2e8),
             "stage3_prefetch_bucket_size": int(5e8), "stage3_param_persistence_threshold": int(1e6),
             "stage3_unit_max_numel": int(2e8)}
-    if offload != "none":
+    if offload == "compact":
+        zcfg["compact_master"] = True
+    elif offload != "none":
         zcfg["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": offload}
     conf = {
         "train_micro_batch_size_per_gpu": mb,
@@ -104,7 +138,8 @@ def main():
         "wall_clock_breakdown": False,
     }
     log(f"model={args.model} params={cfg.num_params() / 1e9:.2f}B world={world} mb={mb} ga={ga} seq={args.seq} "
-        f"zero={args.zero} offload={offload}")
+        f"zero={args.zero} offload={offload} ckpt={ckpt} hbm={hbm / 2**30:.0f} GiB "
+        f"planned={plan_memory(cfg, mb, args.seq, world, offload, ckpt == 'on') / 2**30:.0f} GiB")
     t0 = time.time()
     torch.manual_seed(1234)
     model = GPTNeoX(cfg, device=dev, dtype=torch.bfloat16)
@@ -125,12 +160,28 @@ def main():
             engine.step()
         return loss
 
+    def timed_step():
+        """Warmup step with synchronised per-phase timing (outside the timed region)."""
+        ph = {"fwd": 0.0, "bwd": 0.0, "step": 0.0}
+        loss = None
+        for i in range(ga):
+            for name, fn in (("fwd", lambda: engine(batches[i], labels=batches[i])),
+                             ("bwd", lambda: engine.backward(loss)), ("step", engine.step)):
+                torch.cuda.synchronize()
+                t = time.time()
+                r = fn()
+                torch.cuda.synchronize()
+                ph[name] += time.time() - t
+                if name == "fwd":
+                    loss = r
+        return loss, ph
+
     for i in range(args.warmup):
         ts = time.time()
-        loss = train_step()
-        torch.cuda.synchronize()
-        log(f"warmup {i} loss={float(loss):.4f} {time.time() - ts:.2f}s "
-            f"peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+        loss, ph = timed_step()
+        log(f"warmup {i} loss={float(loss.detach()):.4f} {time.time() - ts:.2f}s "
+            + " ".join(f"{k}={v:.2f}s" for k, v in ph.items())
+            + f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
 
     dist.barrier()
     torch.cuda.synchronize()
@@ -158,7 +209,7 @@ def main():
     global_batch = mb * ga * world
     tokens = global_batch * args.seq * args.steps
     tps = tokens / elapsed
-    flops_tok = cfg.flops_per_token(args.seq, recompute=True)
+    flops_tok = cfg.flops_per_token(args.seq, recompute=False)
     ms_step = elapsed / args.steps * 1000.0
     out = {
         "metric": "tokens/sec (node) GPT-NeoX-20B ZeRO-3" if args.model == "gpt-neox-20b" else f"tokens/sec {args.model}",
@@ -175,7 +226,7 @@ def main():
         "data": "synthetic random tokens, random-init weights",
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq,
                    "parallelism": f"zero{args.zero}-dp{world}", "micro_batch": mb, "grad_accum": ga,
-                   "offload": offload, "activation_checkpointing": True,
+                   "offload": offload, "activation_checkpointing": ckpt == "on",
                    "params_per_gpu": round(cfg.num_params() / world / 1e9, 3),
                    "model_tflops_per_gpu": round(tps * flops_tok / world / 1e12, 1),
                    "final_loss": round(float(loss), 4),

@@ -184,7 +184,8 @@ class GPTNeoX(nn.Module):
 
 
 def lm_loss(logits, labels):
-    return F.cross_entropy(logits.float().view(-1, logits.shape[-1]), labels.reshape(-1))
+    """Mean next-token loss (labels already aligned with logits); fused HIP kernel on GPU."""
+    return native.cross_entropy(logits, labels)
 
 
 # -------------------------------------------------------------------------- pipeline form

@@ -46,6 +46,12 @@ class FusedAdam(torch.optim.Optimizer):
         st = self.state_for(state_key)
         hi = w.numel() if hi is None else hi
         b1, b2 = group["betas"]
+        if w.dtype == torch.int16:  # compact master: w holds the residual, `out` the bf16 high half
+            native.adam_compact_(out, w[lo:hi], g[lo:hi], st["exp_avg"][lo:hi], st["exp_avg_sq"][lo:hi],
+                                 group["lr"], b1, b2, group["eps"], group["weight_decay"],
+                                 step if step is not None else st["step"], group["bias_correction"], grad_scale,
+                                 bool(self.adam_w_mode))
+            return
         native.adam_flat_(w[lo:hi], g[lo:hi], st["exp_avg"][lo:hi], st["exp_avg_sq"][lo:hi], out, group["lr"], b1, b2,
                           group["eps"], group["weight_decay"], step if step is not None else st["step"],
                           group["bias_correction"], grad_scale, bool(self.adam_w_mode))

@@ -64,6 +64,24 @@ void adam_flat(Tensor w, Tensor g, Tensor m, Tensor v, OptT out, double lr, doub
                         optr, ot, n, a, cur_stream());
 }
 
+// Compact master: hi = bf16 model weights (updated in place), res = int16 residual.
+void adam_compact(Tensor hi, Tensor res, Tensor g, Tensor m, Tensor v, double lr, double beta1, double beta2,
+                  double eps, double wd, double bc1, double bc2, double grad_scale, bool adamw) {
+  check_dev(hi, "hi"); check_dev(res, "res"); check_dev(g, "g"); check_dev(m, "exp_avg"); check_dev(v, "exp_avg_sq");
+  const int64_t n = hi.numel();
+  TORCH_CHECK(hi.scalar_type() == at::kBFloat16 && res.scalar_type() == at::kShort, "adam_compact: bf16 hi, int16 res");
+  TORCH_CHECK(res.numel() == n && g.numel() == n && m.numel() == n && v.numel() == n, "adam_compact: size mismatch");
+  TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat, "adam states must be fp32");
+  for (const Tensor* t : {&hi, &res, &g, &m, &v})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & (t->element_size() * 4 - 1)) == 0,
+                "adam_compact: operands must be aligned to 4 elements");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(hi.device());
+  dsa::AdamArgs a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2,
+                  (float)grad_scale, adamw ? 1 : 0};
+  dsa::launch_adam_compact(hi.data_ptr(), res.data_ptr(), g.data_ptr(), dcode(g), m.data_ptr<float>(),
+                           v.data_ptr<float>(), n, a, cur_stream());
+}
+
 // meta: device int64 table built by ops/adam.py (see optim.hip adam_multi_kernel)
 void adam_multi(Tensor meta, int64_t T, int64_t total_chunks, int64_t chunk, int64_t wt, int64_t gt, int64_t ot,
                 double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2,
@@ -284,6 +302,35 @@ Tensor softmax_bwd(Tensor dy, Tensor y, double scale) {
   return dx;
 }
 
+// Fused softmax cross-entropy. logits [R, V] 16-bit, labels [R] int64 (<0 = ignored)
+// -> (per-row loss fp32 [R], lse fp32 [R])
+std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels) {
+  check_dev(logits, "logits"); check_dev(labels, "labels");
+  TORCH_CHECK(logits.dim() == 2 && logits.scalar_type() != at::kFloat, "xent: 16-bit [rows, vocab] logits");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0), "xent: int64 labels per row");
+  TORCH_CHECK(logits.size(1) % 8 == 0, "xent: vocab must be a multiple of 8");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  const int64_t R = logits.size(0);
+  Tensor loss = at::empty({R}, logits.options().dtype(at::kFloat));
+  Tensor lse = at::empty({R}, logits.options().dtype(at::kFloat));
+  dsa::launch_xent_fwd(logits.data_ptr(), labels.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(),
+                       R, (int)logits.size(1), dcode(logits), cur_stream());
+  return {loss, lse};
+}
+
+// dloss: fp32 [R] per-row upstream grads, or a single element broadcast to every row
+Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dloss) {
+  check_dev(logits, "logits"); check_dev(dloss, "dloss");
+  TORCH_CHECK(dloss.scalar_type() == at::kFloat && (dloss.numel() == 1 || dloss.numel() == logits.size(0)),
+              "xent_bwd: dloss");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  Tensor dx = at::empty_like(logits);
+  dsa::launch_xent_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(), dloss.data_ptr<float>(),
+                       dloss.numel() == 1 ? 0 : 1, dx.data_ptr(), logits.size(0), (int)logits.size(1), dcode(logits),
+                       cur_stream());
+  return dx;
+}
+
 // Fused attention. q,k,v [B, H, S, D] contiguous 16-bit -> (o [B,H,S,D], lse [B,H,S] fp32)
 std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale) {
   check_dev(q, "q"); check_dev(k, "k"); check_dev(v, "v");
@@ -323,6 +370,8 @@ std::vector<Tensor> flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Te
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("rotary_split_fwd", &rotary_split_fwd);
@@ -331,6 +380,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_bwd", &softmax_bwd);
   m.doc() = "deeperspeed_amd CDNA4 (gfx950) HIP kernels";
   m.def("adam_flat", &adam_flat);
+  m.def("adam_compact", &adam_compact);
   m.def("adam_multi", &adam_multi);
   m.def("sumsq_accum", &sumsq_accum);
   m.def("scale_copy", &scale_copy);

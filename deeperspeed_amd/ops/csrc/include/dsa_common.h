@@ -200,3 +200,19 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }  // namespace dsa
 
 #define DSA_CHECK_LAUNCH() (void)hipGetLastError()
+
+// dtype-code -> type dispatch for host launchers (codes: DType above)
+#define DSA_DISPATCH_T(code, T, ...)                      \
+  switch (code) {                                          \
+    case dsa::kF32: { using T = float; __VA_ARGS__; } break;    \
+    case dsa::kBF16: { using T = dsa::bf16_t; __VA_ARGS__; } break;  \
+    case dsa::kF16: { using T = dsa::f16_t; __VA_ARGS__; } break;    \
+    default: break;                                        \
+  }
+
+#define DSA_DISPATCH_16(code, T, ...)                      \
+  switch (code) {                                          \
+    case dsa::kBF16: { using T = dsa::bf16_t; __VA_ARGS__; } break;  \
+    case dsa::kF16: { using T = dsa::f16_t; __VA_ARGS__; } break;    \
+    default: break;                                        \
+  }

@@ -25,6 +25,8 @@ struct LambArgs {
 // optim.hip
 void launch_adam_flat(void* w, int wt, const void* g, int gt, float* m, float* v, void* out, int ot, int64_t n,
                       AdamArgs a, hipStream_t s);
+void launch_adam_compact(void* hi, void* res, const void* g, int gt, float* m, float* v, int64_t n, AdamArgs a,
+                         hipStream_t s);
 void launch_adam_multi(const int64_t* meta, int T, int64_t total_chunks, int64_t chunk, int wt, int gt, int ot,
                        AdamArgs a, hipStream_t s);
 void launch_sumsq_accum(const void* x, int xt, int64_t n, float* workspace, float* out, hipStream_t s);
@@ -60,6 +62,12 @@ void launch_softmax_fwd(const void* x, void* y, const void* mask, int64_t R, int
                         int causal, int dt, hipStream_t s);
 void launch_softmax_bwd(const void* dy, const void* y, void* dx, int64_t R, int C, float scale, int dt,
                         hipStream_t s);
+
+// loss.hip: fused softmax cross-entropy over [rows, V] 16-bit logits
+void launch_xent_fwd(const void* x, const int64_t* labels, float* loss, float* lse, int64_t rows, int V, int dt,
+                     hipStream_t s);
+void launch_xent_bwd(const void* x, const int64_t* labels, const float* lse, const float* dloss, int64_t dloss_stride,
+                     void* dx, int64_t rows, int V, int dt, hipStream_t s);
 
 // flash_attn.hip: q,k,v,o [BH, S, D] (D in 64/96/128), lse/delta [BH, S] fp32
 bool flash_supported(int D);

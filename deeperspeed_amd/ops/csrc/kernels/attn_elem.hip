@@ -218,12 +218,6 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const T* __restrict__ 
 }
 
 // --------------------------------------------------------------------------------------
-#define DSA_DISPATCH_16(code, T, ...)                      \
-  switch (code) {                                          \
-    case kBF16: { using T = bf16_t; __VA_ARGS__; } break;  \
-    case kF16: { using T = f16_t; __VA_ARGS__; } break;    \
-    default: break;                                        \
-  }
 
 #define DSA_DISPATCH_SNV(nv, NV, ...)                                \
   switch (nv) {                                                      \

@@ -259,13 +259,6 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict_
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
-#define DSA_DISPATCH_T2(code, T, ...)                     \
-  switch (code) {                                          \
-    case kF32: { using T = float; __VA_ARGS__; } break;    \
-    case kBF16: { using T = bf16_t; __VA_ARGS__; } break;  \
-    case kF16: { using T = f16_t; __VA_ARGS__; } break;    \
-    default: break;                                        \
-  }
 
 #define DSA_DISPATCH_NV(nv, NV, ...)                                \
   switch (nv) {                                                      \
@@ -284,7 +277,7 @@ void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_o
                    hipStream_t s) {
   if (rows <= 0) return;
   const int nv = (H / (dt == kF32 ? 4 : 8) + LN_THREADS - 1) / LN_THREADS;
-  DSA_DISPATCH_T2(dt, T, DSA_DISPATCH_NV(nv, NV,
+  DSA_DISPATCH_T(dt, T, DSA_DISPATCH_NV(nv, NV,
     hipLaunchKernelGGL((ln_fwd_kernel<T, NV>), dim3((unsigned)rows), dim3(LN_THREADS), 0, s,
                        (const T*)x, (const T*)res, (const T*)bias, (T*)sum_out, (const T*)gamma,
                        (const T*)beta, (T*)y, mean, rstd, H, eps)));
@@ -299,7 +292,7 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
   if (rows <= 0) return;
   const int grid = ln_bwd_grid(rows);
   const int nv = (H / (dt == kF32 ? 4 : 8) + LN_THREADS - 1) / LN_THREADS;
-  DSA_DISPATCH_T2(dt, T,
+  DSA_DISPATCH_T(dt, T,
     DSA_DISPATCH_NV(nv, NV, hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(grid), dim3(LN_THREADS), 0, s,
                        (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
                        partial, rows, H));
@@ -317,7 +310,7 @@ void launch_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, i
   int64_t g = (n / vn + 255) / 256;
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
-  DSA_DISPATCH_T2(dt, T,
+  DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((bias_gelu_fwd_kernel<T>), dim3((unsigned)g), dim3(256), 0, s,
                        (const T*)x, (const T*)b, (T*)y, n, C, approx));
 }
@@ -339,7 +332,7 @@ void launch_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx
   const int vn = dt == kF32 ? 4 : 8;
   const int cblocks = (C / vn + 255) / 256;
   const int rc = bias_gelu_row_chunks(rows, C, dt);
-  DSA_DISPATCH_T2(dt, T,
+  DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((bias_gelu_bwd_kernel<T>), dim3(cblocks, rc), dim3(256), 0, s,
                        (const T*)dy, (const T*)x, (const T*)b, (T*)dx, db ? partial : nullptr, rows, C, approx);
     if (db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 63) / 64), dim3(256), 0, s, partial, rc, C,
@@ -376,7 +369,7 @@ void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C
   const int vn = dt == kF32 ? 4 : 8;
   const int cblocks = (C / vn + 255) / 256;
   const int rc = bias_gelu_row_chunks(rows, C, dt);
-  DSA_DISPATCH_T2(dt, T,
+  DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((colsum_partial_kernel<T>), dim3(cblocks, rc), dim3(256), 0, s, (const T*)x, partial,
                        rows, C);
     hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 63) / 64), dim3(256), 0, s, partial, rc, C, (T*)out,

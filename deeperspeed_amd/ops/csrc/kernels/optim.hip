@@ -62,6 +62,59 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(TW* __restrict__ w, cons
   }
 }
 
+// Compact fp32 master: the master is held EXACTLY as (bf16 high half, int16 residual):
+//   bits(master) = (hi << 16) + residual,  hi = (bits + 0x8000) >> 16  (round half away on the
+//   magnitude, i.e. RNE except on exact ties), residual in [-32768, 32767].
+// The bf16 high half IS the model weight, so the fp32 master costs 2 B/param instead of 4.
+__device__ __forceinline__ float compact_decode(uint16_t hi, int16_t r) {
+  return __uint_as_float((uint32_t)((int32_t)((uint32_t)hi << 16) + (int32_t)r));
+}
+__device__ __forceinline__ void compact_encode(float f, uint16_t& hi, int16_t& r) {
+  const uint32_t b = __float_as_uint(f);
+  const uint32_t h = (b + 0x8000u) >> 16;
+  hi = (uint16_t)h;
+  r = (int16_t)(int32_t)(b - (h << 16));
+}
+
+template <typename TG>
+__global__ void __launch_bounds__(256) adam_compact_kernel(uint16_t* __restrict__ hi, int16_t* __restrict__ res,
+                                                           const TG* __restrict__ g, float* __restrict__ m,
+                                                           float* __restrict__ v, int64_t n, AdamArgs a) {
+  const int64_t nvec = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    const int64_t e = i * 4;
+    const ushort4 h4 = *reinterpret_cast<const ushort4*>(hi + e);
+    const short4 r4 = *reinterpret_cast<const short4*>(res + e);
+    float wf[4] = {compact_decode(h4.x, r4.x), compact_decode(h4.y, r4.y), compact_decode(h4.z, r4.z),
+                   compact_decode(h4.w, r4.w)};
+    float gf[4], mf[4], vf[4];
+    load_n<TG, 4>(g + e, gf);
+    load_n<float, 4>(m + e, mf);
+    load_n<float, 4>(v + e, vf);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) adam_elem(wf[k], gf[k], mf[k], vf[k], a);
+    ushort4 ho;
+    short4 ro;
+    compact_encode(wf[0], ho.x, ro.x);
+    compact_encode(wf[1], ho.y, ro.y);
+    compact_encode(wf[2], ho.z, ro.z);
+    compact_encode(wf[3], ho.w, ro.w);
+    *reinterpret_cast<ushort4*>(hi + e) = ho;
+    *reinterpret_cast<short4*>(res + e) = ro;
+    store_n<float, 4>(m + e, mf);
+    store_n<float, 4>(v + e, vf);
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t e = nvec * 4 + threadIdx.x; e < n; e += blockDim.x) {
+      float wf = compact_decode(hi[e], res[e]), gf = Conv<TG>::load(g, e), mf = m[e], vf = v[e];
+      adam_elem(wf, gf, mf, vf, a);
+      compact_encode(wf, hi[e], res[e]);
+      m[e] = mf; v[e] = vf;
+    }
+  }
+}
+
 // Multi-tensor form: one launch covers a list of (possibly unaligned) tensors.
 // `meta` is a device int64 table:
 //   [0,T) w ptrs, [T,2T) g ptrs, [2T,3T) m ptrs, [3T,4T) v ptrs, [4T,5T) out ptrs,
@@ -224,13 +277,6 @@ static inline int grid_for(int64_t work, int block = 256, int cap = 2048) {
   return (int)g;
 }
 
-#define DSA_DISPATCH_T(code, T, ...)                      \
-  switch (code) {                                          \
-    case kF32: { using T = float; __VA_ARGS__; } break;    \
-    case kBF16: { using T = bf16_t; __VA_ARGS__; } break;  \
-    case kF16: { using T = f16_t; __VA_ARGS__; } break;    \
-    default: break;                                        \
-  }
 
 void launch_adam_flat(void* w, int wt, const void* g, int gt, float* m, float* v, void* out, int ot,
                       int64_t n, AdamArgs a, hipStream_t s) {
@@ -238,6 +284,14 @@ void launch_adam_flat(void* w, int wt, const void* g, int gt, float* m, float* v
   DSA_DISPATCH_T(wt, TW, DSA_DISPATCH_T(gt, TG, DSA_DISPATCH_T(ot, TO,
     hipLaunchKernelGGL((adam_flat_kernel<TW, TG, TO>), dim3(grid), dim3(256), 0, s,
                        (TW*)w, (const TG*)g, m, v, (TO*)out, n, a))));
+}
+
+void launch_adam_compact(void* hi, void* res, const void* g, int gt, float* m, float* v, int64_t n, AdamArgs a,
+                         hipStream_t s) {
+  const int grid = grid_for(n / 4, 256, 4096);
+  DSA_DISPATCH_T(gt, TG,
+    hipLaunchKernelGGL((adam_compact_kernel<TG>), dim3(grid), dim3(256), 0, s, (uint16_t*)hi, (int16_t*)res,
+                       (const TG*)g, m, v, n, a));
 }
 
 void launch_adam_multi(const int64_t* meta, int T, int64_t total_chunks, int64_t chunk, int wt, int gt,

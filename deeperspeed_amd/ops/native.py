@@ -190,6 +190,22 @@ def adam_flat_(w, g, m, v, out, lr, beta1, beta2, eps, weight_decay, step, bias_
         out.copy_(wf)
 
 
+def adam_compact_(hi, res, g, m, v, lr, beta1, beta2, eps, weight_decay, step, bias_correction, grad_scale, adamw):
+    """Adam/AdamW on a compact master: `hi` (bf16 model weights) + `res` (int16 residual) hold
+    the exact fp32 master (runtime/zero/compact_master.py); both are updated in place."""
+    bc1 = 1.0 - beta1 ** step if bias_correction else 1.0
+    bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
+    if hi.is_cuda:
+        hip_ops().adam_compact(hi, res, g, m, v, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale, adamw)
+        return
+    from ..runtime.zero import compact_master as cm
+    w = cm.decode(hi, res)
+    adam_flat_(w, g, m, v, None, lr, beta1, beta2, eps, weight_decay, step, bias_correction, grad_scale, adamw)
+    h, r = cm.encode(w)
+    hi.copy_(h)
+    res.copy_(r)
+
+
 def scale_copy_(x: torch.Tensor, y: torch.Tensor, scale: float = 1.0, scale_tensor: Optional[torch.Tensor] = None):
     if x.is_cuda and x.data_ptr() % (x.element_size() * 4) == 0 and y.data_ptr() % (y.element_size() * 4) == 0:
         hip_ops().scale_copy(x, y, scale_tensor, scale)
@@ -239,3 +255,31 @@ def _cpu_flatten():
         pass
     from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
     return _flatten_dense_tensors, _unflatten_dense_tensors
+
+
+# --------------------------------------------------------------------------- fused LM loss
+class _CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        x = logits.reshape(-1, logits.shape[-1]).contiguous()
+        lab = labels.reshape(-1).contiguous()
+        rows, lse = hip_ops().xent_fwd(x, lab)
+        nvalid = (lab >= 0).sum().clamp_min(1).float()
+        ctx.save_for_backward(x, lab, lse, nvalid)
+        ctx.shape = logits.shape
+        return rows.sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, g):
+        x, lab, lse, nvalid = ctx.saved_tensors
+        dx = hip_ops().xent_bwd(x, lab, lse, (g.float() / nvalid).reshape(1).contiguous())
+        return dx.view(ctx.shape), None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Mean token cross-entropy (labels < 0 ignored) on 16-bit logits without fp32 copies
+    of the [tokens, vocab] tensor; fp32 PyTorch path on CPU / fp32 logits."""
+    if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float16) and logits.shape[-1] % 8 == 0:
+        return _CrossEntropyFn.apply(logits, labels)
+    return torch.nn.functional.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), labels.reshape(-1),
+                                             ignore_index=-100)

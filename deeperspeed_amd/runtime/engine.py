@@ -593,7 +593,7 @@ class DeepSpeedEngine(Module):
                       dynamic_loss_args=self._dynamic_args(), fp32_reduce=self.allreduce_always_fp32(),
                       gradient_predivide_factor=self.gradient_predivide_factor(),
                       gradient_accumulation_steps=self.gradient_accumulation_steps(),
-                      offload_optimizer=zc.offload_optimizer,
+                      offload_optimizer=zc.offload_optimizer, compact_master=bool(zc.compact_master),
                       timers=self.timers if self.wall_clock_breakdown() else None, verbose=self.global_rank == 0)
         if stage in (ZERO_OPTIMIZATION_OPTIMIZER_STATES, ZERO_OPTIMIZATION_GRADIENTS):
             from .zero.stage_1_and_2 import DeepSpeedZeroOptimizer

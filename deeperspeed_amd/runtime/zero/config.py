@@ -40,6 +40,9 @@ _SCALARS = {
     # MI355X extension: run grad reduction in the model dtype even when the
     # global fp32_allreduce default applies (kept off by default for parity).
     "round_robin_gradients": False,
+    # MI355X extension: hold the fp32 master exactly as bf16 weight + int16 residual
+    # (runtime/zero/compact_master.py), 14 instead of 16 B/param of model state.
+    "compact_master": False,
 }
 
 _OFFLOAD_PARAM_DEFAULTS = dict(device=None, nvme_path=None, buffer_count=5, buffer_size=int(1e8),

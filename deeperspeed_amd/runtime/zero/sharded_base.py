@@ -31,6 +31,7 @@ from ...ops import native
 from ...ops.adam.fused_adam import FusedAdam
 from ...utils.logging import logger
 from ..fp16.loss_scaler import DynamicLossScaler, LossScaler
+from . import compact_master as cm
 from .layout import FlatGroup, layout_signature, params_to_shard, shards_to_params
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
@@ -49,8 +50,10 @@ class ShardedOptimizerBase:
 
     def __init__(self, init_optimizer, dp_process_group=None, mpu=None, clip_grad=0.0, static_loss_scale=1.0,
                  dynamic_loss_scale=False, dynamic_loss_args=None, fp32_reduce=False, gradient_predivide_factor=1.0,
-                 gradient_accumulation_steps=1, offload_optimizer=None, timers=None, verbose=False):
+                 gradient_accumulation_steps=1, offload_optimizer=None, timers=None, verbose=False,
+                 compact_master=False):
         self.optimizer = init_optimizer
+        self.compact_master = bool(compact_master)
         self.dp_group = dp_process_group
         self.mpu = mpu
         self.clip_grad = float(clip_grad or 0.0)
@@ -122,7 +125,17 @@ class ShardedOptimizerBase:
         right device, rebind inner optimizer param groups to the masters."""
         host = self.offload is not None and self.offload.get("device") in ("cpu", "nvme")
         pin = bool(self.offload and self.offload.get("pin_memory", True)) and torch.cuda.is_available()
+        if self.compact_master:
+            if self.offload is not None or not self.fused:
+                raise ValueError("compact_master needs the fused Adam optimizer and no optimizer offload")
+            for g in self.groups:
+                if g.dtype != torch.bfloat16 or g.shard_param is None:
+                    raise ValueError("compact_master needs bf16 model parameters")
         for g in self.groups:
+            if self.compact_master:
+                # the bf16 shard already equals the master's high half: residual starts at 0
+                g.master = torch.zeros(g.shard_numel, dtype=torch.int16, device=g.shard_param.device)
+                continue
             m = init_shard_fn(g).float()
             if host:
                 hm = torch.empty(g.shard_numel, dtype=torch.float32, pin_memory=pin)
@@ -371,7 +384,7 @@ class ShardedOptimizerBase:
             "partition_count": self.dp_world,
             "layout": layout_signature(self.groups),
             "fp32_groups_key": self._fp32_key(),
-            self._fp32_key(): [g.master.detach().cpu() for g in self.groups],
+            self._fp32_key(): [self.master_fp32(g) for g in self.groups],
         }
         return sd
 
@@ -399,7 +412,10 @@ class ShardedOptimizerBase:
             masters, moments = self._elastic_merge(state_dict_list, key)
         if load_from_fp32_weights:
             for g, m in zip(self.groups, masters):
-                g.master.copy_(m.to(g.master.device))
+                if self.compact_master:
+                    cm.encode_into(m, g.shard_param, g.master)
+                else:
+                    g.master.copy_(m.to(g.master.device))
             self._refresh_params_from_master()
         if load_optimizer_states:
             self._load_moments(moments)
@@ -450,12 +466,20 @@ class ShardedOptimizerBase:
                 else:
                     st[k] = v
 
+    def master_fp32(self, g: FlatGroup) -> torch.Tensor:
+        """This rank's fp32 master shard of group g as a host tensor (checkpoints, tests)."""
+        if self.compact_master:
+            return cm.decode_chunked(g.shard_param, g.master, torch.empty(g.shard_numel, dtype=torch.float32))
+        return g.master.detach().cpu()
+
     def _refresh_params_from_master(self):
         """Copy master -> low-precision shard/params after a fp32 restore."""
         for g in self.groups:
             for b in g.buckets:
                 out = self._bucket_out(g, b)
-                if out is not None and out.data_ptr() != g.master.data_ptr():
+                if self.compact_master:
+                    pass  # the bf16 shard is the master's high half already
+                elif out is not None and out.data_ptr() != g.master.data_ptr():
                     out.copy_(g.master[b.shard_offset: b.shard_offset + b.chunk].to(out.device))
                 self._after_bucket_update(g, b)
         self._post_step()

@@ -91,13 +91,15 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                  prefetch_bucket_size=int(5e7), max_live_parameters=int(1e9), max_reuse_distance=int(1e9),
                  param_persistence_threshold=int(1e5), unit_max_numel=int(2e8), fp32_reduce=False,
                  gradient_predivide_factor=1.0, gradient_accumulation_steps=1, offload_optimizer=None,
-                 offload_param=None, timers=None, overlap_comm=True, sub_group_size=int(1e12), verbose=False):
+                 offload_param=None, timers=None, overlap_comm=True, sub_group_size=int(1e12), verbose=False,
+                 compact_master=False):
         super().__init__(init_optimizer, dp_process_group=dp_process_group, mpu=mpu, clip_grad=clip_grad,
                          static_loss_scale=static_loss_scale, dynamic_loss_scale=dynamic_loss_scale,
                          dynamic_loss_args=dynamic_loss_args, fp32_reduce=fp32_reduce,
                          gradient_predivide_factor=gradient_predivide_factor,
                          gradient_accumulation_steps=gradient_accumulation_steps,
-                         offload_optimizer=offload_optimizer, timers=timers, verbose=verbose)
+                         offload_optimizer=offload_optimizer, timers=timers, verbose=verbose,
+                         compact_master=compact_master)
         self.module = module
         self.stage = 3
         self.prefetch_bucket_size = int(prefetch_bucket_size)

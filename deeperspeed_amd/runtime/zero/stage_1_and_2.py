@@ -45,13 +45,14 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
                  static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None, reduce_bucket_size=int(5e8),
                  allgather_bucket_size=int(5e8), overlap_comm=True, reduce_scatter=True, fp32_reduce=False,
                  gradient_predivide_factor=1.0, gradient_accumulation_steps=1, offload_optimizer=None, timers=None,
-                 postscale_gradients=True, verbose=False):
+                 postscale_gradients=True, verbose=False, compact_master=False):
         super().__init__(init_optimizer, dp_process_group=dp_process_group, mpu=mpu, clip_grad=clip_grad,
                          static_loss_scale=static_loss_scale, dynamic_loss_scale=dynamic_loss_scale,
                          dynamic_loss_args=dynamic_loss_args, fp32_reduce=fp32_reduce,
                          gradient_predivide_factor=gradient_predivide_factor,
                          gradient_accumulation_steps=gradient_accumulation_steps,
-                         offload_optimizer=offload_optimizer, timers=timers, verbose=verbose)
+                         offload_optimizer=offload_optimizer, timers=timers, verbose=verbose,
+                         compact_master=compact_master)
         assert stage in (0, 1, 2)
         self.stage = stage
         self.sharded = stage >= 1
@@ -307,7 +308,9 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
                     c0 = b.arena_offset + self.dp_rank * b.chunk
                     g.shard_param[b.shard_offset: b.shard_offset + b.chunk].copy_(g.arena[c0: c0 + b.chunk])
             src = g.shard_param if g.shard_param is not None else g.arena
-            if g.master.data_ptr() != src.data_ptr():
+            if self.compact_master:
+                g.master.zero_()  # bf16 shard is now the exact master
+            elif g.master.data_ptr() != src.data_ptr():
                 g.master.copy_(src.float().to(g.master.device))
 
     def zero_grad(self, set_to_none=True):

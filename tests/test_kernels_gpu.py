@@ -200,3 +200,37 @@ def test_flash_attention_lse_and_large_logits():
     s = s.masked_fill(torch.ones(256, 256, dtype=torch.bool, device=_dev()).triu(1), float("-inf"))
     torch.testing.assert_close(lse, torch.logsumexp(s, -1), atol=2e-2, rtol=1e-3)
     torch.testing.assert_close(o.float(), torch.softmax(s, -1) @ v.float(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("V", [512, 50432, 1000])
+def test_fused_cross_entropy(dtype, V):
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(0)
+    x = (3 * torch.randn(2, 37, V, device=_dev())).to(dtype).requires_grad_(True)
+    lab = torch.randint(0, V, (2, 37), device=_dev())
+    lab[0, :5] = -100  # ignored rows
+    loss = native.cross_entropy(x, lab)
+    loss.backward()
+    xr = x.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(xr.view(-1, V), lab.view(-1), ignore_index=-100)
+    ref.backward()
+    torch.testing.assert_close(loss, ref, atol=2e-4, rtol=2e-4)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=1e-4, rtol=2e-2)
+
+
+def test_adam_compact_matches_fp32_master():
+    """Compact master (bf16 hi + int16 residual) must track the fp32 master bit for bit."""
+    from deeperspeed_amd.ops import native
+    from deeperspeed_amd.runtime.zero import compact_master as cm
+    torch.manual_seed(0)
+    n = 1 << 20 | 3
+    w = torch.randn(n, device=_dev())
+    hi, res = cm.encode(w)
+    m1, v1, m2, v2 = (torch.zeros(n, device=_dev()) for _ in range(4))
+    for step in range(1, 6):
+        g = torch.randn(n, device=_dev()).to(torch.bfloat16)
+        native.adam_flat_(w, g, m1, v1, None, 1e-3, 0.9, 0.95, 1e-8, 0.01, step, True, 0.7, True)
+        native.adam_compact_(hi, res, g, m2, v2, 1e-3, 0.9, 0.95, 1e-8, 0.01, step, True, 0.7, True)
+    assert torch.equal(cm.decode(hi, res).view(torch.int32), w.view(torch.int32))
+    assert torch.equal(m1, m2) and torch.equal(v1, v2)

@@ -20,7 +20,9 @@ def _train_and_dump(out_dir, stage, ga, offload, steps=3, hidden=32):
     torch.manual_seed(42)
     model = SimpleModel(hidden)
     zero = {"reduce_bucket_size": 500, "stage3_unit_max_numel": 600, "stage3_param_persistence_threshold": 10}
-    if offload:
+    if offload == "compact":
+        zero["compact_master"] = True
+    elif offload:
         zero["offload_optimizer"] = {"device": "cpu", "states": offload}
     cfg = base_config(stage=stage, mb=4, ga=ga, **zero)
     if stage == 0:
@@ -40,10 +42,11 @@ def _train_and_dump(out_dir, stage, ga, offload, steps=3, hidden=32):
         sd = engine.optimizer.gathered_state_dict(engine.module)
     else:
         sd = {k: v.detach().cpu().clone() for k, v in engine.module.state_dict().items()}
-    masters = torch.cat([g.master.detach().cpu().float() for g in engine.optimizer.groups]) \
+    masters = torch.cat([engine.optimizer.master_fp32(g).float() for g in engine.optimizer.groups]) \
         if hasattr(engine.optimizer, "groups") else None
     if rank == 0:
-        torch.save({"sd": sd, "loss": float(loss)}, os.path.join(out_dir, f"s{stage}_ga{ga}_{offload}.pt"))
+        torch.save({"sd": sd, "loss": float(loss), "masters": masters},
+                   os.path.join(out_dir, f"s{stage}_ga{ga}_{offload}.pt"))
 
 
 @pytest.mark.parametrize("ga", [1, 2])
