@@ -88,6 +88,19 @@ def get_config(name: str, **overrides) -> GPTNeoXConfig:
     return GPTNeoXConfig(**d)
 
 
+class LinearBiasGeLU(nn.Linear):
+    """dense_h_to_4h: GEMM without bias, then the fused bias+GeLU HIP kernel.  Keeping the
+    whole op inside this module's forward matters for ZeRO-3: a module's parameters are
+    gathered by its own forward hooks, so they must not be touched from a parent's forward."""
+
+    def __init__(self, in_features, out_features, approximate=False, device=None, dtype=None):
+        super().__init__(in_features, out_features, device=device, dtype=dtype)
+        self.approximate = approximate
+
+    def forward(self, x):
+        return native.bias_gelu(F.linear(x, self.weight), self.bias, self.approximate)
+
+
 class NeoXAttention(nn.Module):
     def __init__(self, cfg: GPTNeoXConfig, device=None, dtype=None):
         super().__init__()
@@ -99,26 +112,25 @@ class NeoXAttention(nn.Module):
     def forward(self, x):
         cfg = self.cfg
         B, S, H = x.shape
-        qkv = F.linear(x, self.query_key_value.weight, self.query_key_value.bias)
+        qkv = self.query_key_value(x)
         q, k, v = rotary_split(qkv, cfg.num_heads, cfg.head_dim, cfg.rotary_dim, cfg.rotary_base,
                                qscale=1.0 / math.sqrt(cfg.head_dim))
         ctx = attention(q, k, v, causal=True, softmax_scale=1.0, dropout_p=cfg.attention_dropout,
                         training=self.training)
         ctx = ctx.transpose(1, 2).reshape(B, S, H)
-        return F.linear(ctx, self.dense.weight, self.dense.bias)
+        return self.dense(ctx)
 
 
 class NeoXMLP(nn.Module):
     def __init__(self, cfg: GPTNeoXConfig, device=None, dtype=None):
         super().__init__()
         self.cfg = cfg
-        self.dense_h_to_4h = nn.Linear(cfg.hidden_size, cfg.intermediate_size, device=device, dtype=dtype)
+        self.dense_h_to_4h = LinearBiasGeLU(cfg.hidden_size, cfg.intermediate_size, cfg.gelu_approximate,
+                                            device=device, dtype=dtype)
         self.dense_4h_to_h = nn.Linear(cfg.intermediate_size, cfg.hidden_size, device=device, dtype=dtype)
 
     def forward(self, x):
-        h = F.linear(x, self.dense_h_to_4h.weight)  # bias fused into the GeLU kernel
-        h = native.bias_gelu(h, self.dense_h_to_4h.bias, self.cfg.gelu_approximate)
-        return F.linear(h, self.dense_4h_to_h.weight, self.dense_4h_to_h.bias)
+        return self.dense_4h_to_h(self.dense_h_to_4h(x))
 
 
 class NeoXTransformerLayer(nn.Module):
@@ -177,7 +189,7 @@ class GPTNeoX(nn.Module):
         for layer in self.layers:
             x = layer(x)
         x = self.final_layer_norm(x)
-        logits = F.linear(x, self.embed_out.weight)
+        logits = self.embed_out(x)
         if labels is None:
             return logits
         return lm_loss(logits, labels)
@@ -211,7 +223,7 @@ class _FinalPipe(nn.Module):
         nn.init.normal_(self.embed_out.weight, 0.0, cfg.init_std)
 
     def forward(self, x):
-        return F.linear(self.final_layer_norm(x), self.embed_out.weight)
+        return self.embed_out(self.final_layer_norm(x))
 
 
 def to_pipeline(cfg: GPTNeoXConfig, num_stages: int, topology=None, partition_method="type:NeoXTransformerLayer",
