@@ -1,0 +1,2 @@
+from .cpu_adam import DeepSpeedCPUAdam
+from .fused_adam import FusedAdam

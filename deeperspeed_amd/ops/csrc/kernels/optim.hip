@@ -212,7 +212,8 @@ __global__ void __launch_bounds__(256) scale_copy_kernel(const TI* __restrict__ 
 // Mirrors the 3-kernel structure of csrc/lamb/fused_lamb_cuda_kernel.cu:185-310 but
 // with wave64 reductions and a device-resident coefficient (no host sync).
 // ---------------------------------------------------------------------------
-// LambArgs (launchers.h): adamw = 1 folds decay into the update (LAMB default).
+// LambArgs (launchers.h): adamw = 1 puts eps outside the sqrt (reference eps_mode 1), lr is the
+// bias-corrected step size lr*sqrt(bc2)/bc1 and grad_scale the inverse loss scale.
 
 template <typename TW, typename TG>
 __global__ void __launch_bounds__(256) lamb_stage1_kernel(const TW* __restrict__ w, const TG* __restrict__ g,
@@ -225,12 +226,13 @@ __global__ void __launch_bounds__(256) lamb_stage1_kernel(const TW* __restrict__
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
     float wf = Conv<TW>::load(w, e);
     float gf = Conv<TG>::load(g, e) * a.grad_scale;
-    if (!a.adamw && a.weight_decay != 0.f) gf = fmaf(a.weight_decay, wf, gf);
     float mf = fmaf(a.beta1, m[e], (1.f - a.beta1) * gf);
     float vf = fmaf(a.beta2, v[e], (1.f - a.beta2) * gf * gf);
     m[e] = mf; v[e] = vf;
-    float u = (mf / a.bc1) / (sqrtf(vf / a.bc2) + a.eps);
-    if (a.adamw && a.weight_decay != 0.f) u = fmaf(a.weight_decay, wf, u);
+    // LAMB update direction (reference fused_lamb_cuda_kernel.cu:185-230): no bias correction
+    // inside u (it is folded into the step size), eps outside (adamw=1) or inside the sqrt
+    const float denom = a.adamw ? sqrtf(vf) + a.eps : sqrtf(vf + a.eps);
+    const float u = mf / denom + a.weight_decay * wf;
     upd[e] = u;
     sw = fmaf(wf, wf, sw);
     su = fmaf(u, u, su);
@@ -248,8 +250,7 @@ __global__ void __launch_bounds__(256) lamb_finish_kernel(const float* __restric
   if (threadIdx.x == 0) {
     const float wn = sqrtf(sw), un = sqrtf(su);
     float c = 1.f;
-    if (wn > 0.f && un > 0.f) c = wn / un;
-    c = fminf(fmaxf(c, a.min_coeff), a.max_coeff);
+    if (wn > 0.f && un > 0.f) c = fminf(fmaxf(wn / un, a.min_coeff), a.max_coeff);
     coeff_out[0] = c;
   }
 }

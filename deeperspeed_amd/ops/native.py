@@ -283,3 +283,35 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         return _CrossEntropyFn.apply(logits, labels)
     return torch.nn.functional.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), labels.reshape(-1),
                                              ignore_index=-100)
+
+
+# --------------------------------------------------------------------------- LAMB
+def lamb_(w, g, m, v, out, lr, beta1, beta2, eps, weight_decay, step, bias_correction, grad_scale, max_coeff,
+          min_coeff, eps_outside_sqrt=True, coeff_out=None):
+    """One LAMB step on one tensor (reference semantics, fused_lamb_cuda_kernel.cu:185-310):
+    u = m/(sqrt(v)+eps) + wd*w, coeff = clamp(|w|/|u|, min, max) (1 if either norm is 0),
+    w -= lr*sqrt(bc2)/bc1 * coeff * u.  Returns the coefficient as a 1-element fp32 tensor
+    (device-resident on GPU: no host sync)."""
+    bc1 = 1.0 - beta1 ** step if bias_correction else 1.0
+    bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
+    step_size = lr * math.sqrt(bc2) / bc1
+    if coeff_out is None:
+        coeff_out = torch.empty(1, dtype=torch.float32, device=w.device)
+    if w.is_cuda:
+        upd = torch.empty(w.numel(), dtype=torch.float32, device=w.device)
+        hip_ops().lamb(w, g, m, v, upd, out, step_size, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale,
+                       max_coeff, min_coeff, bool(eps_outside_sqrt), _workspace(w.device, 4096), coeff_out)
+        return coeff_out
+    gf = g.float() * grad_scale
+    m.mul_(beta1).add_(gf, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(gf, gf, value=1 - beta2)
+    denom = v.sqrt().add_(eps) if eps_outside_sqrt else (v + eps).sqrt()
+    wf = w.float()
+    u = m / denom + weight_decay * wf
+    wn, un = wf.norm(), u.norm()
+    c = torch.where((wn > 0) & (un > 0), (wn / un).clamp(min_coeff, max_coeff), torch.ones_like(wn))
+    w.copy_(wf - step_size * c * u)
+    if out is not None:
+        out.copy_(w)
+    coeff_out.copy_(c.reshape(1))
+    return coeff_out

@@ -575,6 +575,14 @@ class DeepSpeedEngine(Module):
     def _configure_fp16_optimizer(self, optimizer):
         from .zero.stage_1_and_2 import DeepSpeedZeroOptimizer
         dynamic = self.dynamic_loss_scale() and not self.bfloat16_enabled()
+        if getattr(optimizer, "requires_per_param_masters", False):
+            # per-tensor optimizer math (LAMB trust ratio): reference engine.py picks
+            # FP16_UnfusedOptimizer for non-fused-Adam optimizers
+            from .fp16.unfused_optimizer import FP16_UnfusedOptimizer
+            return FP16_UnfusedOptimizer(optimizer, static_loss_scale=self.loss_scale() or 1.0,
+                                         dynamic_loss_scale=dynamic, dynamic_loss_args=self._dynamic_args(),
+                                         mpu=self.mpu, clip_grad=self.gradient_clipping(),
+                                         verbose=self.global_rank == 0)
         return DeepSpeedZeroOptimizer(optimizer, stage=0, dp_process_group=self.data_parallel_group, mpu=self.mpu,
                                       clip_grad=self.gradient_clipping(), static_loss_scale=self.loss_scale() or 1.0,
                                       dynamic_loss_scale=dynamic, dynamic_loss_args=self._dynamic_args(),

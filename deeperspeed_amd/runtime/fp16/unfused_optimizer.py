@@ -1,0 +1,139 @@
+"""Mixed-precision wrapper with one fp32 master per parameter (no flattening).
+
+Reference parity: deepspeed/runtime/fp16/unfused_optimizer.py:1-407 (`FP16_UnfusedOptimizer`),
+used for optimizers whose math is per-tensor (LAMB's trust ratio): flattening the model into
+one arena would merge the per-layer norms.  bf16/fp16 gradients are unscaled and clipped
+straight into the fp32 master grads (one fused pass per tensor), the inner optimizer runs on
+the masters and the low-precision params are refreshed from them.  The data-parallel
+all-reduce of the model gradients is done by the engine before `step` (engine.py
+buffered_allreduce_fallback), exactly like the reference.
+"""
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from ...utils.logging import logger
+from ..utils import CheckOverflow, get_grad_norm
+from .loss_scaler import DynamicLossScaler, LossScaler
+
+
+class FP16_UnfusedOptimizer:
+    def __init__(self, init_optimizer, static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None,
+                 verbose=True, mpu=None, clip_grad=0.0, fused_lamb_legacy=False):
+        self.optimizer = init_optimizer
+        self.mpu = mpu
+        self.clip_grad = float(clip_grad or 0.0)
+        self.fused_lamb_legacy = fused_lamb_legacy
+        self.fp16_groups, self.fp32_groups = [], []
+        for group in self.optimizer.param_groups:
+            lp = list(group["params"])
+            masters = []
+            for p in lp:
+                m = p.detach().clone().float()
+                m.requires_grad_(False)
+                masters.append(m)
+            self.fp16_groups.append(lp)
+            self.fp32_groups.append(masters)
+            group["params"] = masters
+        if dynamic_loss_scale:
+            self.loss_scaler = DynamicLossScaler(**(dynamic_loss_args or {}))
+            self.dynamic_loss_scale = True
+        else:
+            self.loss_scaler = LossScaler(scale=static_loss_scale)
+            self.dynamic_loss_scale = False
+        self.overflow = False
+        self.overflow_checker = CheckOverflow(self.fp16_groups, mpu=mpu)
+        self._global_grad_norm = 0.0
+        if verbose:
+            logger.info(f"FP16_UnfusedOptimizer: {sum(len(g) for g in self.fp16_groups)} params with fp32 masters")
+
+    # ----------------------------------------------------------------- properties
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    @property
+    def loss_scale(self):
+        return self.loss_scaler.loss_scale
+
+    @property
+    def cur_scale(self):
+        return self.loss_scaler.loss_scale
+
+    def get_global_grad_norm(self):
+        return self._global_grad_norm
+
+    # ----------------------------------------------------------------- steps
+    def zero_grad(self, set_to_none=True):
+        for group in self.fp16_groups:
+            for p in group:
+                if set_to_none:
+                    p.grad = None
+                elif p.grad is not None:
+                    p.grad.detach_()
+                    p.grad.zero_()
+
+    def backward(self, loss, retain_graph=False):
+        (loss.float() * self.loss_scale).backward(retain_graph=retain_graph)
+
+    def step(self, closure=None):
+        params = [p for g in self.fp16_groups for p in g]
+        self.overflow = self.overflow_checker.has_overflow(params)
+        prev = self.loss_scale
+        if self.dynamic_loss_scale or self.overflow:
+            self.loss_scaler.update_scale(self.overflow)
+        if self.overflow:
+            logger.info(f"[deepspeed] fp16 dynamic loss scale overflow! Skipping step. Attempted loss scale: "
+                        f"{prev}, reducing to {self.loss_scale}")
+            self.zero_grad()
+            return self.overflow
+        norm = get_grad_norm(params, mpu=self.mpu) / prev
+        self._global_grad_norm = norm
+        coef = 1.0 / prev
+        if self.clip_grad > 0 and norm > self.clip_grad:
+            coef *= self.clip_grad / (norm + 1e-6)
+        for lp_group, fp_group in zip(self.fp16_groups, self.fp32_groups):
+            for p, m in zip(lp_group, fp_group):
+                if p.grad is None:
+                    m.grad = None
+                    continue
+                m.grad = p.grad.detach().float().mul_(coef)
+        self.optimizer.step()
+        for lp_group, fp_group in zip(self.fp16_groups, self.fp32_groups):
+            for p, m in zip(lp_group, fp_group):
+                m.grad = None
+                p.data.copy_(m.data)
+        self.zero_grad()
+        return self.overflow
+
+    # ----------------------------------------------------------------- checkpoints
+    def state_dict(self):
+        return {"dynamic_loss_scale": self.dynamic_loss_scale, "cur_scale": self.loss_scale,
+                "loss_scaler": self.loss_scaler.state_dict(), "overflow": self.overflow,
+                "optimizer_state_dict": self.optimizer.state_dict(),
+                "fp32_groups": [[m.detach().cpu() for m in g] for g in self.fp32_groups]}
+
+    def load_state_dict(self, sd, load_optimizer_states=True):
+        self.dynamic_loss_scale = sd.get("dynamic_loss_scale", self.dynamic_loss_scale)
+        if "loss_scaler" in sd:
+            self.loss_scaler.load_state_dict(sd["loss_scaler"])
+        self.overflow = sd.get("overflow", False)
+        if load_optimizer_states:
+            self.optimizer.load_state_dict(sd["optimizer_state_dict"])
+        for cur, saved in zip(self.fp32_groups, sd["fp32_groups"]):
+            for m, s in zip(cur, saved):
+                m.data.copy_(s.to(m.device))
+        for lp_group, fp_group in zip(self.fp16_groups, self.fp32_groups):
+            for p, m in zip(lp_group, fp_group):
+                p.data.copy_(m.data)
+
+    def refresh_fp32_params(self):
+        for lp_group, fp_group in zip(self.fp16_groups, self.fp32_groups):
+            for p, m in zip(lp_group, fp_group):
+                m.data.copy_(p.data.float())

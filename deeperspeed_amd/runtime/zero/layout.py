@@ -120,7 +120,7 @@ def build_size_buckets(group: FlatGroup, world: int, bucket_size: int) -> FlatGr
     arena_off = shard_off = 0
     blists = []
     for p in order:
-        n = _round_up(p.numel(), ALIGN)
+        n = _round_up(p.ds_numel if hasattr(p, "ds_numel") else p.numel(), ALIGN)
         if cur and cur_n + n > bucket_size:
             blists.append(cur)
             cur, cur_n = [], 0

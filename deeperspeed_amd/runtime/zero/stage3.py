@@ -58,6 +58,10 @@ def _empty_like(dtype, device):
     return t
 
 
+def _numel(p):
+    return p.ds_numel if hasattr(p, "ds_tensor") else p.numel()
+
+
 def _in_backward():
     return torch._C._current_graph_task_id() != -1
 
@@ -71,7 +75,7 @@ class ZeroUnit:
         self.status = ZeroParamStatus.NOT_AVAILABLE
         self.works = []
         self.fulls = []
-        self.numel = sum(p.numel() for p in self.params)
+        self.numel = sum(_numel(p) for p in self.params)
         self.persistent = False
         self.active = 0
         self.in_backward = False
@@ -126,6 +130,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self._build_shards()
         self._alloc_master_and_state(lambda g: g.shard_param.float())
         self._register_hooks()
+        for m in module.modules():
+            for p in m.__dict__.get("_external_params", []):
+                self.register_external_parameter(m, p)
         if verbose or True:
             n = sum(u.numel for u in self._units)
             logger.info(f"ZeRO-3: {len(self._units)} units, {n / 1e9:.3f}B params, dp_world={self.dp_world}, "
@@ -153,7 +160,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             sub = subtree_params(m)
             if not sub:
                 return
-            n = sum(p.numel() for p in sub)
+            n = sum(_numel(p) for p in sub)
             kids = [c for c in m.children() if any(True for _ in c.parameters())]
             if n <= self.unit_max_numel or not kids:
                 make(m, sub)
@@ -163,11 +170,22 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             make(m, list(m.parameters(recurse=False)))
 
         visit(root)
+        # module -> unit whose hooks run around it (nearest ancestor unit root)
+        self._unit_of_module = {}
+
+        def label(m, cur):
+            cur = getattr(m, "_zero_unit", None) or cur
+            self._unit_of_module[id(m)] = cur
+            for c in m.children():
+                label(c, cur)
+
+        label(root, None)
         for u in self._units:
             u.persistent = u.numel <= self.persistence_threshold and not self.single
             for p in u.params:
-                p.ds_numel = p.numel()
-                p.ds_shape = p.shape
+                if not hasattr(p, "ds_tensor"):  # zero.Init params carry their full shape
+                    p.ds_numel = p.numel()
+                    p.ds_shape = p.shape
                 p.ds_id = id(p)
                 p.ds_unit = u
                 p.ds_status = ZeroParamStatus.AVAILABLE
@@ -181,15 +199,23 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             for b in g.buckets:
                 for i, p in enumerate(b.params):
                     ov = b.chunk_overlap(r, i)
+                    src = p.data.reshape(-1)
+                    if src.numel() == 0 and hasattr(p, "ds_tensor"):
+                        # zero.Init partition: re-layout one parameter at a time (collective,
+                        # every rank walks the same bucket order)
+                        from .partition_parameters import _gather_full
+                        src = _gather_full(p, self.dp_group)
                     if ov is None:
                         continue
                     p0, c0, ln = ov
-                    src = p.data.reshape(-1)
-                    if src.numel() == 0 and hasattr(p, "ds_tensor"):
-                        raise RuntimeError("zero.Init partitioned params must be adopted via GatheredParameters")
                     g.shard_param[b.shard_offset + c0: b.shard_offset + c0 + ln].copy_(src[p0: p0 + ln])
             gdt = self._grad_dtype(g)
             g.shard_grad = torch.zeros(g.shard_numel, dtype=gdt, device=dev)
+        for u in self._units:
+            for p in u.params:
+                p._ds_owner = self
+                if hasattr(p, "ds_tensor"):
+                    del p.ds_tensor  # adopted into the flat shard layout
         # release full parameters / bind permanently (single rank)
         for u in self._units:
             for g, b in u.buckets:
@@ -365,6 +391,10 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             for i, p in enumerate(b.params):
                 if p.requires_grad:
                     p.grad = gf[b.offsets[i]: b.offsets[i] + b.numels[i]].view(p.ds_shape)
+        # parameters this unit's forward borrowed (register_external_parameter) are needed
+        # by its backward too; their grads land in their owner's buffers
+        for x in u.external:
+            self._pre_backward(x)
 
     def _grad_ready(self, p):
         u = self._unit_of_param[id(p)]
@@ -469,11 +499,33 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     # ------------------------------------------------------------------ model state helpers
     def register_external_parameter(self, module, param):
         owner = self.unit_of(param)
-        mu = getattr(module, "_zero_unit", None)
+        mu = self._unit_of_module.get(id(module))
         if owner is None or mu is None or owner is mu:
             return
         if owner not in mu.external:
             mu.external.append(owner)
+
+    def write_back_params(self, params):
+        """Copy edited full parameters (currently gathered) back into this rank's shard and
+        fp32 master (zero.GatheredParameters(modifier_rank=...) exit path)."""
+        want = {id(p) for p in params}
+        for g in self.groups:
+            for b in g.buckets:
+                for i, p in enumerate(b.params):
+                    if id(p) not in want:
+                        continue
+                    ov = b.chunk_overlap(self.dp_rank, i)
+                    if ov is None:
+                        continue
+                    p0, c0, ln = ov
+                    lo = b.shard_offset + c0
+                    src = p.data.reshape(-1)[p0: p0 + ln]
+                    if g.shard_param[lo: lo + ln].data_ptr() != src.data_ptr():
+                        g.shard_param[lo: lo + ln].copy_(src)
+                    if self.compact_master:
+                        g.master[lo: lo + ln].zero_()
+                    else:
+                        g.master[lo: lo + ln].copy_(g.shard_param[lo: lo + ln].float().to(g.master.device))
 
     def gathered_state_dict(self, module, prefix=""):
         """Full (consolidated) low-precision state dict; every rank participates."""

@@ -234,3 +234,22 @@ def test_adam_compact_matches_fp32_master():
         native.adam_compact_(hi, res, g, m2, v2, 1e-3, 0.9, 0.95, 1e-8, 0.01, step, True, 0.7, True)
     assert torch.equal(cm.decode(hi, res).view(torch.int32), w.view(torch.int32))
     assert torch.equal(m1, m2) and torch.equal(v1, v2)
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_lamb_kernel_matches_cpu(gdt):
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(0)
+    n = 100003
+    w = torch.randn(n)
+    wg = w.to(_dev())
+    m, v = torch.zeros(n), torch.zeros(n)
+    mg, vg = m.to(_dev()), v.to(_dev())
+    out = torch.empty(n, dtype=torch.bfloat16, device=_dev())
+    for step in range(1, 4):
+        g = torch.randn(n).to(gdt)
+        c1 = native.lamb_(w, g, m, v, None, 1e-2, 0.9, 0.999, 1e-8, 0.01, step, True, 0.5, 10.0, 0.01)
+        c2 = native.lamb_(wg, g.to(_dev()), mg, vg, out, 1e-2, 0.9, 0.999, 1e-8, 0.01, step, True, 0.5, 10.0, 0.01)
+        assert abs(float(c1) - float(c2)) < 1e-4 * abs(float(c1))
+    torch.testing.assert_close(wg.cpu(), w, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(out.float().cpu(), w, atol=1e-2, rtol=1e-2)
