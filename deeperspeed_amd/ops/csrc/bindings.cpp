@@ -302,6 +302,48 @@ Tensor softmax_bwd(Tensor dy, Tensor y, double scale) {
   return dx;
 }
 
+// 1-bit compression. worker: m, err fp32 [n] (n % 8 == 0) -> (packed uint8 [n/8], scale [1]);
+// err is updated in place with the new compression error.
+std::vector<Tensor> onebit_worker_compress(Tensor m, Tensor err, Tensor ws) {
+  check_dev(m, "m"); check_dev(err, "err");
+  TORCH_CHECK(m.scalar_type() == at::kFloat && err.scalar_type() == at::kFloat && m.numel() == err.numel() &&
+              m.numel() % 8 == 0, "onebit: fp32 m/err of equal length, multiple of 8");
+  TORCH_CHECK(ws.numel() >= 1024 && ws.scalar_type() == at::kFloat, "onebit: workspace");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(m.device());
+  Tensor packed = at::empty({m.numel() / 8}, m.options().dtype(at::kByte));
+  Tensor scale = at::empty({1}, m.options());
+  dsa::launch_onebit_worker(m.data_ptr<float>(), err.data_ptr<float>(), m.numel(), packed.data_ptr<uint8_t>(),
+                            scale.data_ptr<float>(), ws.data_ptr<float>(), cur_stream());
+  return {packed, scale};
+}
+
+// server: signs uint8 [P * nbytes], scales fp32 [P], server_err fp32 [nbytes*8] (updated)
+std::vector<Tensor> onebit_server_compress(Tensor signs, Tensor scales, Tensor server_err, Tensor ws) {
+  check_dev(signs, "signs"); check_dev(scales, "scales"); check_dev(server_err, "server_err");
+  const int64_t P = scales.numel();
+  const int64_t nbytes = server_err.numel() / 8;
+  TORCH_CHECK(signs.scalar_type() == at::kByte && signs.numel() == P * nbytes && server_err.numel() % 8 == 0,
+              "onebit_server: shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(signs.device());
+  Tensor packed = at::empty({nbytes}, signs.options());
+  Tensor scale = at::empty({1}, scales.options());
+  dsa::launch_onebit_server(signs.data_ptr<uint8_t>(), scales.data_ptr<float>(), (int)P, nbytes,
+                            server_err.data_ptr<float>(), packed.data_ptr<uint8_t>(), scale.data_ptr<float>(),
+                            ws.data_ptr<float>(), cur_stream());
+  return {packed, scale};
+}
+
+// unpack: signs uint8 [P * nbytes_per], scales fp32 [P] -> out fp32 [P * nbytes_per * 8]
+void onebit_unpack(Tensor signs, Tensor scales, Tensor out) {
+  check_dev(signs, "signs"); check_dev(out, "out");
+  const int64_t P = scales.numel();
+  TORCH_CHECK(signs.numel() % P == 0 && out.numel() == signs.numel() * 8 && out.scalar_type() == at::kFloat &&
+              (reinterpret_cast<uintptr_t>(out.data_ptr()) & 15) == 0, "onebit_unpack: shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(signs.device());
+  dsa::launch_onebit_unpack(signs.data_ptr<uint8_t>(), scales.data_ptr<float>(), (int)P, signs.numel() / P,
+                            out.data_ptr<float>(), cur_stream());
+}
+
 // Fused softmax cross-entropy. logits [R, V] 16-bit, labels [R] int64 (<0 = ignored)
 // -> (per-row loss fp32 [R], lse fp32 [R])
 std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels) {
@@ -370,6 +412,9 @@ std::vector<Tensor> flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Te
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("onebit_worker_compress", &onebit_worker_compress);
+  m.def("onebit_server_compress", &onebit_server_compress);
+  m.def("onebit_unpack", &onebit_unpack);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);

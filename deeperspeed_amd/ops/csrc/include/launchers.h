@@ -69,6 +69,14 @@ void launch_xent_fwd(const void* x, const int64_t* labels, float* loss, float* l
 void launch_xent_bwd(const void* x, const int64_t* labels, const float* lse, const float* dloss, int64_t dloss_stride,
                      void* dx, int64_t rows, int V, int dt, hipStream_t s);
 
+// onebit.hip: 1-bit error-compensated compression (ws >= 1024 floats)
+void launch_onebit_worker(const float* m, float* err, int64_t n, uint8_t* packed, float* scale_out, float* ws,
+                          hipStream_t s);
+void launch_onebit_server(const uint8_t* signs, const float* scales, int P, int64_t nbytes, float* server_err,
+                          uint8_t* packed, float* scale_out, float* ws, hipStream_t s);
+void launch_onebit_unpack(const uint8_t* signs, const float* scales, int P, int64_t nbytes_per, float* out,
+                          hipStream_t s);
+
 // flash_attn.hip: q,k,v,o [BH, S, D] (D in 64/96/128), lse/delta [BH, S] fp32
 bool flash_supported(int D);
 void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,

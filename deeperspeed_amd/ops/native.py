@@ -315,3 +315,55 @@ def lamb_(w, g, m, v, out, lr, beta1, beta2, eps, weight_decay, step, bias_corre
         out.copy_(w)
     coeff_out.copy_(c.reshape(1))
     return coeff_out
+
+
+# --------------------------------------------------------------------------- 1-bit compression
+_BITW = None
+
+
+def _packbits(bits: torch.Tensor) -> torch.Tensor:
+    global _BITW
+    if _BITW is None:
+        _BITW = torch.tensor([128, 64, 32, 16, 8, 4, 2, 1], dtype=torch.int32)
+    return (bits.view(-1, 8).to(torch.int32) * _BITW.to(bits.device)).sum(1).to(torch.uint8)
+
+
+def _unpackbits(packed: torch.Tensor) -> torch.Tensor:
+    """uint8 [..., nb] -> float +-1 [..., nb*8] (MSB first)."""
+    shifts = torch.arange(7, -1, -1, device=packed.device, dtype=torch.int32)
+    bits = (packed.to(torch.int32).unsqueeze(-1) >> shifts) & 1
+    return bits.reshape(*packed.shape[:-1], -1).float().mul_(2).sub_(1)
+
+
+def _ef_pack(c: torch.Tensor, err: torch.Tensor):
+    scale = c.norm() / math.sqrt(c.numel())
+    pos = c >= 0
+    err.copy_(c - scale * (pos.float() * 2 - 1))
+    return _packbits(pos), scale.reshape(1).float()
+
+
+def onebit_worker_compress(m: torch.Tensor, err: torch.Tensor):
+    """Error-compensated sign compression of `m` (fp32, numel % 8 == 0); updates `err`.
+    Returns (packed uint8 [n/8], scale fp32 [1])."""
+    if m.is_cuda:
+        return tuple(hip_ops().onebit_worker_compress(m, err, _workspace(m.device, 2048)))
+    return _ef_pack(m + err, err)
+
+
+def onebit_server_compress(signs: torch.Tensor, scales: torch.Tensor, server_err: torch.Tensor):
+    """Average P received sign chunks (signs uint8 [P*nb], scales [P]) into the server chunk,
+    add the server error, re-compress.  Returns (packed [nb], scale [1])."""
+    if signs.is_cuda:
+        return tuple(hip_ops().onebit_server_compress(signs, scales, server_err, _workspace(signs.device, 2048)))
+    P = scales.numel()
+    vals = _unpackbits(signs.view(P, -1)) * scales.view(P, 1)
+    return _ef_pack(server_err + vals.sum(0) / P, server_err)
+
+
+def onebit_unpack(signs: torch.Tensor, scales: torch.Tensor, out: torch.Tensor):
+    if signs.is_cuda:
+        hip_ops().onebit_unpack(signs, scales, out)
+        return out
+    P = scales.numel()
+    out.copy_((_unpackbits(signs.view(P, -1)) * scales.view(P, 1)).view(-1))
+    return out

@@ -525,7 +525,7 @@ class DeepSpeedEngine(Module):
         if self.zero_optimization():
             assert not self.amp_enabled(), "Amp and ZeRO are not currently compatible"
             self.optimizer = self._configure_zero_optimizer(basic_optimizer)
-        elif self.fp16_enabled() and name not in (ONEBIT_ADAM_OPTIMIZER, ONEBIT_LAMB_OPTIMIZER):
+        elif self.fp16_enabled():
             self.optimizer = self._configure_fp16_optimizer(basic_optimizer)
         else:
             self.optimizer = basic_optimizer

@@ -253,3 +253,27 @@ def test_lamb_kernel_matches_cpu(gdt):
         assert abs(float(c1) - float(c2)) < 1e-4 * abs(float(c1))
     torch.testing.assert_close(wg.cpu(), w, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(out.float().cpu(), w, atol=1e-2, rtol=1e-2)
+
+
+def test_onebit_kernels_match_cpu_reference():
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(0)
+    P, nb = 4, 1000
+    n = P * nb * 8
+    m = torch.randn(n)
+    err = 0.1 * torch.randn(n)
+    pk_c, sc_c = native.onebit_worker_compress(m, err_c := err.clone())
+    pk_g, sc_g = native.onebit_worker_compress(m.to(_dev()), err_g := err.to(_dev()))
+    assert torch.equal(pk_g.cpu(), pk_c)
+    torch.testing.assert_close(sc_g.cpu(), sc_c, rtol=1e-5, atol=0)
+    torch.testing.assert_close(err_g.cpu(), err_c, rtol=1e-5, atol=1e-6)
+    signs = torch.randint(0, 256, (P * nb,), dtype=torch.uint8)
+    scales = torch.rand(P)
+    serr = 0.05 * torch.randn(nb * 8)
+    sp_c, ss_c = native.onebit_server_compress(signs, scales, serr_c := serr.clone())
+    sp_g, ss_g = native.onebit_server_compress(signs.to(_dev()), scales.to(_dev()), serr_g := serr.to(_dev()))
+    assert (sp_g.cpu() != sp_c).sum() <= 2  # sign of values within fp rounding of 0 may differ
+    torch.testing.assert_close(ss_g.cpu(), ss_c, rtol=1e-5, atol=0)
+    out_c = native.onebit_unpack(signs, scales, torch.empty(n))
+    out_g = native.onebit_unpack(signs.to(_dev()), scales.to(_dev()), torch.empty(n, device=_dev()))
+    assert torch.equal(out_g.cpu(), out_c)
