@@ -16,6 +16,12 @@ import torch
 from . import builder
 
 _hip = None
+_flop_sink = None  # set by the FLOPs profiler while it is active: callable(macs)
+
+
+def _macs(n):
+    if _flop_sink is not None:
+        _flop_sink(float(n))
 
 
 def hip_ops():
@@ -46,6 +52,7 @@ class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, eps):
         x = x.contiguous()
+        _macs(5 * x.numel())
         if x.is_cuda:
             y, mean, rstd, _ = hip_ops().ln_fwd(x, gamma, beta, eps, None, None)
         else:
@@ -103,6 +110,7 @@ class _BiasGeluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias, approx):
         x = x.contiguous()
+        _macs(2 * x.numel())
         if x.is_cuda:
             y = hip_ops().bias_gelu_fwd(x, bias, approx)
         else:
@@ -228,6 +236,8 @@ class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, scale):
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        B, H, S, D = q.shape
+        _macs(2 * B * H * S * S * D * (0.5 if causal else 1.0))
         o, lse = hip_ops().flash_attn_fwd(q, k, v, causal, scale)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal, ctx.scale = causal, scale
@@ -263,6 +273,7 @@ class _CrossEntropyFn(torch.autograd.Function):
     def forward(ctx, logits, labels):
         x = logits.reshape(-1, logits.shape[-1]).contiguous()
         lab = labels.reshape(-1).contiguous()
+        _macs(3 * x.numel())
         rows, lse = hip_ops().xent_fwd(x, lab)
         nvalid = (lab >= 0).sum().clamp_min(1).float()
         ctx.save_for_backward(x, lab, lse, nvalid)
