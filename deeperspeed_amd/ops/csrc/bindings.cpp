@@ -344,6 +344,81 @@ void onebit_unpack(Tensor signs, Tensor scales, Tensor out) {
                             out.data_ptr<float>(), cur_stream());
 }
 
+// ----------------------------------------------------------------------------- block-sparse attention
+// sdd: A [Z,H,Mr,K], B [Z,H,Nr,K] (B given row-major by N: C = A B^T), nz int32 [nnz,3] -> C [Z,nnz,blk,blk]
+Tensor sparse_sdd(Tensor A, Tensor B, Tensor nz, int64_t blk, double alpha) {
+  check_dev(A, "A"); check_dev(B, "B"); check_dev(nz, "nz");
+  TORCH_CHECK(A.dim() == 4 && B.dim() == 4 && A.size(0) == B.size(0) && A.size(1) == B.size(1) &&
+              A.size(3) == B.size(3) && A.scalar_type() == B.scalar_type() && A.scalar_type() != at::kFloat,
+              "sparse_sdd: A/B must be 16-bit [Z,H,*,K] with matching Z,H,K");
+  TORCH_CHECK(A.size(3) % 32 == 0 && blk % 16 == 0 && A.size(2) % blk == 0 && B.size(2) % blk == 0,
+              "sparse_sdd: K % 32, block % 16 and rows % block must be 0");
+  TORCH_CHECK(nz.scalar_type() == at::kInt && nz.dim() == 2 && nz.size(1) == 3, "sparse_sdd: nz int32 [nnz,3]");
+  const int64_t nnz = nz.size(0);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  Tensor C = at::empty({A.size(0), nnz, blk, blk}, A.options());
+  dsa::launch_sparse_sdd(A.data_ptr(), B.data_ptr(), C.data_ptr(), nz.data_ptr<int>(), (int)nnz, (int)A.size(0),
+                         (int)A.size(1), (int)A.size(2), (int)B.size(2), (int)A.size(3), (int)blk, (float)alpha,
+                         dcode(A), cur_stream());
+  return C;
+}
+
+// dsd: S [Z,nnz,blk,blk] with CSR (rowptr [H*nbr+1], cols [nnz]); Dt [Z,H,N,Kd] -> C [Z,H,nbr*blk,N]
+Tensor sparse_dsd(Tensor S, Tensor rowptr, Tensor cols, Tensor Dt, int64_t H, int64_t nbr, int64_t blk) {
+  check_dev(S, "S"); check_dev(Dt, "Dt"); check_dev(rowptr, "rowptr"); check_dev(cols, "cols");
+  TORCH_CHECK(S.dim() == 4 && S.size(2) == blk && S.size(3) == blk && S.scalar_type() == Dt.scalar_type() &&
+              Dt.dim() == 4 && Dt.size(0) == S.size(0) && Dt.size(1) == H, "sparse_dsd: shapes");
+  TORCH_CHECK(Dt.size(2) % 16 == 0 && Dt.size(3) % blk == 0 && blk % 16 == 0, "sparse_dsd: N % 16, K % block");
+  TORCH_CHECK(rowptr.scalar_type() == at::kInt && rowptr.numel() == H * nbr + 1 && cols.scalar_type() == at::kInt &&
+              cols.numel() == S.size(1), "sparse_dsd: CSR");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
+  Tensor C = at::empty({S.size(0), H, nbr * blk, Dt.size(2)}, S.options());
+  dsa::launch_sparse_dsd(S.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(), Dt.data_ptr(), C.data_ptr(),
+                         (int)S.size(1), (int)S.size(0), (int)H, (int)nbr, (int)Dt.size(2), (int)Dt.size(3), (int)blk,
+                         dcode(S), cur_stream());
+  return C;
+}
+
+// in-place softmax over the non-zero blocks of each row
+void sparse_softmax_fwd(Tensor x, Tensor rowptr, Tensor cols, int64_t H, int64_t nbr, double scale, OptT rpe,
+                        OptT kpm, OptT attn, bool kpm_mul, bool attn_mul) {
+  check_dev(x, "x");
+  const int64_t blk = x.size(2), S = nbr * blk;
+  int64_t rsz = 0, rsh = 0, rsr = 0, ksz = 0, asr = 0;
+  if (rpe.has_value()) {
+    TORCH_CHECK(rpe->dim() == 4 && rpe->size(2) == S && rpe->size(3) == S && rpe->stride(3) == 1 &&
+                rpe->scalar_type() == x.scalar_type(), "sparse softmax: rpe [Z|1,H|1,S,S]");
+    rsz = rpe->size(0) == 1 ? 0 : rpe->stride(0);
+    rsh = rpe->size(1) == 1 ? 0 : rpe->stride(1);
+    rsr = rpe->stride(2);
+  }
+  if (kpm.has_value()) {
+    TORCH_CHECK(kpm->dim() == 2 && kpm->size(1) == S && kpm->stride(1) == 1 && kpm->scalar_type() == x.scalar_type(),
+                "sparse softmax: key padding mask [Z,S]");
+    ksz = kpm->size(0) == 1 ? 0 : kpm->stride(0);
+  }
+  if (attn.has_value()) {
+    TORCH_CHECK(attn->dim() == 2 && attn->size(0) == S && attn->size(1) == S && attn->stride(1) == 1 &&
+                attn->scalar_type() == x.scalar_type(), "sparse softmax: attn mask [S,S]");
+    asr = attn->stride(0);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  dsa::launch_sparse_softmax_fwd(x.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(), (int)x.size(1),
+                                 (int)x.size(0), (int)H, (int)nbr, (int)blk,
+                                 rpe.has_value() ? rpe->data_ptr() : nullptr, rsz, rsh, rsr,
+                                 kpm.has_value() ? kpm->data_ptr() : nullptr, ksz,
+                                 attn.has_value() ? attn->data_ptr() : nullptr, asr, kpm_mul ? 1 : 0,
+                                 attn_mul ? 1 : 0, (float)scale, dcode(x), cur_stream());
+}
+
+void sparse_softmax_bwd(Tensor y, Tensor dy, Tensor rowptr, int64_t H, int64_t nbr, double scale) {
+  check_dev(y, "y"); check_dev(dy, "dy");
+  TORCH_CHECK(y.sizes() == dy.sizes() && y.scalar_type() == dy.scalar_type(), "sparse softmax bwd: shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
+  dsa::launch_sparse_softmax_bwd(y.data_ptr(), dy.data_ptr(), rowptr.data_ptr<int>(), (int)y.size(1), (int)y.size(0),
+                                 (int)H, (int)nbr, (int)y.size(2), (float)scale, dcode(y), cur_stream());
+}
+
 // Fused softmax cross-entropy. logits [R, V] 16-bit, labels [R] int64 (<0 = ignored)
 // -> (per-row loss fp32 [R], lse fp32 [R])
 std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels) {
@@ -415,6 +490,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("onebit_worker_compress", &onebit_worker_compress);
   m.def("onebit_server_compress", &onebit_server_compress);
   m.def("onebit_unpack", &onebit_unpack);
+  m.def("sparse_sdd", &sparse_sdd);
+  m.def("sparse_dsd", &sparse_dsd);
+  m.def("sparse_softmax_fwd", &sparse_softmax_fwd);
+  m.def("sparse_softmax_bwd", &sparse_softmax_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);

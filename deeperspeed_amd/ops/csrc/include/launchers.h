@@ -77,6 +77,18 @@ void launch_onebit_server(const uint8_t* signs, const float* scales, int P, int6
 void launch_onebit_unpack(const uint8_t* signs, const float* scales, int P, int64_t nbytes_per, float* out,
                           hipStream_t s);
 
+// sparse_attn.hip: block-sparse attention (LUTs from ops/sparse_attention)
+void launch_sparse_sdd(const void* A, const void* B, void* C, const int* nz, int nnz, int Z, int H, int Mr, int Nr,
+                       int K, int blk, float alpha, int dt, hipStream_t s);
+void launch_sparse_dsd(const void* S, const int* rowptr, const int* cols, const void* Dt, void* C, int nnz, int Z,
+                       int H, int nbr, int N, int Kd, int blk, int dt, hipStream_t s);
+void launch_sparse_softmax_fwd(void* x, const int* rowptr, const int* cols, int nnz, int Z, int H, int nbr, int blk,
+                               const void* rpe, int64_t rpe_sz, int64_t rpe_sh, int64_t rpe_sr, const void* kpm,
+                               int64_t kpm_sz, const void* attn, int64_t attn_sr, int kpm_mul, int attn_mul,
+                               float scale, int dt, hipStream_t s);
+void launch_sparse_softmax_bwd(const void* y, void* dy, const int* rowptr, int nnz, int Z, int H, int nbr, int blk,
+                               float scale, int dt, hipStream_t s);
+
 // flash_attn.hip: q,k,v,o [BH, S, D] (D in 64/96/128), lse/delta [BH, S] fp32
 bool flash_supported(int D);
 void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,

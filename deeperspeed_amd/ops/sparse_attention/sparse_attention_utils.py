@@ -1,0 +1,97 @@
+"""Helpers to adopt block-sparse attention in existing (HuggingFace BERT/RoBERTa) models
+(reference parity: deepspeed/ops/sparse_attention/sparse_attention_utils.py:12-225)."""
+
+import torch
+import torch.nn.functional as F
+
+from .bert_sparse_self_attention import BertSparseSelfAttention
+from .sparsity_config import SparsityConfig
+
+
+class SparseAttentionUtils:
+    @staticmethod
+    def extend_position_embedding(model, max_position):
+        """Tile the learned position embeddings up to `max_position` (bert / roberta)."""
+        if hasattr(model, "bert"):
+            emb = model.bert.embeddings.position_embeddings
+            orig = emb.weight.size(0)
+            assert max_position > orig
+            mult = max(1, max_position // orig)
+            emb.weight.data = emb.weight.repeat(mult, 1)
+        elif hasattr(model, "roberta"):
+            emb = model.roberta.embeddings.position_embeddings
+            orig, dim = emb.weight.shape
+            orig -= 2  # roberta keeps 2 offset positions
+            mult = max(1, max_position // orig)
+            assert max_position > orig
+            max_position += 2
+            ext = emb.weight.new_empty(max_position, dim)
+            k = 2
+            for _ in range(mult):
+                ext[k:k + orig] = emb.weight[2:]
+                k += orig
+            emb.weight.data = ext
+        else:
+            raise ValueError('Please extend "extend_position_embedding" function to support your model type. '
+                             'It currently only supports "bert" & "roberta"!')
+        model.config.max_position_embeddings = max_position
+        print(f"Extended position embeddings to {orig * mult}")
+        return model
+
+    @staticmethod
+    def update_tokenizer_model_max_length(tokenizer, max_position):
+        tokenizer.model_max_length = max_position
+        tokenizer.init_kwargs["model_max_length"] = max_position
+        print(f"updated tokenizer model max imum length to {max_position}")
+        return tokenizer
+
+    @staticmethod
+    def replace_model_self_attention_with_sparse_self_attention(model, max_position,
+                                                                 sparsity_config=SparsityConfig(num_heads=4)):
+        if hasattr(model, "bert"):
+            model.config.max_position_embeddings = max_position
+            SparseAttentionUtils.replace_self_attention_layer_with_sparse_self_attention_layer(
+                model.config, model.bert.encoder.layer, sparsity_config)
+        elif hasattr(model, "roberta"):
+            model.config.max_position_embeddings = max_position + 2
+            SparseAttentionUtils.replace_self_attention_layer_with_sparse_self_attention_layer(
+                model.config, model.roberta.encoder.layer, sparsity_config)
+        else:
+            raise ValueError('Please extend "update_model_self_attention_to_sparse_self_attention" function to '
+                             'support your model type. It currently only supports "bert" & "roberta"!')
+        return model
+
+    @staticmethod
+    def replace_self_attention_layer_with_sparse_self_attention_layer(config, layers,
+                                                                       sparsity_config=SparsityConfig(num_heads=4)):
+        for layer in layers:
+            old = layer.attention.self
+            new = BertSparseSelfAttention(config, sparsity_config)
+            new.query, new.key, new.value = old.query, old.key, old.value
+            layer.attention.self = new
+        return layers
+
+    @staticmethod
+    def pad_to_block_size(block_size, input_ids, attention_mask, token_type_ids, position_ids, inputs_embeds,
+                          pad_token_id, model_embeddings):
+        """Pad the sequence dimension to a multiple of `block_size`; returns
+        (pad_len, input_ids, attention_mask, token_type_ids, position_ids, inputs_embeds)."""
+        batch_size, seq_len = input_ids.shape if input_ids is not None else inputs_embeds.shape[:-1]
+        pad_len = (block_size - seq_len % block_size) % block_size
+        if pad_len > 0:
+            if inputs_embeds is not None:
+                pad_ids = inputs_embeds.new_full((batch_size, pad_len), pad_token_id, dtype=torch.long)
+                inputs_embeds = torch.cat([inputs_embeds, model_embeddings(pad_ids)], dim=-2)
+            if input_ids is not None:
+                input_ids = F.pad(input_ids, (0, pad_len), value=pad_token_id)
+            if position_ids is not None:
+                position_ids = F.pad(position_ids, (0, pad_len), value=pad_token_id)
+            attention_mask = F.pad(attention_mask, (0, pad_len), value=False)
+            token_type_ids = F.pad(token_type_ids, (0, pad_len), value=0)
+        return pad_len, input_ids, attention_mask, token_type_ids, position_ids, inputs_embeds
+
+    @staticmethod
+    def unpad_sequence_output(pad_len, sequence_output):
+        if pad_len > 0:
+            sequence_output = sequence_output[:, :-pad_len]
+        return sequence_output

@@ -277,3 +277,76 @@ def test_onebit_kernels_match_cpu_reference():
     out_c = native.onebit_unpack(signs, scales, torch.empty(n))
     out_g = native.onebit_unpack(signs.to(_dev()), scales.to(_dev()), torch.empty(n, device=_dev()))
     assert torch.equal(out_g.cpu(), out_c)
+
+
+def _sp_layout(H, nb, seed):
+    g = torch.Generator().manual_seed(seed)
+    lay = (torch.rand(H, nb, nb, generator=g) < 0.4).long()
+    lay[:, torch.arange(nb), torch.arange(nb)] = 1
+    return lay
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("blk", [16, 32, 64])
+@pytest.mark.parametrize("mode,ta,tb", [("sdd", False, True), ("sdd", True, False), ("dsd", False, False),
+                                        ("dsd", True, False), ("dds", False, False), ("dds", False, True)])
+def test_block_sparse_matmul_hip_vs_cpu(dtype, blk, mode, ta, tb):
+    import deeperspeed_amd.ops.sparse_attention as sa
+    torch.manual_seed(0)
+    H, nb, Z, D = 3, 6, 2, 64
+    S = nb * blk
+    lay = _sp_layout(H, nb, blk)
+    nnz = int(lay.sum())
+    mm = sa.MatMul(lay, blk, mode, trans_a=ta, trans_b=tb)
+    if mode == "sdd":
+        a = torch.randn(Z, H, *((D, S) if ta else (S, D)))
+        b = torch.randn(Z, H, *((S, D) if tb else (D, S)))
+    elif mode == "dsd":
+        a = torch.randn(Z, nnz, blk, blk) * 0.2
+        b = torch.randn(Z, H, *((D, S) if tb else (S, D)))
+    else:
+        a = torch.randn(Z, H, *((S, D) if ta else (D, S)))
+        b = torch.randn(Z, nnz, blk, blk) * 0.2
+    a, b = a.to(dtype), b.to(dtype)
+    ref = mm(a.float(), b.float())
+    ag, bg = a.to(_dev()).requires_grad_(True), b.to(_dev()).requires_grad_(True)
+    out = mm(ag, bg)
+    tol = 5e-2 if dtype == torch.bfloat16 else 1e-2
+    torch.testing.assert_close(out.float().cpu(), ref, atol=tol * 4, rtol=tol)
+    g = torch.randn_like(ref)
+    ga, gb = torch.autograd.grad(out, (ag, bg), g.to(dtype).to(_dev()))
+    ar, br = a.float().requires_grad_(True), b.float().requires_grad_(True)
+    ra, rb = torch.autograd.grad(mm(ar, br), (ar, br), g.to(dtype).float())
+    torch.testing.assert_close(ga.float().cpu(), ra, atol=tol * 8, rtol=tol)
+    torch.testing.assert_close(gb.float().cpu(), rb, atol=tol * 8, rtol=tol)
+
+
+@pytest.mark.parametrize("blk", [16, 64])
+def test_block_sparse_softmax_and_attention_hip(blk):
+    import deeperspeed_amd.ops.sparse_attention as sa
+    torch.manual_seed(0)
+    H, nb, Z = 2, 4, 2
+    S = nb * blk
+    lay = _sp_layout(H, nb, 7)
+    x = torch.randn(Z, int(lay.sum()), blk, blk).to(torch.bfloat16)
+    rpe = torch.randn(1, H, S, S).to(torch.bfloat16)
+    kpm = (torch.rand(Z, S) > 0.2).to(torch.bfloat16)
+    kpm[:, 0] = 1
+    sm = sa.Softmax(lay, blk)
+    ref = sm(x.float(), scale=0.5, rpe=rpe.float(), key_padding_mask=kpm.float(), key_padding_mask_mode="mul")
+    xg = x.to(_dev()).requires_grad_(True)
+    y = sm(xg, scale=0.5, rpe=rpe.to(_dev()), key_padding_mask=kpm.to(_dev()), key_padding_mask_mode="mul")
+    torch.testing.assert_close(y.float().cpu(), ref, atol=2e-2, rtol=2e-2)
+    g = torch.randn_like(ref).to(torch.bfloat16)
+    (gx,) = torch.autograd.grad(y, xg, g.to(_dev()))
+    xr = x.float().requires_grad_(True)
+    (rx,) = torch.autograd.grad(sm(xr, scale=0.5, rpe=rpe.float(), key_padding_mask=kpm.float(),
+                                   key_padding_mask_mode="mul"), xr, g.float())
+    torch.testing.assert_close(gx.float().cpu(), rx, atol=3e-2, rtol=3e-2)
+    # full module on a Fixed layout, bf16 HIP vs fp32 CPU
+    cfg = sa.FixedSparsityConfig(num_heads=4, block=blk, num_local_blocks=2)
+    att = sa.SparseSelfAttention(cfg, max_seq_length=S * 2)
+    q, k, v = (torch.randn(2, 4, S * 2, 64) for _ in range(3))
+    ref = att(q, k, v)
+    out = att(*(t.to(torch.bfloat16).to(_dev()) for t in (q, k, v)))
+    torch.testing.assert_close(out.float().cpu(), ref, atol=5e-2, rtol=5e-2)

@@ -1,0 +1,175 @@
+"""Block-sparse attention (reference tests/unit/test_sparse_attention.py): layouts identical to
+the reference's pure-Python configs, MatMul sdd/dsd/dds (all transpositions) and Softmax (scale,
+rpe, masks) vs dense PyTorch, gradients, and SparseSelfAttention == dense attention on a dense
+layout.  CPU here; the HIP kernels are compared against these in test_kernels_gpu.py."""
+
+import importlib.util
+import os
+import random
+
+import pytest
+import torch
+
+import deeperspeed_amd.ops.sparse_attention as sa
+
+REF = "/root/reference/deepspeed/ops/sparse_attention/sparsity_config.py"
+
+
+def _ref_module():
+    if not os.path.exists(REF):
+        pytest.skip("reference sources not mounted")
+    spec = importlib.util.spec_from_file_location("ref_sparsity_config", REF)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)  # plain torch + random, no native code
+    return mod
+
+
+CASES = [
+    ("DenseSparsityConfig", dict(num_heads=2, block=16)),
+    ("FixedSparsityConfig", dict(num_heads=4, block=16, num_local_blocks=4, num_global_blocks=1)),
+    ("FixedSparsityConfig", dict(num_heads=4, block=16, num_local_blocks=4, num_global_blocks=2,
+                                 attention="unidirectional")),
+    ("FixedSparsityConfig", dict(num_heads=4, block=16, different_layout_per_head=True, num_local_blocks=4,
+                                 num_global_blocks=1, horizontal_global_attention=True,
+                                 num_different_global_patterns=4)),
+    ("VariableSparsityConfig", dict(num_heads=2, block=16, num_random_blocks=2, local_window_blocks=[2, 3],
+                                    global_block_indices=[0, 5])),
+    ("VariableSparsityConfig", dict(num_heads=2, block=16, local_window_blocks=[4], global_block_indices=[1],
+                                    global_block_end_indices=[3], attention="unidirectional")),
+    ("BigBirdSparsityConfig", dict(num_heads=2, block=16, num_random_blocks=2, num_sliding_window_blocks=3)),
+    ("BigBirdSparsityConfig", dict(num_heads=2, block=16, attention="unidirectional")),
+    ("BSLongformerSparsityConfig", dict(num_heads=2, block=16, num_sliding_window_blocks=5,
+                                        global_block_indices=[0, 4], global_block_end_indices=[2, 6])),
+    ("BSLongformerSparsityConfig", dict(num_heads=2, block=16, attention="unidirectional")),
+    ("LocalSlidingWindowSparsityConfig", dict(num_heads=2, block=16, num_sliding_window_blocks=3)),
+]
+
+
+@pytest.mark.parametrize("name,kw", CASES)
+@pytest.mark.parametrize("seq", [256, 336])
+def test_layouts_match_reference(name, kw, seq):
+    ref = _ref_module()
+    random.seed(1234)
+    a = getattr(ref, name)(**kw).make_layout(seq)
+    random.seed(1234)
+    b = getattr(sa, name)(**kw).make_layout(seq)
+    assert torch.equal(a, b)
+
+
+def _layout(H=2, nb=6, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    lay = (torch.rand(H, nb, nb, generator=g) < 0.5).long()
+    lay[:, torch.arange(nb), torch.arange(nb)] = 1  # every row has a block
+    return lay
+
+
+def _mask(lay, blk):
+    return lay.repeat_interleave(blk, 1).repeat_interleave(blk, 2).bool()
+
+
+def _to_sparse(dense, lay, blk):
+    nz = lay.nonzero()
+    Z, H, S, _ = dense.shape
+    v = dense.view(Z, H, S // blk, blk, S // blk, blk).permute(0, 1, 2, 4, 3, 5)
+    return v[:, nz[:, 0], nz[:, 1], nz[:, 2]]
+
+
+def _to_dense(sp, lay, blk):
+    nz = lay.nonzero()
+    H, nb, _ = lay.shape
+    Z = sp.shape[0]
+    out = torch.zeros(Z, H, nb, nb, blk, blk, dtype=sp.dtype)
+    out[:, nz[:, 0], nz[:, 1], nz[:, 2]] = sp
+    return out.permute(0, 1, 2, 4, 3, 5).reshape(Z, H, nb * blk, nb * blk)
+
+
+@pytest.mark.parametrize("mode", ["sdd", "dsd", "dds"])
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+def test_matmul_matches_dense(mode, ta, tb):
+    torch.manual_seed(0)
+    blk, H, nb, Z, D = 16, 2, 5, 2, 24
+    S = nb * blk
+    lay = _layout(H, nb)
+    mm = sa.MatMul(lay, blk, mode, trans_a=ta, trans_b=tb)
+    mask = _mask(lay, blk)
+    if mode == "sdd":
+        a = torch.randn(Z, H, *((D, S) if ta else (S, D)), requires_grad=True)
+        b = torch.randn(Z, H, *((S, D) if tb else (D, S)), requires_grad=True)
+        out = mm(a, b)
+        ae = a.transpose(-1, -2) if ta else a
+        be = b.transpose(-1, -2) if tb else b
+        ref = _to_sparse(ae @ be, lay, blk)
+    elif mode == "dsd":
+        sp = torch.randn(Z, int(lay.sum()), blk, blk, requires_grad=True)
+        b = torch.randn(Z, H, *((D, S) if tb else (S, D)), requires_grad=True)
+        a = sp
+        out = mm(sp, b)
+        dense = _to_dense(sp, lay, blk)
+        ref = (dense.transpose(-1, -2) if ta else dense) @ (b.transpose(-1, -2) if tb else b)
+    else:
+        a = torch.randn(Z, H, *((S, D) if ta else (D, S)), requires_grad=True)
+        sp = torch.randn(Z, int(lay.sum()), blk, blk, requires_grad=True)
+        b = sp
+        out = mm(a, sp)
+        dense = _to_dense(sp, lay, blk)
+        ref = (a.transpose(-1, -2) if ta else a) @ (dense.transpose(-1, -2) if tb else dense)
+    torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
+    g = torch.randn_like(out)
+    ga, gb = torch.autograd.grad(out, (a, b), g)
+    ra, rb = torch.autograd.grad(ref, (a, b), g)
+    torch.testing.assert_close(ga, ra, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(gb, rb, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("kpm_mode,attn_mode", [("add", "add"), ("mul", "mul")])
+def test_softmax_matches_dense(kpm_mode, attn_mode):
+    torch.manual_seed(0)
+    blk, H, nb, Z = 16, 2, 4, 2
+    S = nb * blk
+    lay = _layout(H, nb, seed=3)
+    x = torch.randn(Z, int(lay.sum()), blk, blk, requires_grad=True)
+    rpe = torch.randn(1, H, S, S)
+    kpm = (torch.rand(Z, S) > 0.2).float() if kpm_mode == "mul" else torch.randn(Z, S)
+    attn = (torch.rand(S, S) > 0.3).float() if attn_mode == "mul" else torch.randn(S, S)
+    attn[:, 0] = 1.0
+    kpm[:, 0] = 1.0
+    y = sa.Softmax(lay, blk)(x, scale=0.3, rpe=rpe, key_padding_mask=kpm, attn_mask=attn,
+                             key_padding_mask_mode=kpm_mode, attn_mask_mode=attn_mode)
+    dense = _to_dense(x, lay, blk) * 0.3 + rpe
+    km = torch.where(kpm == 0, float("-inf"), 0.0) if kpm_mode == "mul" else kpm
+    am = torch.where(attn == 0, float("-inf"), 0.0) if attn_mode == "mul" else attn
+    dense = dense + km[:, None, None, :] + am
+    dense = dense.masked_fill(~_mask(lay, blk), float("-inf"))
+    ref = _to_sparse(torch.softmax(dense, -1).nan_to_num(0.0), lay, blk)
+    torch.testing.assert_close(y, ref, atol=1e-5, rtol=1e-5)
+    g = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(y, x, g)
+    (rx,) = torch.autograd.grad(ref, x, g)
+    torch.testing.assert_close(gx, rx, atol=1e-5, rtol=1e-4)
+
+
+def test_sparse_self_attention_dense_layout_equals_attention():
+    torch.manual_seed(0)
+    cfg = sa.DenseSparsityConfig(num_heads=2, block=16)
+    attn = sa.SparseSelfAttention(cfg, max_seq_length=64)
+    q, k, v = (torch.randn(2, 2, 64, 32) for _ in range(3))
+    out = attn(q, k, v)
+    ref = torch.softmax(q @ k.transpose(-1, -2) / 32 ** 0.5, -1) @ v
+    torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
+
+
+def test_bert_sparse_self_attention_and_utils():
+    from types import SimpleNamespace
+    torch.manual_seed(0)
+    cfg = SimpleNamespace(hidden_size=64, num_attention_heads=4)
+    layer = sa.BertSparseSelfAttention(cfg, sa.FixedSparsityConfig(num_heads=4, block=16))
+    x = torch.randn(2, 48, 64)
+    mask = torch.ones(2, 48)
+    y = layer(x, mask)
+    assert y.shape == (2, 48, 64)
+    ids = torch.ones(2, 40, dtype=torch.long)
+    pad, ids2, am, tt, pos, emb = sa.SparseAttentionUtils.pad_to_block_size(
+        16, ids, torch.ones(2, 40), torch.zeros(2, 40, dtype=torch.long), None, None, 0, None)
+    assert pad == 8 and ids2.shape == (2, 48) and am.shape == (2, 48) and bool(am[0, -1] == 0)
+    assert sa.SparseAttentionUtils.unpad_sequence_output(pad, torch.zeros(2, 48, 4)).shape == (2, 40, 4)
