@@ -26,7 +26,7 @@ class SparseLayout:
             layout = layout.unsqueeze(0)
         self.layout, self.block = layout, int(block)
         self.H, self.nbr, self.nbc = layout.shape
-        nz = layout.nonzero()
+        nz = layout.nonzero().contiguous()
         self.nnz = nz.shape[0]
         self.nz = nz.to(torch.int32)
         self.rowptr = torch.cat([torch.zeros(1, dtype=torch.int64), layout.sum(-1).reshape(-1).cumsum(0)]).to(torch.int32)
@@ -34,7 +34,7 @@ class SparseLayout:
         idx = torch.full(layout.shape, -1, dtype=torch.int64)
         idx[nz[:, 0], nz[:, 1], nz[:, 2]] = torch.arange(self.nnz)
         lt = layout.transpose(1, 2)
-        nzt = lt.nonzero()
+        nzt = lt.nonzero().contiguous()
         self.perm_t = idx[nzt[:, 0], nzt[:, 2], nzt[:, 1]]  # transposed order -> original index
         self.rowptr_t = torch.cat([torch.zeros(1, dtype=torch.int64), lt.sum(-1).reshape(-1).cumsum(0)]).to(torch.int32)
         self.cols_t = nzt[:, 2].to(torch.int32)
@@ -44,7 +44,7 @@ class SparseLayout:
     def dev(self, device):
         key = str(device)
         if key not in self._dev:
-            t = lambda x: x.to(device)  # noqa: E731
+            t = lambda x: x.contiguous().to(device)  # noqa: E731 (nonzero() results are column-major)
             self._dev[key] = dict(nz=t(self.nz), rowptr=t(self.rowptr), cols=t(self.cols), perm_t=t(self.perm_t),
                                   rowptr_t=t(self.rowptr_t), cols_t=t(self.cols_t), nz_t=t(self.nz_t))
         return self._dev[key]
