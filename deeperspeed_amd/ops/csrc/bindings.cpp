@@ -280,14 +280,16 @@ Tensor softmax_fwd(Tensor x, OptT mask, double scale, bool causal, int64_t heads
               dsa::softmax_max_cols());
   if (mask.has_value()) {
     check_dev(*mask, "mask");
-    TORCH_CHECK(mask->scalar_type() == x.scalar_type() && mask->size(-1) == C && mask->size(-2) == Sq,
-                "softmax: mask must be [B,1,Sq,C] in the score dtype");
-    TORCH_CHECK(mask->numel() / (Sq * C) * heads * Sq * C == x.numel(), "softmax: mask batch mismatch");
+    TORCH_CHECK(mask->scalar_type() == x.scalar_type() && mask->size(-1) == C &&
+                (mask->size(-2) == Sq || mask->size(-2) == 1) && mask->is_contiguous(),
+                "softmax: mask must be [B,1,Sq|1,C] in the score dtype");
+    TORCH_CHECK(mask->numel() / (mask->size(-2) * C) * heads * Sq * C == x.numel(), "softmax: mask batch mismatch");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Tensor y = at::empty_like(x);
   dsa::launch_softmax_fwd(x.data_ptr(), y.data_ptr(), mask.has_value() ? mask->data_ptr() : nullptr, R, (int)C,
-                          (int)Sq, (int)heads, (float)scale, causal ? 1 : 0, dcode(x), cur_stream());
+                          (int)Sq, (int)heads, (float)scale, causal ? 1 : 0,
+                          mask.has_value() ? (int)mask->size(-2) : 1, dcode(x), cur_stream());
   return y;
 }
 
@@ -419,6 +421,42 @@ void sparse_softmax_bwd(Tensor y, Tensor dy, Tensor rowptr, int64_t H, int64_t n
                                  (int)H, (int)nbr, (int)y.size(2), (float)scale, dcode(y), cur_stream());
 }
 
+// ----------------------------------------------------------------------------- dropout
+std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, int64_t offset) {
+  check_dev(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty_like(x);
+  Tensor mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  dsa::launch_dropout_fwd(x.data_ptr(), y.data_ptr(), mask.data_ptr<uint8_t>(), x.numel(), (float)p, (uint64_t)seed,
+                          (uint64_t)offset, dcode(x), cur_stream());
+  return {y, mask};
+}
+
+// y = res + dropout(x + bias); x/res [rows, C], bias [C]
+std::vector<Tensor> bias_dropout_residual(Tensor x, Tensor bias, Tensor res, double p, int64_t seed, int64_t offset) {
+  check_dev(x, "x"); check_dev(bias, "bias"); check_dev(res, "res");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(bias.numel() == C && res.sizes() == x.sizes() && x.scalar_type() == res.scalar_type() &&
+              bias.scalar_type() == x.scalar_type(), "bias_dropout_residual: shapes/dtypes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty_like(x);
+  Tensor mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  dsa::launch_bias_dropout_residual(x.data_ptr(), bias.data_ptr(), res.data_ptr(), y.data_ptr(),
+                                    mask.data_ptr<uint8_t>(), x.numel() / C, (int)C, (float)p, (uint64_t)seed,
+                                    (uint64_t)offset, dcode(x), cur_stream());
+  return {y, mask};
+}
+
+Tensor dropout_bwd(Tensor dy, Tensor mask, double p) {
+  check_dev(dy, "dy"); check_dev(mask, "mask");
+  TORCH_CHECK(mask.numel() == dy.numel() && mask.scalar_type() == at::kByte, "dropout_bwd: mask");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  Tensor dx = at::empty_like(dy);
+  dsa::launch_dropout_bwd(dy.data_ptr(), mask.data_ptr<uint8_t>(), dx.data_ptr(), dy.numel(), (float)p, dcode(dy),
+                          cur_stream());
+  return dx;
+}
+
 // Fused softmax cross-entropy. logits [R, V] 16-bit, labels [R] int64 (<0 = ignored)
 // -> (per-row loss fp32 [R], lse fp32 [R])
 std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels) {
@@ -494,6 +532,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sparse_dsd", &sparse_dsd);
   m.def("sparse_softmax_fwd", &sparse_softmax_fwd);
   m.def("sparse_softmax_bwd", &sparse_softmax_bwd);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("bias_dropout_residual", &bias_dropout_residual);
+  m.def("dropout_bwd", &dropout_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
   m.def("flash_attn_fwd", &flash_attn_fwd);

@@ -59,7 +59,7 @@ void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, voi
                              int S, int NH, int HD, int ROT, float qscale, int dt, hipStream_t s);
 int softmax_max_cols();
 void launch_softmax_fwd(const void* x, void* y, const void* mask, int64_t R, int C, int Sq, int heads, float scale,
-                        int causal, int dt, hipStream_t s);
+                        int causal, int mask_rows, int dt, hipStream_t s);
 void launch_softmax_bwd(const void* dy, const void* y, void* dx, int64_t R, int C, float scale, int dt,
                         hipStream_t s);
 
@@ -88,6 +88,13 @@ void launch_sparse_softmax_fwd(void* x, const int* rowptr, const int* cols, int 
                                float scale, int dt, hipStream_t s);
 void launch_sparse_softmax_bwd(const void* y, void* dy, const int* rowptr, int nnz, int Z, int H, int nbr, int blk,
                                float scale, int dt, hipStream_t s);
+
+// dropout.hip: counter-based Philox dropout (seed, offset) with uint8 keep-masks
+void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed, uint64_t offset,
+                        int dt, hipStream_t s);
+void launch_bias_dropout_residual(const void* x, const void* bias, const void* res, void* y, uint8_t* mask,
+                                  int64_t rows, int C, float p, uint64_t seed, uint64_t offset, int dt, hipStream_t s);
+void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, int dt, hipStream_t s);
 
 // flash_attn.hip: q,k,v,o [BH, S, D] (D in 64/96/128), lse/delta [BH, S] fp32
 bool flash_supported(int D);

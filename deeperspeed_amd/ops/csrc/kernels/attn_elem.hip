@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(256) rotary_split_bwd_kernel(const T* __restri
 template <typename T, int NV>
 __global__ void __launch_bounds__(256) softmax_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           const T* __restrict__ mask, int64_t R, int C, int Sq,
-                                                          int heads, float scale, int causal) {
+                                                          int heads, float scale, int causal, int mask_rows) {
   __shared__ float red[32];
   constexpr int VN = 8;
   const int64_t r = blockIdx.x;
@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) softmax_fwd_kernel(const T* __restrict__ 
   const T* mr = nullptr;
   if (mask) {
     const int64_t bidx = r / ((int64_t)heads * Sq);
-    mr = mask + (bidx * Sq + q) * (int64_t)C;
+    mr = mask + (bidx * mask_rows + (mask_rows == 1 ? 0 : q)) * (int64_t)C;  // [B,1,1|Sq,C]
   }
   float vals[NV][VN];
   float mx = -INFINITY;
@@ -253,12 +253,12 @@ void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, voi
 int softmax_max_cols() { return 16 * 256 * 8; }
 
 void launch_softmax_fwd(const void* x, void* y, const void* mask, int64_t R, int C, int Sq, int heads, float scale,
-                        int causal, int dt, hipStream_t s) {
+                        int causal, int mask_rows, int dt, hipStream_t s) {
   if (R <= 0) return;
   const int nv = (C / 8 + 255) / 256;
   DSA_DISPATCH_16(dt, T, DSA_DISPATCH_SNV(nv, NV,
     hipLaunchKernelGGL((softmax_fwd_kernel<T, NV>), dim3((unsigned)R), dim3(256), 0, s, (const T*)x, (T*)y,
-                       (const T*)mask, R, C, Sq, heads, scale, causal)));
+                       (const T*)mask, R, C, Sq, heads, scale, causal, mask_rows)));
 }
 
 void launch_softmax_bwd(const void* dy, const void* y, void* dx, int64_t R, int C, float scale, int dt,

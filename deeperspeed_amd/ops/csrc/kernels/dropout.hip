@@ -1,0 +1,117 @@
+// Dropout with a counter-based Philox4x32-10 generator (replaces csrc/transformer/dropout_kernels.cu,
+// which draws from curand with a (seed, offset) context).  Element i uses counter
+// (offset + i/4) under key = seed, so any launch is reproducible from (seed, offset) alone:
+// activation-checkpoint recomputation and the backward pass never need stored RNG state.
+// Masks are stored as uint8 (1 = keep); kept values are scaled by 1/(1-p).
+#include "../include/dsa_common.h"
+#include "../include/launchers.h"
+
+namespace dsa {
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    const uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += W0;
+    key.y += W1;
+  }
+  return ctr;
+}
+
+// 4 uniform draws in [0, 1) for element group g (elements 4g..4g+3)
+__device__ __forceinline__ void uniform4(uint64_t seed, uint64_t offset, uint64_t g, float (&u)[4]) {
+  const uint64_t c = offset + g;
+  const uint4 r = philox4x32_10(make_uint4((uint32_t)c, (uint32_t)(c >> 32), 0u, 0u),
+                                make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  const float k = 2.3283064365386963e-10f;  // 2^-32
+  u[0] = r.x * k; u[1] = r.y * k; u[2] = r.z * k; u[3] = r.w * k;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                          uint8_t* __restrict__ mask, int64_t n, float p,
+                                                          uint64_t seed, uint64_t offset) {
+  const float scale = 1.f / (1.f - p);
+  const int64_t ngroups = (n + 3) / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += stride) {
+    float u[4];
+    uniform4(seed, offset, g, u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = 4 * g + k;
+      if (i < n) {
+        const bool keep = u[k] >= p;
+        mask[i] = keep;
+        Conv<T>::store(y, i, keep ? Conv<T>::load(x, i) * scale : 0.f);
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bias_dropout_residual_kernel(const T* __restrict__ x, const T* __restrict__ b,
+                                                                    const T* __restrict__ res, T* __restrict__ y,
+                                                                    uint8_t* __restrict__ mask, int64_t n, int C,
+                                                                    float p, uint64_t seed, uint64_t offset) {
+  const float scale = 1.f / (1.f - p);
+  const int64_t ngroups = (n + 3) / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups; g += stride) {
+    float u[4];
+    uniform4(seed, offset, g, u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = 4 * g + k;
+      if (i < n) {
+        const bool keep = u[k] >= p;
+        mask[i] = keep;
+        const float v = Conv<T>::load(x, i) + Conv<T>::load(b, (int)(i % C));
+        Conv<T>::store(y, i, Conv<T>::load(res, i) + (keep ? v * scale : 0.f));
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                          T* __restrict__ dx, int64_t n, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    Conv<T>::store(dx, i, mask[i] ? Conv<T>::load(dy, i) * scale : 0.f);
+}
+
+static inline unsigned dgrid(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed, uint64_t offset,
+                        int dt, hipStream_t s) {
+  if (n <= 0) return;
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((dropout_fwd_kernel<T>), dim3(dgrid((n + 3) / 4)), dim3(256), 0, s, (const T*)x, (T*)y, mask,
+                       n, p, seed, offset));
+}
+
+void launch_bias_dropout_residual(const void* x, const void* bias, const void* res, void* y, uint8_t* mask,
+                                  int64_t rows, int C, float p, uint64_t seed, uint64_t offset, int dt,
+                                  hipStream_t s) {
+  const int64_t n = rows * C;
+  if (n <= 0) return;
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((bias_dropout_residual_kernel<T>), dim3(dgrid((n + 3) / 4)), dim3(256), 0, s, (const T*)x,
+                       (const T*)bias, (const T*)res, (T*)y, mask, n, C, p, seed, offset));
+}
+
+void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, int dt, hipStream_t s) {
+  if (n <= 0) return;
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((dropout_bwd_kernel<T>), dim3(dgrid(n)), dim3(256), 0, s, (const T*)dy, mask, (T*)dx, n,
+                       1.f / (1.f - p)));
+}
+
+}  // namespace dsa

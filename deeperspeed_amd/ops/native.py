@@ -378,3 +378,69 @@ def onebit_unpack(signs: torch.Tensor, scales: torch.Tensor, out: torch.Tensor):
     P = scales.numel()
     out.copy_((_unpackbits(signs.view(P, -1)) * scales.view(P, 1)).view(-1))
     return out
+
+
+# --------------------------------------------------------------------------- dropout (Philox)
+def _draw_seed(generator=None):
+    """64-bit seed from a CPU generator (the default one is saved/restored by activation
+    checkpointing, so recomputation replays the same masks)."""
+    return int(torch.randint(0, 2 ** 62, (1,), generator=generator).item())
+
+
+class _DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        if x.is_cuda:
+            y, mask = hip_ops().dropout_fwd(x.contiguous(), p, seed, 0)
+        else:
+            g = torch.Generator().manual_seed(seed)
+            mask = (torch.rand(x.shape, generator=g) >= p).to(torch.uint8)
+            y = (x.float() * mask / (1 - p)).to(x.dtype)
+        ctx.save_for_backward(mask)
+        ctx.p = p
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (mask,) = ctx.saved_tensors
+        if dy.is_cuda:
+            return hip_ops().dropout_bwd(dy.contiguous(), mask, ctx.p), None, None
+        return (dy.float() * mask / (1 - ctx.p)).to(dy.dtype), None, None
+
+
+def dropout(x, p, training=True, generator=None):
+    if not training or p <= 0:
+        return x
+    return _DropoutFn.apply(x, float(p), _draw_seed(generator))
+
+
+class _BiasDropoutResidualFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, res, p, seed):
+        if x.is_cuda:
+            y, mask = hip_ops().bias_dropout_residual(x.contiguous(), bias, res.contiguous(), p, seed, 0)
+        else:
+            g = torch.Generator().manual_seed(seed)
+            mask = (torch.rand(x.shape, generator=g) >= p).to(torch.uint8)
+            y = (res.float() + (x.float() + bias.float()) * mask / (1 - p)).to(x.dtype)
+        ctx.save_for_backward(mask)
+        ctx.p = p
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (mask,) = ctx.saved_tensors
+        if dy.is_cuda:
+            dx = hip_ops().dropout_bwd(dy.contiguous(), mask, ctx.p)
+            db = colsum(dx.reshape(-1, dx.shape[-1]))
+        else:
+            dx = (dy.float() * mask / (1 - ctx.p)).to(dy.dtype)
+            db = dx.reshape(-1, dx.shape[-1]).float().sum(0).to(dy.dtype)
+        return dx, db, dy, None, None
+
+
+def bias_dropout_residual(x, bias, residual, p, training=True, generator=None):
+    """residual + dropout(x + bias), one fused pass (reference dropout_kernels.cu ForwardWithBias)."""
+    if not training or p <= 0:
+        return residual + (x + bias)
+    return _BiasDropoutResidualFn.apply(x, bias, residual, float(p), _draw_seed(generator))

@@ -1,0 +1,192 @@
+"""DeepSpeed BERT transformer layer for MI355X.
+
+Reference parity: deepspeed/ops/transformer/transformer.py:39-614 (`DeepSpeedTransformerConfig`,
+`DeepSpeedTransformerFunction`, `DeepSpeedTransformerLayer`) and the layer dataflow of
+csrc/transformer/ds_transformer_cuda.cpp:147-292 (same parameter names and shapes, pre-LN and
+post-LN, tanh GeLU, additive attention mask [B,1,1,S], attention-prob and hidden dropout).
+
+Built from the framework's HIP kernels + hipBLASLt GEMMs instead of one monolithic C++
+layer: fused LayerNorm, bias+tanh-GeLU, row softmax with a broadcast additive mask, Philox
+dropout, and bias+dropout+residual fusion, composed under autograd (so ZeRO-3 hooks,
+activation checkpointing and mixed precision work unchanged).  Memory flags:
+`gelu_checkpoint` is inherent (the GeLU kernel keeps only its input), `attn_dropout_checkpoint`
+stores the 1-byte dropout mask instead of the dropped probabilities, `normalize_invertible` and
+`stochastic_mode` are accepted for config compatibility (deterministic kernels either way).
+"""
+
+import json
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import native
+from ..attention import masked_softmax
+
+
+class TransformerConfig:
+    def __init__(self, batch_size, hidden_size, intermediate_size, heads, attn_dropout_ratio, hidden_dropout_ratio,
+                 num_hidden_layers, initializer_range):
+        self.layer_id = -1
+        self.batch_size = batch_size
+        self.hidden_size = hidden_size
+        self.intermediate_size = intermediate_size
+        self.heads = heads
+        self.attn_dropout_ratio = attn_dropout_ratio
+        self.hidden_dropout_ratio = hidden_dropout_ratio
+        self.num_hidden_layers = num_hidden_layers
+        self.initializer_range = initializer_range
+
+
+class DeepSpeedTransformerConfig(TransformerConfig):
+    def __init__(self, batch_size=-1, hidden_size=-1, intermediate_size=-1, heads=-1, attn_dropout_ratio=-1,
+                 hidden_dropout_ratio=-1, num_hidden_layers=-1, initializer_range=-1, layer_norm_eps=1e-12,
+                 local_rank=-1, seed=-1, fp16=False, pre_layer_norm=True, normalize_invertible=False,
+                 gelu_checkpoint=False, adjust_init_range=True, attn_dropout_checkpoint=False, stochastic_mode=False,
+                 huggingface=False, training=True, bf16=False):
+        super().__init__(batch_size, hidden_size, intermediate_size if intermediate_size > 0 else 4 * hidden_size,
+                         heads, attn_dropout_ratio, hidden_dropout_ratio, num_hidden_layers, initializer_range)
+        self.fp16 = fp16
+        self.bf16 = bf16
+        self.pre_layer_norm = pre_layer_norm
+        self.local_rank = local_rank
+        self.seed = seed
+        self.normalize_invertible = normalize_invertible
+        self.gelu_checkpoint = gelu_checkpoint
+        self.adjust_init_range = adjust_init_range
+        self.test_gemm = False
+        self.layer_norm_eps = layer_norm_eps
+        self.training = training
+        self.is_grad_enabled = True
+        self.attn_dropout_checkpoint = attn_dropout_checkpoint
+        self.stochastic_mode = stochastic_mode
+        self.huggingface = huggingface
+
+    @classmethod
+    def from_dict(cls, json_object):
+        config = DeepSpeedTransformerConfig()
+        for k, v in json_object.items():
+            config.__dict__[k] = v
+        return config
+
+    @classmethod
+    def from_json_file(cls, json_file):
+        with open(json_file, "r", encoding="utf-16") as reader:
+            return cls.from_dict(json.loads(reader.read()))
+
+
+def _gelu_tanh(x, b):
+    return native.bias_gelu(x, b, approximate=True)
+
+
+class DeepSpeedTransformerFunction:
+    """Functional form of the layer (reference exposes an autograd.Function with this name)."""
+
+    @staticmethod
+    def apply(input, input_mask, layer, grads, layer_id, attn_qkvw, attn_qkvb, attn_ow, attn_ob, attn_nw, attn_nb,
+              inter_w, inter_b, output_w, output_b, norm_w, norm_b, config):
+        cfg = config
+        training = cfg.training
+        B, S, Hd = input.shape
+        nh = cfg.heads
+        hd = Hd // nh
+        gen = layer._generator if layer is not None else None
+        eps = cfg.layer_norm_eps
+        x = input
+        inp = native.layer_norm(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
+        qkv = F.linear(inp, attn_qkvw, attn_qkvb)
+        q, k, v = qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, hd]
+        scores = torch.matmul(q, k.transpose(-1, -2))
+        mask = None
+        if input_mask is not None:
+            mask = input_mask.to(scores.dtype)
+            if mask.dim() == 2:
+                mask = mask[:, None, None, :]
+            mask = mask.reshape(B, 1, -1, S).contiguous()
+        probs = masked_softmax(scores, mask, 1.0 / math.sqrt(hd), False, nh)
+        probs = native.dropout(probs, cfg.attn_dropout_ratio, training, gen)
+        ctx = torch.matmul(probs, v).transpose(1, 2).reshape(B, S, Hd)
+        attn_out = F.linear(ctx, attn_ow)
+        add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen)
+        ff1_inp = native.layer_norm(add_res, attn_nw, attn_nb, eps)
+        inter = _gelu_tanh(F.linear(ff1_inp, inter_w), inter_b)
+        out = F.linear(inter, output_w)
+        if cfg.pre_layer_norm:
+            out = native.bias_dropout_residual(out, output_b, add_res, cfg.hidden_dropout_ratio, training, gen)
+        else:
+            out = native.bias_dropout_residual(out, output_b, ff1_inp, cfg.hidden_dropout_ratio, training, gen)
+            out = native.layer_norm(out, norm_w, norm_b, eps)
+        if grads is not None:  # reference test hook: collect gradients of the intermediates
+            for t in (out, add_res, ff1_inp):
+                if t.requires_grad:
+                    t.register_hook(lambda g, _l=grads: _l.append(g))
+        return out
+
+
+class DeepSpeedTransformerLayer(nn.Module):
+    layer_id = 0
+
+    def __init__(self, config, initial_weights=None, initial_biases=None):
+        super().__init__()
+        self.config = config
+        self.config.layer_id = DeepSpeedTransformerLayer.layer_id
+        DeepSpeedTransformerLayer.layer_id += 1
+        if self.config.local_rank >= 0 and torch.cuda.is_available():
+            torch.cuda.set_device(self.config.local_rank)
+        H, I = config.hidden_size, config.intermediate_size
+        self._generator = None
+        if config.seed >= 0:
+            self._generator = torch.Generator().manual_seed(config.seed + config.layer_id)
+        if initial_weights is None and initial_biases is None:
+            self.attn_qkvw = nn.Parameter(torch.empty(3 * H, H))
+            self.attn_qkvb = nn.Parameter(torch.empty(3 * H))
+            self.attn_ow = nn.Parameter(torch.empty(H, H))
+            self.attn_ob = nn.Parameter(torch.empty(H))
+            self.attn_nw = nn.Parameter(torch.empty(H))
+            self.attn_nb = nn.Parameter(torch.empty(H))
+            self.inter_w = nn.Parameter(torch.empty(I, H))
+            self.inter_b = nn.Parameter(torch.empty(I))
+            self.output_w = nn.Parameter(torch.empty(H, I))
+            self.output_b = nn.Parameter(torch.empty(H))
+            self.norm_w = nn.Parameter(torch.empty(H))
+            self.norm_b = nn.Parameter(torch.empty(H))
+            self.init_transformer_weights(config.adjust_init_range)
+        else:  # unit-test path: weights supplied as [q, k, v, o, attn_norm, inter, output, norm]
+            self.attn_qkvw = nn.Parameter(torch.cat([w.detach() for w in initial_weights[:3]], 0).clone())
+            self.attn_qkvb = nn.Parameter(torch.zeros(3 * H))
+            self.attn_ow, self.attn_ob = initial_weights[3], initial_biases[3]
+            self.attn_nw, self.attn_nb = initial_weights[4], initial_biases[4]
+            self.inter_w, self.inter_b = initial_weights[5], initial_biases[5]
+            self.output_w, self.output_b = initial_weights[6], initial_biases[6]
+            self.norm_w, self.norm_b = initial_weights[7], initial_biases[7]
+        dtype = torch.float16 if config.fp16 else (torch.bfloat16 if getattr(config, "bf16", False) else None)
+        if dtype is not None:
+            self.to(dtype)
+
+    @torch.no_grad()
+    def init_transformer_weights(self, adjust_init_range=False):
+        std = self.config.initializer_range
+        out_std = std / math.sqrt(2.0 * self.config.num_hidden_layers) if adjust_init_range else std
+        self.attn_qkvw.normal_(0.0, std)
+        self.attn_qkvb.zero_()
+        self.attn_ow.normal_(0.0, out_std)
+        self.attn_ob.zero_()
+        self.attn_nw.fill_(1.0)
+        self.attn_nb.zero_()
+        self.inter_w.normal_(0.0, std)
+        self.inter_b.zero_()
+        self.output_w.normal_(0.0, out_std)
+        self.output_b.zero_()
+        self.norm_w.fill_(1.0)
+        self.norm_b.zero_()
+
+    def forward(self, hidden_states, attention_mask=None, head_mask=None, encoder_hidden_states=None,
+                encoder_attention_mask=None, output_attentions=False, grads=None):
+        self.config.training = self.training
+        self.config.is_grad_enabled = torch.is_grad_enabled()
+        out = DeepSpeedTransformerFunction.apply(hidden_states, attention_mask, self, grads, self.config.layer_id,
+                                                 self.attn_qkvw, self.attn_qkvb, self.attn_ow, self.attn_ob,
+                                                 self.attn_nw, self.attn_nb, self.inter_w, self.inter_b,
+                                                 self.output_w, self.output_b, self.norm_w, self.norm_b, self.config)
+        return (out,) if self.config.huggingface else out

@@ -350,3 +350,47 @@ def test_block_sparse_softmax_and_attention_hip(blk):
     ref = att(q, k, v)
     out = att(*(t.to(torch.bfloat16).to(_dev()) for t in (q, k, v)))
     torch.testing.assert_close(out.float().cpu(), ref, atol=5e-2, rtol=5e-2)
+
+
+def test_dropout_kernels():
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(0)
+    x = torch.randn(4096, 1024, device=_dev(), dtype=torch.bfloat16)
+    y, mask = native.hip_ops().dropout_fwd(x, 0.25, 1234, 0)
+    keep = mask.float().mean().item()
+    assert abs(keep - 0.75) < 0.01
+    torch.testing.assert_close(y.float(), (x.float() * mask / 0.75), atol=1e-2, rtol=1e-2)
+    y2, mask2 = native.hip_ops().dropout_fwd(x, 0.25, 1234, 0)
+    assert torch.equal(mask, mask2)  # counter-based: reproducible from (seed, offset)
+    _, mask3 = native.hip_ops().dropout_fwd(x, 0.25, 1235, 0)
+    assert not torch.equal(mask, mask3)
+    b = torch.randn(1024, device=_dev(), dtype=torch.bfloat16)
+    r = torch.randn_like(x)
+    z, m = native.hip_ops().bias_dropout_residual(x, b, r, 0.1, 99, 0)
+    torch.testing.assert_close(z.float(), r.float() + (x.float() + b.float()) * m / 0.9, atol=3e-2, rtol=2e-2)
+    dx = native.hip_ops().dropout_bwd(y, mask, 0.25)
+    torch.testing.assert_close(dx.float(), y.float() * mask / 0.75, atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("preln", [True, False])
+def test_deepspeed_transformer_layer_gpu_vs_cpu(preln):
+    import copy
+    from deeperspeed_amd.ops.transformer import DeepSpeedTransformerConfig, DeepSpeedTransformerLayer
+    torch.manual_seed(0)
+    cfg = DeepSpeedTransformerConfig(batch_size=4, hidden_size=256, heads=4, attn_dropout_ratio=0.1,
+                                     hidden_dropout_ratio=0.1, num_hidden_layers=4, initializer_range=0.02,
+                                     pre_layer_norm=preln, training=False)
+    cpu = DeepSpeedTransformerLayer(cfg).eval()
+    gpu = copy.deepcopy(cpu).to(_dev()).to(torch.bfloat16)
+    x = torch.randn(4, 128, 256)
+    m = torch.zeros(4, 1, 1, 128)
+    m[1, ..., -20:] = -10000.0
+    ref = cpu(x, m)
+    xg = x.to(_dev()).to(torch.bfloat16).requires_grad_(True)
+    out = gpu(xg, m.to(_dev()).to(torch.bfloat16))
+    torch.testing.assert_close(out.float().cpu(), ref, atol=6e-2, rtol=6e-2)
+    out.float().sum().backward()
+    assert torch.isfinite(xg.grad).all() and gpu.attn_qkvw.grad is not None
+    gpu.train()
+    y1 = gpu(xg.detach(), m.to(_dev()).to(torch.bfloat16))
+    assert torch.isfinite(y1).all()

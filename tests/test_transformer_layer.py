@@ -1,0 +1,102 @@
+"""DeepSpeedTransformerLayer (reference tests/unit/test_cuda_forward.py / test_cuda_backward.py):
+equivalence with a HuggingFace BertLayer (post-LN) and a hand-written pre-LN layer, forward and
+backward, module_inject round trip, dropout reproducibility."""
+
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from deeperspeed_amd.module_inject import replace_transformer_layer, revert_transformer_layer
+from deeperspeed_amd.ops.transformer import DeepSpeedTransformerConfig, DeepSpeedTransformerLayer
+
+transformers = pytest.importorskip("transformers")
+from transformers.models.bert.modeling_bert import BertConfig, BertLayer  # noqa: E402
+
+
+def _hf_config():
+    return BertConfig(hidden_size=64, num_attention_heads=4, intermediate_size=256, hidden_act="gelu_new",
+                      hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.1, num_hidden_layers=2,
+                      initializer_range=0.02, layer_norm_eps=1e-12, attn_implementation="eager")
+
+
+class _Wrap(nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        self.layer = BertLayer(cfg)
+
+
+def _mask(B, S):
+    m = torch.ones(B, S)
+    m[0, -5:] = 0
+    return ((1.0 - m) * -10000.0)[:, None, None, :]
+
+
+def test_postln_matches_huggingface_fwd_bwd():
+    torch.manual_seed(0)
+    cfg = _hf_config()
+    hf = _Wrap(cfg).eval()
+    ds = replace_transformer_layer(BertLayer, copy.deepcopy(hf), micro_batch_size=2, bert_config=cfg, seed=1,
+                                   preln=False, fp16=False, training=False).eval()
+    assert isinstance(ds.layer, DeepSpeedTransformerLayer)
+    x = torch.randn(2, 24, 64, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    m = _mask(2, 24)
+    r = hf.layer(x, attention_mask=m)
+    ref = r[0] if isinstance(r, tuple) else r
+    out = ds.layer(x2, m)
+    torch.testing.assert_close(out, ref, atol=1e-4, rtol=1e-4)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    out.backward(g)
+    torch.testing.assert_close(x2.grad, x.grad, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(ds.layer.inter_w.grad, hf.layer.intermediate.dense.weight.grad, atol=1e-4, rtol=1e-3)
+    q, k, v = ds.layer.attn_qkvw.grad.split(64, 0)
+    torch.testing.assert_close(k, hf.layer.attention.self.key.weight.grad, atol=1e-4, rtol=1e-3)
+    back = revert_transformer_layer(BertLayer, ds, cfg, preln=False)
+    for (n1, p1), (n2, p2) in zip(hf.named_parameters(), back.named_parameters()):
+        assert n1 == n2 and torch.equal(p1, p2), n1
+
+
+def _preln_reference(layer, x, m):
+    c = layer.config
+    H, nh = c.hidden_size, c.heads
+    B, S, _ = x.shape
+    h = F.layer_norm(x, (H,), layer.norm_w, layer.norm_b, c.layer_norm_eps)
+    q, k, v = F.linear(h, layer.attn_qkvw, layer.attn_qkvb).view(B, S, 3, nh, H // nh).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(q @ k.transpose(-1, -2) / (H // nh) ** 0.5 + m, -1)
+    ctx = (p @ v).transpose(1, 2).reshape(B, S, H)
+    a = x + F.linear(ctx, layer.attn_ow, layer.attn_ob)
+    h2 = F.layer_norm(a, (H,), layer.attn_nw, layer.attn_nb, c.layer_norm_eps)
+    f = F.gelu(F.linear(h2, layer.inter_w, layer.inter_b), approximate="tanh")
+    return a + F.linear(f, layer.output_w, layer.output_b)
+
+
+def test_preln_matches_reference_math():
+    torch.manual_seed(0)
+    cfg = DeepSpeedTransformerConfig(batch_size=2, hidden_size=64, heads=4, attn_dropout_ratio=0.1,
+                                     hidden_dropout_ratio=0.1, num_hidden_layers=2, initializer_range=0.02,
+                                     pre_layer_norm=True, training=False)
+    layer = DeepSpeedTransformerLayer(cfg).eval()
+    with torch.no_grad():
+        for p in layer.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    x = torch.randn(2, 16, 64)
+    m = _mask(2, 16)
+    torch.testing.assert_close(layer(x, m), _preln_reference(layer, x, m), atol=1e-4, rtol=1e-4)
+
+
+def test_dropout_training_reproducible():
+    cfg = DeepSpeedTransformerConfig(batch_size=2, hidden_size=64, heads=4, attn_dropout_ratio=0.2,
+                                     hidden_dropout_ratio=0.2, num_hidden_layers=2, initializer_range=0.02, seed=7)
+    torch.manual_seed(0)
+    a = DeepSpeedTransformerLayer(cfg).train()
+    b = copy.deepcopy(a)
+    b._generator = torch.Generator().manual_seed(cfg.seed + a.config.layer_id)
+    a._generator = torch.Generator().manual_seed(cfg.seed + a.config.layer_id)
+    x = torch.randn(2, 16, 64)
+    ya, yb = a(x), b(x)
+    assert torch.equal(ya, yb)
+    assert not torch.allclose(ya, a.eval()(x))
