@@ -592,6 +592,16 @@ class DeepSpeedEngine(Module):
                                       timers=self.timers if self.wall_clock_breakdown() else None,
                                       verbose=self.global_rank == 0)
 
+    def _offload_with_aio(self, off):
+        """The NVMe swapper needs the `aio` section next to the offload settings."""
+        if off is None:
+            return None
+        off = dict(off)
+        aio = getattr(self._config, "aio_config", None)
+        if aio:
+            off["aio"] = dict(aio)
+        return off
+
     def _configure_zero_optimizer(self, optimizer):
         stage = self.zero_optimization_stage()
         zc = self._config.zero_config
@@ -601,7 +611,8 @@ class DeepSpeedEngine(Module):
                       dynamic_loss_args=self._dynamic_args(), fp32_reduce=self.allreduce_always_fp32(),
                       gradient_predivide_factor=self.gradient_predivide_factor(),
                       gradient_accumulation_steps=self.gradient_accumulation_steps(),
-                      offload_optimizer=zc.offload_optimizer, compact_master=bool(zc.compact_master),
+                      offload_optimizer=self._offload_with_aio(zc.offload_optimizer),
+                      compact_master=bool(zc.compact_master),
                       timers=self.timers if self.wall_clock_breakdown() else None, verbose=self.global_rank == 0)
         if stage in (ZERO_OPTIMIZATION_OPTIMIZER_STATES, ZERO_OPTIMIZATION_GRADIENTS):
             from .zero.stage_1_and_2 import DeepSpeedZeroOptimizer

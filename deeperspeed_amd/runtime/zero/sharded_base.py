@@ -75,6 +75,8 @@ class ShardedOptimizerBase:
         self.overflow = False
         self.offload = offload_optimizer
         self.offload_states = (offload_optimizer or {}).get("states", "all") if offload_optimizer else None
+        self.nvme = bool(offload_optimizer) and offload_optimizer.get("device") == "nvme"
+        self._swapper = None
         self.fused = isinstance(init_optimizer, FusedAdam) or getattr(init_optimizer, "supports_flat_update", False)
         self.groups: List[FlatGroup] = []
         self.is_gradient_accumulation_boundary = True
@@ -131,6 +133,9 @@ class ShardedOptimizerBase:
             for g in self.groups:
                 if g.dtype != torch.bfloat16 or g.shard_param is None:
                     raise ValueError("compact_master needs bf16 model parameters")
+        if self.nvme:
+            self._setup_nvme(init_shard_fn)
+            return
         for g in self.groups:
             if self.compact_master:
                 # the bf16 shard already equals the master's high half: residual starts at 0
@@ -160,6 +165,58 @@ class ShardedOptimizerBase:
                 else:
                     st["exp_avg"] = torch.zeros(g.shard_numel, dtype=torch.float32, device=self.device)
                     st["exp_avg_sq"] = torch.zeros(g.shard_numel, dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------------ NVMe (ZeRO-Infinity)
+    def _setup_nvme(self, init_shard_fn):
+        """fp32 master + Adam moments live on NVMe, one file per (group, bucket, tensor); the
+        step streams them through pinned buffers (runtime/swap_tensor/optimizer_utils.py)."""
+        import os
+        from ..swap_tensor.optimizer_utils import PipelinedOptimizerSwapper, log_swap_config
+        path = self.offload.get("nvme_path") or "/tmp/deeperspeed_amd_nvme"
+        folder = os.path.join(path, f"zero_stage_{self._zero_stage()}", f"rank{self.dp_rank}_mp{self.mp_rank}")
+        aio = self.offload.get("aio") or {}
+        self._swapper = PipelinedOptimizerSwapper(folder, aio_config=aio)
+        log_swap_config(folder, aio)
+        for gi, g in enumerate(self.groups):
+            m = init_shard_fn(g).float()
+            for bi, b in enumerate(g.buckets):
+                lo, hi = b.shard_offset, b.shard_offset + b.chunk
+                self._swapper.register((gi, bi), {"master": m[lo:hi].detach().cpu()})
+            del m
+            g.master = torch.zeros(0, dtype=torch.float32)  # placeholder key for the inner optimizer
+        for gi, pg in enumerate(self.optimizer.param_groups):
+            pg["params"] = [g.master for g in self.groups if g.group_index == gi]
+        self.optimizer.state.clear()
+        for g in self.groups:
+            self.optimizer.state[g.master] = {"step": 0, "exp_avg": torch.zeros(0), "exp_avg_sq": torch.zeros(0)}
+
+    def _nvme_read_group(self, gi, name) -> torch.Tensor:
+        g = self.groups[gi]
+        return torch.cat([self._swapper.read((gi, bi), name) for bi in range(len(g.buckets))]) if g.buckets \
+            else torch.zeros(0)
+
+    def _nvme_write_group(self, gi, name, value: torch.Tensor):
+        g = self.groups[gi]
+        value = value.reshape(-1).float().cpu()
+        for bi, b in enumerate(g.buckets):
+            self._swapper.write((gi, bi), name, value[b.shard_offset: b.shard_offset + b.chunk])
+
+    def _offload_nvme_step(self, grad_scale, grp_steps):
+        from ...ops.adam.cpu_adam import cpu_adam_update_flat
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", getattr(self.optimizer, "adamw_mode", True)))
+        keys = [(gi, bi) for gi, g in enumerate(self.groups) for bi in range(len(g.buckets))]
+
+        def update(key, t):
+            gi, bi = key
+            g = self.groups[gi]
+            b = g.buckets[bi]
+            lo, hi = b.shard_offset, b.shard_offset + b.chunk
+            grad_host = g.shard_grad[lo:hi].to("cpu", dtype=torch.float32, non_blocking=False)
+            cpu_adam_update_flat(t["master"], grad_host, t["exp_avg"], t["exp_avg_sq"], self._inner_group(g),
+                                 grp_steps[id(g)], grad_scale, adamw, out_device=self._bucket_out(g, b))
+            self._after_bucket_update(g, b)
+
+        self._swapper.update(keys, update)
 
     def _inner_group(self, g: FlatGroup):
         return self.optimizer.param_groups[g.group_index]
@@ -293,6 +350,8 @@ class ShardedOptimizerBase:
             st = self.optimizer.state[g.master]
             st["step"] = st.get("step", 0) + 1
             grp_steps[id(g)] = st["step"]
+        if self.nvme:
+            return self._offload_nvme_step(grad_scale, grp_steps)
         if self.offload_states == "master" and torch.cuda.is_available():
             return self._offload_master_step(grad_scale, grp_steps)
         return self._offload_all_step(grad_scale, grp_steps)
@@ -370,6 +429,12 @@ class ShardedOptimizerBase:
 
     def state_dict(self):
         base = self.optimizer.state_dict()
+        if self.nvme:  # moments live on NVMe: materialise them for the checkpoint
+            for gi in range(len(self.groups)):
+                st = base.get("state", {}).get(gi)
+                if st is not None:
+                    st["exp_avg"] = self._nvme_read_group(gi, "exp_avg")
+                    st["exp_avg_sq"] = self._nvme_read_group(gi, "exp_avg_sq")
         # move state tensors to cpu (checkpoint files are host tensors)
         for k, v in base.get("state", {}).items():
             for kk, vv in list(v.items()):
@@ -411,7 +476,10 @@ class ShardedOptimizerBase:
         else:
             masters, moments = self._elastic_merge(state_dict_list, key)
         if load_from_fp32_weights:
-            for g, m in zip(self.groups, masters):
+            for gi, (g, m) in enumerate(zip(self.groups, masters)):
+                if self.nvme:
+                    self._nvme_write_group(gi, "master", m)
+                    continue
                 if self.compact_master:
                     cm.encode_into(m, g.shard_param, g.master)
                 else:
@@ -458,7 +526,9 @@ class ShardedOptimizerBase:
                 continue
             st = self.optimizer.state[g.master]
             for k, v in s.items():
-                if torch.is_tensor(v) and k in st and torch.is_tensor(st[k]) and st[k].numel() == v.numel():
+                if self.nvme and torch.is_tensor(v) and k in ("exp_avg", "exp_avg_sq"):
+                    self._nvme_write_group(gi, k, v)
+                elif torch.is_tensor(v) and k in st and torch.is_tensor(st[k]) and st[k].numel() == v.numel():
                     st[k].copy_(v.to(st[k].device))
                 elif torch.is_tensor(v):
                     st[k] = v.to(g.master.device if not (self.offload and self.offload_states == "all")
@@ -468,6 +538,8 @@ class ShardedOptimizerBase:
 
     def master_fp32(self, g: FlatGroup) -> torch.Tensor:
         """This rank's fp32 master shard of group g as a host tensor (checkpoints, tests)."""
+        if self.nvme:
+            return self._nvme_read_group(self.groups.index(g), "master")
         if self.compact_master:
             return cm.decode_chunked(g.shard_param, g.master, torch.empty(g.shard_numel, dtype=torch.float32))
         return g.master.detach().cpu()
@@ -477,7 +549,11 @@ class ShardedOptimizerBase:
         for g in self.groups:
             for b in g.buckets:
                 out = self._bucket_out(g, b)
-                if self.compact_master:
+                if self.nvme:
+                    if out is not None:
+                        out.copy_(self._swapper.read((self.groups.index(g), g.buckets.index(b)), "master")
+                                  .to(out.device, out.dtype))
+                elif self.compact_master:
                     pass  # the bf16 shard is the master's high half already
                 elif out is not None and out.data_ptr() != g.master.data_ptr():
                     out.copy_(g.master[b.shard_offset: b.shard_offset + b.chunk].to(out.device))
