@@ -15,6 +15,8 @@
 // become A operands.  Workgroup = 4 waves = 64 rows (queries for fwd/dQ, keys for dK/dV).
 // Backward is FA2-style without atomics: one kernel owns dK/dV per key block, one owns dQ
 // per query block (both recompute P from the saved LSE).
+#include <cstdlib>
+
 #include "../include/dsa_common.h"
 #include "../include/launchers.h"
 
@@ -402,6 +404,439 @@ __global__ void __launch_bounds__(256) bwd_dq_kernel(const uint16_t* __restrict_
   }
 }
 
+// ======================================================================== forward v2
+// 32x32x16 MFMA, S^T = K Q^T formulation (one wave = 32 queries, WG = 128 queries):
+//  * Q^T is the B operand and stays in registers for the whole key loop;
+//  * S^T's C layout gives every lane one query (col) and 16 keys per tile, so the softmax
+//    max / sum are in-lane plus one xor-32 shuffle, and the rescale of O^T is per lane;
+//  * P^T is used as the B operand of O^T = V^T P^T straight from registers: the k (key)
+//    index of both operands follows the C-layout permutation {4h..4h+3, 8+4h..8+4h+3};
+//  * V^T fragments come from ds_read_b64_tr_b16 on the natural [key][d] V tile;
+//  * K/V tiles are double-buffered in LDS; the next tile's global loads are issued before
+//    the current tile's MFMAs and written to the other buffer afterwards (1 barrier/tile).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <typename T> struct Mfma32;
+template <> struct Mfma32<bf16_t> {
+  __device__ __forceinline__ static f32x16 run(s16x8 a, s16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
+};
+template <> struct Mfma32<f16_t> {
+  __device__ __forceinline__ static f32x16 run(s16x8 a, s16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  }
+};
+
+constexpr int BM2 = 128;
+constexpr int BN2 = 64;
+
+template <int D>
+__device__ __forceinline__ void tile_load(uint4 (&r)[D / 32], const uint16_t* __restrict__ g, int r0, int S) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int k = 0; k < D / 32; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    const int row = c / CH, ch = c - row * CH;
+    r[k] = (r0 + row < S) ? *reinterpret_cast<const uint4*>(g + (int64_t)(r0 + row) * D + ch * 8)
+                          : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void tile_store(uint16_t* lds, const uint4 (&r)[D / 32]) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int k = 0; k < D / 32; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    const int row = c / CH, ch = c - row * CH;
+    *reinterpret_cast<uint4*>(lds + row * (D + 8) + ch * 8) = r[k];
+  }
+}
+
+__device__ __forceinline__ s16x8 pack8(const float* v, int base) {
+  s16x8 out;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = (short)f32_to_bf16(v[base + j]);
+  return out;
+}
+__device__ __forceinline__ s16x8 pack8_h(const float* v, int base) {
+  s16x8 out;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = (short)f32_to_f16(v[base + j]);
+  return out;
+}
+
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                        const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
+                                                        float* __restrict__ LSE, int S, float scale) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int TS = BN2 * (D + 8);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  const int64_t bh = blockIdx.y;
+  const int qb = blockIdx.x * BM2;
+  const int myq = qb + 32 * w + c32;
+  const uint16_t* Qb = Q + bh * (int64_t)S * D;
+  const uint16_t* Kb = K + bh * (int64_t)S * D;
+  const uint16_t* Vb = V + bh * (int64_t)S * D;
+
+  s16x8 qf[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks)
+    qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Qb + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const float sl2 = scale * 1.4426950408889634f;
+
+  const int kend = CAUSAL ? min(S, qb + BM2) : S;
+  const int ntiles = (kend + BN2 - 1) / BN2;
+  uint4 kr[D / 32], vr[D / 32];
+  tile_load<D>(kr, Kb, 0, S);
+  tile_load<D>(vr, Vb, 0, S);
+  tile_store<D>(smem, kr);
+  tile_store<D>(smem + TS, vr);
+  __syncthreads();
+  for (int it = 0; it < ntiles; ++it) {
+    const int j0 = it * BN2;
+    const bool has_next = it + 1 < ntiles;
+    if (has_next) {
+      tile_load<D>(kr, Kb, j0 + BN2, S);
+      tile_load<D>(vr, Vb, j0 + BN2, S);
+    }
+    const uint16_t* Ks = smem + (it & 1) * 2 * TS;
+    const uint16_t* Vs = Ks + TS;
+    float sv[32];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks)
+        acc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), qf[ks], acc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[16 * t + r] = acc[r];
+    }
+    // keys of value index 16t+r: j0 + 32t + 8(r>>2) + 4h + (r&3); this lane's query is myq
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+        float x = sv[16 * t + r] * sl2;
+        if (key >= S || (CAUSAL && key > myq)) x = -INFINITY;
+        sv[16 * t + r] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const float p = (mn == -INFINITY) ? 0.f : exp2f(sv[i] - mn);
+      sv[i] = p;
+      ps += p;
+    }
+    ps += __shfl_xor(ps, 32, 64);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    // O^T += V^T P^T over the 64 keys (4 steps of 16)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const s16x8 pf = (sizeof(T) == 2 && __is_same(T, bf16_t)) ? pack8(sv, 8 * ks) : pack8_h(sv, 8 * ks);
+      const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const uint16_t* a0 = Vs + row1 * (D + 8) + 32 * dt + 16 * (g16 & 1) + 4 * pc;
+        const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * (D + 8)));
+        o[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, pf, o[dt]);
+      }
+    }
+    if (has_next) {
+      uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
+      tile_store<D>(nxt, kr);
+      tile_store<D>(nxt + TS, vr);
+    }
+    __syncthreads();
+  }
+  if (myq < S) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* orow = O + (bh * (int64_t)S + myq) * D;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        ushort4 v4;
+        v4.x = to16<T>(o[dt][4 * rb + 0] * inv);
+        v4.y = to16<T>(o[dt][4 * rb + 1] * inv);
+        v4.z = to16<T>(o[dt][4 * rb + 2] * inv);
+        v4.w = to16<T>(o[dt][4 * rb + 3] * inv);
+        *reinterpret_cast<ushort4*>(orow + 32 * dt + 8 * rb + 4 * h) = v4;
+      }
+    if (h == 0)
+      LSE[bh * (int64_t)S + myq] = (m == -INFINITY) ? -INFINITY : (m + log2f(l)) * 0.6931471805599453f;
+  }
+}
+
+// ======================================================================== backward v2
+// dK/dV: one wave = 32 keys (lane = key column of S = Q K^T); K, V are B operands held in
+// registers; per 64-query tile: S, dP (A = Q / dO rows from LDS), P, dS in registers (query
+// index per value from the C layout, LSE/Delta broadcast from LDS), then
+//   dV^T += dO^T P   (A = dO^T via tr reads, B = P from registers)
+//   dK^T += Q^T dS   (A = Q^T via tr reads,  B = dS from registers)
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(const uint16_t* __restrict__ Q,
+                                                             const uint16_t* __restrict__ K,
+                                                             const uint16_t* __restrict__ V,
+                                                             const uint16_t* __restrict__ dO,
+                                                             const float* __restrict__ LSE,
+                                                             const float* __restrict__ DELTA,
+                                                             uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
+                                                             int S, float scale) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int TS = BN2 * (D + 8);
+  float* stats = reinterpret_cast<float*>(smem + 4 * TS);  // [2 stages][LSE 64 | DELTA 64]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  const int64_t bh = blockIdx.y;
+  const int kb = blockIdx.x * BM2;
+  const int mykey = kb + 32 * w + c32;
+  const int64_t base = bh * (int64_t)S * D;
+  const float sl2 = scale * 1.4426950408889634f;
+
+  s16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) {
+    kf[ks] = mykey < S ? *reinterpret_cast<const s16x8*>(K + base + (int64_t)mykey * D + 16 * ks + 8 * h) : s16x8{};
+    vf[ks] = mykey < S ? *reinterpret_cast<const s16x8*>(V + base + (int64_t)mykey * D + 16 * ks + 8 * h) : s16x8{};
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+
+  const int qstart = CAUSAL ? kb : 0;
+  const int ntiles = qstart < S ? (S - qstart + BN2 - 1) / BN2 : 0;
+  uint4 qr[D / 32], orr[D / 32];
+  float st_l = 0.f, st_d = 0.f;
+  auto load_tile = [&](int i0) {
+    tile_load<D>(qr, Q + base, i0, S);
+    tile_load<D>(orr, dO + base, i0, S);
+    if (threadIdx.x < BN2) {
+      const int q = i0 + threadIdx.x;
+      st_l = q < S ? LSE[bh * (int64_t)S + q] * 1.4426950408889634f : 0.f;
+      st_d = q < S ? DELTA[bh * (int64_t)S + q] : 0.f;
+    }
+  };
+  auto store_tile = [&](int stage) {
+    uint16_t* b = smem + stage * 2 * TS;
+    tile_store<D>(b, qr);
+    tile_store<D>(b + TS, orr);
+    if (threadIdx.x < BN2) {
+      stats[stage * 2 * BN2 + threadIdx.x] = st_l;
+      stats[stage * 2 * BN2 + BN2 + threadIdx.x] = st_d;
+    }
+  };
+  if (ntiles > 0) {
+    load_tile(qstart);
+    store_tile(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < ntiles; ++it) {
+    const int i0 = qstart + it * BN2;
+    const bool has_next = it + 1 < ntiles;
+    if (has_next) load_tile(i0 + BN2);
+    const uint16_t* Qs = smem + (it & 1) * 2 * TS;
+    const uint16_t* Os = Qs + TS;
+    const float* lse_s = stats + (it & 1) * 2 * BN2;
+    const float* del_s = lse_s + BN2;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), kf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), vf[ks], pacc);
+      }
+      float pv[16], dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+        const int q = i0 + qi;
+        float p = exp2f(sacc[r] * sl2 - lse_s[qi]);
+        if (q >= S || mykey >= S || (CAUSAL && mykey > q)) p = 0.f;
+        pv[r] = p;
+        dsv[r] = p * (pacc[r] - del_s[qi]);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ks = 2 * t + kk;
+        const s16x8 pf = __is_same(T, bf16_t) ? pack8(pv, 8 * kk) : pack8_h(pv, 8 * kk);
+        const s16x8 sf = __is_same(T, bf16_t) ? pack8(dsv, 8 * kk) : pack8_h(dsv, 8 * kk);
+        const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
+          const s16x4 ox = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + row1 * (D + 8) + col));
+          const s16x4 oy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (row1 + 8) * (D + 8) + col));
+          dv[dt] = Mfma32<T>::run(s16x8{ox[0], ox[1], ox[2], ox[3], oy[0], oy[1], oy[2], oy[3]}, pf, dv[dt]);
+          const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + row1 * (D + 8) + col));
+          const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * (D + 8) + col));
+          dk[dt] = Mfma32<T>::run(s16x8{qx[0], qx[1], qx[2], qx[3], qy[0], qy[1], qy[2], qy[3]}, sf, dk[dt]);
+        }
+      }
+    }
+    if (has_next) store_tile((it + 1) & 1);
+    __syncthreads();
+  }
+  if (mykey < S) {
+    uint16_t* dkr = dK + base + (int64_t)mykey * D;
+    uint16_t* dvr = dV + base + (int64_t)mykey * D;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        ushort4 a4, b4;
+        a4.x = to16<T>(dk[dt][4 * rb + 0] * scale); a4.y = to16<T>(dk[dt][4 * rb + 1] * scale);
+        a4.z = to16<T>(dk[dt][4 * rb + 2] * scale); a4.w = to16<T>(dk[dt][4 * rb + 3] * scale);
+        b4.x = to16<T>(dv[dt][4 * rb + 0]); b4.y = to16<T>(dv[dt][4 * rb + 1]);
+        b4.z = to16<T>(dv[dt][4 * rb + 2]); b4.w = to16<T>(dv[dt][4 * rb + 3]);
+        *reinterpret_cast<ushort4*>(dkr + 32 * dt + 8 * rb + 4 * h) = a4;
+        *reinterpret_cast<ushort4*>(dvr + 32 * dt + 8 * rb + 4 * h) = b4;
+      }
+  }
+}
+
+// dQ: one wave = 32 queries (lane = query column of S^T = K Q^T); Q and dO are B operands in
+// registers; per 64-key tile: S^T, dP^T (A = K / V rows from LDS), dS^T in registers, then
+//   dQ^T += K^T dS^T   (A = K^T via tr reads, B = dS^T from registers)
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __restrict__ Q,
+                                                           const uint16_t* __restrict__ K,
+                                                           const uint16_t* __restrict__ V,
+                                                           const uint16_t* __restrict__ dO,
+                                                           const float* __restrict__ LSE,
+                                                           const float* __restrict__ DELTA, uint16_t* __restrict__ dQ,
+                                                           int S, float scale) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int TS = BN2 * (D + 8);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  const int64_t bh = blockIdx.y;
+  const int qb = blockIdx.x * BM2;
+  const int myq = qb + 32 * w + c32;
+  const int64_t base = bh * (int64_t)S * D;
+  const float sl2 = scale * 1.4426950408889634f;
+
+  s16x8 qf[D / 16], of[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) {
+    qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Q + base + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
+    of[ks] = myq < S ? *reinterpret_cast<const s16x8*>(dO + base + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
+  }
+  const float lse2 = myq < S ? LSE[bh * (int64_t)S + myq] * 1.4426950408889634f : 0.f;
+  const float dl = myq < S ? DELTA[bh * (int64_t)S + myq] : 0.f;
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+
+  const int kend = CAUSAL ? min(S, qb + BM2) : S;
+  const int ntiles = (kend + BN2 - 1) / BN2;
+  uint4 kr[D / 32], vr[D / 32];
+  tile_load<D>(kr, K + base, 0, S);
+  tile_load<D>(vr, V + base, 0, S);
+  tile_store<D>(smem, kr);
+  tile_store<D>(smem + TS, vr);
+  __syncthreads();
+  for (int it = 0; it < ntiles; ++it) {
+    const int j0 = it * BN2;
+    const bool has_next = it + 1 < ntiles;
+    if (has_next) {
+      tile_load<D>(kr, K + base, j0 + BN2, S);
+      tile_load<D>(vr, V + base, j0 + BN2, S);
+    }
+    const uint16_t* Ks = smem + (it & 1) * 2 * TS;
+    const uint16_t* Vs = Ks + TS;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        sacc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), qf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), of[ks], pacc);
+      }
+      float dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+        float p = exp2f(sacc[r] * sl2 - lse2);
+        if (key >= S || myq >= S || (CAUSAL && key > myq)) p = 0.f;
+        dsv[r] = p * (pacc[r] - dl);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ks = 2 * t + kk;
+        const s16x8 sf = __is_same(T, bf16_t) ? pack8(dsv, 8 * kk) : pack8_h(dsv, 8 * kk);
+        const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
+          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * (D + 8) + col));
+          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * (D + 8) + col));
+          dq[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, sf, dq[dt]);
+        }
+      }
+    }
+    if (has_next) {
+      uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
+      tile_store<D>(nxt, kr);
+      tile_store<D>(nxt + TS, vr);
+    }
+    __syncthreads();
+  }
+  if (myq < S) {
+    uint16_t* dqr = dQ + base + (int64_t)myq * D;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        ushort4 v4;
+        v4.x = to16<T>(dq[dt][4 * rb + 0] * scale); v4.y = to16<T>(dq[dt][4 * rb + 1] * scale);
+        v4.z = to16<T>(dq[dt][4 * rb + 2] * scale); v4.w = to16<T>(dq[dt][4 * rb + 3] * scale);
+        *reinterpret_cast<ushort4*>(dqr + 32 * dt + 8 * rb + 4 * h) = v4;
+      }
+  }
+}
+
+template <int D> constexpr int dkdv_v2_lds() { return 2 * 2 * BN2 * (D + 8) * 2 + 2 * 2 * BN2 * 4; }
+
+template <int D> constexpr int fwd_v2_lds() { return 2 * 2 * BN2 * (D + 8) * 2; }
+
 template <int D> constexpr int fwd_lds() { return (2 * BN * (D + 8) + 4 * 16 * (BN + 8)) * 2; }
 template <int D> constexpr int dkdv_lds() { return (2 * BN * (D + 8)) * 2 + 2 * BN * 4 + 4 * 2 * 16 * (BN + 8) * 2; }
 template <int D> constexpr int dq_lds() { return (2 * BN * (D + 8) + 4 * 16 * (BN + 8)) * 2; }
@@ -431,6 +866,14 @@ bool flash_supported(int D) { return D == 64 || D == 96 || D == 128; }
 
 void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                       bool causal, float scale, int dt, hipStream_t s) {
+  static const bool v1 = getenv("DSA_FLASH_FWD_V1") != nullptr;
+  if (!v1) {
+    dim3 grid2((S + fa::BM2 - 1) / fa::BM2, BH);
+    FA_DISPATCH(dt, D, causal,
+      hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC>), grid2, dim3(256), fa::fwd_v2_lds<DD>(), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale));
+    return;
+  }
   dim3 grid((S + fa::BM - 1) / fa::BM, BH);
   FA_DISPATCH(dt, D, causal,
     hipLaunchKernelGGL((fa::fwd_kernel<T, DD, CC>), grid, dim3(256), fa::fwd_lds<DD>(), s, (const uint16_t*)q,
@@ -441,15 +884,25 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
                       float* delta, void* dq, void* dk, void* dv, int BH, int S, int D, bool causal, float scale,
                       int dt, hipStream_t s) {
   const int64_t rows = (int64_t)BH * S;
+  static const bool v1 = getenv("DSA_FLASH_BWD_V1") != nullptr;
   FA_DISPATCH(dt, D, causal,
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const uint16_t*)dout, (const uint16_t*)o, delta, rows);
-    hipLaunchKernelGGL((fa::bwd_dkdv_kernel<T, DD, CC>), dim3((S + fa::BM - 1) / fa::BM, BH), dim3(256),
-                       fa::dkdv_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                       (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale);
-    hipLaunchKernelGGL((fa::bwd_dq_kernel<T, DD, CC>), dim3((S + fa::BM - 1) / fa::BM, BH), dim3(256),
-                       fa::dq_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                       (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale));
+    if (!v1) {
+      hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2, BH), dim3(256),
+                         fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale);
+      hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2, BH), dim3(256),
+                         fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale);
+    } else {
+      hipLaunchKernelGGL((fa::bwd_dkdv_kernel<T, DD, CC>), dim3((S + fa::BM - 1) / fa::BM, BH), dim3(256),
+                         fa::dkdv_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale);
+      hipLaunchKernelGGL((fa::bwd_dq_kernel<T, DD, CC>), dim3((S + fa::BM - 1) / fa::BM, BH), dim3(256),
+                         fa::dq_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale);
+    });
 }
 
 }  // namespace dsa
