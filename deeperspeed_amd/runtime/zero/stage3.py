@@ -112,7 +112,14 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self.persistence_threshold = int(param_persistence_threshold)
         self.unit_max_numel = int(unit_max_numel)
         self.offload_param = offload_param
-        self.single = self.dp_world == 1
+        # ZeRO-Infinity parameter offload: bf16 shards in pinned host memory ("cpu") or in a
+        # file-backed mapping on the NVMe path ("nvme"); every fetch stages the unit's chunk to
+        # HBM before the all-gather, the (offloaded) optimizer writes updated shards back.
+        self.param_offload = bool(offload_param) and offload_param.get("device") in ("cpu", "nvme")
+        if self.param_offload and self.offload is None:
+            raise ValueError("offload_param requires offload_optimizer (cpu or nvme) in ZeRO stage 3")
+        self.compute_device = self.device
+        self.single = self.dp_world == 1 and not self.param_offload
         self._pending = []
         self._fwd_trace: List[int] = []
         self._bwd_trace: List[int] = []
@@ -193,9 +200,10 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def _build_shards(self):
         """Create per-group bf16 shards from the (currently full) parameters, then free them."""
         r = self.dp_rank
-        for g in self.groups:
+        for gi, g in enumerate(self.groups):
             dev = g.params[0].device if g.params[0].is_cuda else self.device
-            g.shard_param = torch.zeros(g.shard_numel, dtype=g.dtype, device=dev)
+            self.compute_device = dev
+            g.shard_param = self._alloc_param_shard(gi, g, dev)
             for b in g.buckets:
                 for i, p in enumerate(b.params):
                     ov = b.chunk_overlap(r, i)
@@ -225,7 +233,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                         p.data = g.shard_param[off: off + b.numels[i]].view(p.ds_shape)
                         p.grad = g.shard_grad[off: off + b.numels[i]].view(p.ds_shape)
                     else:
-                        p.data = _empty_like(g.dtype, g.shard_param.device)
+                        p.data = _empty_like(g.dtype, self.compute_device)
             u.status = ZeroParamStatus.AVAILABLE if self.single else ZeroParamStatus.NOT_AVAILABLE
         if not self.single:
             for u in self._units:
@@ -234,6 +242,23 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                     self._wait(u)
         if torch.cuda.is_available():
             torch.cuda.empty_cache()
+
+    def _alloc_param_shard(self, gi, g, dev):
+        if not self.param_offload:
+            return torch.zeros(g.shard_numel, dtype=g.dtype, device=dev)
+        if self.offload_param.get("device") == "nvme":
+            import os
+            folder = os.path.join(self.offload_param.get("nvme_path") or "/tmp/deeperspeed_amd_nvme", "zero_stage_3",
+                                  f"params_rank{self.dp_rank}_mp{self.mp_rank}")
+            os.makedirs(folder, exist_ok=True)
+            path = os.path.join(folder, f"group{gi}.swp")
+            if os.path.exists(path):
+                os.remove(path)
+            t = torch.from_file(path, shared=True, size=max(1, g.shard_numel), dtype=g.dtype)[:g.shard_numel]
+            t.zero_()
+            return t
+        pin = bool(self.offload_param.get("pin_memory", True)) and torch.cuda.is_available()
+        return torch.zeros(g.shard_numel, dtype=g.dtype, pin_memory=pin)
 
     def _grad_dtype(self, g):
         if self.single:
@@ -248,8 +273,10 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             return
         u.works, u.fulls = [], []
         for g, b in u.buckets:
-            full = torch.empty(b.numel, dtype=g.dtype, device=g.shard_param.device)
+            full = torch.empty(b.numel, dtype=g.dtype, device=self.compute_device)
             chunk = g.shard_param[b.shard_offset: b.shard_offset + b.chunk]
+            if self.param_offload:
+                chunk = chunk.to(self.compute_device, non_blocking=chunk.is_pinned())
             if _dist_ready() and self.dp_world > 1:
                 u.works.append(dist.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True))
             else:
@@ -277,7 +304,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         if u.status == ZeroParamStatus.INFLIGHT:
             self._wait(u)
         for g, b in u.buckets:
-            e = _empty_like(g.dtype, g.shard_param.device)
+            e = _empty_like(g.dtype, self.compute_device)
             for p in b.params:
                 p.data = e
                 p.ds_status = ZeroParamStatus.NOT_AVAILABLE
@@ -386,7 +413,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         u.bw_expected = sum(1 for p in u.params if p.requires_grad)
         u.bw_ready = 0
         for g, b in u.buckets:
-            gf = torch.zeros(b.numel, dtype=g.dtype, device=g.shard_param.device)
+            gf = torch.zeros(b.numel, dtype=g.dtype, device=self.compute_device)
             u.grad_fulls.append(gf)
             for i, p in enumerate(b.params):
                 if p.requires_grad:

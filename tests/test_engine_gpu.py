@@ -16,7 +16,7 @@ def _env():
     os.environ.setdefault("WORLD_SIZE", "1")
 
 
-def _run(stage, offload=None, steps=4, ga=2):
+def _run(stage, offload=None, steps=4, ga=2, offload_param=None):
     _env()
     import deeperspeed_amd as ds
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
@@ -27,6 +27,8 @@ def _run(stage, offload=None, steps=4, ga=2):
     z = {"stage": stage, "reduce_bucket_size": int(5e6)}
     if offload:
         z["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": offload}
+    if offload_param:
+        z["offload_param"] = {"device": offload_param, "pin_memory": True, "nvme_path": "/tmp/dsa_pnvme"}
     conf = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": ga,
             "optimizer": {"type": "Adam", "params": {"lr": 3e-4}}, "fp16": {"enabled": True, "type": "bfloat16"},
             "fp32_allreduce": False, "gradient_clipping": 1.0, "zero_optimization": z}
@@ -109,3 +111,10 @@ def test_multirank_on_one_gpu_matches_single(tmp_path, stage, compact):
     assert b[-1] < b[0]
     for x, y in zip(a, b):
         assert abs(x - y) < 2e-2 * max(1.0, abs(x)), (a, b)
+
+
+@pytest.mark.parametrize("dev", ["cpu", "nvme"])
+def test_engine_param_offload(dev):
+    base = _run(3, "all", steps=3, ga=1)
+    off = _run(3, "all", steps=3, ga=1, offload_param=dev)
+    assert abs(base[-1] - off[-1]) < 5e-2 * max(1.0, abs(base[-1]))
