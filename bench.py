@@ -41,10 +41,14 @@ def parse():
     p.add_argument("--grad-accum", type=int, default=None)
     p.add_argument("--seq", type=int, default=2048)
     p.add_argument("--zero", type=int, default=3)
-    p.add_argument("--offload", type=str, default="auto", choices=["auto", "none", "compact", "master", "all"])
+    p.add_argument("--offload", type=str, default="auto", choices=["auto", "none", "compact", "master", "all", "nvme"])
     p.add_argument("--ckpt", type=str, default="auto", choices=["auto", "on", "off"],
                    help="activation checkpointing; auto = off when activations fit in HBM next to the shards")
     p.add_argument("--layers", type=int, default=None, help="override depth (memory experiments only)")
+    p.add_argument("--sparse", type=str, default=None,
+                   help="block-sparse attention mode (bigbird|fixed|bslongformer|variable|local) - BASELINE config 5")
+    p.add_argument("--block", type=int, default=64, help="sparse attention block size")
+    p.add_argument("--nvme-path", type=str, default="/tmp/dsa_nvme", help="ZeRO-Infinity swap folder (--offload nvme)")
     p.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (0 = off)")
     p.add_argument("--local_rank", type=int, default=None)
     return p.parse_args()
@@ -61,7 +65,7 @@ def plan_memory(cfg, mb, seq, world, offload, ckpt):
     recompute, one s*b*h layer input with it.  Transients: two gathered ZeRO-3 units, the
     logits (fp32 for the loss) and allocator slack."""
     p = cfg.num_params()
-    per_param = {"none": 16, "compact": 14, "master": 12, "all": 4}[offload]
+    per_param = {"none": 16, "compact": 14, "master": 12, "all": 4, "nvme": 4}[offload]
     states = p * per_param / world
     sbh = seq * mb * cfg.hidden_size
     act_layer = 2 * sbh if ckpt else 36 * sbh
@@ -102,6 +106,8 @@ def main():
     native.hip_ops()  # fail loudly if the HIP extension is missing
 
     over = {"num_layers": args.layers} if args.layers else {}
+    if args.sparse:
+        over["sparse_attention"] = {"mode": args.sparse, "block": args.block}
     cfg = get_config(args.model, max_seq_len=args.seq, checkpoint_activations=True, **over)
     big = cfg.num_params() > 5e9
     mb = args.micro_batch or (4 if big else 8)
@@ -123,6 +129,9 @@ def main():
             "stage3_unit_max_numel": int(2e8)}
     if offload == "compact":
         zcfg["compact_master"] = True
+    elif offload == "nvme":
+        zcfg["offload_optimizer"] = {"device": "nvme", "nvme_path": args.nvme_path, "pin_memory": True,
+                                     "states": "all"}
     elif offload != "none":
         zcfg["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": offload}
     conf = {
@@ -212,7 +221,8 @@ def main():
     flops_tok = cfg.flops_per_token(args.seq, recompute=False)
     ms_step = elapsed / args.steps * 1000.0
     out = {
-        "metric": "tokens/sec (node) GPT-NeoX-20B ZeRO-3" if args.model == "gpt-neox-20b" else f"tokens/sec {args.model}",
+        "metric": ("tokens/sec (node) GPT-NeoX-20B ZeRO-3" if args.model == "gpt-neox-20b" else
+                   f"tokens/sec {args.model}") + (f" block-sparse {args.sparse} seq{args.seq}" if args.sparse else ""),
         "value": round(tps, 2),
         "unit": "tokens/s",
         "n_gpus": world,
@@ -226,7 +236,7 @@ def main():
         "data": "synthetic random tokens, random-init weights",
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq,
                    "parallelism": f"zero{args.zero}-dp{world}", "micro_batch": mb, "grad_accum": ga,
-                   "offload": offload, "activation_checkpointing": ckpt == "on",
+                   "offload": offload, "activation_checkpointing": ckpt == "on", "sparse_attention": args.sparse,
                    "params_per_gpu": round(cfg.num_params() / world / 1e9, 3),
                    "model_tflops_per_gpu": round(tps * flops_tok / world / 1e12, 1),
                    "final_loss": round(float(loss), 4),

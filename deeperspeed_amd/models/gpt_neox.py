@@ -44,6 +44,9 @@ class GPTNeoXConfig:
     init_std: float = 0.02
     hidden_dropout: float = 0.0
     attention_dropout: float = 0.0
+    # block-sparse attention (GPT-NeoX `attention_config` sparse types), e.g.
+    # {"mode": "bigbird", "block": 64, "num_random_blocks": 1, "num_sliding_window_blocks": 3}
+    sparse_attention: Optional[dict] = None
 
     def __post_init__(self):
         if self.intermediate_size is None:
@@ -101,11 +104,28 @@ class LinearBiasGeLU(nn.Linear):
         return native.bias_gelu(F.linear(x, self.weight), self.bias, self.approximate)
 
 
+def make_sparsity_config(cfg: GPTNeoXConfig):
+    """Causal (unidirectional) SparsityConfig from cfg.sparse_attention."""
+    from ..ops import sparse_attention as sa
+    d = dict(cfg.sparse_attention)
+    mode = d.pop("mode", "bigbird").lower()
+    classes = {"fixed": sa.FixedSparsityConfig, "variable": sa.VariableSparsityConfig,
+               "bigbird": sa.BigBirdSparsityConfig, "bslongformer": sa.BSLongformerSparsityConfig,
+               "local": sa.LocalSlidingWindowSparsityConfig, "dense": sa.DenseSparsityConfig}
+    cls = classes[mode]
+    if mode != "dense":
+        d.setdefault("attention", "unidirectional")
+    return cls(num_heads=cfg.num_heads, **d)
+
+
 class NeoXAttention(nn.Module):
-    def __init__(self, cfg: GPTNeoXConfig, device=None, dtype=None):
+    def __init__(self, cfg: GPTNeoXConfig, device=None, dtype=None, layer_number: int = 0):
         super().__init__()
         h = cfg.hidden_size
         self.cfg = cfg
+        self.layer_number = layer_number
+        self._sparsity = make_sparsity_config(cfg) if cfg.sparse_attention else None
+        self._sp_ops = {}
         self.query_key_value = nn.Linear(h, 3 * h, device=device, dtype=dtype)
         self.dense = nn.Linear(h, h, device=device, dtype=dtype)
 
@@ -115,10 +135,33 @@ class NeoXAttention(nn.Module):
         qkv = self.query_key_value(x)
         q, k, v = rotary_split(qkv, cfg.num_heads, cfg.head_dim, cfg.rotary_dim, cfg.rotary_base,
                                qscale=1.0 / math.sqrt(cfg.head_dim))
-        ctx = attention(q, k, v, causal=True, softmax_scale=1.0, dropout_p=cfg.attention_dropout,
-                        training=self.training)
+        if self._sparsity is not None:
+            ctx = self._sparse_attention(q, k, v)
+        else:
+            ctx = attention(q, k, v, causal=True, softmax_scale=1.0, dropout_p=cfg.attention_dropout,
+                            training=self.training)
         ctx = ctx.transpose(1, 2).reshape(B, S, H)
         return self.dense(ctx)
+
+
+    def _sparse_ops(self, S):
+        if S not in self._sp_ops:
+            import random
+            from ..ops.sparse_attention import MatMul, Softmax
+            state = random.getstate()
+            random.seed(1234 + self.layer_number)  # identical random blocks on every rank
+            layout = self._sparsity.make_layout(S)
+            random.setstate(state)
+            blk = self._sparsity.block
+            self._sp_ops[S] = (MatMul(layout, blk, "sdd", trans_b=True), MatMul(layout, blk, "dsd"),
+                               Softmax(layout, blk))
+        return self._sp_ops[S]
+
+    def _sparse_attention(self, q, k, v):
+        """Block-sparse causal attention (q is pre-scaled): SDD -> causal sparse softmax -> DSD."""
+        sdd, dsd, softmax = self._sparse_ops(q.shape[2])
+        w = softmax(sdd(q, k), scale=1.0, causal=True)
+        return dsd(w, v)
 
 
 class NeoXMLP(nn.Module):
@@ -143,7 +186,7 @@ class NeoXTransformerLayer(nn.Module):
         self.input_layernorm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
         self.post_attention_layernorm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device,
                                                               dtype=dtype)
-        self.attention = NeoXAttention(cfg, device, dtype)
+        self.attention = NeoXAttention(cfg, device, dtype, layer_number)
         self.mlp = NeoXMLP(cfg, device, dtype)
 
     def _block(self, x):

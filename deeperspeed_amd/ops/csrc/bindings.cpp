@@ -383,7 +383,7 @@ Tensor sparse_dsd(Tensor S, Tensor rowptr, Tensor cols, Tensor Dt, int64_t H, in
 
 // in-place softmax over the non-zero blocks of each row
 void sparse_softmax_fwd(Tensor x, Tensor rowptr, Tensor cols, int64_t H, int64_t nbr, double scale, OptT rpe,
-                        OptT kpm, OptT attn, bool kpm_mul, bool attn_mul) {
+                        OptT kpm, OptT attn, bool kpm_mul, bool attn_mul, bool causal) {
   check_dev(x, "x");
   const int64_t blk = x.size(2), S = nbr * blk;
   int64_t rsz = 0, rsh = 0, rsr = 0, ksz = 0, asr = 0;
@@ -410,7 +410,7 @@ void sparse_softmax_fwd(Tensor x, Tensor rowptr, Tensor cols, int64_t H, int64_t
                                  rpe.has_value() ? rpe->data_ptr() : nullptr, rsz, rsh, rsr,
                                  kpm.has_value() ? kpm->data_ptr() : nullptr, ksz,
                                  attn.has_value() ? attn->data_ptr() : nullptr, asr, kpm_mul ? 1 : 0,
-                                 attn_mul ? 1 : 0, (float)scale, dcode(x), cur_stream());
+                                 attn_mul ? 1 : 0, (float)scale, causal ? 1 : 0, dcode(x), cur_stream());
 }
 
 void sparse_softmax_bwd(Tensor y, Tensor dy, Tensor rowptr, int64_t H, int64_t nbr, double scale) {

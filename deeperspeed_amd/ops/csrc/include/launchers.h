@@ -85,7 +85,7 @@ void launch_sparse_dsd(const void* S, const int* rowptr, const int* cols, const 
 void launch_sparse_softmax_fwd(void* x, const int* rowptr, const int* cols, int nnz, int Z, int H, int nbr, int blk,
                                const void* rpe, int64_t rpe_sz, int64_t rpe_sh, int64_t rpe_sr, const void* kpm,
                                int64_t kpm_sz, const void* attn, int64_t attn_sr, int kpm_mul, int attn_mul,
-                               float scale, int dt, hipStream_t s);
+                               float scale, int causal, int dt, hipStream_t s);
 void launch_sparse_softmax_bwd(const void* y, void* dy, const int* rowptr, int nnz, int Z, int H, int nbr, int blk,
                                float scale, int dt, hipStream_t s);
 

@@ -121,11 +121,13 @@ struct SoftmaxArgs {
   const uint16_t* attn; int64_t attn_sr;
   int kpm_mul, attn_mul;
   float scale;
+  int causal;  // extension: col > row -> -inf (causal LM without a dense S x S mask)
 };
 
 template <typename T>
 __device__ __forceinline__ float sm_val(const uint16_t* x, int64_t off, int z, int h, int row, int col,
                                         const SoftmaxArgs& a) {
+  if (a.causal && col > row) return -INFINITY;
   float v = M<T>::ld(x[off]) * a.scale;
   if (a.rpe) v += M<T>::ld(a.rpe[z * a.rpe_sz + h * a.rpe_sh + (int64_t)row * a.rpe_sr + col]);
   if (a.kpm) {
@@ -231,11 +233,11 @@ void launch_sparse_dsd(const void* S, const int* rowptr, const int* cols, const 
 void launch_sparse_softmax_fwd(void* x, const int* rowptr, const int* cols, int nnz, int Z, int H, int nbr, int blk,
                                const void* rpe, int64_t rpe_sz, int64_t rpe_sh, int64_t rpe_sr, const void* kpm,
                                int64_t kpm_sz, const void* attn, int64_t attn_sr, int kpm_mul, int attn_mul,
-                               float scale, int dt, hipStream_t s) {
+                               float scale, int causal, int dt, hipStream_t s) {
   const int64_t total = (int64_t)Z * H * nbr * blk;
   if (total == 0) return;
   sp::SoftmaxArgs a{(const uint16_t*)rpe, rpe_sz, rpe_sh, rpe_sr, (const uint16_t*)kpm, kpm_sz,
-                    (const uint16_t*)attn, attn_sr, kpm_mul, attn_mul, scale};
+                    (const uint16_t*)attn, attn_sr, kpm_mul, attn_mul, scale, causal};
   DSA_DISPATCH_16(dt, T,
     hipLaunchKernelGGL((sp::sparse_softmax_fwd_kernel<T>), dim3(waves_grid(total)), dim3(256), 0, s, (uint16_t*)x,
                        rowptr, cols, nnz, H, nbr, blk, total, a));

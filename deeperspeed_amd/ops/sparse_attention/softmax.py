@@ -17,7 +17,7 @@ def _as4(rpe):
 
 class _SparseSoftmaxFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, L, scale, rpe, kpm, attn, kpm_mode, attn_mode):
+    def forward(ctx, x, L, scale, rpe, kpm, attn, kpm_mode, attn_mode, causal=False):
         if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16):
             d = L.dev(x.device)
             y = x.contiguous().clone()
@@ -25,9 +25,9 @@ class _SparseSoftmaxFn(torch.autograd.Function):
                                                 None if rpe is None else _as4(rpe).contiguous(),
                                                 None if kpm is None else kpm.contiguous(),
                                                 None if attn is None else attn.contiguous(),
-                                                kpm_mode == "mul", attn_mode == "mul")
+                                                kpm_mode == "mul", attn_mode == "mul", bool(causal))
         else:
-            y = _softmax_ref(x, L, scale, rpe, kpm, attn, kpm_mode, attn_mode)
+            y = _softmax_ref(x, L, scale, rpe, kpm, attn, kpm_mode, attn_mode, causal)
         ctx.save_for_backward(y)
         ctx.L, ctx.scale = L, scale
         return y
@@ -41,7 +41,7 @@ class _SparseSoftmaxFn(torch.autograd.Function):
             native.hip_ops().sparse_softmax_bwd(y, dx, L.dev(y.device)["rowptr"], L.H, L.nbr, ctx.scale)
         else:
             dx = _softmax_bwd_ref(y, dy, L, ctx.scale)
-        return dx, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None
 
 
 def _dense_index(L, device):
@@ -53,7 +53,7 @@ def _dense_index(L, device):
     return nz[:, 0].view(-1, 1, 1), rows, cols
 
 
-def _softmax_ref(x, L, scale, rpe, kpm, attn, kpm_mode, attn_mode):
+def _softmax_ref(x, L, scale, rpe, kpm, attn, kpm_mode, attn_mode, causal=False):
     Z, S = x.shape[0], L.nbr * L.block
     hh, rows, cols = _dense_index(L, x.device)
     v = x.float() * scale
@@ -68,6 +68,8 @@ def _softmax_ref(x, L, scale, rpe, kpm, attn, kpm_mode, attn_mode):
         m = attn.float()
         m = torch.where(m == 0, float("-inf"), 0.0) if attn_mode == "mul" else m
         v = v + m[rows, cols].unsqueeze(0)
+    if causal:
+        v = v.masked_fill((cols > rows).unsqueeze(0), float("-inf"))
     dense = torch.full((Z, L.H, S, S), float("-inf"), device=x.device)
     dense[:, hh, rows, cols] = v
     p = torch.softmax(dense, -1).nan_to_num(0.0)
@@ -94,10 +96,12 @@ class Softmax:
         self.bench = bench
 
     def __call__(self, x, scale=1.0, rpe=None, key_padding_mask=None, attn_mask=None, key_padding_mask_mode="add",
-                 attn_mask_mode="add"):
+                 attn_mask_mode="add", causal=False):
+        """`causal` (extension): mask col > row inside the non-zero blocks, so unidirectional
+        layouts need no dense [S, S] attention mask."""
         for name, t in (("relative position embedding", rpe), ("Attention mask", attn_mask),
                         ("Key padding mask", key_padding_mask)):
             if t is not None and t.dtype != x.dtype:
                 raise ValueError(f"{name} must be {x.dtype}")
         return _SparseSoftmaxFn.apply(x, self.L, float(scale), rpe, key_padding_mask, attn_mask,
-                                      key_padding_mask_mode, attn_mask_mode)
+                                      key_padding_mask_mode, attn_mask_mode, bool(causal))

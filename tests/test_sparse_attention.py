@@ -173,3 +173,28 @@ def test_bert_sparse_self_attention_and_utils():
         16, ids, torch.ones(2, 40), torch.zeros(2, 40, dtype=torch.long), None, None, 0, None)
     assert pad == 8 and ids2.shape == (2, 48) and am.shape == (2, 48) and bool(am[0, -1] == 0)
     assert sa.SparseAttentionUtils.unpad_sequence_output(pad, torch.zeros(2, 48, 4)).shape == (2, 40, 4)
+
+
+def test_neox_sparse_attention_dense_layout_matches_dense_model():
+    """GPT-NeoX with a dense 'sparse' layout must equal the dense causal model."""
+    from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
+    torch.manual_seed(0)
+    cfg = get_config("tiny", num_layers=2, checkpoint_activations=False)
+    dense = GPTNeoX(cfg)
+    cfg2 = get_config("tiny", num_layers=2, checkpoint_activations=False,
+                      sparse_attention={"mode": "dense", "block": 16})
+    sparse = GPTNeoX(cfg2)
+    sparse.load_state_dict(dense.state_dict())
+    ids = torch.randint(0, cfg.vocab_size, (2, 64))
+    torch.testing.assert_close(sparse(ids), dense(ids), atol=1e-4, rtol=1e-4)
+    cfg3 = get_config("tiny", num_layers=2, checkpoint_activations=False,
+                      sparse_attention={"mode": "bigbird", "block": 16, "num_random_blocks": 1})
+    m3 = GPTNeoX(cfg3)
+    m3.load_state_dict(dense.state_dict())
+    loss = m3(ids, labels=ids)
+    loss.backward()
+    assert torch.isfinite(loss)
+    # causality: the logits at position t must not depend on tokens after t
+    ids2 = ids.clone()
+    ids2[:, 40:] = (ids2[:, 40:] + 1) % cfg.vocab_size
+    torch.testing.assert_close(m3(ids)[:, :40], m3(ids2)[:, :40], atol=1e-5, rtol=1e-5)
