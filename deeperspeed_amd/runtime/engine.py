@@ -26,6 +26,7 @@ from torch.nn.modules import Module
 
 from ..ops.adam.fused_adam import FusedAdam
 from ..utils.distributed import init_distributed
+from ..utils import comm
 from ..utils.logging import log_dist, logger
 from ..utils.timer import SynchronizedWallClockTimer, ThroughputTimer
 from ..version import __version__
@@ -679,6 +680,10 @@ class DeepSpeedEngine(Module):
         return prescaled_loss
 
     def forward(self, *inputs, **kwargs):
+        with comm.trace_range("engine.forward"):
+            return self._forward_impl(*inputs, **kwargs)
+
+    def _forward_impl(self, *inputs, **kwargs):
         if self.flops_profiler_enabled() and self.global_steps == self.flops_profiler_profile_step() and \
                 self.global_rank == 0:
             from ..profiling.flops_profiler import FlopsProfiler
@@ -714,6 +719,10 @@ class DeepSpeedEngine(Module):
             self.buffered_allreduce_fallback(elements_per_buffer=bucket_size)
 
     def backward(self, loss, allreduce_gradients=True, release_loss=False):
+        with comm.trace_range("engine.backward"):
+            return self._backward_impl(loss, allreduce_gradients, release_loss)
+
+    def _backward_impl(self, loss, allreduce_gradients=True, release_loss=False):
         if not allreduce_gradients:
             logger.warning("Argument `allreduce_gradients` is deprecated, ignored, and will soon be removed")
         if self.gradient_accumulation_steps() > 1:
@@ -803,6 +812,10 @@ class DeepSpeedEngine(Module):
         self.global_samples += self.train_batch_size()
 
     def step(self, lr_kwargs=None):
+        with comm.trace_range("engine.step"):
+            return self._step_impl(lr_kwargs)
+
+    def _step_impl(self, lr_kwargs=None):
         if self.wall_clock_breakdown():
             self.timers("step_microstep").start()
             self.timers("step").start()

@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 
 from ...ops import native
+from ...utils import comm
 from ...ops.adam.fused_adam import FusedAdam
 from ...utils.logging import logger
 from ..fp16.loss_scaler import DynamicLossScaler, LossScaler
@@ -244,7 +245,7 @@ class ShardedOptimizerBase:
                 native.sumsq_accumulate(t, buf)
         if _dist_ready():
             if self._grads_are_sharded() and self.dp_world > 1:
-                dist.all_reduce(buf, group=self.dp_group)
+                comm.all_reduce(buf, group=self.dp_group, tag="zero.norm")
             if self.mp_world > 1:
                 dist.all_reduce(buf, group=self.mpu.get_model_parallel_group())
         return buf
@@ -282,6 +283,8 @@ class ShardedOptimizerBase:
         return overflow, total
 
     def step(self, closure=None):
+        if comm.DEBUG:
+            comm.verify_collective_order(self.dp_group)
         if self.timers is not None:
             self.timers("optimizer_step").start()
         overflow, total = self._check_overflow_and_scale()

@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ...utils.logging import logger
+from ...utils import comm
 from .layout import ALIGN, FlatGroup, build_unit_buckets
 from .sharded_base import ShardedOptimizerBase, _dist_ready
 
@@ -278,7 +279,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             if self.param_offload:
                 chunk = chunk.to(self.compute_device, non_blocking=chunk.is_pinned())
             if _dist_ready() and self.dp_world > 1:
-                u.works.append(dist.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True))
+                u.works.append(comm.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True,
+                                                           tag=f"zero3.gather.u{u.uid}"))
             else:
                 full.copy_(chunk)
             u.fulls.append(full)
@@ -292,6 +294,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             for w in u.works:
                 w.wait()
             u.works = []
+            if comm.DEBUG:
+                for full in u.fulls:
+                    comm.check_replicated(full, self.dp_group, f"zero3 unit {u.uid} gathered bucket")
             u.status = ZeroParamStatus.AVAILABLE
             for p in u.params:
                 p.ds_status = ZeroParamStatus.AVAILABLE
@@ -455,7 +460,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             direct = (out_slice.dtype == src.dtype) and self.gradient_accumulation_steps == 1 and \
                 not self._grads_nonzero
             out = out_slice if direct else torch.empty(b.chunk, dtype=src.dtype, device=src.device)
-            work = dist.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True)
+            work = comm.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True,
+                                              tag=f"zero3.reduce.u{u.uid}")
             if direct:
                 self._pending.append((work, None))
             else:

@@ -24,6 +24,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from ...utils import comm
 from ...utils.logging import logger
 from .layout import ALIGN, FlatGroup, build_size_buckets
 from .sharded_base import ShardedOptimizerBase, _dist_ready
@@ -218,7 +219,7 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
             else:
                 target = dst_full[b.shard_offset: b.shard_offset + b.numel]
                 target.copy_(src)
-            work = dist.all_reduce(target, group=self.dp_group, async_op=True) if (_dist_ready() and world > 1) \
+            work = comm.all_reduce(target, group=self.dp_group, async_op=True, tag="zero.allreduce") if (_dist_ready() and world > 1) \
                 else None
             self._pending.append((work, None))
             return
@@ -229,7 +230,7 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
         else:
             out = out_slice
         if _dist_ready() and world > 1:
-            work = dist.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True)
+            work = comm.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True, tag="zero.reduce")
         else:
             out.copy_(src[: b.chunk])
             work = None
@@ -282,7 +283,7 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
         full = g.arena[b.arena_offset: b.arena_offset + b.numel]
         chunk = g.shard_param[b.shard_offset: b.shard_offset + b.chunk]
         if _dist_ready() and self.dp_world > 1:
-            w = dist.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True)
+            w = comm.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True, tag="zero.gather")
             self._ag_works.append(w)
         else:
             full[: b.chunk].copy_(chunk)

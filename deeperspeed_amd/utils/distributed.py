@@ -37,6 +37,9 @@ def init_distributed(dist_backend="nccl", auto_mpi_discovery=True, distributed_p
     for v, d in (("RANK", "0"), ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0"), ("MASTER_ADDR", "127.0.0.1"),
                  ("MASTER_PORT", str(distributed_port))):
         os.environ.setdefault(v, d)
+    # failed / timed-out RCCL collectives abort the process (the launcher then tears the job
+    # down) instead of hanging every rank
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ["LOCAL_RANK"]) % max(1, torch.cuda.device_count()))
     if not dist.is_initialized():
