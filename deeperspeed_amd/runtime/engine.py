@@ -225,8 +225,9 @@ class DeepSpeedEngine(Module):
         os.makedirs(log_dir, exist_ok=True)
         try:
             from torch.utils.tensorboard import SummaryWriter
-        except Exception:  # tensorboard not installed: keep a minimal event sink
-            return _NullSummaryWriter(log_dir)
+        except Exception:  # tensorboard not installed: native event-file writer
+            from ..utils.tb_writer import EventFileWriter
+            return EventFileWriter(log_dir)
         return SummaryWriter(log_dir=log_dir)
 
     def wall_clock_breakdown(self):
