@@ -51,6 +51,10 @@ def parse():
     p.add_argument("--nvme-path", type=str, default="/tmp/dsa_nvme", help="ZeRO-Infinity swap folder (--offload nvme)")
     p.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (0 = off)")
     p.add_argument("--local_rank", type=int, default=None)
+    p.add_argument("--max-live", type=float, default=None,
+                   help="override stage3_max_live_parameters (default: planned from spare HBM)")
+    p.add_argument("--dist-backend", type=str, default="nccl",
+                   help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU")
     return p.parse_args()
 
 
@@ -98,9 +102,13 @@ def main():
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
     from deeperspeed_amd.ops import native
 
-    ds.init_distributed(dist_backend="nccl")
+    ds.init_distributed(dist_backend=args.dist_backend)
     rank = dist.get_rank()
-    local = int(os.environ["LOCAL_RANK"])
+    # one rank per GPU; more ranks than GPUs (a rehearsal of the N-GPU path on one card)
+    # share the device and split its memory budget
+    ndev = torch.cuda.device_count()
+    local = int(os.environ["LOCAL_RANK"]) % ndev
+    share = -(-int(os.environ.get("LOCAL_WORLD_SIZE", "1")) // ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     native.hip_ops()  # fail loudly if the HIP extension is missing
@@ -113,7 +121,7 @@ def main():
     mb = args.micro_batch or (4 if big else 8)
     ga = args.grad_accum or (4 if big else 2)
     hbm = torch.cuda.get_device_properties(local).total_memory
-    budget = 0.97 * hbm
+    budget = 0.97 * hbm / share
     # model-state layout: everything in HBM (16 B/param) > compact fp32 master (14 B/param)
     # > fp32 master offloaded to host (12 B/param in HBM); then recompute only if needed
     offload = args.offload
@@ -124,9 +132,19 @@ def main():
     if ckpt == "auto":
         ckpt = "off" if plan_memory(cfg, mb, args.seq, world, offload, False) < budget else "on"
     cfg.checkpoint_activations = ckpt == "on"
+    # ZeRO-3 parameter retention (stage3_max_live_parameters): HBM left after states and
+    # activations keeps gathered bf16 units resident between their forward and backward use
+    # and across the micro-batches of one optimizer step, so a unit is all-gathered once per
+    # step instead of twice per micro-batch when the whole model fits (it does at N>=2 on
+    # 288 GB parts: 41 GB of bf16 weights for 20B)
+    spare = budget - plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on")
+    live = int(max(0.0, min(spare / 2, cfg.num_params() * 1.0)))
+    if args.max_live is not None:
+        live = int(args.max_live)
     zcfg = {"stage": args.zero, "overlap_comm": True, "reduce_bucket_size": int(2e8),
             "stage3_prefetch_bucket_size": int(5e8), "stage3_param_persistence_threshold": int(1e6),
-            "stage3_unit_max_numel": int(2e8)}
+            "stage3_unit_max_numel": int(2e8), "stage3_max_live_parameters": live,
+            "stage3_max_reuse_distance": int(2 * cfg.num_params())}
     if offload == "compact":
         zcfg["compact_master"] = True
     elif offload == "nvme":
@@ -147,7 +165,7 @@ def main():
         "wall_clock_breakdown": False,
     }
     log(f"model={args.model} params={cfg.num_params() / 1e9:.2f}B world={world} mb={mb} ga={ga} seq={args.seq} "
-        f"zero={args.zero} offload={offload} ckpt={ckpt} hbm={hbm / 2**30:.0f} GiB "
+        f"zero={args.zero} offload={offload} ckpt={ckpt} live={live / 1e9:.1f}B hbm={hbm / 2**30:.0f} GiB "
         f"planned={plan_memory(cfg, mb, args.seq, world, offload, ckpt == 'on') / 2**30:.0f} GiB")
     t0 = time.time()
     torch.manual_seed(1234)

@@ -129,6 +129,13 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self._bwd_pos = 0
         self._units: List[ZeroUnit] = []
         self._unit_of_param: Dict[int, ZeroUnit] = {}
+        # gathered-parameter retention (reference stage3_max_live_parameters /
+        # stage3_max_reuse_distance): live numel of non-persistent gathered units and the
+        # per-trace-position distance (in elements) to each unit's next use
+        self._live_numel = 0
+        self.gathered_numel = 0  # elements all-gathered so far (stats / tests)
+        self._reuse_f: Dict[int, int] = {}
+        self._reuse_b: Dict[int, int] = {}
         self._assign_units(module)
         self.groups = self._split_groups()
         for g in self.groups:
@@ -273,6 +280,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         if u.status != ZeroParamStatus.NOT_AVAILABLE:
             return
         u.works, u.fulls = [], []
+        if not u.persistent:
+            self._live_numel += u.numel
+        self.gathered_numel += u.numel
         for g, b in u.buckets:
             full = torch.empty(b.numel, dtype=g.dtype, device=self.compute_device)
             chunk = g.shard_param[b.shard_offset: b.shard_offset + b.chunk]
@@ -315,6 +325,39 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                 p.ds_status = ZeroParamStatus.NOT_AVAILABLE
         u.fulls = []
         u.status = ZeroParamStatus.NOT_AVAILABLE
+        if not u.persistent:
+            self._live_numel -= u.numel
+
+    def _compute_reuse(self):
+        """Distance (in parameter elements) from each trace position to the unit's next use,
+        cyclic over one micro-batch (forward trace then backward trace)."""
+        order = [u for u in self._fwd_trace] + [u for u in self._bwd_trace]
+        n, nf = len(order), len(self._fwd_trace)
+        numel = [self._units[uid].numel for uid in order]
+        self._reuse_f, self._reuse_b = {}, {}
+        for i, uid in enumerate(order):
+            d = 0
+            for k in range(1, n + 1):
+                j = (i + k) % n
+                if order[j] == uid:
+                    break
+                d += numel[j]
+            if i < nf:
+                self._reuse_f[i] = d
+            else:
+                self._reuse_b[i - nf] = d
+
+    def _maybe_release(self, u: ZeroUnit, phase: str):
+        """Release after use unless the unit is reused within stage3_max_reuse_distance and the
+        live-parameter budget (stage3_max_live_parameters) still has room."""
+        if self.single or u.persistent or not self._trace_frozen:
+            self._release(u)
+            return
+        pos = getattr(u, "last_fpos" if phase == "f" else "last_bpos", None)
+        d = (self._reuse_f if phase == "f" else self._reuse_b).get(pos)
+        if d is not None and d <= self.max_reuse_distance and self._live_numel <= self.max_live_parameters:
+            return
+        self._release(u)
 
     def gather_units(self, units):
         for u in units:
@@ -367,6 +410,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                 self._fwd_trace.append(u.uid)
             elif self._fwd_pos < len(self._fwd_trace) and self._fwd_trace[self._fwd_pos] == u.uid:
                 self._prefetch(self._fwd_trace, self._fwd_pos)
+            u.last_fpos = self._fwd_pos
             self._fwd_pos += 1
         self._fetch(u)
         for x in u.external:
@@ -380,7 +424,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         if torch.is_grad_enabled():
             self._register_bw_hooks(u, output)
         if u.active == 0 and not _in_backward():
-            self._release(u)
+            self._maybe_release(u, "f")
             for x in u.external:
                 if x.active == 0:
                     self._release(x)
@@ -410,6 +454,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             self._bwd_trace.append(u.uid)
         elif self._bwd_pos < len(self._bwd_trace) and self._bwd_trace[self._bwd_pos] == u.uid:
             self._prefetch(self._bwd_trace, self._bwd_pos)
+        u.last_bpos = self._bwd_pos
         self._bwd_pos += 1
         self._fetch(u)
         self._wait(u)
@@ -468,7 +513,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                 self._pending.append((work, functools.partial(_accum, out_slice, out)))
         u.grad_fulls = []
         if u.active == 0:
-            self._release(u)
+            self._maybe_release(u, "b")
 
     _grads_nonzero = False
 
@@ -487,11 +532,12 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         for u in self._units:
             u.reduced = False
             u.in_backward = False
-            if u.active == 0:
-                self._release(u)
+            if u.active == 0 and u.status != ZeroParamStatus.NOT_AVAILABLE:
+                self._maybe_release(u, "b")
         self._grads_nonzero = True
         if not self._trace_frozen and self._fwd_trace:
             self._trace_frozen = True
+            self._compute_reuse()
         self._bwd_pos = 0
 
     overlapping_partition_gradients_reduce_epilogue = reduce_epilogue
@@ -510,6 +556,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def _post_step(self):
         if self.single:
             return
+        for u in self._units:  # retained gathered copies are stale after the update
+            if not u.persistent and u.active == 0:
+                self._release(u)
         for u in self._units:
             if u.persistent:
                 self._release(u, force=True)

@@ -27,6 +27,9 @@ def _train_and_dump(out_dir, stage, ga, offload, steps=3, hidden=32):
     elif offload in ("param_cpu", "param_nvme"):
         zero["offload_optimizer"] = {"device": "cpu", "states": "all"}
         zero["offload_param"] = {"device": offload.split("_")[1], "nvme_path": os.path.join(out_dir, "pnvme")}
+    elif offload in ("retain", "noretain"):
+        zero["stage3_max_live_parameters"] = 10**9 if offload == "retain" else 0
+        zero["stage3_max_reuse_distance"] = 10**9 if offload == "retain" else 0
     elif offload:
         zero["offload_optimizer"] = {"device": "cpu", "states": offload}
     cfg = base_config(stage=stage, mb=4, ga=ga, **zero)
@@ -49,8 +52,9 @@ def _train_and_dump(out_dir, stage, ga, offload, steps=3, hidden=32):
         sd = {k: v.detach().cpu().clone() for k, v in engine.module.state_dict().items()}
     masters = torch.cat([engine.optimizer.master_fp32(g).float() for g in engine.optimizer.groups]) \
         if hasattr(engine.optimizer, "groups") else None
+    gathered = getattr(engine.optimizer, "gathered_numel", 0)
     if rank == 0:
-        torch.save({"sd": sd, "loss": float(loss), "masters": masters},
+        torch.save({"sd": sd, "loss": float(loss), "masters": masters, "gathered": gathered},
                    os.path.join(out_dir, f"s{stage}_ga{ga}_{offload}.pt"))
 
 
@@ -176,3 +180,30 @@ def test_zero3_param_offload_matches(tmp_path, dev):
     for k in a["sd"]:
         assert torch.equal(a["sd"][k], b["sd"][k]), k
     assert torch.equal(a["masters"], b["masters"])
+
+
+def test_zero3_param_retention(tmp_path):
+    """stage3_max_live_parameters / stage3_max_reuse_distance: keeping gathered units resident
+    across forward->backward and across micro-batches must not change the math, and must cut
+    the all-gather volume."""
+    run_distributed(_train_and_dump, 2, str(tmp_path), 3, 2, "noretain")
+    run_distributed(_train_and_dump, 2, str(tmp_path), 3, 2, "retain")
+    a = torch.load(os.path.join(tmp_path, "s3_ga2_noretain.pt"), weights_only=True)
+    b = torch.load(os.path.join(tmp_path, "s3_ga2_retain.pt"), weights_only=True)
+    for k in a["sd"]:
+        assert torch.equal(a["sd"][k], b["sd"][k]), k
+    assert torch.equal(a["masters"], b["masters"])
+    assert b["gathered"] < 0.6 * a["gathered"], (a["gathered"], b["gathered"])
+
+
+def test_reuse_distance_table():
+    """Reuse distances are measured in parameter elements between uses, cyclic over
+    forward + backward of one micro-batch (reference stage3.py PrefetchCoordinator semantics)."""
+    from types import SimpleNamespace
+    from deeperspeed_amd.runtime.zero.stage3 import DeepSpeedZeroOptimizer_Stage3 as Z3
+    z = Z3.__new__(Z3)
+    z._units = [SimpleNamespace(numel=n) for n in (10, 20, 30)]
+    z._fwd_trace, z._bwd_trace = [0, 1, 2], [2, 1, 0]
+    z._compute_reuse()
+    assert z._reuse_f == {0: 50 + 30 + 20, 1: 30 + 30, 2: 0}
+    assert z._reuse_b == {0: 20 + 10 + 10 + 20, 1: 10 + 10, 2: 0}
