@@ -208,3 +208,34 @@ def test_gradient_noise_scale():
         m.bias.grad = torch.randn(4)
         gns.update()
     assert gns.noise_scale is not None and gns.n_updates == 4
+
+
+def test_batch_size_scheduler():
+    """bs_schedules.BatchSizeScheduler: truncated linear ramp, merged duplicate intervals,
+    stepwise lookup (reference bs_schedules.py:28-56)."""
+    from deeperspeed_amd.runtime.bs_schedules import BatchSizeScheduler
+    s = BatchSizeScheduler(final_batch_size=16, num_intervals=8, warmup_num_steps=10000)
+    assert s.schedule == {0: 1, 1428: 3, 2857: 5, 4285: 7, 5714: 9, 7142: 11, 8571: 13, 10000: 16}
+    seen = []
+    for _ in range(10002):
+        s.step()
+        if not seen or seen[-1][1] != s.current_batch_size:
+            seen.append((s.last_batch_iteration, s.current_batch_size))
+    assert seen == [(0, 1), (1428, 3), (2857, 5), (4285, 7), (5714, 9), (7142, 11), (8571, 13), (10000, 16)]
+    # duplicates merge: sizes 2,2,2,3 -> two intervals
+    d = BatchSizeScheduler(final_batch_size=3, min_batch_size_multiplier=0.5, warmup_num_steps=30, num_intervals=4)
+    assert d.schedule == {0: 2, 30: 3}
+    d.load_state_dict({"last_batch_iteration": 29})
+    d.step()
+    assert d.current_batch_size == 3 and d.state_dict() == {"last_batch_iteration": 30}
+
+
+def test_pipe_visualizer():
+    from deeperspeed_amd.runtime.pipe.pipe_visualizer import pipeline_visualizer, schedule_grid
+    grid = schedule_grid(4, 4)
+    for row in grid:  # every stage runs each micro-batch forward and backward once
+        cells = " / ".join(row)
+        assert cells.count("fwd") == 4 and cells.count("bwd") == 4
+    out = pipeline_visualizer(4, 4)
+    assert "GPU 3" in out and "Idle Time: 24" in out and "Non Idle Time: 32" in out
+    assert "reduce_grads" in pipeline_visualizer(2, 2, include_all=True)
