@@ -8,11 +8,15 @@ the per-GPU micro-batch and gradient-accumulation are fixed as N grows).
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Each step is a full training step through the framework: forward + backward of every
-micro-batch (activation recompute on), ZeRO-3 all-gathers / reduce-scatters over RCCL,
-global-norm clipping, fused Adam on the fp32 master, bf16 parameter refresh.  With a
-single GPU the 20B model's optimizer state does not fit in 288 GB next to the moments, so
-the fp32 master is offloaded to pinned host memory (ZeRO-Offload, master-only mode) and
-streamed through the step; with N >= 2 everything stays in HBM.
+micro-batch, ZeRO-3 all-gathers / reduce-scatters over RCCL, global-norm clipping, fused Adam
+on the fp32 master, bf16 parameter refresh.  A memory planner picks the layout per N: on one
+GPU the 20B model's states only fit as 14 B/param (compact fp32 master = bf16 weight + int16
+residual) with activation recompute; with N >= 2 the shards shrink, recompute turns off and
+the spare HBM keeps gathered parameters resident across micro-batches
+(stage3_max_live_parameters).
+
+`--pipe P` switches to BASELINE config 4 (PipelineModule PP=P x DP=N/P, ZeRO-1 or 1-bit
+Adam via `--optimizer onebitadam`).
 
 Rank 0 prints ONE JSON line.  `vs_baseline` divides by the only DeeperSpeed-derived
 number BASELINE.md gives for this model/metric (410 tokens/s per GPU: the reference's best
@@ -53,6 +57,11 @@ def parse():
     p.add_argument("--local_rank", type=int, default=None)
     p.add_argument("--max-live", type=float, default=None,
                    help="override stage3_max_live_parameters (default: planned from spare HBM)")
+    p.add_argument("--pipe", type=int, default=1,
+                   help="pipeline stages (BASELINE config 4: --model gpt3-6.7b --pipe 4 on 8 GPUs = PP4 x DP2)")
+    p.add_argument("--optimizer", type=str, default="adam", choices=["adam", "onebitadam", "onebitlamb", "lamb"],
+                   help="1-bit optimizers run without ZeRO (reference restriction)")
+    p.add_argument("--freeze-step", type=int, default=2, help="1-bit optimizers: full-precision warm-up steps")
     p.add_argument("--dist-backend", type=str, default="nccl",
                    help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU")
     return p.parse_args()
@@ -167,6 +176,8 @@ def main():
     log(f"model={args.model} params={cfg.num_params() / 1e9:.2f}B world={world} mb={mb} ga={ga} seq={args.seq} "
         f"zero={args.zero} offload={offload} ckpt={ckpt} live={live / 1e9:.1f}B hbm={hbm / 2**30:.0f} GiB "
         f"planned={plan_memory(cfg, mb, args.seq, world, offload, ckpt == 'on') / 2**30:.0f} GiB")
+    if args.pipe > 1:
+        return run_pipeline(args, cfg, mb, ga, world, rank, dev)
     t0 = time.time()
     torch.manual_seed(1234)
     model = GPTNeoX(cfg, device=dev, dtype=torch.bfloat16)
@@ -258,7 +269,87 @@ def main():
                    "params_per_gpu": round(cfg.num_params() / world / 1e9, 3),
                    "model_tflops_per_gpu": round(tps * flops_tok / world / 1e12, 1),
                    "final_loss": round(float(loss), 4),
+                   "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+                   "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on") / 2**30, 1),
+                   "max_live_parameters": live,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N), BASELINE.md derived target"},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _optimizer_block(args):
+    if args.optimizer == "adam":
+        return {"type": "Adam", "params": {"lr": 1e-4, "betas": [0.9, 0.95], "eps": 1e-8, "weight_decay": 0.01}}
+    if args.optimizer == "lamb":
+        return {"type": "Lamb", "params": {"lr": 1e-3, "weight_decay": 0.01}}
+    name = {"onebitadam": "OneBitAdam", "onebitlamb": "OneBitLamb"}[args.optimizer]
+    return {"type": name, "params": {"lr": 1e-4, "freeze_step": args.freeze_step, "comm_backend_name": "nccl"}}
+
+
+def run_pipeline(args, cfg, mb, ga, world, rank, dev):
+    """BASELINE config 4: GPT-NeoX/GPT-3 as a PipelineModule, PP=args.pipe x DP=world/pipe,
+    1F1B schedule with `ga` micro-batches per step, p2p activations over RCCL, ZeRO-1 (Adam)
+    or 1-bit Adam/LAMB on the data-parallel group."""
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.gpt_neox import to_pipeline
+    from deeperspeed_amd.runtime.pipe.topology import PipeDataParallelTopology
+    assert world % args.pipe == 0, f"world {world} not divisible by --pipe {args.pipe}"
+    dp = world // args.pipe
+    onebit = args.optimizer.startswith("onebit")
+    cfg.checkpoint_activations = False  # the pipeline module checkpoints per layer itself
+    torch.manual_seed(1234)
+    topo = PipeDataParallelTopology(num_pp=args.pipe, num_dp=dp)
+    model = to_pipeline(cfg, num_stages=None, topology=topo, activation_checkpoint_interval=1 if args.ckpt != "off" else 0)
+    conf = {"train_micro_batch_size_per_gpu": mb, "gradient_accumulation_steps": ga,
+            "optimizer": _optimizer_block(args), "fp16": {"enabled": True, "type": "bfloat16"},
+            "fp32_allreduce": False, "gradient_clipping": 0.0 if onebit else 1.0, "steps_per_print": 1000000}
+    if not onebit:
+        conf["zero_optimization"] = {"stage": 1, "reduce_bucket_size": int(2e8)}
+    t0 = time.time()
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=[p for p in model.parameters()],
+                                    config_params=conf)
+    log(f"pipeline PP={args.pipe} DP={dp} stage={engine.stage_id} params/stage="
+        f"{sum(p.numel() for p in engine.module.parameters()) / 1e9:.2f}B optimizer={args.optimizer} "
+        f"ready in {time.time() - t0:.1f}s mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321 + engine.grid.get_data_parallel_id())
+    batches = [torch.randint(0, cfg.vocab_size, (mb, args.seq), device=dev, generator=g) for _ in range(ga)]
+
+    def train_step():
+        return engine.train_batch(iter([(b, b) for b in batches]))
+
+    for i in range(args.warmup):
+        ts = time.time()
+        loss = train_step()
+        torch.cuda.synchronize()
+        log(f"warmup {i} loss={float(loss):.4f} {time.time() - ts:.2f}s "
+            f"peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+    dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.time()
+    for _ in range(args.steps):
+        loss = train_step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.time() - t_start], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    global_batch = mb * ga * dp
+    tps = global_batch * args.seq * args.steps / elapsed
+    out = {
+        "metric": f"tokens/sec {args.model} PipelineModule PP{args.pipe}xDP{dp} {args.optimizer}",
+        "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1000.0, 2), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic random tokens, random-init weights",
+        "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq,
+                   "parallelism": f"pp{args.pipe}-dp{dp}" + ("" if onebit else "-zero1"), "micro_batch": mb,
+                   "grad_accum": ga, "optimizer": args.optimizer,
+                   "model_tflops_per_gpu": round(tps * cfg.flops_per_token(args.seq) / world / 1e12, 1),
+                   "final_loss": round(float(loss), 4),
+                   "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1)},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -35,10 +35,19 @@ def _peer(stage):
     return _grid.stage_to_global(stage_id=stage)
 
 
+def _host_staged(t):
+    """gloo has no device-memory send/recv: stage through host memory (CPU tests and
+    several-ranks-on-one-GPU rehearsals only; RCCL moves device memory directly)."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
 def send(tensor, dest_stage, async_op=False, fp32_comm=False):
     src_stage = _grid.get_stage_id()
     _is_valid_send_recv(src_stage, dest_stage)
     t = tensor.float() if (fp32_comm and tensor.dtype == torch.bfloat16) else tensor
+    if _host_staged(t):
+        dist.send(t.detach().cpu().contiguous(), _peer(dest_stage))
+        return None
     work = dist.isend(t.contiguous(), _peer(dest_stage))
     if async_op:
         return work
@@ -49,6 +58,12 @@ def send(tensor, dest_stage, async_op=False, fp32_comm=False):
 def recv(tensor, src_stage, async_op=False, fp32_comm=False):
     dest_stage = _grid.get_stage_id()
     _is_valid_send_recv(src_stage, dest_stage)
+    if _host_staged(tensor):
+        buf = torch.empty(tensor.shape, dtype=torch.float32 if (fp32_comm and tensor.dtype == torch.bfloat16)
+                          else tensor.dtype)
+        dist.recv(buf, _peer(src_stage))
+        tensor.copy_(buf)
+        return None
     if fp32_comm and tensor.dtype == torch.bfloat16:
         buf = torch.empty(tensor.shape, dtype=torch.float32, device=tensor.device)
         work = dist.irecv(buf, _peer(src_stage))
@@ -64,6 +79,10 @@ def recv(tensor, src_stage, async_op=False, fp32_comm=False):
 
 def send_many(tensors: List[torch.Tensor], dest_stage, fp32_comm=False):
     """Send a list of tensors in one batched call (one RCCL group launch)."""
+    if tensors and _host_staged(tensors[0]):
+        for t in tensors:
+            send(t, dest_stage, fp32_comm=fp32_comm)
+        return
     ops = []
     peer = _peer(dest_stage)
     keep = []
@@ -77,6 +96,10 @@ def send_many(tensors: List[torch.Tensor], dest_stage, fp32_comm=False):
 
 
 def recv_many(tensors: List[torch.Tensor], src_stage, fp32_comm=False):
+    if tensors and _host_staged(tensors[0]):
+        for t in tensors:
+            recv(t, src_stage, fp32_comm=fp32_comm)
+        return
     ops, staged = [], []
     peer = _peer(src_stage)
     for t in tensors:
