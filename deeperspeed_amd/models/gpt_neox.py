@@ -273,6 +273,9 @@ def to_pipeline(cfg: GPTNeoXConfig, num_stages: int, topology=None, partition_me
                 activation_checkpoint_interval=0, **kw):
     """GPT-NeoX as a PipelineModule (embedding, N blocks, final norm + head)."""
     from ..runtime.pipe.module import LayerSpec, PipelineModule
+    # only transformer blocks are recomputed: a checkpointed embedding would see integer token
+    # ids as its only input and return an output that does not require grad
+    kw.setdefault("checkpointable_layers", ["NeoXTransformerLayer"])
     specs = [LayerSpec(_EmbedPipe, cfg)]
     for i in range(cfg.num_layers):
         specs.append(LayerSpec(NeoXTransformerLayer, cfg, i))

@@ -433,6 +433,18 @@ template <> struct Mfma32<f16_t> {
 constexpr int BM2 = 128;
 constexpr int BN2 = 64;
 
+// raw v_exp_f32 (no denormal range fix-up: softmax weights below 2^-126 are zero anyway)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// 1-D grid -> task id such that consecutive tasks (the row blocks of one head, which share its
+// K/V) run on the same XCD and hit that XCD's L2: the hardware deals workgroups round-robin to
+// the 8 XCDs, so XCD x = lin % 8 receives the contiguous task range [base_x, base_x + count_x).
+// Bijective for any n (also n % 8 != 0).  Placement only affects speed, never correctness.
+__device__ __forceinline__ int xcd_task(int lin, int n) {
+  const int xcd = lin & 7, slot = lin >> 3, q = n >> 3, r = n & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
 template <int D>
 __device__ __forceinline__ void tile_load(uint4 (&r)[D / 32], const uint16_t* __restrict__ g, int r0, int S) {
   constexpr int CH = D / 8;
@@ -478,8 +490,11 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
-  const int64_t bh = blockIdx.y;
-  const int qb = blockIdx.x * BM2;
+  // heaviest (last) causal row block of each head first, heads grouped per XCD
+  const int nqb = (S + BM2 - 1) / BM2;
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int64_t bh = task / nqb;
+  const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
   const int myq = qb + 32 * w + c32;
   const uint16_t* Qb = Q + bh * (int64_t)S * D;
   const uint16_t* Kb = K + bh * (int64_t)S * D;
@@ -526,28 +541,36 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[16 * t + r] = acc[r];
     }
-    // keys of value index 16t+r: j0 + 32t + 8(r>>2) + 4h + (r&3); this lane's query is myq
+    // keys of value index 16t+r: j0 + 32t + 8(r>>2) + 4h + (r&3); this lane's query is myq.
+    // Masking is only needed on the diagonal / ragged tiles (wave-uniform branch).
+    if ((j0 + BN2 > S) || (CAUSAL && j0 + BN2 - 1 > qb + 32 * w)) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          if (key >= S || (CAUSAL && key > myq)) sv[16 * t + r] = -INFINITY;
+        }
+    }
+    // running max on raw scores (scale > 0 preserves order), exponent in the log2 domain:
+    // p = 2^(s * scale*log2e - m) as one packed FMA + one v_exp_f32 per element
     float mx = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-        float x = sv[16 * t + r] * sl2;
-        if (key >= S || (CAUSAL && key > myq)) x = -INFINITY;
-        sv[16 * t + r] = x;
-        mx = fmaxf(mx, x);
-      }
+    for (int i = 0; i < 32; ++i) mx = fmaxf(mx, sv[i]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
-    float ps = 0.f;
+    const float mn = fmaxf(m, mx * sl2);
+    const float mu = (mn == -INFINITY) ? 0.f : mn;
+    const float alpha = fast_exp2(m - mu);
+    // two partial sums keep the dependent add chain short
+    float ps = 0.f, ps1 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      const float p = (mn == -INFINITY) ? 0.f : exp2f(sv[i] - mn);
-      sv[i] = p;
-      ps += p;
+    for (int i = 0; i < 32; i += 2) {
+      sv[i] = fast_exp2(fmaf(sv[i], sl2, -mu));
+      sv[i + 1] = fast_exp2(fmaf(sv[i + 1], sl2, -mu));
+      ps += sv[i];
+      ps1 += sv[i + 1];
     }
+    ps += ps1;
     ps += __shfl_xor(ps, 32, 64);
     l = l * alpha + ps;
     m = mn;
@@ -615,8 +638,10 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
-  const int64_t bh = blockIdx.y;
-  const int kb = blockIdx.x * BM2;
+  const int nkb = (S + BM2 - 1) / BM2;
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int64_t bh = task / nkb;
+  const int kb = (task - (int)bh * nkb) * BM2;
   const int mykey = kb + 32 * w + c32;
   const int64_t base = bh * (int64_t)S * D;
   const float sl2 = scale * 1.4426950408889634f;
@@ -682,11 +707,20 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-        const int q = i0 + qi;
-        float p = exp2f(sacc[r] * sl2 - lse_s[qi]);
-        if (q >= S || mykey >= S || (CAUSAL && mykey > q)) p = 0.f;
-        pv[r] = p;
-        dsv[r] = p * (pacc[r] - del_s[qi]);
+        pv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse_s[qi]));
+      }
+      // wave-uniform: ragged tail or a query of this sub-tile before the wave's last key
+      if ((i0 + 32 * t + 32 > S) || (kb + 32 * w + 32 > S) || (CAUSAL && kb + 32 * w + 31 > i0 + 32 * t)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = i0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          if (q >= S || mykey >= S || (CAUSAL && mykey > q)) pv[r] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+        dsv[r] = pv[r] * (pacc[r] - del_s[qi]);
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -743,8 +777,10 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
-  const int64_t bh = blockIdx.y;
-  const int qb = blockIdx.x * BM2;
+  const int nqb = (S + BM2 - 1) / BM2;
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int64_t bh = task / nqb;
+  const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
   const int myq = qb + 32 * w + c32;
   const int64_t base = bh * (int64_t)S * D;
   const float sl2 = scale * 1.4426950408889634f;
@@ -792,12 +828,16 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
       }
       float dsv[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-        float p = exp2f(sacc[r] * sl2 - lse2);
-        if (key >= S || myq >= S || (CAUSAL && key > myq)) p = 0.f;
-        dsv[r] = p * (pacc[r] - dl);
+      for (int r = 0; r < 16; ++r) dsv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse2));
+      if ((j0 + 32 * t + 32 > S) || (qb + 32 * w + 32 > S) || (CAUSAL && j0 + 32 * t + 31 > qb + 32 * w)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          if (key >= S || myq >= S || (CAUSAL && key > myq)) dsv[r] = 0.f;
+        }
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dsv[r] = dsv[r] * (pacc[r] - dl);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ks = 2 * t + kk;
@@ -870,7 +910,7 @@ void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, floa
   if (!v1) {
     dim3 grid2((S + fa::BM2 - 1) / fa::BM2, BH);
     FA_DISPATCH(dt, D, causal,
-      hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC>), grid2, dim3(256), fa::fwd_v2_lds<DD>(), s,
+      hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC>), dim3(grid2.x * grid2.y), dim3(256), fa::fwd_v2_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale));
     return;
   }
@@ -889,10 +929,10 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const uint16_t*)dout, (const uint16_t*)o, delta, rows);
     if (!v1) {
-      hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2, BH), dim3(256),
+      hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
                          fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                          (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale);
-      hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2, BH), dim3(256),
+      hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
                          fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                          (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale);
     } else {

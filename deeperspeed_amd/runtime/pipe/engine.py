@@ -556,7 +556,7 @@ class PipelineEngine(DeepSpeedEngine):
 
     def _zero_grads(self, inputs):
         for t in self._as_list(inputs):
-            if torch.is_tensor(t) and t.grad is not None:
+            if torch.is_tensor(t) and t.is_leaf and t.grad is not None:
                 t.grad.data.zero_()
 
     # ------------------------------------------------------------------ disabled DeepSpeedEngine APIs

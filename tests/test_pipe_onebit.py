@@ -12,7 +12,7 @@ import torch
 from common import run_distributed
 
 
-def _body(out_dir, steps=8, freeze=3):
+def _body(out_dir, steps=8, freeze=3, ckpt_interval=1):
     import torch.distributed as dist
     import deeperspeed_amd as ds
     from deeperspeed_amd.models.gpt_neox import get_config, to_pipeline
@@ -20,8 +20,10 @@ def _body(out_dir, steps=8, freeze=3):
     torch.manual_seed(0)
     cfg = get_config("tiny", num_layers=4, max_seq_len=32)
     topo = PipeDataParallelTopology(num_pp=2, num_dp=2)
+    # per-block activation checkpointing as in the bench (the embedding stage must not be
+    # checkpointed: its only input is integer token ids)
     model = to_pipeline(cfg, num_stages=None, topology=topo, partition_method="uniform", seed_layers=True,
-                        base_seed=11)
+                        base_seed=11, activation_checkpoint_interval=ckpt_interval)
     conf = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2,
             "optimizer": {"type": "OneBitAdam", "params": {"lr": 2e-3, "freeze_step": freeze, "betas": [0.9, 0.9],
                                                             "comm_backend_name": "nccl"}},
