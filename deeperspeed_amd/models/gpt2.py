@@ -19,7 +19,7 @@ from ..ops import native
 from ..ops.attention import attention
 from ..runtime.activation_checkpointing import checkpointing as ds_ckpt
 from ..runtime.zero.partition_parameters import register_external_parameter
-from .gpt_neox import LinearBiasGeLU, lm_loss
+from .gpt_neox import LinearBiasGeLU, OutputLinear, lm_loss, skip_unread_outputs
 
 
 @dataclass
@@ -85,7 +85,14 @@ class GPT2Block(nn.Module):
         self.attn = GPT2Attention(cfg, device, dtype)
         self.ln_2 = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
         self.c_fc = LinearBiasGeLU(cfg.hidden_size, 4 * cfg.hidden_size, approximate=True, device=device, dtype=dtype)
-        self.c_proj = nn.Linear(4 * cfg.hidden_size, cfg.hidden_size, device=device, dtype=dtype)
+        # feeds only the block's final residual sum: skipped during recompute
+        self.c_proj = OutputLinear(4 * cfg.hidden_size, cfg.hidden_size, device=device, dtype=dtype)
+
+    def _block_ckpt(self, x):
+        if ds_ckpt.is_recomputing():
+            with skip_unread_outputs():
+                return self._block(x)
+        return self._block(x)
 
     def _block(self, x):
         x = x + self.attn(self.ln_1(x))
@@ -93,7 +100,7 @@ class GPT2Block(nn.Module):
 
     def forward(self, x):
         if self.cfg.checkpoint_activations and self.training and torch.is_grad_enabled():
-            return ds_ckpt.checkpoint(self._block, x)
+            return ds_ckpt.checkpoint(self._block_ckpt, x)
         return self._block(x)
 
 

@@ -104,6 +104,65 @@ class LinearBiasGeLU(nn.Linear):
         return native.bias_gelu(F.linear(x, self.weight), self.bias, self.approximate)
 
 
+class _GradOnlyLinear(torch.autograd.Function):
+    """y = x W^T + b whose VALUE is never read: forward returns a zero-stride placeholder and
+    costs nothing; backward produces the exact input / weight / bias gradients."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return x.new_zeros(1).expand(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (g2 @ weight).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = g2.t() @ x.reshape(-1, x.shape[-1])
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g2.sum(0)
+        return dx, dw, db
+
+
+_SKIP_OUTPUTS = 0
+
+
+class skip_unread_outputs:
+    """Context for the recompute of ONE checkpointed block whose result is the checkpoint's
+    own output: inside it, OutputLinear layers flagged `skip_in_recompute` produce gradients
+    only.  (Never set for multi-block checkpoint segments, where block i's output is block
+    i+1's input.)"""
+
+    def __enter__(self):
+        global _SKIP_OUTPUTS
+        _SKIP_OUTPUTS += 1
+
+    def __exit__(self, *exc):
+        global _SKIP_OUTPUTS
+        _SKIP_OUTPUTS -= 1
+
+
+class OutputLinear(nn.Linear):
+    """Final projection of a residual branch (attention `dense` with parallel residual, MLP
+    `dense_4h_to_h`).
+
+    Its output only enters the block's residual sum, which no backward reads.  During the
+    block's activation recompute (inside backward) the GEMM is therefore skipped and only
+    gradients are formed: that removes ~20 % of the recomputed forward FLOPs of a GPT-NeoX
+    block."""
+
+    skip_in_recompute = True
+
+    def forward(self, x):
+        if _SKIP_OUTPUTS and self.skip_in_recompute and torch.is_grad_enabled():
+            return _GradOnlyLinear.apply(x, self.weight, self.bias)
+        return F.linear(x, self.weight, self.bias)
+
+
 def make_sparsity_config(cfg: GPTNeoXConfig):
     """Causal (unidirectional) SparsityConfig from cfg.sparse_attention."""
     from ..ops import sparse_attention as sa
@@ -127,7 +186,9 @@ class NeoXAttention(nn.Module):
         self._sparsity = make_sparsity_config(cfg) if cfg.sparse_attention else None
         self._sp_ops = {}
         self.query_key_value = nn.Linear(h, 3 * h, device=device, dtype=dtype)
-        self.dense = nn.Linear(h, h, device=device, dtype=dtype)
+        self.dense = OutputLinear(h, h, device=device, dtype=dtype)
+        # with a sequential residual the attention output feeds post_attention_layernorm
+        self.dense.skip_in_recompute = cfg.use_parallel_residual
 
     def forward(self, x):
         cfg = self.cfg
@@ -170,7 +231,7 @@ class NeoXMLP(nn.Module):
         self.cfg = cfg
         self.dense_h_to_4h = LinearBiasGeLU(cfg.hidden_size, cfg.intermediate_size, cfg.gelu_approximate,
                                             device=device, dtype=dtype)
-        self.dense_4h_to_h = nn.Linear(cfg.intermediate_size, cfg.hidden_size, device=device, dtype=dtype)
+        self.dense_4h_to_h = OutputLinear(cfg.intermediate_size, cfg.hidden_size, device=device, dtype=dtype)
 
     def forward(self, x):
         return self.dense_4h_to_h(self.dense_h_to_4h(x))
@@ -197,9 +258,15 @@ class NeoXTransformerLayer(nn.Module):
         x = x + a
         return x + self.mlp(self.post_attention_layernorm(x))
 
+    def _block_ckpt(self, x):
+        if ds_ckpt.is_recomputing():
+            with skip_unread_outputs():
+                return self._block(x)
+        return self._block(x)
+
     def forward(self, x):
         if self.cfg.checkpoint_activations and self.training and torch.is_grad_enabled():
-            return ds_ckpt.checkpoint(self._block, x)
+            return ds_ckpt.checkpoint(self._block_ckpt, x)
         return self._block(x)
 
 

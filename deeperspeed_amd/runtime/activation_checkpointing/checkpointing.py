@@ -169,6 +169,17 @@ def _gather(rec):
     return full[:n].view(shape)
 
 
+_RECOMPUTE_DEPTH = 0
+
+
+def is_recomputing() -> bool:
+    """True while a checkpointed function is being re-run inside backward.  Modules whose
+    forward OUTPUT is not needed by any backward (e.g. the projection that feeds only a residual
+    sum) can skip computing it then and produce gradients only (models/gpt_neox.py
+    OutputLinear)."""
+    return _RECOMPUTE_DEPTH > 0
+
+
 class CheckpointFunction(torch.autograd.Function):
     """Reentrant checkpoint: forward under no_grad, recompute inside backward."""
 
@@ -243,8 +254,13 @@ class CheckpointFunction(torch.autograd.Function):
         if ctx.fwd_cuda_rng_state is not None:
             _set_cuda_rng_state(ctx.fwd_cuda_rng_state)
         get_cuda_rng_tracker().set_states(ctx.fwd_cuda_rng_state_tracker)
-        with torch.enable_grad():
-            outputs = ctx.run_function(*detached)
+        global _RECOMPUTE_DEPTH
+        _RECOMPUTE_DEPTH += 1
+        try:
+            with torch.enable_grad():
+                outputs = ctx.run_function(*detached)
+        finally:
+            _RECOMPUTE_DEPTH -= 1
         torch.set_rng_state(bwd_cpu_rng)
         if bwd_cuda_rng is not None:
             _set_cuda_rng_state(bwd_cuda_rng)
