@@ -5,6 +5,7 @@ PDSH_MAX_FAN_OUT = 1024
 OPENMPI_LAUNCHER = "openmpi"
 SLURM_LAUNCHER = "slurm"
 MVAPICH_LAUNCHER = "mvapich"
+MOSAICML_LAUNCHER = "mosaicml"
 MVAPICH_TMP_HOSTFILE = "/tmp/deeperspeed_amd_mvapich_hostfile"
 TORCH_DISTRIBUTED_DEFAULT_PORT = 29500
 DEFAULT_HOSTFILE = "/job/hostfile"

@@ -1,8 +1,9 @@
 """Multi-node launch back-ends (reference parity: deepspeed/launcher/multinode_runner.py:1-292):
-PDSH, OpenMPI, MVAPICH and Slurm.  Each builds the command that starts
+PDSH, OpenMPI, MVAPICH, Slurm and MosaicML.  Each builds the command that starts
 `deeperspeed_amd.launcher.launch` (PDSH) or the user script directly (MPI/Slurm, rank from the
 MPI environment) on every node."""
 
+import json
 import os
 import shutil
 import sys
@@ -135,3 +136,35 @@ class SlurmRunner(MultiNodeRunner):
             cmd += self.args.launcher_args.split()
         exports = "--export=ALL" + "".join(f",{k}={v}" for k, v in self.exports.items())
         return cmd + [exports, sys.executable, "-u", self.user_script] + self.user_arguments
+
+
+class MosaicMLRunner(MultiNodeRunner):
+    """MosaicML platform back-end (reference multinode_runner.py:256-292).  The platform starts
+    one copy of this command per node and provides NODE_RANK / MASTER_ADDR / MASTER_PORT in the
+    environment; JSON user arguments are re-serialised compactly (and nested `config_files`
+    strings decoded) so they survive the platform's argument passing."""
+
+    def backend_exists(self):
+        return True
+
+    def parse_user_args(self):
+        out = []
+        for arg in self.args.user_args:
+            if arg.startswith("{") and arg.endswith("}"):
+                try:
+                    d = json.loads(arg)
+                    if "config_files" in d:
+                        d["config_files"] = {k: json.loads(v) for k, v in d["config_files"].items()}
+                except json.JSONDecodeError as e:
+                    raise ValueError("user arguments must be plain JSON (no comments, lowercase true/false)") from e
+                arg = json.dumps(d, separators=(",", ":"))
+            out.append(arg)
+        return out
+
+    def get_cmd(self, environment, active_resources):
+        for key in ("NODE_RANK", "MASTER_ADDR", "MASTER_PORT"):
+            if key not in os.environ:
+                raise RuntimeError(f"{self.name}: {key} must be set by the platform")
+        return [sys.executable, "-u", "-m", "deeperspeed_amd.launcher.launch", f"--world_info={self.world_info_base64}",
+                f"--node_rank={os.environ['NODE_RANK']}", f"--master_addr={os.environ['MASTER_ADDR']}",
+                f"--master_port={os.environ['MASTER_PORT']}", self.user_script] + self.user_arguments

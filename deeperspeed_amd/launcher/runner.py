@@ -19,7 +19,7 @@ import sys
 from copy import deepcopy
 
 from ..utils.logging import logger
-from .constants import (DEEPSPEED_ENVIRONMENT_NAME, DEFAULT_HOSTFILE, EXPORT_ENVS, MVAPICH_LAUNCHER,
+from .constants import (DEEPSPEED_ENVIRONMENT_NAME, DEFAULT_HOSTFILE, EXPORT_ENVS, MOSAICML_LAUNCHER, MVAPICH_LAUNCHER,
                         OPENMPI_LAUNCHER, PDSH_LAUNCHER, SLURM_LAUNCHER, TORCH_DISTRIBUTED_DEFAULT_PORT)
 
 DEEPSPEED_ENVIRONMENT_PATHS = [os.path.expanduser("~"), "."]
@@ -40,7 +40,7 @@ def parse_args(args=None):
                    help="Port used by torch.distributed for communication during training.")
     p.add_argument("--master_addr", default="", type=str, help="IP address of node 0.")
     p.add_argument("--launcher", default=PDSH_LAUNCHER, type=str,
-                   help="Multi-node launcher backend: pdsh, openmpi, mvapich, slurm.")
+                   help="Multi-node launcher backend: pdsh, openmpi, mvapich, slurm, mosaicml.")
     p.add_argument("--launcher_args", default="", type=str, help="Extra arguments for the launcher backend.")
     p.add_argument("--force_multi", action="store_true", help="Force multi-node launch mode on one node.")
     p.add_argument("--comment", default="", type=str, help="Slurm --comment.")
@@ -181,7 +181,7 @@ def main(args=None):
             cmd.append("--detect_xgmi_pairs")
         cmd += [args.user_script] + args.user_args
     else:
-        from .multinode_runner import MVAPICHRunner, OpenMPIRunner, PDSHRunner, SlurmRunner
+        from .multinode_runner import MosaicMLRunner, MVAPICHRunner, OpenMPIRunner, PDSHRunner, SlurmRunner
         launcher = args.launcher.lower()
         if launcher == PDSH_LAUNCHER:
             runner = PDSHRunner(args, world_info_base64)
@@ -191,6 +191,8 @@ def main(args=None):
             runner = MVAPICHRunner(args, world_info_base64, resource_pool)
         elif launcher == SLURM_LAUNCHER:
             runner = SlurmRunner(args, world_info_base64, resource_pool)
+        elif launcher == MOSAICML_LAUNCHER:
+            runner = MosaicMLRunner(args, world_info_base64)
         else:
             raise NotImplementedError(f"Unknown launcher {args.launcher}")
         if not runner.backend_exists():

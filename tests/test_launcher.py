@@ -83,6 +83,23 @@ def test_multinode_cmds():
     assert sl.get_cmd({}, {})[:3] == ["srun", "-n", "8"]
 
 
+def test_mosaicml_runner(monkeypatch):
+    from deeperspeed_amd.launcher.multinode_runner import MosaicMLRunner
+    args = SimpleNamespace(user_script="train.py", launcher_args="",
+                           user_args=['{"a": true, "config_files": {"c": "{\\"x\\": 1}"}}', "--y"])
+    wi = dsrun.encode_world_info({"h0": [0, 1]})
+    mm = MosaicMLRunner(args, wi)
+    assert mm.user_arguments == ['{"a":true,"config_files":{"c":{"x":1}}}', "--y"]
+    monkeypatch.setenv("NODE_RANK", "3")
+    monkeypatch.setenv("MASTER_ADDR", "10.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "1234")
+    cmd = mm.get_cmd({}, {})
+    assert cmd[2:4] == ["-m", "deeperspeed_amd.launcher.launch"]
+    assert "--node_rank=3" in cmd and "--master_addr=10.0.0.1" in cmd and cmd[-3:] == ["train.py"] + mm.user_arguments
+    with pytest.raises(ValueError):
+        MosaicMLRunner(SimpleNamespace(user_script="t.py", user_args=["{bad}"]), wi)
+
+
 _SCRIPT = textwrap.dedent("""
     import os, sys, argparse
     import torch.distributed as dist
