@@ -16,6 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import native
+from ..ops.linear import Linear
 from ..ops.attention import attention
 from ..runtime.activation_checkpointing import checkpointing as ds_ckpt
 from ..runtime.zero.partition_parameters import register_external_parameter
@@ -66,8 +67,8 @@ class GPT2Attention(nn.Module):
     def __init__(self, cfg: GPT2Config, device=None, dtype=None):
         super().__init__()
         self.cfg = cfg
-        self.c_attn = nn.Linear(cfg.hidden_size, 3 * cfg.hidden_size, device=device, dtype=dtype)
-        self.c_proj = nn.Linear(cfg.hidden_size, cfg.hidden_size, device=device, dtype=dtype)
+        self.c_attn = Linear(cfg.hidden_size, 3 * cfg.hidden_size, device=device, dtype=dtype)
+        self.c_proj = Linear(cfg.hidden_size, cfg.hidden_size, device=device, dtype=dtype)
 
     def forward(self, x):
         B, S, H = x.shape

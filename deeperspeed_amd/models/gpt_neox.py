@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import native
+from ..ops.linear import Linear, grad_only_linear, linear
 from ..ops.attention import attention, rotary_split
 from ..runtime.activation_checkpointing import checkpointing as ds_ckpt
 
@@ -101,31 +102,7 @@ class LinearBiasGeLU(nn.Linear):
         self.approximate = approximate
 
     def forward(self, x):
-        return native.bias_gelu(F.linear(x, self.weight), self.bias, self.approximate)
-
-
-class _GradOnlyLinear(torch.autograd.Function):
-    """y = x W^T + b whose VALUE is never read: forward returns a zero-stride placeholder and
-    costs nothing; backward produces the exact input / weight / bias gradients."""
-
-    @staticmethod
-    def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
-        ctx.has_bias = bias is not None
-        return x.new_zeros(1).expand(*x.shape[:-1], weight.shape[0])
-
-    @staticmethod
-    def backward(ctx, g):
-        x, weight = ctx.saved_tensors
-        g2 = g.reshape(-1, g.shape[-1])
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = (g2 @ weight).view(x.shape)
-        if ctx.needs_input_grad[1]:
-            dw = g2.t() @ x.reshape(-1, x.shape[-1])
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = g2.sum(0)
-        return dx, dw, db
+        return native.bias_gelu(linear(x, self.weight), self.bias, self.approximate)
 
 
 _SKIP_OUTPUTS = 0
@@ -159,8 +136,8 @@ class OutputLinear(nn.Linear):
 
     def forward(self, x):
         if _SKIP_OUTPUTS and self.skip_in_recompute and torch.is_grad_enabled():
-            return _GradOnlyLinear.apply(x, self.weight, self.bias)
-        return F.linear(x, self.weight, self.bias)
+            return grad_only_linear(x, self.weight, self.bias)
+        return linear(x, self.weight, self.bias)
 
 
 def make_sparsity_config(cfg: GPTNeoXConfig):
@@ -185,7 +162,7 @@ class NeoXAttention(nn.Module):
         self.layer_number = layer_number
         self._sparsity = make_sparsity_config(cfg) if cfg.sparse_attention else None
         self._sp_ops = {}
-        self.query_key_value = nn.Linear(h, 3 * h, device=device, dtype=dtype)
+        self.query_key_value = Linear(h, 3 * h, device=device, dtype=dtype)
         self.dense = OutputLinear(h, h, device=device, dtype=dtype)
         # with a sequential residual the attention output feeds post_attention_layernorm
         self.dense.skip_in_recompute = cfg.use_parallel_residual
@@ -279,7 +256,7 @@ class GPTNeoX(nn.Module):
         self.embed_in = nn.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
         self.layers = nn.ModuleList([NeoXTransformerLayer(cfg, i, device, dtype) for i in range(cfg.num_layers)])
         self.final_layer_norm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
-        self.embed_out = nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
+        self.embed_out = Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
         self.reset_parameters()
 
     @torch.no_grad()
@@ -329,7 +306,7 @@ class _FinalPipe(nn.Module):
     def __init__(self, cfg, device=None, dtype=None):
         super().__init__()
         self.final_layer_norm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
-        self.embed_out = nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
+        self.embed_out = Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
         nn.init.normal_(self.embed_out.weight, 0.0, cfg.init_std)
 
     def forward(self, x):

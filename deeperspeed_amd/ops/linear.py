@@ -1,0 +1,130 @@
+"""Linear layers whose weight-gradient GEMM accumulates straight into the bound gradient.
+
+The engine binds `p.grad` of every ZeRO-managed parameter to a view of a flat gradient
+arena (ZeRO-0/1, single-rank ZeRO-3) or of a unit's gathered gradient bucket (ZeRO-3).
+Stock autograd then forms each weight gradient in a fresh [out, in] buffer and
+`AccumulateGrad` adds it into the bound view: one extra read + write of the full gradient
+per micro-batch (an elementwise add over every weight; 2.5 % of a 20B step on MI355X).
+
+Here the wgrad is one hipBLASLt GEMM with beta = 1 (`grad.addmm_(dy^T, x)`), which reads
+the bound gradient in the epilogue and accumulates in fp32 before rounding once.  The
+backward returns None for that parameter; autograd's AccumulateGrad node still runs and fires
+the parameter's post-accumulate-grad hooks (the ZeRO bucket bookkeeping) in the usual order.
+When no gradient is bound (first use, ZeRO-2 buckets that steal `p.grad`, plain torch
+training), the layer returns the gradient to autograd as usual.
+
+Reference counterpart: the weight-gradient GEMMs of `csrc/transformer/ds_transformer_cuda.cpp`
+(`_ff1.Backward`, `_ff2.Backward`, `_attn_out_linear.Backward`, `_qkv_linear.Backward`,
+`ds_transformer_cuda.cpp:370-540`), which write into the parameter's `.grad` storage.
+
+Set DSA_FUSE_WGRAD=0 to disable (identical math up to one rounding of the accumulate).
+"""
+
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+FUSE_WGRAD = os.environ.get("DSA_FUSE_WGRAD", "1") != "0"
+
+
+_count = [0]  # in-place accumulations performed (tests / diagnostics)
+
+
+def fused_wgrad_count() -> int:
+    return _count[0]
+
+
+def _bound_grad(p: torch.Tensor):
+    g = p.grad
+    if g is None or g.shape != p.shape or g.dtype != p.dtype or g.device != p.device:
+        return None
+    return g
+
+
+def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, bias, need_w: bool,
+                           need_b: bool):
+    """Weight/bias gradients of y = x W^T (+ b) for flattened g2 = dy [M, out], x2 = x [M, in].
+
+    Returns (dw, db) for autograd, or None entries for parameters whose gradient was
+    accumulated in place."""
+    dw = db = None
+    fuse = FUSE_WGRAD and need_w and (bias is None or not need_b or _bound_grad(bias) is not None)
+    gw = _bound_grad(weight) if fuse else None
+    if gw is not None and gw.is_contiguous():
+        gw.addmm_(g2.t(), x2)
+        if bias is not None and need_b:
+            bias.grad.add_(g2.sum(0))
+        _count[0] += 1
+        # returning None still runs the leaf's AccumulateGrad node, which leaves the bound
+        # gradient untouched and fires its post-accumulate hooks (ZeRO bucket bookkeeping)
+        return None, None
+    if need_w:
+        dw = g2.t() @ x2
+    if bias is not None and need_b:
+        db = g2.sum(0)
+    return dw, db
+
+
+class _AccumLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.bias = bias
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        bias = ctx.bias
+        g2 = g.reshape(-1, g.shape[-1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (g2 @ weight).view(x.shape)
+        dw, db = accumulate_param_grads(g2, x.reshape(-1, x.shape[-1]), weight, bias, ctx.needs_input_grad[1],
+                                        bias is not None and ctx.needs_input_grad[2])
+        return dx, dw, db
+
+
+class _GradOnlyLinear(torch.autograd.Function):
+    """y = x W^T + b whose VALUE is never read: forward returns a zero-stride placeholder and
+    costs nothing; backward produces the exact input / weight / bias gradients."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.bias = bias
+        return x.new_zeros(1).expand(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        bias = ctx.bias
+        g2 = g.reshape(-1, g.shape[-1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (g2 @ weight).view(x.shape)
+        dw, db = accumulate_param_grads(g2, x.reshape(-1, x.shape[-1]), weight, bias, ctx.needs_input_grad[1],
+                                        bias is not None and ctx.needs_input_grad[2])
+        return dx, dw, db
+
+
+def linear(x, weight, bias=None):
+    """F.linear whose weight gradient accumulates in place when a gradient is bound."""
+    if torch.is_grad_enabled() and weight.requires_grad:
+        return _AccumLinear.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+def grad_only_linear(x, weight, bias=None):
+    return _GradOnlyLinear.apply(x, weight, bias)
+
+
+class Linear(nn.Linear):
+    """nn.Linear with in-place weight-gradient accumulation (state-dict compatible)."""
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias)
