@@ -67,22 +67,25 @@ def parse():
     return p.parse_args()
 
 
-def plan_memory(cfg, mb, seq, world, offload, ckpt):
+def plan_memory(cfg, mb, seq, world, offload, ckpt, ga=1):
     """Bytes of HBM one rank needs: ZeRO-3 model states + activations + transient buffers.
 
-    States per parameter: bf16 weight shard 2 B + bf16 grad shard 2 B + fp32 moments 8 B
-    + fp32 master 4 B (2 B int16 residual with compact_master, 0 B when offloaded).
-    Calibrated on MI355X: 20B, N=1, compact, recompute on -> planned 279 GiB, measured peak
-    274.7 GiB.  Activations per layer with the fused attention
-    kernel (no S x S scores), measured on MI355X: ~36 * s * b * h bytes in bf16 without
-    recompute, one s*b*h layer input with it.  Transients: two gathered ZeRO-3 units, the
-    logits (fp32 for the loss) and allocator slack."""
+    States per parameter: bf16 weight shard 2 B + gradient shard + fp32 moments 8 B + fp32
+    master 4 B (2 B int16 residual with compact_master, 0 B when offloaded).  The gradient
+    shard is bf16 (2 B) on one rank (gradients accumulate in place into the bound shard) and
+    fp32 (4 B) for N >= 2 with gradient accumulation (reduce-scattered micro-batch gradients
+    are summed in fp32).  Measured on MI355X (DSA_MEMTRACE=1, profiles/aux/memtrace_*.log):
+    20B, N=1, compact, recompute on -> planned 279 GiB, peak 274.7 GiB; activations of one
+    GPT-NeoX layer without recompute = 32.0 * s * b * h bytes (budgeted as 34), one s*b*h
+    layer input with it.  Transients: two gathered ZeRO-3 units, the logits (bf16 + grad,
+    fused HIP cross-entropy) and allocator slack."""
     p = cfg.num_params()
-    per_param = {"none": 16, "compact": 14, "master": 12, "all": 4, "nvme": 4}[offload]
+    grad = 4 if (world > 1 and ga > 1) else 2
+    per_param = {"none": 14, "compact": 12, "master": 10, "all": 2, "nvme": 2}[offload] + grad
     states = p * per_param / world
     sbh = seq * mb * cfg.hidden_size
-    act_layer = 2 * sbh if ckpt else 36 * sbh
-    acts = cfg.num_layers * act_layer + (36 * sbh if ckpt else 0)
+    act_layer = 2 * sbh if ckpt else 34 * sbh
+    acts = cfg.num_layers * act_layer + (34 * sbh if ckpt else 0)
     logits = seq * mb * cfg.vocab_size * 4  # bf16 logits + bf16 grad (fused HIP cross-entropy)
     transient = 2 * 2 * 2e8 * 2 + logits + 2 * 2**30
     return states + acts + transient
@@ -126,28 +129,30 @@ def main():
     if args.sparse:
         over["sparse_attention"] = {"mode": args.sparse, "block": args.block}
     cfg = get_config(args.model, max_seq_len=args.seq, checkpoint_activations=True, **over)
-    big = cfg.num_params() > 5e9
+    big = get_config(args.model).num_params() > 5e9  # batch shape of the full model, also under --layers
     mb = args.micro_batch or (4 if big else 8)
     ga = args.grad_accum or (4 if big else 2)
     hbm = torch.cuda.get_device_properties(local).total_memory
     budget = 0.97 * hbm / share
-    # model-state layout: everything in HBM (16 B/param) > compact fp32 master (14 B/param)
-    # > fp32 master offloaded to host (12 B/param in HBM); then recompute only if needed
+    # model-state layout: compact fp32 master (bf16 weight + int16 residual, exact, same Adam
+    # bytes as a separate fp32 master, 2 B/param less) > everything in HBM > fp32 master
+    # offloaded to host; then recompute only if needed
     offload = args.offload
     if offload == "auto":
-        offload = next((o for o in ("none", "compact", "master")
-                        if plan_memory(cfg, mb, args.seq, world, o, True) < budget), "master")
+        offload = next((o for o in ("compact", "none", "master")
+                        if plan_memory(cfg, mb, args.seq, world, o, True, ga) < budget), "master")
     ckpt = args.ckpt
     if ckpt == "auto":
-        ckpt = "off" if plan_memory(cfg, mb, args.seq, world, offload, False) < budget else "on"
+        ckpt = "off" if plan_memory(cfg, mb, args.seq, world, offload, False, ga) < budget else "on"
     cfg.checkpoint_activations = ckpt == "on"
     # ZeRO-3 parameter retention (stage3_max_live_parameters): HBM left after states and
     # activations keeps gathered bf16 units resident between their forward and backward use
     # and across the micro-batches of one optimizer step, so a unit is all-gathered once per
     # step instead of twice per micro-batch when the whole model fits (it does at N>=2 on
     # 288 GB parts: 41 GB of bf16 weights for 20B)
-    spare = budget - plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on")
-    live = int(max(0.0, min(spare / 2, cfg.num_params() * 1.0)))
+    # keep a reserve of 3 % of HBM for allocator fragmentation and RCCL/runtime buffers
+    spare = budget - plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) - 0.03 * hbm / share
+    live = int(max(0.0, min(spare / 2, cfg.num_params() * 1.0)))  # bf16 elements
     if args.max_live is not None:
         live = int(args.max_live)
     zcfg = {"stage": args.zero, "overlap_comm": True, "reduce_bucket_size": int(2e8),
@@ -175,7 +180,7 @@ def main():
     }
     log(f"model={args.model} params={cfg.num_params() / 1e9:.2f}B world={world} mb={mb} ga={ga} seq={args.seq} "
         f"zero={args.zero} offload={offload} ckpt={ckpt} live={live / 1e9:.1f}B hbm={hbm / 2**30:.0f} GiB "
-        f"planned={plan_memory(cfg, mb, args.seq, world, offload, ckpt == 'on') / 2**30:.0f} GiB")
+        f"planned={plan_memory(cfg, mb, args.seq, world, offload, ckpt == 'on', ga) / 2**30:.0f} GiB")
     if args.pipe > 1:
         return run_pipeline(args, cfg, mb, ga, world, rank, dev)
     t0 = time.time()
@@ -212,7 +217,26 @@ def main():
                 ph[name] += time.time() - t
                 if name == "fwd":
                     loss = r
+                if memtrace:
+                    log(f"mem after micro {i} {name}: {torch.cuda.memory_allocated() / 2**30:.2f} GiB "
+                        f"(peak {torch.cuda.max_memory_allocated() / 2**30:.2f})")
         return loss, ph
+
+    memtrace = os.environ.get("DSA_MEMTRACE", "0") == "1"
+    if memtrace:  # per-layer activation footprint of the first forward (planner calibration)
+        layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
+        marks = []
+
+        def _mark(m, inp, out, idx=[0]):
+            if len(marks) < len(layers):
+                marks.append(torch.cuda.memory_allocated())
+                if len(marks) in (1, 2, len(layers)):
+                    log(f"mem after layer {len(marks) - 1} fwd: {marks[-1] / 2**30:.2f} GiB")
+                if len(marks) == len(layers) and len(marks) > 2:
+                    log(f"activation bytes/layer = {(marks[-1] - marks[1]) / (len(marks) - 2) / 2**20:.1f} MiB "
+                        f"= {(marks[-1] - marks[1]) / (len(marks) - 2) / (args.seq * mb * cfg.hidden_size):.2f} sbh")
+        for m in layers:
+            m.register_forward_hook(_mark)
 
     for i in range(args.warmup):
         ts = time.time()
@@ -270,7 +294,7 @@ def main():
                    "model_tflops_per_gpu": round(tps * flops_tok / world / 1e12, 1),
                    "final_loss": round(float(loss), 4),
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
-                   "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on") / 2**30, 1),
+                   "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) / 2**30, 1),
                    "max_live_parameters": live,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N), BASELINE.md derived target"},
     }
