@@ -114,6 +114,95 @@ __global__ void __launch_bounds__(256) rotary_split_bwd_kernel(const T* __restri
   }
 }
 
+// Row form of rotary_split for the common (head_dim, rotary_dim) pairs: one thread per
+// (b, s, head, q|k|v) row of HD elements, the row held in registers so the rotate-half
+// partner is a compile-time register (no partner reloads, no 64-bit index math per element).
+// Consecutive threads read consecutive HD-element pieces of the qkv row (fully used 16-B
+// loads); each thread writes one contiguous HD-element row of q, k or v.
+template <typename T, int HD, int ROT>
+__global__ void __launch_bounds__(256) rotary_split_fwd_row_kernel(const T* __restrict__ qkv, T* __restrict__ q,
+                                                                   T* __restrict__ k, T* __restrict__ v,
+                                                                   const float2* __restrict__ cs, int rows, int S,
+                                                                   int NH, float qscale) {
+  constexpr int NVEC = HD / 8;
+  constexpr int HALF = ROT / 2;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * 3) return;
+  const int which = t % 3;
+  const int item = t / 3;  // (b, s, h)
+  const int h = item % NH;
+  const int bs = item / NH;
+  const int s = bs % S;
+  const int b = bs / S;
+  const T* src = qkv + (int64_t)t * HD;
+  float x[NVEC][8];
+#pragma unroll
+  for (int i = 0; i < NVEC; ++i) Vec16<T>::load(src + 8 * i, x[i]);
+  if (ROT > 0 && which < 2) {
+    const float2* c = cs + (int64_t)s * HALF;
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) {
+      const float2 cc = c[i];
+      const float a = x[i / 8][i % 8], p = x[(i + HALF) / 8][(i + HALF) % 8];
+      x[i / 8][i % 8] = a * cc.x - p * cc.y;
+      x[(i + HALF) / 8][(i + HALF) % 8] = p * cc.x + a * cc.y;
+    }
+  }
+  if (which == 0) {
+#pragma unroll
+    for (int i = 0; i < NVEC; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[i][j] *= qscale;
+  }
+  T* dst = (which == 0 ? q : (which == 1 ? k : v)) + (((int64_t)b * NH + h) * S + s) * HD;
+#pragma unroll
+  for (int i = 0; i < NVEC; ++i) Vec16<T>::store(dst + 8 * i, x[i]);
+}
+
+template <typename T, int HD, int ROT>
+__global__ void __launch_bounds__(256) rotary_split_bwd_row_kernel(const T* __restrict__ dq, const T* __restrict__ dk,
+                                                                   const T* __restrict__ dv, T* __restrict__ dqkv,
+                                                                   const float2* __restrict__ cs, int rows, int S,
+                                                                   int NH, float qscale) {
+  constexpr int NVEC = HD / 8;
+  constexpr int HALF = ROT / 2;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * 3) return;
+  const int which = t % 3;
+  const int item = t / 3;
+  const int h = item % NH;
+  const int bs = item / NH;
+  const int s = bs % S;
+  const int b = bs / S;
+  const T* src = (which == 0 ? dq : (which == 1 ? dk : dv)) + (((int64_t)b * NH + h) * S + s) * HD;
+  float g[NVEC][8];
+#pragma unroll
+  for (int i = 0; i < NVEC; ++i) Vec16<T>::load(src + 8 * i, g[i]);
+  if (ROT > 0 && which < 2) {
+    const float2* c = cs + (int64_t)s * HALF;
+    // y1 = x1 c - x2 s ; y2 = x2 c + x1 s  =>  dx1 = dy1 c + dy2 s ; dx2 = dy2 c - dy1 s
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) {
+      const float2 cc = c[i];
+      const float a = g[i / 8][i % 8], p = g[(i + HALF) / 8][(i + HALF) % 8];
+      g[i / 8][i % 8] = a * cc.x + p * cc.y;
+      g[(i + HALF) / 8][(i + HALF) % 8] = p * cc.x - a * cc.y;
+    }
+  }
+  if (which == 0) {
+#pragma unroll
+    for (int i = 0; i < NVEC; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[i][j] *= qscale;
+  }
+  T* dst = dqkv + (int64_t)t * HD;
+#pragma unroll
+  for (int i = 0; i < NVEC; ++i) Vec16<T>::store(dst + 8 * i, g[i]);
+}
+
+// (HD, ROT) pairs of the GPT-NeoX / GPT-3 presets; anything else takes the vector kernels.
+#define DSA_ROTARY_ROW_CASES(X) X(64, 16) X(64, 64) X(80, 20) X(96, 24) X(96, 96) X(128, 32) X(128, 64) X(128, 128)
+
 // --------------------------------------------------------------------------------------
 // Softmax over rows of scores [R, C] with row r belonging to query position
 // q = r % Sq (causal: keys > q + (C - Sq) masked). Optional additive mask [Bm, Sq, C]
@@ -236,6 +325,17 @@ static int elem_grid(int64_t work) {
 
 void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const float* cs, int B, int S, int NH,
                              int HD, int ROT, float qscale, int dt, hipStream_t s) {
+  const int rows = B * S * NH;
+  const int grid = (rows * 3 + 255) / 256;
+#define DSA_ROT_FWD(hd, rot)                                                                                   \
+  if (HD == hd && ROT == rot) {                                                                                \
+    DSA_DISPATCH_16(dt, T,                                                                                     \
+      hipLaunchKernelGGL((rotary_split_fwd_row_kernel<T, hd, rot>), dim3(grid), dim3(256), 0, s, (const T*)qkv, \
+                         (T*)q, (T*)k, (T*)v, (const float2*)cs, rows, S, NH, qscale));                        \
+    return;                                                                                                    \
+  }
+  if ((int64_t)rows * 3 < (1LL << 31)) { DSA_ROTARY_ROW_CASES(DSA_ROT_FWD) }
+#undef DSA_ROT_FWD
   const int64_t work = (int64_t)B * S * NH * 3 * HD / 8;
   DSA_DISPATCH_16(dt, T,
     hipLaunchKernelGGL((rotary_split_fwd_kernel<T>), dim3(elem_grid(work)), dim3(256), 0, s, (const T*)qkv, (T*)q,
@@ -244,6 +344,17 @@ void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const f
 
 void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, void* dqkv, const float* cs, int B,
                              int S, int NH, int HD, int ROT, float qscale, int dt, hipStream_t s) {
+  const int rows = B * S * NH;
+  const int grid = (rows * 3 + 255) / 256;
+#define DSA_ROT_BWD(hd, rot)                                                                                   \
+  if (HD == hd && ROT == rot) {                                                                                \
+    DSA_DISPATCH_16(dt, T,                                                                                     \
+      hipLaunchKernelGGL((rotary_split_bwd_row_kernel<T, hd, rot>), dim3(grid), dim3(256), 0, s, (const T*)dq,  \
+                         (const T*)dk, (const T*)dv, (T*)dqkv, (const float2*)cs, rows, S, NH, qscale));       \
+    return;                                                                                                    \
+  }
+  if ((int64_t)rows * 3 < (1LL << 31)) { DSA_ROTARY_ROW_CASES(DSA_ROT_BWD) }
+#undef DSA_ROT_BWD
   const int64_t work = (int64_t)B * S * NH * 3 * HD / 8;
   DSA_DISPATCH_16(dt, T,
     hipLaunchKernelGGL((rotary_split_bwd_kernel<T>), dim3(elem_grid(work)), dim3(256), 0, s, (const T*)dq,

@@ -96,7 +96,7 @@ def test_sumsq_and_colsum():
     assert torch.allclose(native.colsum(y).float(), y.float().sum(0), atol=0.2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("hd,rot", [(96, 24), (128, 32), (64, 64)])
+@pytest.mark.parametrize("hd,rot", [(96, 24), (128, 32), (64, 64), (96, 96), (32, 8)])
 def test_rotary_split_matches_reference(hd, rot):
     from deeperspeed_amd.ops import attention as A
     torch.manual_seed(3)
