@@ -74,8 +74,9 @@ class GPT2Attention(nn.Module):
         B, S, H = x.shape
         nh, hd = self.cfg.num_heads, self.cfg.head_dim
         q, k, v = self.c_attn(x).view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)
-        ctx = attention(q.contiguous(), k.contiguous(), v.contiguous(), causal=True, softmax_scale=1.0 / math.sqrt(hd))
-        return self.c_proj(ctx.transpose(1, 2).reshape(B, S, H))
+        ctx = attention(q.contiguous(), k.contiguous(), v.contiguous(), causal=True, softmax_scale=1.0 / math.sqrt(hd),
+                        out_layout="bshd")
+        return self.c_proj(ctx.reshape(B, S, H))
 
 
 class GPT2Block(nn.Module):

@@ -123,6 +123,31 @@ class skip_unread_outputs:
         _SKIP_OUTPUTS -= 1
 
 
+class _GradOnlySum(torch.autograd.Function):
+    """Residual sum whose value is never read (the recomputed block output): no kernel in
+    forward, the incoming gradient passed to every summand in backward."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        ctx.n = len(xs)
+        return xs[0].new_zeros(1).expand(xs[0].shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g,) * ctx.n
+
+
+def residual_sum(*xs):
+    """x + branch outputs; inside skip_unread_outputs() (the recompute of a checkpointed block,
+    whose output only seeds backward) the two full-tensor adds are skipped."""
+    if _SKIP_OUTPUTS and torch.is_grad_enabled():
+        return _GradOnlySum.apply(*xs)
+    out = xs[0] + xs[1]
+    for x in xs[2:]:
+        out = out + x
+    return out
+
+
 class OutputLinear(nn.Linear):
     """Final projection of a residual branch (attention `dense` with parallel residual, MLP
     `dense_4h_to_h`).
@@ -177,7 +202,8 @@ class NeoXAttention(nn.Module):
             ctx = self._sparse_attention(q, k, v)
         else:
             ctx = attention(q, k, v, causal=True, softmax_scale=1.0, dropout_p=cfg.attention_dropout,
-                            training=self.training)
+                            training=self.training, out_layout="bshd")
+            return self.dense(ctx.reshape(B, S, H))  # [B,S,NH,HD] written by the kernel: free view
         ctx = ctx.transpose(1, 2).reshape(B, S, H)
         return self.dense(ctx)
 
@@ -231,9 +257,9 @@ class NeoXTransformerLayer(nn.Module):
         a = self.attention(self.input_layernorm(x))
         if self.cfg.use_parallel_residual:
             m = self.mlp(self.post_attention_layernorm(x))
-            return x + a + m
+            return residual_sum(x, a, m)
         x = x + a
-        return x + self.mlp(self.post_attention_layernorm(x))
+        return residual_sum(x, self.mlp(self.post_attention_layernorm(x)))
 
     def _block_ckpt(self, x):
         if ds_ckpt.is_recomputing():

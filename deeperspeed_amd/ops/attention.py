@@ -131,18 +131,20 @@ def masked_softmax(scores, mask=None, scale: float = 1.0, causal: bool = False, 
 
 
 def attention(q, k, v, causal: bool = True, mask=None, softmax_scale: float = 1.0, dropout_p: float = 0.0,
-              training: bool = False, use_flash=None):
-    """q,k,v [B,NH,S,HD] -> [B,NH,S,HD].  q is expected pre-scaled when softmax_scale == 1.
-    The fused kernel is used for self-attention without mask/dropout unless `use_flash` is
-    False or DSA_FLASH_ATTN=0."""
+              training: bool = False, use_flash=None, out_layout: str = "bhsd"):
+    """q,k,v [B,NH,S,HD] -> [B,NH,S,HD] (out_layout "bhsd") or [B,S,NH,HD] ("bshd", which the
+    flash kernel writes directly so `.reshape(B, S, NH*HD)` is free).  q is expected
+    pre-scaled when softmax_scale == 1.  The fused kernel is used for self-attention without
+    mask/dropout unless `use_flash` is False or DSA_FLASH_ATTN=0."""
     if use_flash is None:
         use_flash = os.environ.get("DSA_FLASH_ATTN", "1") != "0"
     if (use_flash and q.is_cuda and dropout_p == 0.0 and mask is None and q.shape == k.shape == v.shape
             and native.has_flash_attention(q)):
-        return native.flash_attention(q, k, v, causal, softmax_scale)
+        return native.flash_attention(q, k, v, causal, softmax_scale, out_layout=out_layout)
     B, NH, S, HD = q.shape
     scores = torch.matmul(q, k.transpose(-1, -2))
     probs = masked_softmax(scores, mask, softmax_scale, causal, NH)
     if dropout_p > 0 and training:
         probs = torch.nn.functional.dropout(probs, p=dropout_p)
-    return torch.matmul(probs, v)
+    out = torch.matmul(probs, v)
+    return out.transpose(1, 2) if out_layout == "bshd" else out

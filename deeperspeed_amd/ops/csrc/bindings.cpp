@@ -486,8 +486,9 @@ Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dloss) {
   return dx;
 }
 
-// Fused attention. q,k,v [B, H, S, D] contiguous 16-bit -> (o [B,H,S,D], lse [B,H,S] fp32)
-std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale) {
+// Fused attention. q,k,v [B, H, S, D] contiguous 16-bit -> (o, lse [B,H,S] fp32) with o [B,H,S,D], or
+// [B,S,H,D] when out_bshd (token-major: viewed as [B,S,H*D] by the output projection, no transpose).
+std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, double scale, bool out_bshd) {
   check_dev(q, "q"); check_dev(k, "k"); check_dev(v, "v");
   TORCH_CHECK(q.dim() == 4 && q.sizes() == k.sizes() && q.sizes() == v.sizes(), "flash_attn: q/k/v shape mismatch");
   TORCH_CHECK(q.scalar_type() != at::kFloat && q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(),
@@ -496,29 +497,36 @@ std::vector<Tensor> flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, do
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
   TORCH_CHECK(dsa::flash_supported((int)D), "flash_attn: head dim must be 64, 96 or 128");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
-  Tensor o = at::empty_like(q);
+  Tensor o = out_bshd ? at::empty({B, S, H, D}, q.options()) : at::empty_like(q);
   Tensor lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   dsa::launch_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)(B * H),
-                        (int)S, (int)D, causal, (float)scale, dcode(q), cur_stream());
+                        (int)S, (int)D, causal, (float)scale, dcode(q), cur_stream(), out_bshd ? (int)H : 0);
   return {o, lse};
 }
 
+// dout and o in the layout flash_attn_fwd produced (o_bshd: [B,S,H,D]); dq, dk, dv [B,H,S,D].
 std::vector<Tensor> flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal,
-                                   double scale) {
-  for (auto* t : {&dout, &q, &k, &v, &o}) {
+                                   double scale, bool o_bshd) {
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
+  for (auto* t : {&q, &k, &v}) {
     check_dev(*t, "flash_attn_bwd");
     TORCH_CHECK(t->sizes() == q.sizes() && t->scalar_type() == q.scalar_type() && t->is_contiguous(),
-                "flash_attn_bwd: operands must match q");
+                "flash_attn_bwd: q/k/v must match");
+  }
+  const std::vector<int64_t> oshape = o_bshd ? std::vector<int64_t>{B, S, H, D} : std::vector<int64_t>{B, H, S, D};
+  for (auto* t : {&dout, &o}) {
+    check_dev(*t, "flash_attn_bwd");
+    TORCH_CHECK(t->sizes() == at::IntArrayRef(oshape) && t->scalar_type() == q.scalar_type() && t->is_contiguous(),
+                "flash_attn_bwd: dout/o must be contiguous in the forward's output layout");
   }
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == q.numel() / q.size(3),
               "flash_attn_bwd: lse");
-  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
   Tensor dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
   Tensor delta = at::empty_like(lse);
   dsa::launch_flash_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                         delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)(B * H), (int)S,
-                        (int)D, causal, (float)scale, dcode(q), cur_stream());
+                        (int)D, causal, (float)scale, dcode(q), cur_stream(), o_bshd ? (int)H : 0);
   return {dq, dk, dv};
 }
 

@@ -99,9 +99,9 @@ void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n
 // flash_attn.hip: q,k,v,o [BH, S, D] (D in 64/96/128), lse/delta [BH, S] fp32
 bool flash_supported(int D);
 void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
-                      bool causal, float scale, int dt, hipStream_t s);
+                      bool causal, float scale, int dt, hipStream_t s, int onh = 0);
 void launch_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                       float* delta, void* dq, void* dk, void* dv, int BH, int S, int D, bool causal, float scale,
-                      int dt, hipStream_t s);
+                      int dt, hipStream_t s, int onh = 0);
 
 }  // namespace dsa

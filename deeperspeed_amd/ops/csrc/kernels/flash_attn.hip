@@ -197,20 +197,31 @@ __global__ void __launch_bounds__(256) fwd_kernel(const uint16_t* __restrict__ Q
   }
 }
 
+// O / dO addressing: onh == 0 -> [B*H, S, D] (head-major, like q/k/v); onh == H -> [B, S, H, D]
+// (token-major: the attention output is consumed as [B, S, H*D] by the output projection with
+// no transpose copy, and its gradient arrives in that layout).
+template <int D>
+__device__ __forceinline__ int64_t o_base(int64_t bh, int S, int onh) {
+  return onh ? ((bh / onh) * (int64_t)S * onh + bh % onh) * D : bh * (int64_t)S * D;
+}
+template <int D>
+__device__ __forceinline__ int o_ld(int onh) { return onh ? onh * D : D; }
+
 // ======================================================================== backward: delta
 template <typename T, int D>
 __global__ void __launch_bounds__(256) delta_kernel(const uint16_t* __restrict__ dO, const uint16_t* __restrict__ O,
-                                                    float* __restrict__ delta, int64_t rows) {
-  // 8 lanes per row, 16-byte loads
+                                                    float* __restrict__ delta, int64_t rows, int S, int onh) {
+  // 8 lanes per row, 16-byte loads; row = bh * S + s (delta is head-major like LSE)
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t row = t >> 3;
   const int sub = t & 7;
   float acc = 0.f;
   if (row < rows) {
+    const int64_t off = o_base<D>(row / S, S, onh) + (row % S) * o_ld<D>(onh);
     for (int c = sub; c < D / 8; c += 8) {
       float a[8], b[8];
-      Vec16<T>::load(reinterpret_cast<const T*>(dO) + row * D + c * 8, a);
-      Vec16<T>::load(reinterpret_cast<const T*>(O) + row * D + c * 8, b);
+      Vec16<T>::load(reinterpret_cast<const T*>(dO) + off + c * 8, a);
+      Vec16<T>::load(reinterpret_cast<const T*>(O) + off + c * 8, b);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc = fmaf(a[j], b[j], acc);
     }
@@ -446,13 +457,14 @@ __device__ __forceinline__ int xcd_task(int lin, int n) {
 }
 
 template <int D>
-__device__ __forceinline__ void tile_load(uint4 (&r)[D / 32], const uint16_t* __restrict__ g, int r0, int S) {
+__device__ __forceinline__ void tile_load(uint4 (&r)[D / 32], const uint16_t* __restrict__ g, int r0, int S,
+                                          int ld = D) {
   constexpr int CH = D / 8;
 #pragma unroll
   for (int k = 0; k < D / 32; ++k) {
     const int c = threadIdx.x + 256 * k;
     const int row = c / CH, ch = c - row * CH;
-    r[k] = (r0 + row < S) ? *reinterpret_cast<const uint4*>(g + (int64_t)(r0 + row) * D + ch * 8)
+    r[k] = (r0 + row < S) ? *reinterpret_cast<const uint4*>(g + (int64_t)(r0 + row) * ld + ch * 8)
                           : make_uint4(0, 0, 0, 0);
   }
 }
@@ -484,7 +496,7 @@ __device__ __forceinline__ s16x8 pack8_h(const float* v, int base) {
 template <typename T, int D, bool CAUSAL>
 __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
-                                                        float* __restrict__ LSE, int S, float scale) {
+                                                        float* __restrict__ LSE, int S, float scale, int onh) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -600,7 +612,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   }
   if (myq < S) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
-    uint16_t* orow = O + (bh * (int64_t)S + myq) * D;
+    uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh);
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -631,7 +643,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
                                                              const float* __restrict__ LSE,
                                                              const float* __restrict__ DELTA,
                                                              uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
-                                                             int S, float scale) {
+                                                             int S, float scale, int onh) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   float* stats = reinterpret_cast<float*>(smem + 4 * TS);  // [2 stages][LSE 64 | DELTA 64]
@@ -644,6 +656,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   const int kb = (task - (int)bh * nkb) * BM2;
   const int mykey = kb + 32 * w + c32;
   const int64_t base = bh * (int64_t)S * D;
+  const int64_t obase = o_base<D>(bh, S, onh);
   const float sl2 = scale * 1.4426950408889634f;
 
   s16x8 kf[D / 16], vf[D / 16];
@@ -664,7 +677,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   float st_l = 0.f, st_d = 0.f;
   auto load_tile = [&](int i0) {
     tile_load<D>(qr, Q + base, i0, S);
-    tile_load<D>(orr, dO + base, i0, S);
+    tile_load<D>(orr, dO + obase, i0, S, o_ld<D>(onh));
     if (threadIdx.x < BN2) {
       const int q = i0 + threadIdx.x;
       st_l = q < S ? LSE[bh * (int64_t)S + q] * 1.4426950408889634f : 0.f;
@@ -771,7 +784,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
                                                            const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ LSE,
                                                            const float* __restrict__ DELTA, uint16_t* __restrict__ dQ,
-                                                           int S, float scale) {
+                                                           int S, float scale, int onh) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -789,7 +802,9 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) {
     qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Q + base + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
-    of[ks] = myq < S ? *reinterpret_cast<const s16x8*>(dO + base + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
+    of[ks] = myq < S ? *reinterpret_cast<const s16x8*>(dO + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh) +
+                                                         16 * ks + 8 * h)
+                     : s16x8{};
   }
   const float lse2 = myq < S ? LSE[bh * (int64_t)S + myq] * 1.4426950408889634f : 0.f;
   const float dl = myq < S ? DELTA[bh * (int64_t)S + myq] : 0.f;
@@ -905,13 +920,14 @@ template <int D> constexpr int dq_lds() { return (2 * BN * (D + 8) + 4 * 16 * (B
 bool flash_supported(int D) { return D == 64 || D == 96 || D == 128; }
 
 void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
-                      bool causal, float scale, int dt, hipStream_t s) {
+                      bool causal, float scale, int dt, hipStream_t s, int onh) {
   static const bool v1 = getenv("DSA_FLASH_FWD_V1") != nullptr;
-  if (!v1) {
+  if (!v1 || onh) {
     dim3 grid2((S + fa::BM2 - 1) / fa::BM2, BH);
     FA_DISPATCH(dt, D, causal,
       hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC>), dim3(grid2.x * grid2.y), dim3(256), fa::fwd_v2_lds<DD>(), s,
-                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale));
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale,
+                         onh));
     return;
   }
   dim3 grid((S + fa::BM - 1) / fa::BM, BH);
@@ -922,19 +938,20 @@ void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, floa
 
 void launch_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                       float* delta, void* dq, void* dk, void* dv, int BH, int S, int D, bool causal, float scale,
-                      int dt, hipStream_t s) {
+                      int dt, hipStream_t s, int onh) {
   const int64_t rows = (int64_t)BH * S;
-  static const bool v1 = getenv("DSA_FLASH_BWD_V1") != nullptr;
+  static const bool v1_env = getenv("DSA_FLASH_BWD_V1") != nullptr;
+  const bool v1 = v1_env && onh == 0;  // the v1 kernels read dO head-major only
   FA_DISPATCH(dt, D, causal,
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
-                       (const uint16_t*)dout, (const uint16_t*)o, delta, rows);
+                       (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
     if (!v1) {
       hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
                          fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale);
+                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh);
       hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
                          fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale);
+                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale, onh);
     } else {
       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<T, DD, CC>), dim3((S + fa::BM - 1) / fa::BM, BH), dim3(256),
                          fa::dkdv_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,

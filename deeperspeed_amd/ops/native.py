@@ -234,24 +234,27 @@ def has_flash_attention(q: torch.Tensor) -> bool:
 
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale):
+    def forward(ctx, q, k, v, causal, scale, out_bshd):
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         B, H, S, D = q.shape
         _macs(2 * B * H * S * S * D * (0.5 if causal else 1.0))
-        o, lse = hip_ops().flash_attn_fwd(q, k, v, causal, scale)
+        o, lse = hip_ops().flash_attn_fwd(q, k, v, causal, scale, out_bshd)
         ctx.save_for_backward(q, k, v, o, lse)
-        ctx.causal, ctx.scale = causal, scale
+        ctx.causal, ctx.scale, ctx.out_bshd = causal, scale, out_bshd
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
-        dq, dk, dv = hip_ops().flash_attn_bwd(do.contiguous(), q, k, v, o, lse, ctx.causal, ctx.scale)
-        return dq, dk, dv, None, None
+        dq, dk, dv = hip_ops().flash_attn_bwd(do.contiguous(), q, k, v, o, lse, ctx.causal, ctx.scale, ctx.out_bshd)
+        return dq, dk, dv, None, None, None
 
 
-def flash_attention(q, k, v, causal=True, scale=1.0):
-    return _FlashAttnFn.apply(q, k, v, causal, scale)
+def flash_attention(q, k, v, causal=True, scale=1.0, out_layout="bhsd"):
+    """q, k, v [B, H, S, D] -> o [B, H, S, D] (out_layout "bhsd") or [B, S, H, D] ("bshd": the
+    token-major layout the output projection reads, written directly by the kernel)."""
+    assert out_layout in ("bhsd", "bshd")
+    return _FlashAttnFn.apply(q, k, v, causal, scale, out_layout == "bshd")
 
 
 # --------------------------------------------------------------------------- flatten

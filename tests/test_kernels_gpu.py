@@ -195,7 +195,7 @@ def test_flash_attention_lse_and_large_logits():
     q = (8 * torch.randn(1, 2, 256, 128, device=_dev())).to(torch.bfloat16)
     k = torch.randn(1, 2, 256, 128, device=_dev()).to(torch.bfloat16)
     v = torch.randn(1, 2, 256, 128, device=_dev()).to(torch.bfloat16)
-    o, lse = native.hip_ops().flash_attn_fwd(q.contiguous(), k.contiguous(), v.contiguous(), True, 0.125)
+    o, lse = native.hip_ops().flash_attn_fwd(q.contiguous(), k.contiguous(), v.contiguous(), True, 0.125, False)
     s = (q.float() @ k.float().transpose(-1, -2)) * 0.125
     s = s.masked_fill(torch.ones(256, 256, dtype=torch.bool, device=_dev()).triu(1), float("-inf"))
     torch.testing.assert_close(lse, torch.logsumexp(s, -1), atol=2e-2, rtol=1e-3)
@@ -394,3 +394,25 @@ def test_deepspeed_transformer_layer_gpu_vs_cpu(preln):
     gpu.train()
     y1 = gpu(xg.detach(), m.to(_dev()).to(torch.bfloat16))
     assert torch.isfinite(y1).all()
+
+
+@pytest.mark.parametrize("D", [64, 96, 128])
+@pytest.mark.parametrize("S,causal", [(256, True), (200, False)])
+def test_flash_attention_bshd_output(D, S, causal):
+    """Token-major output layout ([B,S,H,D], written by the kernel) matches the head-major
+    result transposed, forward and backward (dO read token-major)."""
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(1)
+    B, H = 2, 5
+    qkv = [torch.randn(B, H, S, D, device=_dev(), dtype=torch.bfloat16) for _ in range(3)]
+    a = [t.clone().requires_grad_(True) for t in qkv]
+    b = [t.clone().requires_grad_(True) for t in qkv]
+    o1 = native.flash_attention(*a, causal, D ** -0.5)
+    o2 = native.flash_attention(*b, causal, D ** -0.5, out_layout="bshd")
+    assert o2.shape == (B, S, H, D) and o2.is_contiguous()
+    torch.testing.assert_close(o2, o1.transpose(1, 2), atol=0, rtol=0)
+    do = torch.randn(B, S, H, D, device=_dev(), dtype=torch.bfloat16)
+    o1.backward(do.transpose(1, 2))
+    o2.backward(do)
+    for x, y in zip(a, b):
+        torch.testing.assert_close(y.grad, x.grad, atol=0, rtol=0)
