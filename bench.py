@@ -130,28 +130,44 @@ def main():
         over["sparse_attention"] = {"mode": args.sparse, "block": args.block}
     cfg = get_config(args.model, max_seq_len=args.seq, checkpoint_activations=True, **over)
     big = get_config(args.model).num_params() > 5e9  # batch shape of the full model, also under --layers
-    mb = args.micro_batch or (4 if big else 8)
-    ga = args.grad_accum or (4 if big else 2)
     hbm = torch.cuda.get_device_properties(local).total_memory
     budget = 0.97 * hbm / share
-    # model-state layout: compact fp32 master (bf16 weight + int16 residual, exact, same Adam
-    # bytes as a separate fp32 master, 2 B/param less) > everything in HBM > fp32 master
-    # offloaded to host; then recompute only if needed
-    offload = args.offload
-    if offload == "auto":
-        offload = next((o for o in ("compact", "none", "master")
-                        if plan_memory(cfg, mb, args.seq, world, o, True, ga) < budget), "master")
-    ckpt = args.ckpt
-    if ckpt == "auto":
-        ckpt = "off" if plan_memory(cfg, mb, args.seq, world, offload, False, ga) < budget else "on"
+    reserve = 0.03 * hbm / share  # allocator fragmentation, RCCL / runtime buffers
+
+    def layout(mb, ga):
+        """Model-state layout for one (micro-batch, grad-accum): compact fp32 master (bf16
+        weight + int16 residual: exact, same Adam bytes as a separate fp32 master, 2 B/param
+        less) > everything in HBM > fp32 master on the host; then recompute only if needed."""
+        offload = args.offload
+        if offload == "auto":
+            offload = next((o for o in ("compact", "none", "master")
+                            if plan_memory(cfg, mb, args.seq, world, o, True, ga) < budget), "master")
+        ckpt = args.ckpt
+        if ckpt == "auto":
+            ckpt = "off" if plan_memory(cfg, mb, args.seq, world, offload, False, ga) < budget else "on"
+        return offload, ckpt, plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga)
+
+    # Per-GPU work is fixed at 16 sequences per optimizer step for the big models (weak
+    # scaling).  When the shards are small enough (N >= 4 for 20B), micro-batch 8 x 2 runs
+    # without recompute AND keeps every gathered unit resident: hipBLASLt is ~4 % faster at
+    # M = 16384 tokens than at 8192 (profiles/aux/gemm_m16k.log) and the per-micro-batch
+    # ZeRO-3 gradient reduce-scatters halve.  Otherwise micro-batch 4 x 4.
+    if args.micro_batch or args.grad_accum or not big:
+        mb = args.micro_batch or (4 if big else 8)
+        ga = args.grad_accum or (4 if big else 2)
+        offload, ckpt, planned = layout(mb, ga)
+    else:
+        for mb, ga in ((8, 2), (4, 4)):
+            offload, ckpt, planned = layout(mb, ga)
+            if ckpt == "off" and planned + 2 * cfg.num_params() + reserve < budget:
+                break
     cfg.checkpoint_activations = ckpt == "on"
     # ZeRO-3 parameter retention (stage3_max_live_parameters): HBM left after states and
     # activations keeps gathered bf16 units resident between their forward and backward use
     # and across the micro-batches of one optimizer step, so a unit is all-gathered once per
     # step instead of twice per micro-batch when the whole model fits (it does at N>=2 on
     # 288 GB parts: 41 GB of bf16 weights for 20B)
-    # keep a reserve of 3 % of HBM for allocator fragmentation and RCCL/runtime buffers
-    spare = budget - plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) - 0.03 * hbm / share
+    spare = budget - planned - reserve
     live = int(max(0.0, min(spare / 2, cfg.num_params() * 1.0)))  # bf16 elements
     if args.max_live is not None:
         live = int(args.max_live)

@@ -131,21 +131,22 @@ def build(name: str, jobs: Optional[int] = None, verbose: bool = False) -> str:
         objs.append(obj)
         if not os.path.exists(obj):
             todo.append(_compile_cmd(kind, name, src, obj))
-    jobs = jobs or int(os.environ.get("MAX_JOBS", min(8, os.cpu_count() or 4)))
-    if todo:
-        with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
-            for out in ex.map(_run, todo):
-                if verbose and out.strip():
-                    print(out)
     out = _so_path(name)
     stamp = out + ".hash"
     link_h = _hash([], "|".join(objs))
-    if not os.path.exists(out) or not os.path.exists(stamp) or open(stamp).read() != link_h:
-        tmp = out + ".tmp"
-        _run(_link_cmd(kind, objs, tmp))
-        os.replace(tmp, out)
-        with open(stamp, "w") as f:
-            f.write(link_h)
+    if os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == link_h:
+        return out  # up to date with every source and flag (object files not needed)
+    jobs = jobs or int(os.environ.get("MAX_JOBS", min(8, os.cpu_count() or 4)))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
+            for log in ex.map(_run, todo):
+                if verbose and log.strip():
+                    print(log)
+    tmp = out + ".tmp"
+    _run(_link_cmd(kind, objs, tmp))
+    os.replace(tmp, out)
+    with open(stamp, "w") as f:
+        f.write(link_h)
     return out
 
 
