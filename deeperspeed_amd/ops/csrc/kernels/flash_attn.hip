@@ -493,7 +493,12 @@ __device__ __forceinline__ s16x8 pack8_h(const float* v, int base) {
   return out;
 }
 
-template <typename T, int D, bool CAUSAL>
+// LAZY: the running max m is raised only when a tile's max exceeds it by more than
+// LAZY_TH (log2 units, i.e. P <= 2^8 in between), decided per wave: most tiles then skip the
+// O / l rescale (D/32*16 + 1 multiplies per lane) and alpha's exp.  Exact up to rounding.
+constexpr float LAZY_TH = 8.0f;
+
+template <typename T, int D, bool CAUSAL, bool LAZY = true>
 __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                         float* __restrict__ LSE, int S, float scale, int onh) {
@@ -570,9 +575,18 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
 #pragma unroll
     for (int i = 0; i < 32; ++i) mx = fmaxf(mx, sv[i]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx * sl2);
-    const float mu = (mn == -INFINITY) ? 0.f : mn;
-    const float alpha = fast_exp2(m - mu);
+    const float mt = mx * sl2;
+    if (!LAZY || __any(mt > m + LAZY_TH)) {  // wave-uniform
+      const float mn = fmaxf(m, mt);
+      const float alpha = fast_exp2(m - ((mn == -INFINITY) ? 0.f : mn));
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    }
+    const float mu = (m == -INFINITY) ? 0.f : m;
     // two partial sums keep the dependent add chain short
     float ps = 0.f, ps1 = 0.f;
 #pragma unroll
@@ -584,12 +598,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     }
     ps += ps1;
     ps += __shfl_xor(ps, 32, 64);
-    l = l * alpha + ps;
-    m = mn;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    l += ps;
     // O^T += V^T P^T over the 64 keys (4 steps of 16)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -922,12 +931,18 @@ bool flash_supported(int D) { return D == 64 || D == 96 || D == 128; }
 void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                       bool causal, float scale, int dt, hipStream_t s, int onh) {
   static const bool v1 = getenv("DSA_FLASH_FWD_V1") != nullptr;
+  static const bool eager = getenv("DSA_FLASH_EAGER_RESCALE") != nullptr;
   if (!v1 || onh) {
     dim3 grid2((S + fa::BM2 - 1) / fa::BM2, BH);
     FA_DISPATCH(dt, D, causal,
-      hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC>), dim3(grid2.x * grid2.y), dim3(256), fa::fwd_v2_lds<DD>(), s,
-                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale,
-                         onh));
+      if (eager)
+        hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, false>), dim3(grid2.x * grid2.y), dim3(256),
+                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                           (uint16_t*)o, lse, S, scale, onh);
+      else
+        hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true>), dim3(grid2.x * grid2.y), dim3(256),
+                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                           (uint16_t*)o, lse, S, scale, onh));
     return;
   }
   dim3 grid((S + fa::BM - 1) / fa::BM, BH);

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--S", type=int, default=2048)
     ap.add_argument("--D", type=int, nargs="+", default=[96, 128, 64])
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--flash-only", action="store_true", help="skip the unfused path (profiling runs)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for D in a.D:
@@ -40,9 +41,9 @@ def main():
         do = torch.randn_like(q)
         flops_f = 4 * a.B * a.H * a.S * a.S * D / 2  # causal
         res = {"B": a.B, "H": a.H, "S": a.S, "D": D}
-        for name, fn in (("flash", lambda: native.flash_attention(q, k, v, True, D ** -0.5)),
-                         ("unfused", lambda: attention(q, k, v, causal=True, softmax_scale=D ** -0.5,
-                                                       use_flash=False))):
+        paths = [("flash", lambda: native.flash_attention(q, k, v, True, D ** -0.5)),
+                 ("unfused", lambda: attention(q, k, v, causal=True, softmax_scale=D ** -0.5, use_flash=False))]
+        for name, fn in paths[:1] if a.flash_only else paths:
             tf = timeit(lambda: fn(), a.iters)
             o = fn()
             tb = timeit(lambda: torch.autograd.grad(o, (q, k, v), do, retain_graph=True), a.iters)
