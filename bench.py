@@ -308,7 +308,7 @@ def main():
                    "offload": offload, "activation_checkpointing": ckpt == "on", "sparse_attention": args.sparse,
                    "params_per_gpu": round(cfg.num_params() / world / 1e9, 3),
                    "model_tflops_per_gpu": round(tps * flops_tok / world / 1e12, 1),
-                   "final_loss": round(float(loss), 4),
+                   "final_loss": round(float(loss.detach()), 4),
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
                    "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) / 2**30, 1),
                    "max_live_parameters": live,
@@ -388,7 +388,7 @@ def run_pipeline(args, cfg, mb, ga, world, rank, dev):
                    "parallelism": f"pp{args.pipe}-dp{dp}" + ("" if onebit else "-zero1"), "micro_batch": mb,
                    "grad_accum": ga, "optimizer": args.optimizer,
                    "model_tflops_per_gpu": round(tps * cfg.flops_per_token(args.seq) / world / 1e12, 1),
-                   "final_loss": round(float(loss), 4),
+                   "final_loss": round(float(loss.detach()), 4),
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1)},
     }
     if rank == 0:
