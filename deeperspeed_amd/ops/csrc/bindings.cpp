@@ -241,6 +241,31 @@ Tensor colsum(Tensor x) {
   return out;
 }
 
+// y = x^T for a 2-D 16-bit x [R, C] (unit column stride, any 16-byte aligned row stride).
+// With colsum_out ([C], x's dtype) the column sums of x are also written (accum: added) there.
+Tensor transpose2d(Tensor x, OptT colsum_out, bool accum) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "transpose2d: x must be a 2-D GPU tensor, unit column stride");
+  const int dt = dcode(x);
+  TORCH_CHECK(dt != dsa::kCodeF32, "transpose2d: 16-bit dtypes only");
+  const int64_t R = x.size(0), C = x.size(1), ldx = x.stride(0);
+  TORCH_CHECK(dsa::transpose_supported(R, C), "transpose2d: rows must be a multiple of 128 and cols of 64");
+  TORCH_CHECK(aligned16(x.data_ptr()) && ldx % 8 == 0, "transpose2d: rows must be 16-byte aligned");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty({C, R}, x.options());
+  Tensor partial;
+  void* cptr = nullptr;
+  if (colsum_out.has_value()) {
+    check_dev(*colsum_out, "colsum_out");
+    TORCH_CHECK(colsum_out->numel() == C && colsum_out->scalar_type() == x.scalar_type(),
+                "transpose2d: colsum_out must be [C] in x's dtype");
+    partial = at::empty({dsa::transpose_partial_rows(R) * C}, x.options().dtype(at::kFloat));
+    cptr = colsum_out->data_ptr();
+  }
+  dsa::launch_transpose(x.data_ptr(), y.data_ptr(), partial.defined() ? partial.data_ptr<float>() : nullptr, cptr,
+                        accum ? 1 : 0, R, (int)C, ldx, dt, cur_stream());
+  return y;
+}
+
 // ----------------------------------------------------------------------------- attention elementwise
 // qkv [B,S,NH*3*HD] (NeoX per-head q|k|v) -> q,k,v [B,NH,S,HD]; cs [S, ROT/2, 2] fp32
 std::vector<Tensor> rotary_split_fwd(Tensor qkv, Tensor cs, int64_t NH, int64_t HD, int64_t ROT, double qscale) {
@@ -563,4 +588,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("colsum", &colsum);
+  m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("colsum_out") = py::none(), py::arg("accum") = false);
 }

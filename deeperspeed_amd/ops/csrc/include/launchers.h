@@ -51,6 +51,15 @@ void launch_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx
                           int64_t rows, int C, int approx, int dt, hipStream_t s);
 void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C, int accum, int dt,
                    hipStream_t s);
+// out[c] (+)= sum_r partial[r][c] (fp32 partials, out in dtype dt)
+void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s);
+
+// transpose.hip: y[C][R] = x[R][C] (16-bit; R % 128 == 0, C % 64 == 0, x row stride ldx).  With
+// `partial` ([R/128, C] fp32 scratch) the column sums of x are also (accumulated) into colsum_out[C].
+bool transpose_supported(int64_t R, int64_t C);
+int64_t transpose_partial_rows(int64_t R);
+void launch_transpose(const void* x, void* y, float* partial, void* colsum_out, int colsum_accum, int64_t R, int C,
+                      int64_t ldx, int dt, hipStream_t s);
 
 // attn_elem.hip
 void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const float* cs, int B, int S, int NH,

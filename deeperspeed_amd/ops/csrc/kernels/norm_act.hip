@@ -363,6 +363,11 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const T* __restrict
   for (int j = 0; j < VN; j += 4) *reinterpret_cast<float4*>(p + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
 }
 
+void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s) {
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 63) / 64), dim3(256), 0, s, partial, R, C, (T*)out, accum));
+}
+
 void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C, int accum, int dt,
                    hipStream_t s) {
   if (rows <= 0) return;

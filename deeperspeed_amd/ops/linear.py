@@ -18,6 +18,13 @@ Reference counterpart: the weight-gradient GEMMs of `csrc/transformer/ds_transfo
 `ds_transformer_cuda.cpp:370-540`), which write into the parameter's `.grad` storage.
 
 Set DSA_FUSE_WGRAD=0 to disable (identical math up to one rounding of the accumulate).
+
+Reduction-contiguous wgrad operands (DSA_WGRAD_NT, default on for GPU tensors): hipBLASLt on
+gfx950 runs dW = dy^T x at ~1.1 PF/s with the token-major operands autograd holds, and at
+~1.45 PF/s when both operands are contiguous along the token (reduction) dimension
+(profiles/aux/wgrad_dgrad_variants_neox20b.jsonl).  The HIP transpose kernel
+(ops/csrc/kernels/transpose.hip) makes dy^T and x^T first; the transpose of dy also produces
+the bias gradient (its column sum) from the same read.
 """
 
 from __future__ import annotations
@@ -29,13 +36,25 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 FUSE_WGRAD = os.environ.get("DSA_FUSE_WGRAD", "1") != "0"
+WGRAD_NT = os.environ.get("DSA_WGRAD_NT", "1") != "0"
+# smallest out*in weight that takes the transposed path (the transposes move ~4*M*(out+in)
+# bytes; below this the GEMM saving does not pay for them)
+WGRAD_NT_MIN_NUMEL = int(float(os.environ.get("DSA_WGRAD_NT_MIN_NUMEL", "1e7")))
+# input gradient dx = dy W from W^T [in, out] (reduction-contiguous, one HIP transpose of the
+# weight per use): hipBLASLt ~1.45 vs ~1.28 PF/s at the GPT-NeoX-20B shapes
+DGRAD_NT = os.environ.get("DSA_DGRAD_NT", "1") != "0"
 
 
 _count = [0]  # in-place accumulations performed (tests / diagnostics)
+_nt_count = [0]  # wgrads formed from transposed operands
 
 
 def fused_wgrad_count() -> int:
     return _count[0]
+
+
+def nt_wgrad_count() -> int:
+    return _nt_count[0]
 
 
 def _bound_grad(p: torch.Tensor):
@@ -45,6 +64,31 @@ def _bound_grad(p: torch.Tensor):
     return g
 
 
+def _nt_operands(g2, x2, bias_grad):
+    """(dy^T, x^T) contiguous along the tokens via the HIP transpose, with bias_grad (+)= sum(dy)
+    folded into the transpose of dy; None when the path does not apply."""
+    if not (WGRAD_NT and g2.is_cuda and g2.dtype == x2.dtype
+            and g2.size(1) * x2.size(1) >= WGRAD_NT_MIN_NUMEL):
+        return None
+    from . import native
+    if not (native.transpose_supported(g2) and native.transpose_supported(x2)):
+        return None
+    if bias_grad is not None and (bias_grad.dtype != g2.dtype or not bias_grad.is_contiguous()):
+        return None
+    _nt_count[0] += 1
+    return native.transpose2d(g2, bias_grad, accum=True), native.transpose2d(x2)
+
+
+def input_grad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """dx = g2 @ W for g2 = dy [M, out], W [out, in]."""
+    if (DGRAD_NT and g2.is_cuda and g2.dtype == weight.dtype and weight.numel() >= WGRAD_NT_MIN_NUMEL
+            and g2.size(0) >= 1024):
+        from . import native
+        if native.transpose_supported(weight):
+            return g2 @ native.transpose2d(weight).t()
+    return g2 @ weight
+
+
 def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, bias, need_w: bool,
                            need_b: bool):
     """Weight/bias gradients of y = x W^T (+ b) for flattened g2 = dy [M, out], x2 = x [M, in].
@@ -52,19 +96,28 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     Returns (dw, db) for autograd, or None entries for parameters whose gradient was
     accumulated in place."""
     dw = db = None
-    fuse = FUSE_WGRAD and need_w and (bias is None or not need_b or _bound_grad(bias) is not None)
+    has_b = bias is not None and need_b
+    fuse = FUSE_WGRAD and need_w and (not has_b or _bound_grad(bias) is not None)
     gw = _bound_grad(weight) if fuse else None
     if gw is not None and gw.is_contiguous():
-        gw.addmm_(g2.t(), x2)
-        if bias is not None and need_b:
-            bias.grad.add_(g2.sum(0))
+        nt = _nt_operands(g2, x2, bias.grad if has_b else None)
+        if nt is not None:
+            gw.addmm_(nt[0], nt[1].t())
+        else:
+            gw.addmm_(g2.t(), x2)
+            if has_b:
+                bias.grad.add_(g2.sum(0))
         _count[0] += 1
         # returning None still runs the leaf's AccumulateGrad node, which leaves the bound
         # gradient untouched and fires its post-accumulate hooks (ZeRO bucket bookkeeping)
         return None, None
     if need_w:
+        db = torch.zeros(g2.size(1), dtype=g2.dtype, device=g2.device) if has_b else None
+        nt = _nt_operands(g2, x2, db)
+        if nt is not None:
+            return nt[0] @ nt[1].t(), db
         dw = g2.t() @ x2
-    if bias is not None and need_b:
+    if has_b:
         db = g2.sum(0)
     return dw, db
 
@@ -83,7 +136,7 @@ class _AccumLinear(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1])
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = (g2 @ weight).view(x.shape)
+            dx = input_grad(g2, weight).view(x.shape)
         dw, db = accumulate_param_grads(g2, x.reshape(-1, x.shape[-1]), weight, bias, ctx.needs_input_grad[1],
                                         bias is not None and ctx.needs_input_grad[2])
         return dx, dw, db
@@ -106,7 +159,7 @@ class _GradOnlyLinear(torch.autograd.Function):
         g2 = g.reshape(-1, g.shape[-1])
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = (g2 @ weight).view(x.shape)
+            dx = input_grad(g2, weight).view(x.shape)
         dw, db = accumulate_param_grads(g2, x.reshape(-1, x.shape[-1]), weight, bias, ctx.needs_input_grad[1],
                                         bias is not None and ctx.needs_input_grad[2])
         return dx, dw, db

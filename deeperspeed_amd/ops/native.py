@@ -173,6 +173,28 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     return x.reshape(-1, x.shape[-1]).float().sum(0).to(x.dtype)
 
 
+def transpose_supported(x: torch.Tensor) -> bool:
+    """Shapes/layouts the HIP transpose takes: 2-D 16-bit, rows % 128, cols % 64, unit column
+    stride, 16-byte aligned rows."""
+    return (x.dim() == 2 and x.dtype in (torch.bfloat16, torch.float16) and x.size(0) % 128 == 0
+            and x.size(1) % 64 == 0 and x.size(0) > 0 and x.size(1) > 0 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0)
+
+
+def transpose2d(x: torch.Tensor, colsum_out: Optional[torch.Tensor] = None, accum: bool = False) -> torch.Tensor:
+    """x [R, C] -> contiguous x^T [C, R]; optionally colsum_out (+)= x.sum(0) from the same read
+    (the bias gradient of a linear whose output gradient is x)."""
+    if x.is_cuda:
+        return hip_ops().transpose2d(x, colsum_out, accum)
+    y = x.t().contiguous()
+    if colsum_out is not None:
+        s = x.float().sum(0)
+        if accum:
+            s += colsum_out.float()
+        colsum_out.copy_(s)
+    return y
+
+
 # --------------------------------------------------------------------------- Adam
 def adam_flat_(w, g, m, v, out, lr, beta1, beta2, eps, weight_decay, step, bias_correction, grad_scale, adamw):
     """In-place Adam/AdamW on flat tensors.  `w` is the fp32 master (or the param itself),

@@ -416,3 +416,66 @@ def test_flash_attention_bshd_output(D, S, causal):
     o2.backward(do)
     for x, y in zip(a, b):
         torch.testing.assert_close(y.grad, x.grad, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("R,C,pad", [(128, 64, 0), (256, 192, 0), (1024, 640, 64), (8192, 512, 0)])
+def test_transpose2d_and_fused_colsum(dtype, R, C, pad):
+    """HIP transpose (tr-read LDS tiles) is exact; its fused column sum matches fp32 and
+    accumulates into an existing bias gradient."""
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(2)
+    base = torch.randn(R, C + pad, device=_dev(), dtype=dtype)
+    x = base[:, :C]  # row stride C + pad
+    assert native.transpose_supported(x)
+    y = native.transpose2d(x)
+    assert y.shape == (C, R) and y.is_contiguous()
+    torch.testing.assert_close(y, x.t(), atol=0, rtol=0)
+    out = torch.randn(C, device=_dev(), dtype=dtype)
+    ref = out.float() + x.float().sum(0)
+    y2 = native.transpose2d(x, out, accum=True)
+    torch.testing.assert_close(y2, y, atol=0, rtol=0)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2 * (R ** 0.5), rtol=1e-2)
+    out2 = torch.empty(C, device=_dev(), dtype=dtype)
+    native.transpose2d(x, out2, accum=False)
+    torch.testing.assert_close(out2.float(), x.float().sum(0), atol=2e-2 * (R ** 0.5), rtol=1e-2)
+
+
+@pytest.mark.parametrize("bound", [True, False])
+def test_linear_wgrad_transposed_operands(bound):
+    """dW / db / dx from the reduction-contiguous (transposed) operands match the token-major
+    formulation and an fp32 reference, in place (bound grad) and through autograd."""
+    from deeperspeed_amd.ops import linear as lin
+    torch.manual_seed(3)
+    old = lin.WGRAD_NT_MIN_NUMEL
+    lin.WGRAD_NT_MIN_NUMEL = 0
+    try:
+        M, fin, fout = 1024, 384, 640
+        x0 = torch.randn(2, M // 2, fin, device=_dev(), dtype=torch.bfloat16)
+        g = torch.randn(2, M // 2, fout, device=_dev(), dtype=torch.bfloat16)
+        res = {}
+        for nt in (False, True):
+            lin.WGRAD_NT = lin.DGRAD_NT = nt
+            layer = lin.Linear(fin, fout, device=_dev(), dtype=torch.bfloat16)
+            torch.manual_seed(4)
+            with torch.no_grad():
+                layer.weight.normal_()
+                layer.bias.normal_()
+            if bound:
+                layer.weight.grad = torch.zeros_like(layer.weight)
+                layer.bias.grad = torch.zeros_like(layer.bias)
+            x = x0.clone().requires_grad_(True)
+            n0 = lin.nt_wgrad_count()
+            layer(x).backward(g)
+            assert (lin.nt_wgrad_count() > n0) == nt
+            res[nt] = (layer.weight.grad.float(), layer.bias.grad.float(), x.grad.float(), layer.weight.float())
+        ref_w = g.reshape(M, fout).float().t() @ x0.reshape(M, fin).float()
+        ref_b = g.reshape(M, fout).float().sum(0)
+        for nt in (False, True):
+            ref_x = g.float() @ res[nt][3]
+            torch.testing.assert_close(res[nt][0], ref_w, atol=0.5, rtol=2e-2)
+            torch.testing.assert_close(res[nt][1], ref_b, atol=0.5, rtol=2e-2)
+            torch.testing.assert_close(res[nt][2], ref_x, atol=0.5, rtol=2e-2)
+    finally:
+        lin.WGRAD_NT = lin.DGRAD_NT = True
+        lin.WGRAD_NT_MIN_NUMEL = old
