@@ -171,8 +171,19 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rg = threadIdx.x >> 6;
   float acc = 0.f;
-  if (c < C)
-    for (int r = rg; r < R; r += 4) acc += partial[(int64_t)r * C + c];
+  if (c < C) {
+    // 8 independent loads in flight per thread (the partials are L2-resident; a serial
+    // load-add chain over R/4 rows is pure latency)
+    int r = rg;
+    for (; r + 28 < R; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = partial[(int64_t)(r + 4 * j) * C + c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += v[j];
+    }
+    for (; r < R; r += 4) acc += partial[(int64_t)r * C + c];
+  }
   red[rg][threadIdx.x & 63] = acc;
   __syncthreads();
   if (rg == 0 && c < C) {

@@ -40,6 +40,9 @@ WGRAD_NT = os.environ.get("DSA_WGRAD_NT", "1") != "0"
 # smallest out*in weight that takes the transposed path (the transposes move ~4*M*(out+in)
 # bytes; below this the GEMM saving does not pay for them)
 WGRAD_NT_MIN_NUMEL = int(float(os.environ.get("DSA_WGRAD_NT_MIN_NUMEL", "1e7")))
+# cap on the transient transposed copies (bytes of dy^T + x^T): the LM head's dlogits at 16k
+# tokens (1.65 GB) keeps the token-major formulation instead of adding its copy to the peak
+WGRAD_NT_MAX_BYTES = int(float(os.environ.get("DSA_WGRAD_NT_MAX_BYTES", "1.2e9")))
 # input gradient dx = dy W from W^T [in, out] (reduction-contiguous, one HIP transpose of the
 # weight per use): hipBLASLt ~1.45 vs ~1.28 PF/s at the GPT-NeoX-20B shapes
 DGRAD_NT = os.environ.get("DSA_DGRAD_NT", "1") != "0"
@@ -68,7 +71,8 @@ def _nt_operands(g2, x2, bias_grad):
     """(dy^T, x^T) contiguous along the tokens via the HIP transpose, with bias_grad (+)= sum(dy)
     folded into the transpose of dy; None when the path does not apply."""
     if not (WGRAD_NT and g2.is_cuda and g2.dtype == x2.dtype
-            and g2.size(1) * x2.size(1) >= WGRAD_NT_MIN_NUMEL):
+            and g2.size(1) * x2.size(1) >= WGRAD_NT_MIN_NUMEL
+            and (g2.numel() + x2.numel()) * g2.element_size() <= WGRAD_NT_MAX_BYTES):
         return None
     from . import native
     if not (native.transpose_supported(g2) and native.transpose_supported(x2)):
