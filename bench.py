@@ -254,12 +254,36 @@ def main():
         for m in layers:
             m.register_forward_hook(_mark)
 
+    stashed = 0
+
+    def plan_stash():
+        """Selective recompute from MEASURED headroom: after a warmup step with full recompute,
+        HBM left above the allocator's reserved peak (minus a margin) keeps the attention
+        q, k, v, output and LSE of as many layers as fit (NeoXAttention.stash_outputs), so their
+        recompute skips the QKV GEMM, rotary split and flash forward."""
+        if not cfg.checkpoint_activations or args.sparse or os.environ.get("DSA_STASH", "1") == "0":
+            return 0
+        layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
+        per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
+        margin = float(os.environ.get("DSA_STASH_MARGIN_GIB", "4")) * 2**30
+        free = hbm / share - torch.cuda.max_memory_reserved() - margin
+        n = int(max(0, min(len(layers), free // per_layer)))
+        for m in layers[-n:] if n else []:
+            m.attention.stash_outputs = True
+        log(f"selective recompute: {n}/{len(layers)} layers keep attention outputs "
+            f"({n * per_layer / 2**30:.1f} GiB; reserved peak {torch.cuda.max_memory_reserved() / 2**30:.1f} GiB)")
+        torch.cuda.reset_peak_memory_stats()
+        return n
+
     for i in range(args.warmup):
         ts = time.time()
         loss, ph = timed_step()
         log(f"warmup {i} loss={float(loss.detach()):.4f} {time.time() - ts:.2f}s "
             + " ".join(f"{k}={v:.2f}s" for k, v in ph.items())
-            + f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+            + f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB"
+            + f" reserved={torch.cuda.max_memory_reserved() / 2**30:.1f} GiB")
+        if i == 0 and args.warmup >= 2:
+            stashed = plan_stash()
 
     dist.barrier()
     torch.cuda.synchronize()
@@ -311,7 +335,7 @@ def main():
                    "final_loss": round(float(loss.detach()), 4),
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
                    "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) / 2**30, 1),
-                   "max_live_parameters": live,
+                   "max_live_parameters": live, "stashed_attention_layers": stashed,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N), BASELINE.md derived target"},
     }
     if rank == 0:

@@ -90,8 +90,28 @@ class _RotarySplitFn(torch.autograd.Function):
         return x.to(dq.dtype), None, None, None, None, None
 
 
-def rotary_split(qkv, num_heads: int, head_dim: int, rot_dim: int, base: float = 10000.0, qscale: float = 1.0):
+class _StashedRotarySplitFn(_RotarySplitFn):
+    """Recompute-time stand-in: returns the (q, k, v) the first forward kept (selective
+    recompute) instead of re-running the QKV GEMM's consumer; backward is the rotary split's."""
+
+    @staticmethod
+    def forward(ctx, qkv, cs, nh, hd, rot, qscale, stash):
+        ctx.meta = (nh, hd, rot, qscale)
+        ctx.save_for_backward(cs)
+        return stash
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        return _RotarySplitFn.backward(ctx, dq, dk, dv) + (None,)
+
+
+def rotary_split(qkv, num_heads: int, head_dim: int, rot_dim: int, base: float = 10000.0, qscale: float = 1.0,
+                 stash=None):
+    """stash: (q, k, v) kept from the first forward of a checkpointed block; the returned tensors
+    are those, with the rotary split's backward attached (qkv is then only a gradient handle)."""
     cs = rotary_table(qkv.shape[1], max(rot_dim, 2), base, qkv.device)
+    if stash is not None:
+        return _StashedRotarySplitFn.apply(qkv, cs, num_heads, head_dim, rot_dim, qscale, tuple(stash))
     return _RotarySplitFn.apply(qkv, cs, num_heads, head_dim, rot_dim, qscale)
 
 

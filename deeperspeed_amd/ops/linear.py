@@ -181,7 +181,15 @@ def grad_only_linear(x, weight, bias=None):
 
 
 class Linear(nn.Linear):
-    """nn.Linear with in-place weight-gradient accumulation (state-dict compatible)."""
+    """nn.Linear with in-place weight-gradient accumulation (state-dict compatible).
+
+    `grad_only_next = True` makes the next call a gradient-only linear (its value is never
+    read: selective recompute hands the consumer a kept copy of the output)."""
+
+    grad_only_next = False
 
     def forward(self, x):
+        if self.grad_only_next:
+            self.grad_only_next = False
+            return grad_only_linear(x, self.weight, self.bias)
         return linear(x, self.weight, self.bias)

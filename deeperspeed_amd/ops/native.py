@@ -272,11 +272,37 @@ class _FlashAttnFn(torch.autograd.Function):
         return dq, dk, dv, None, None, None
 
 
-def flash_attention(q, k, v, causal=True, scale=1.0, out_layout="bhsd"):
+class _StashedFlashAttnFn(_FlashAttnFn):
+    """Recompute-time stand-in: (o, lse) kept from the first forward; backward unchanged."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, out_bshd, stash):
+        o, lse = stash
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale, ctx.out_bshd = causal, scale, out_bshd
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        return _FlashAttnFn.backward(ctx, do) + (None,)
+
+
+def flash_attention(q, k, v, causal=True, scale=1.0, out_layout="bhsd", stash=None):
     """q, k, v [B, H, S, D] -> o [B, H, S, D] (out_layout "bhsd") or [B, S, H, D] ("bshd": the
-    token-major layout the output projection reads, written directly by the kernel)."""
+    token-major layout the output projection reads, written directly by the kernel).
+    stash: (o, lse) from flash_attention_fwd_lse of the same inputs (selective recompute)."""
     assert out_layout in ("bhsd", "bshd")
+    if stash is not None:
+        return _StashedFlashAttnFn.apply(q, k, v, causal, scale, out_layout == "bshd", tuple(stash))
     return _FlashAttnFn.apply(q, k, v, causal, scale, out_layout == "bshd")
+
+
+def flash_attention_fwd_lse(q, k, v, causal=True, scale=1.0, out_layout="bhsd"):
+    """Forward only (no autograd): (o, lse) with lse [B*H, S] fp32, for a later stashed backward."""
+    q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+    B, H, S, D = q.shape
+    _macs(2 * B * H * S * S * D * (0.5 if causal else 1.0))
+    return hip_ops().flash_attn_fwd(q, k, v, causal, scale, out_layout == "bshd")
 
 
 # --------------------------------------------------------------------------- flatten

@@ -170,6 +170,7 @@ def _gather(rec):
 
 
 _RECOMPUTE_DEPTH = 0
+_CKPT_FWD_DEPTH = 0
 
 
 def is_recomputing() -> bool:
@@ -178,6 +179,13 @@ def is_recomputing() -> bool:
     sum) can skip computing it then and produce gradients only (models/gpt_neox.py
     OutputLinear)."""
     return _RECOMPUTE_DEPTH > 0
+
+
+def is_checkpoint_forward() -> bool:
+    """True during the first (no_grad) forward of a checkpointed function: values computed now
+    are discarded and recomputed in backward unless a module keeps them (selective recompute,
+    models/gpt_neox.py NeoXAttention.stash_outputs)."""
+    return _CKPT_FWD_DEPTH > 0
 
 
 class CheckpointFunction(torch.autograd.Function):
@@ -191,8 +199,13 @@ class CheckpointFunction(torch.autograd.Function):
         ctx.fwd_cpu_rng_state = torch.get_rng_state()
         ctx.fwd_cuda_rng_state = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
         ctx.fwd_cuda_rng_state_tracker = get_cuda_rng_tracker().get_states()
-        with torch.no_grad():
-            outputs = run_function(*args)
+        global _CKPT_FWD_DEPTH
+        _CKPT_FWD_DEPTH += 1
+        try:
+            with torch.no_grad():
+                outputs = run_function(*args)
+        finally:
+            _CKPT_FWD_DEPTH -= 1
         tensor_idx, saved, non_tensors = [], [], []
         for i, a in enumerate(args):
             if torch.is_tensor(a):
