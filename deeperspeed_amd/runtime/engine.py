@@ -1018,7 +1018,7 @@ class DeepSpeedEngine(Module):
     def _zero3_module_payload(self):
         opt = self.optimizer
         from .zero.layout import layout_signature
-        return {"zero3_param_shards": [g.shard_param.detach().cpu() for g in opt.groups],
+        return {"zero3_param_shards": [opt.param_shard_host(g) for g in opt.groups],
                 "layout": layout_signature(opt.groups), "dp_world_size": opt.dp_world}
 
     def _save_checkpoint(self, save_dir, tag, client_state=None):
@@ -1129,7 +1129,7 @@ class DeepSpeedEngine(Module):
         from .zero.layout import layout_signature
         if payload.get("layout") == layout_signature(opt.groups) and payload.get("dp_world_size") == opt.dp_world:
             for g, s in zip(opt.groups, payload["zero3_param_shards"]):
-                g.shard_param.copy_(s.to(g.shard_param.device))
+                opt.load_param_shard(g, s)
             opt._post_step()
 
     def _load_zero_checkpoint(self, load_dir, tag, load_optimizer_states=True):

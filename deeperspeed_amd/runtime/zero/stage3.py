@@ -119,6 +119,15 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self.param_offload = bool(offload_param) and offload_param.get("device") in ("cpu", "nvme")
         if self.param_offload and self.offload is None:
             raise ValueError("offload_param requires offload_optimizer (cpu or nvme) in ZeRO stage 3")
+        # "nvme": the shard lives only in per-(group, bucket) files behind the aio engine
+        # (runtime/swap_tensor/partitioned_param_swapper.py); "mmap" keeps the older file-backed
+        # mapping through the page cache
+        self.param_nvme = self.param_offload and offload_param.get("device") == "nvme" and \
+            offload_param.get("mode", "aio") == "aio"
+        if self.param_nvme and self.offload_states == "master" and not self.nvme:
+            raise ValueError("offload_param nvme needs the optimizer step on the host (offload_optimizer states 'all' or nvme)")
+        self._pswap = None
+        self._pkey: Dict[int, tuple] = {}
         self.compute_device = self.device
         self.single = self.dp_world == 1 and not self.param_offload
         self._pending = []
@@ -144,6 +153,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                 b.unit.buckets.append((g, b))
         self._build_shards()
         self._alloc_master_and_state(lambda g: g.shard_param.float())
+        if self.param_nvme:
+            for g in self.groups:
+                g.shard_param = None  # the NVMe files are the only copy from here on
         self._register_hooks()
         for m in module.modules():
             for p in m.__dict__.get("_external_params", []):
@@ -227,6 +239,18 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                     g.shard_param[b.shard_offset + c0: b.shard_offset + c0 + ln].copy_(src[p0: p0 + ln])
             gdt = self._grad_dtype(g)
             g.shard_grad = torch.zeros(g.shard_numel, dtype=gdt, device=dev)
+        if self.param_nvme:
+            import os
+            from ..swap_tensor.partitioned_param_swapper import AsyncPartitionedParameterSwapper
+            folder = os.path.join(self.offload_param.get("nvme_path") or "/tmp/deeperspeed_amd_nvme", "zero_stage_3",
+                                  f"params_rank{self.dp_rank}_mp{self.mp_rank}")
+            self._pswap = AsyncPartitionedParameterSwapper(folder, self.groups[0].dtype if self.groups else torch.bfloat16,
+                                                           buffer_count=self.offload_param.get("buffer_count", 5),
+                                                           aio_config=self.offload_param.get("aio"))
+            for gi, g in enumerate(self.groups):
+                for bi, b in enumerate(g.buckets):
+                    self._pkey[id(b)] = (gi, bi)
+                    self._pswap.register((gi, bi), g.shard_param[b.shard_offset: b.shard_offset + b.chunk])
         for u in self._units:
             for p in u.params:
                 p._ds_owner = self
@@ -254,6 +278,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def _alloc_param_shard(self, gi, g, dev):
         if not self.param_offload:
             return torch.zeros(g.shard_numel, dtype=g.dtype, device=dev)
+        if self.param_nvme:
+            return torch.zeros(g.shard_numel, dtype=g.dtype)  # staging for init, dropped after
         if self.offload_param.get("device") == "nvme":
             import os
             folder = os.path.join(self.offload_param.get("nvme_path") or "/tmp/deeperspeed_amd_nvme", "zero_stage_3",
@@ -285,9 +311,12 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self.gathered_numel += u.numel
         for g, b in u.buckets:
             full = torch.empty(b.numel, dtype=g.dtype, device=self.compute_device)
-            chunk = g.shard_param[b.shard_offset: b.shard_offset + b.chunk]
-            if self.param_offload:
-                chunk = chunk.to(self.compute_device, non_blocking=chunk.is_pinned())
+            if self.param_nvme and g.shard_param is None:
+                chunk = self._pswap.read_to_device(self._pkey[id(b)], self.compute_device)
+            else:
+                chunk = g.shard_param[b.shard_offset: b.shard_offset + b.chunk]
+                if self.param_offload:
+                    chunk = chunk.to(self.compute_device, non_blocking=chunk.is_pinned())
             if _dist_ready() and self.dp_world > 1:
                 u.works.append(comm.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True,
                                                            tag=f"zero3.gather.u{u.uid}"))
@@ -550,10 +579,35 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def _prescaled_by(self):
         return float(self.dp_world) if (self.groups and self.groups[0].dtype == torch.float16) else 1.0
 
+    def _bucket_out(self, g, b):
+        if self.param_nvme and g.shard_param is None:
+            return self._pswap.staging(self._pkey[id(b)])
+        return super()._bucket_out(g, b)
+
     def _after_bucket_update(self, g, b):
-        pass
+        if self.param_nvme and g.shard_param is None:
+            self._pswap.swap_out(self._pkey[id(b)])
+
+    def param_shard_host(self, g) -> torch.Tensor:
+        """This rank's low-precision shard of group g as a host tensor (checkpoints)."""
+        if self.param_nvme and g.shard_param is None:
+            out = torch.empty(g.shard_numel, dtype=g.dtype)
+            self._pswap.synchronize_writes()
+            for b in g.buckets:
+                out[b.shard_offset: b.shard_offset + b.chunk].copy_(self._pswap.read(self._pkey[id(b)]))
+            return out
+        return g.shard_param.detach().cpu()
+
+    def load_param_shard(self, g, shard: torch.Tensor):
+        if self.param_nvme and g.shard_param is None:
+            for b in g.buckets:
+                self._pswap.write(self._pkey[id(b)], shard[b.shard_offset: b.shard_offset + b.chunk])
+            return
+        g.shard_param.copy_(shard.to(g.shard_param.device))
 
     def _post_step(self):
+        if self._pswap is not None:
+            self._pswap.synchronize_writes()
         if self.single:
             return
         for u in self._units:  # retained gathered copies are stale after the update
@@ -591,23 +645,42 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         """Copy edited full parameters (currently gathered) back into this rank's shard and
         fp32 master (zero.GatheredParameters(modifier_rank=...) exit path)."""
         want = {id(p) for p in params}
-        for g in self.groups:
-            for b in g.buckets:
-                for i, p in enumerate(b.params):
-                    if id(p) not in want:
-                        continue
-                    ov = b.chunk_overlap(self.dp_rank, i)
-                    if ov is None:
-                        continue
-                    p0, c0, ln = ov
-                    lo = b.shard_offset + c0
-                    src = p.data.reshape(-1)[p0: p0 + ln]
-                    if g.shard_param[lo: lo + ln].data_ptr() != src.data_ptr():
-                        g.shard_param[lo: lo + ln].copy_(src)
-                    if self.compact_master:
-                        g.master[lo: lo + ln].zero_()
-                    else:
-                        g.master[lo: lo + ln].copy_(g.shard_param[lo: lo + ln].float().to(g.master.device))
+        for gi, g in enumerate(self.groups):
+            if self.param_nvme and g.shard_param is None:
+                shard = self.param_shard_host(g)
+                g.shard_param = shard
+                try:
+                    self._write_back_group(gi, g, want)
+                finally:
+                    g.shard_param = None
+                self.load_param_shard(g, shard)
+                continue
+            self._write_back_group(gi, g, want)
+
+    def _write_back_group(self, gi, g, want):
+        for bi, b in enumerate(g.buckets):
+            nvme_master = None
+            for i, p in enumerate(b.params):
+                if id(p) not in want:
+                    continue
+                ov = b.chunk_overlap(self.dp_rank, i)
+                if ov is None:
+                    continue
+                p0, c0, ln = ov
+                lo = b.shard_offset + c0
+                src = p.data.reshape(-1)[p0: p0 + ln]
+                if g.shard_param[lo: lo + ln].data_ptr() != src.data_ptr():
+                    g.shard_param[lo: lo + ln].copy_(src)
+                if self.compact_master:
+                    g.master[lo: lo + ln].zero_()
+                elif self.nvme:  # fp32 master in the optimizer swap files
+                    if nvme_master is None:
+                        nvme_master = self._swapper.read((gi, bi), "master")
+                    nvme_master[c0: c0 + ln].copy_(g.shard_param[lo: lo + ln].float().cpu())
+                else:
+                    g.master[lo: lo + ln].copy_(g.shard_param[lo: lo + ln].float().to(g.master.device))
+            if nvme_master is not None:
+                self._swapper.write((gi, bi), "master", nvme_master)
 
     def gathered_state_dict(self, module, prefix=""):
         """Full (consolidated) low-precision state dict; every rank participates."""
