@@ -30,6 +30,8 @@ class FusedLamb(torch.optim.Optimizer):
         self.lamb_coeffs = []
         self.requires_per_param_masters = True  # trust ratio is per tensor: never flatten
 
+    supports_fused_lp_step = True  # FP16_UnfusedOptimizer passes low-precision grads/outputs
+
     @torch.no_grad()
     def step(self, closure=None, grads=None, output_params=None, scale=1.0, grad_norms=None):
         """`grads`/`output_params`/`scale` follow the reference's legacy fused interface:
@@ -45,6 +47,8 @@ class FusedLamb(torch.optim.Optimizer):
                 g = p.grad if g is None else g
                 if g is None:
                     continue
+                if o is not None and o.data_ptr() == p.data_ptr():
+                    o = None
                 if g.is_sparse:
                     raise RuntimeError("FusedLamb does not support sparse gradients")
                 st = self.state[p]

@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 
 from ...utils.logging import logger
-from ..utils import CheckOverflow, get_grad_norm
+from ..utils import CheckOverflow, get_grad_norm, grad_norm_sq_tensor
 from .loss_scaler import DynamicLossScaler, LossScaler
 
 
@@ -84,7 +84,10 @@ class FP16_UnfusedOptimizer:
 
     def step(self, closure=None):
         params = [p for g in self.fp16_groups for p in g]
-        self.overflow = self.overflow_checker.has_overflow(params)
+        # one multi-tensor reduction gives both the global norm and the overflow flag (the sum
+        # of squares is inf/nan iff some gradient entry is): no per-tensor isinf/isnan passes
+        sq = grad_norm_sq_tensor(params, mpu=self.mpu).item()
+        self.overflow = not math.isfinite(sq)
         prev = self.loss_scale
         if self.dynamic_loss_scale or self.overflow:
             self.loss_scaler.update_scale(self.overflow)
@@ -93,11 +96,21 @@ class FP16_UnfusedOptimizer:
                         f"{prev}, reducing to {self.loss_scale}")
             self.zero_grad()
             return self.overflow
-        norm = get_grad_norm(params, mpu=self.mpu) / prev
+        norm = math.sqrt(sq) / prev
         self._global_grad_norm = norm
         coef = 1.0 / prev
         if self.clip_grad > 0 and norm > self.clip_grad:
             coef *= self.clip_grad / (norm + 1e-6)
+        if getattr(self.optimizer, "supports_fused_lp_step", False):
+            # fused LAMB: low-precision grads read with the unscale/clip factor folded in, the
+            # updated master written back to the low-precision params by the same kernel
+            grads, outs = [], []
+            for lp_group, fp_group in zip(self.fp16_groups, self.fp32_groups):
+                grads.append([p.grad for p in lp_group])
+                outs.append([p.data for p in lp_group])
+            self.optimizer.step(grads=grads, output_params=outs, scale=1.0 / coef)
+            self.zero_grad()
+            return self.overflow
         for lp_group, fp_group in zip(self.fp16_groups, self.fp32_groups):
             for p, m in zip(lp_group, fp_group):
                 if p.grad is None:

@@ -124,6 +124,25 @@ def _dev():
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
 
+def grad_norm_sq_tensor(parameters, mpu=None) -> torch.Tensor:
+    """Sum of squared gradient entries as a 1-element fp32 tensor, without a host sync:
+    multi-tensor `_foreach_norm` (fp32 accumulation) over the gradients, model-parallel
+    duplicates counted once, summed over the model-parallel group."""
+    mp_rank = mpu.get_model_parallel_rank() if mpu is not None else 0
+    grads = [p.grad.data for p in parameters if p.grad is not None and (mp_rank == 0 or is_model_parallel_parameter(p))]
+    dev = grads[0].device if grads else _dev()
+    acc = torch.zeros(1, device=dev, dtype=torch.float32)
+    by_dev = {}
+    for g in grads:
+        by_dev.setdefault((g.device, g.dtype), []).append(g)
+    for (d, _), gs in by_dev.items():
+        norms = torch._foreach_norm(gs, 2, dtype=torch.float32)
+        acc += torch.stack(norms).square().sum().to(dev)
+    if mpu is not None:
+        dist.all_reduce(acc, group=mpu.get_model_parallel_group())
+    return acc
+
+
 def get_grad_norm(parameters, norm_type=2, mpu=None):
     """Global gradient norm; model-parallel duplicates counted once (on mp rank 0)."""
     if isinstance(parameters, torch.Tensor):
@@ -137,6 +156,8 @@ def get_grad_norm(parameters, norm_type=2, mpu=None):
         if mpu is not None:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=mpu.get_model_parallel_group())
         total = t.item()
+    elif norm_type == 2.0:
+        total = grad_norm_sq_tensor(parameters, mpu).item() ** 0.5
     else:
         acc = torch.zeros(1, device=_dev())
         for p in parameters:

@@ -1,0 +1,92 @@
+"""BERT pre-training throughput (the reference's "fastest BERT training"
+numbers, BERT-Large on one V100: seq 128 -> 272 samples/s, 64 TFLOPS; seq 512 -> 52 samples/s,
+53 TFLOPS).
+
+BERT-Large, pre-LN DeepSpeedTransformerLayer encoder (HIP kernels + hipBLASLt), dropout 0.1,
+MLM over 15 % masked positions (20 per 128 tokens) + NSP, LAMB (FusedLamb HIP kernel) through
+deeperspeed_amd.initialize, bf16.  Synthetic token ids / random-init weights.
+
+    python scripts/bench_bert.py --seq 128 --batch 64
+    python scripts/bench_bert.py --seq 512 --batch 16
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+REF = {128: (272.0, 64.0), 512: (52.0, 53.0)}  # samples/s, TFLOPS on 1x V100
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="bert-large")
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--device", default="cuda")
+    args = ap.parse_args()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29541")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.bert import BertForPreTraining, get_config
+
+    dev = torch.device(args.device)
+    ds.init_distributed(dist_backend="nccl" if dev.type == "cuda" else "gloo")
+    over = {"vocab_size": 512, "max_position": args.seq} if args.model == "tiny" else {}
+    cfg = get_config(args.model, **over)
+    torch.manual_seed(0)
+    model = BertForPreTraining(cfg, device=dev, dtype=torch.bfloat16).train()
+    conf = {"train_micro_batch_size_per_gpu": args.batch, "gradient_accumulation_steps": 1,
+            "optimizer": {"type": "Lamb", "params": {"lr": 1e-3, "weight_decay": 0.01}},
+            "fp16": {"enabled": True, "type": "bfloat16"}, "steps_per_print": 10**9}
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    B, S = args.batch, args.seq
+    npred = max(1, round(0.15 * S / 8) * 8 // 1) if S != 128 else 20
+    npred = 20 if S == 128 else (80 if S == 512 else npred)
+    g = torch.Generator(device=dev).manual_seed(1)
+    ids = torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)
+    tt = (torch.arange(S, device=dev)[None] >= S // 2).long().expand(B, S).contiguous()
+    am = torch.ones(B, S, device=dev, dtype=torch.long)
+    pos = torch.stack([torch.randperm(S, device=dev, generator=g)[:npred].sort().values for _ in range(B)])
+    lab = torch.randint(0, cfg.vocab_size, (B, npred), device=dev, generator=g)
+    nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
+
+    def step():
+        loss = engine(ids, tt, am, pos, lab, nsp)
+        engine.backward(loss)
+        engine.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(args.steps):
+        loss = step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = (time.time() - t0) / args.steps
+    sps = B / dt
+    tflops = sps * cfg.flops_per_sample(S, npred) / 1e12
+    ref = REF.get(S)
+    print(json.dumps({"metric": f"BERT pre-training samples/s ({args.model}, seq {S})", "value": round(sps, 1),
+                      "unit": "samples/s", "ms_per_step": round(dt * 1e3, 2), "batch": B, "seq": S,
+                      "masked_per_seq": npred, "model_tflops": round(tflops, 1), "dtype": "bf16",
+                      "optimizer": "FusedLamb", "data": "synthetic", "final_loss": round(float(loss.detach()), 4),
+                      "ref_v100_samples_per_s": ref[0] if ref else None,
+                      "vs_ref_v100": round(sps / ref[0], 2) if ref else None}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
