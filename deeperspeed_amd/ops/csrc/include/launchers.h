@@ -34,6 +34,8 @@ void launch_scale_copy(const void* x, int xt, void* y, int yt, int64_t n, const 
                        hipStream_t s);
 void launch_lamb(void* w, int wt, const void* g, int gt, float* m, float* v, float* upd, void* out, int ot,
                  int64_t n, LambArgs a, float* workspace, float* coeff_out, hipStream_t s);
+void launch_lamb_multi(const int64_t* meta, int T, int64_t total_chunks, int64_t chunk, int wt, int gt, int ot,
+                       LambArgs a, float* partial, float* coeff, hipStream_t s);
 
 // norm_act.hip
 int ln_max_hidden(int dt);

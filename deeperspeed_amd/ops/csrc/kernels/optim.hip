@@ -268,6 +268,97 @@ __global__ void __launch_bounds__(256) lamb_apply_kernel(TW* __restrict__ w, con
   }
 }
 
+// Multi-tensor LAMB: the whole parameter list in three launches (meta table as adam_multi:
+// w, g, m, v, out pointers, numel, chunk prefix).  Stage 1 writes per-chunk partial ||w||^2,
+// ||u||^2; finish reduces each tensor's chunks to its clamped trust ratio; apply recomputes
+// u from the updated moments (no fp32 scratch for u) and steps w.
+template <typename TW, typename TG>
+__global__ void __launch_bounds__(256) lamb_multi_stage1_kernel(const int64_t* __restrict__ meta, int T,
+                                                                int64_t chunk, LambArgs a,
+                                                                float* __restrict__ partial) {
+  __shared__ float red[32];
+  const int64_t* pref = meta + 6 * T;
+  const int64_t c = blockIdx.x;
+  int lo = 0, hi = T - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (pref[mid] <= c) lo = mid; else hi = mid - 1;
+  }
+  const int t = lo;
+  const TW* w = reinterpret_cast<const TW*>(meta[t]);
+  const TG* g = reinterpret_cast<const TG*>(meta[T + t]);
+  float* m = reinterpret_cast<float*>(meta[2 * T + t]);
+  float* v = reinterpret_cast<float*>(meta[3 * T + t]);
+  const int64_t n = meta[5 * T + t];
+  const int64_t start = (c - pref[t]) * chunk;
+  const int64_t end = start + chunk < n ? start + chunk : n;
+  float sw = 0.f, su = 0.f;
+  for (int64_t e = start + threadIdx.x; e < end; e += blockDim.x) {
+    const float wf = Conv<TW>::load(w, e);
+    const float gf = Conv<TG>::load(g, e) * a.grad_scale;
+    const float mf = fmaf(a.beta1, m[e], (1.f - a.beta1) * gf);
+    const float vf = fmaf(a.beta2, v[e], (1.f - a.beta2) * gf * gf);
+    m[e] = mf; v[e] = vf;
+    const float denom = a.adamw ? sqrtf(vf) + a.eps : sqrtf(vf + a.eps);
+    const float u = mf / denom + a.weight_decay * wf;
+    sw = fmaf(wf, wf, sw);
+    su = fmaf(u, u, su);
+  }
+  block_sum2(sw, su, red);
+  if (threadIdx.x == 0) { partial[2 * c] = sw; partial[2 * c + 1] = su; }
+}
+
+__global__ void __launch_bounds__(256) lamb_multi_finish_kernel(const int64_t* __restrict__ meta, int T,
+                                                                const float* __restrict__ partial, LambArgs a,
+                                                                float* __restrict__ coeff) {
+  __shared__ float red[32];
+  const int64_t* pref = meta + 6 * T;
+  const int t = blockIdx.x;
+  float sw = 0.f, su = 0.f;
+  for (int64_t c = pref[t] + threadIdx.x; c < pref[t + 1]; c += blockDim.x) {
+    sw += partial[2 * c];
+    su += partial[2 * c + 1];
+  }
+  block_sum2(sw, su, red);
+  if (threadIdx.x == 0) {
+    const float wn = sqrtf(sw), un = sqrtf(su);
+    float cf = 1.f;
+    if (wn > 0.f && un > 0.f) cf = fminf(fmaxf(wn / un, a.min_coeff), a.max_coeff);
+    coeff[t] = cf;
+  }
+}
+
+template <typename TW, typename TO>
+__global__ void __launch_bounds__(256) lamb_multi_apply_kernel(const int64_t* __restrict__ meta, int T,
+                                                               int64_t chunk, LambArgs a,
+                                                               const float* __restrict__ coeff) {
+  const int64_t* pref = meta + 6 * T;
+  const int64_t c = blockIdx.x;
+  int lo = 0, hi = T - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (pref[mid] <= c) lo = mid; else hi = mid - 1;
+  }
+  const int t = lo;
+  TW* w = reinterpret_cast<TW*>(meta[t]);
+  const float* m = reinterpret_cast<const float*>(meta[2 * T + t]);
+  const float* v = reinterpret_cast<const float*>(meta[3 * T + t]);
+  TO* out = reinterpret_cast<TO*>(meta[4 * T + t]);
+  const int64_t n = meta[5 * T + t];
+  const int64_t start = (c - pref[t]) * chunk;
+  const int64_t end = start + chunk < n ? start + chunk : n;
+  const float s = a.lr * coeff[t];
+  for (int64_t e = start + threadIdx.x; e < end; e += blockDim.x) {
+    const float wf = Conv<TW>::load(w, e);
+    const float vf = v[e];
+    const float denom = a.adamw ? sqrtf(vf) + a.eps : sqrtf(vf + a.eps);
+    const float u = m[e] / denom + a.weight_decay * wf;
+    const float nw = wf - s * u;
+    Conv<TW>::store(w, e, nw);
+    if (out) Conv<TO>::store(out, e, nw);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host launchers (called from bindings.cpp)
 // ---------------------------------------------------------------------------
@@ -333,6 +424,19 @@ void launch_lamb(void* w, int wt, const void* g, int gt, float* m, float* v, flo
   DSA_DISPATCH_T(wt, TW, DSA_DISPATCH_T(ot, TO,
     hipLaunchKernelGGL((lamb_apply_kernel<TW, TO>), dim3(grid_for(n, 256, 4096)), dim3(256), 0, s,
                        (TW*)w, upd, n, a.lr, coeff_out, (TO*)out)));
+}
+
+// partial: 2 * total_chunks floats; coeff: T floats (device-resident trust ratios)
+void launch_lamb_multi(const int64_t* meta, int T, int64_t total_chunks, int64_t chunk, int wt, int gt, int ot,
+                       LambArgs a, float* partial, float* coeff, hipStream_t s) {
+  if (total_chunks <= 0 || T <= 0) return;
+  DSA_DISPATCH_T(wt, TW, DSA_DISPATCH_T(gt, TG,
+    hipLaunchKernelGGL((lamb_multi_stage1_kernel<TW, TG>), dim3((unsigned)total_chunks), dim3(256), 0, s,
+                       meta, T, chunk, a, partial)));
+  hipLaunchKernelGGL(lamb_multi_finish_kernel, dim3((unsigned)T), dim3(256), 0, s, meta, T, partial, a, coeff);
+  DSA_DISPATCH_T(wt, TW, DSA_DISPATCH_T(ot, TO,
+    hipLaunchKernelGGL((lamb_multi_apply_kernel<TW, TO>), dim3((unsigned)total_chunks), dim3(256), 0, s,
+                       meta, T, chunk, a, coeff)));
 }
 
 }  // namespace dsa

@@ -1,14 +1,17 @@
 """FusedLamb: LAMB on the HIP kernels (ops/csrc/kernels/optim.hip lamb_*).
 
 Reference parity: deepspeed/ops/lamb/fused_lamb.py:12-189 (per-parameter launch, trust ratio
-clamped to [min_coeff, max_coeff], `get_lamb_coeffs`).  Three launches per tensor (moments +
-partial norms, norm finish, apply) with the coefficient kept on the device, so a step has no
-host synchronisation; `get_lamb_coeffs()` syncs only when called.
+clamped to [min_coeff, max_coeff], `get_lamb_coeffs`).  On the GPU the whole parameter list is
+updated by three multi-tensor launches (per-chunk moments + partial norms, per-tensor trust
+ratios, apply) instead of the reference's kernel per tensor; coefficients stay on the device,
+so a step has no host synchronisation and `get_lamb_coeffs()` syncs only when called.
 """
 
 import torch
 
 from .. import native
+
+_CHUNK = 65536  # elements per block of the multi-tensor kernels
 
 
 class FusedLamb(torch.optim.Optimizer):
@@ -29,6 +32,8 @@ class FusedLamb(torch.optim.Optimizer):
         self.eps_mode = 0 if eps_inside_sqrt else 1
         self.lamb_coeffs = []
         self.requires_per_param_masters = True  # trust ratio is per tensor: never flatten
+        self.multi_tensor = True  # GPU: one multi-tensor launch set per (dtype, step) bucket
+        self._meta_cache = {}
 
     supports_fused_lp_step = True  # FP16_UnfusedOptimizer passes low-precision grads/outputs
 
@@ -36,34 +41,76 @@ class FusedLamb(torch.optim.Optimizer):
     def step(self, closure=None, grads=None, output_params=None, scale=1.0, grad_norms=None):
         """`grads`/`output_params`/`scale` follow the reference's legacy fused interface:
         optional explicit gradient lists, low-precision output copies and a loss scale the
-        gradients are divided by."""
+        gradients are divided by.  GPU tensors of one (dtype, step) bucket are updated by the
+        multi-tensor kernels: three launches for the whole bucket (per-chunk partial norms,
+        per-tensor trust ratios, apply)."""
         loss = closure() if closure is not None else None
         self.lamb_coeffs = []
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             g_list = grads[gi] if grads is not None else [None] * len(group["params"])
             o_list = output_params[gi] if output_params is not None else [None] * len(group["params"])
+            buckets = {}
             for p, g, o in zip(group["params"], g_list, o_list):
                 g = p.grad if g is None else g
                 if g is None:
                     continue
-                if o is not None and o.data_ptr() == p.data_ptr():
-                    o = None
                 if g.is_sparse:
                     raise RuntimeError("FusedLamb does not support sparse gradients")
+                if o is not None and o.data_ptr() == p.data_ptr():
+                    o = None
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros(p.numel(), dtype=torch.float32, device=p.device)
                     st["exp_avg_sq"] = torch.zeros(p.numel(), dtype=torch.float32, device=p.device)
                 st["step"] += 1
-                w = p.data.view(-1)
-                c = native.lamb_(w, g.contiguous().view(-1), st["exp_avg"], st["exp_avg_sq"],
+                if p.is_cuda and self.multi_tensor:
+                    key = (p.device, p.dtype, g.dtype, o.dtype if o is not None else None, st["step"])
+                    buckets.setdefault(key, []).append((p, g.contiguous(), o))
+                    continue
+                c = native.lamb_(p.data.view(-1), g.contiguous().view(-1), st["exp_avg"], st["exp_avg_sq"],
                                  o.view(-1) if o is not None else None, group["lr"], b1, b2, group["eps"],
                                  group["weight_decay"], st["step"], group["bias_correction"], 1.0 / scale,
                                  group["max_coeff"], group["min_coeff"], self.eps_mode == 1)
                 self.lamb_coeffs.append(c)
+            for (dev, pdt, gdt, odt, step), items in buckets.items():
+                self.lamb_coeffs.append(self._multi_step(dev, pdt, gdt, odt, step, items, group, 1.0 / scale))
         return loss
 
+    def _multi_step(self, dev, pdt, gdt, odt, step, items, group, grad_scale):
+        import math
+        ws = [p.data for p, _, _ in items]
+        gs = [g for _, g, _ in items]
+        ms = [self.state[p]["exp_avg"] for p, _, _ in items]
+        vs = [self.state[p]["exp_avg_sq"] for p, _, _ in items]
+        outs = [o for _, _, o in items]
+        key = tuple(t.data_ptr() for t in ws + gs) + tuple(o.data_ptr() if o is not None else 0 for o in outs)
+        hit = self._meta_cache.get(key)
+        if hit is None:
+            numels = [t.numel() for t in ws]
+            pref = [0]
+            for n in numels:
+                pref.append(pref[-1] + (n + _CHUNK - 1) // _CHUNK)
+            rows = ([t.data_ptr() for t in ws] + [t.data_ptr() for t in gs] + [t.data_ptr() for t in ms] +
+                    [t.data_ptr() for t in vs] + [(o.data_ptr() if o is not None else 0) for o in outs] + numels
+                    + pref)
+            meta = torch.tensor(rows, dtype=torch.int64).to(dev)
+            hit = (meta, len(ws), pref[-1], torch.empty(2 * pref[-1], dtype=torch.float32, device=dev))
+            if len(self._meta_cache) > 64:
+                self._meta_cache.clear()
+            self._meta_cache[key] = hit
+        meta, T, total, partial = hit
+        b1, b2 = group["betas"]
+        bc1 = 1.0 - b1 ** step if group["bias_correction"] else 1.0
+        bc2 = 1.0 - b2 ** step if group["bias_correction"] else 1.0
+        code = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+        coeff = torch.empty(T, dtype=torch.float32, device=dev)
+        native.hip_ops().lamb_multi(meta, T, total, _CHUNK, code[pdt], code[gdt], code[odt or pdt],
+                                    group["lr"] * math.sqrt(bc2) / bc1, b1, b2, group["eps"], group["weight_decay"],
+                                    bc1, bc2, grad_scale, group["max_coeff"], group["min_coeff"],
+                                    self.eps_mode == 1, partial, coeff)
+        return coeff
+
     def get_lamb_coeffs(self):
-        return [float(c) for c in self.lamb_coeffs]
+        return [float(x) for c in self.lamb_coeffs for x in c.reshape(-1).tolist()]

@@ -479,3 +479,32 @@ def test_linear_wgrad_transposed_operands(bound):
     finally:
         lin.WGRAD_NT = lin.DGRAD_NT = True
         lin.WGRAD_NT_MIN_NUMEL = old
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_multi_tensor_lamb_matches_per_tensor(gdt):
+    """FusedLamb's multi-tensor launches (per-chunk partial norms, per-tensor trust ratio)
+    equal the per-tensor kernels: weights, moments, bf16 output copies and coefficients."""
+    from deeperspeed_amd.ops.lamb import FusedLamb
+    torch.manual_seed(5)
+    shapes = [(1000,), (300, 257), (65536 * 2 + 5,), (7,), (1024, 64)]
+    res = {}
+    for multi in (False, True):
+        torch.manual_seed(5)
+        ps = [torch.randn(*s, device=_dev()).requires_grad_(True) for s in shapes]
+        opt = FusedLamb(ps, lr=1e-2, weight_decay=0.01, max_coeff=10.0, min_coeff=0.01)
+        opt.multi_tensor = multi
+        outs = [torch.empty(p.shape, device=_dev(), dtype=torch.bfloat16) for p in ps]
+        for it in range(3):
+            grads = [torch.randn_like(p).to(gdt) for p in ps]
+            opt.step(grads=[grads], output_params=[outs], scale=2.0)
+        res[multi] = ([p.detach().clone() for p in ps], [o.clone() for o in outs],
+                      [opt.state[p]["exp_avg_sq"].clone() for p in ps], opt.get_lamb_coeffs())
+    for a, b in zip(res[False][0], res[True][0]):
+        torch.testing.assert_close(b, a, atol=1e-6, rtol=1e-5)
+    for a, b in zip(res[False][1], res[True][1]):
+        torch.testing.assert_close(b.float(), a.float(), atol=1e-2, rtol=1e-2)
+    for a, b in zip(res[False][2], res[True][2]):
+        torch.testing.assert_close(b, a, atol=1e-7, rtol=1e-5)
+    assert len(res[True][3]) == len(shapes)
+    torch.testing.assert_close(torch.tensor(res[True][3]), torch.tensor(res[False][3]), atol=1e-5, rtol=1e-4)
