@@ -1,0 +1,4 @@
+"""Optimizer-state NVMe swapper at the reference's import path
+(deepspeed/runtime/swap_tensor/partitioned_optimizer_swapper.py); implementation in optimizer_utils.py."""
+
+from .optimizer_utils import PartitionedOptimizerSwapper  # noqa: F401
