@@ -56,7 +56,46 @@ PATHS = [
     ("deepspeed.launcher.multinode_runner", ["PDSHRunner", "OpenMPIRunner", "MVAPICHRunner", "SlurmRunner"]),
     ("deepspeed.env_report", ["main"]),
     ("deepspeed.utils.timer", ["SynchronizedWallClockTimer", "ThroughputTimer"]),
+    # remaining reference module paths (SURVEY §2.1 file inventory)
+    ("deepspeed.constants", ["TORCH_DISTRIBUTED_DEFAULT_PORT", "default_pg_timeout"]),
+    ("deepspeed.git_version_info", ["version", "git_hash", "git_branch", "installed_ops", "compatible_ops"]),
+    ("deepspeed.runtime.constants", ["ROUTE_TRAIN", "ROUTE_EVAL", "ROUTE_PREDICT", "TRAIN_BATCH_SIZE",
+                                     "TRAIN_MICRO_BATCH_SIZE_PER_GPU_DEFAULT", "FP16_LOSS_SCALE_WINDOW_DEFAULT",
+                                     "SPARSE_BIGBIRD_MODE", "GRADIENT_CLIPPING", "CHECKPOINT_TAG_VALIDATION_MODES",
+                                     "PLD_THETA_DEFAULT", "TENSORBOARD_JOB_NAME_DEFAULT"]),
+    ("deepspeed.runtime.zero.constants", ["ZERO_OPTIMIZATION", "ZERO_OPTIMIZATION_STAGE_DEFAULT",
+                                          "ZERO_OPTIMIZATION_REDUCE_BUCKET_SIZE_DEFAULT", "ZERO_OPTIMIZATION_DEFAULT",
+                                          "ZERO3_OPTIMIZATION_OVERLAP_COMM_DEFAULT", "MAX_STAGE_ZERO_OPTIMIZATION"]),
+    ("deepspeed.runtime.zero.offload_constants", ["OFFLOAD_CPU_DEVICE", "OFFLOAD_NVME_DEVICE",
+                                                  "OFFLOAD_PARAM_BUFFER_COUNT_DEFAULT",
+                                                  "OFFLOAD_OPTIMIZER_PIPELINE_READ"]),
+    ("deepspeed.runtime.zero.offload_config", ["get_offload_param_config", "get_offload_optimizer_config"]),
+    ("deepspeed.runtime.swap_tensor.constants", ["AIO_BLOCK_SIZE", "AIO_QUEUE_DEPTH_DEFAULT"]),
+    ("deepspeed.runtime.swap_tensor.aio_config", ["get_aio_config"]),
+    ("deepspeed.runtime.swap_tensor.partitioned_optimizer_swapper", ["PartitionedOptimizerSwapper"]),
+    ("deepspeed.runtime.swap_tensor.pipelined_optimizer_swapper", ["PipelinedOptimizerSwapper"]),
+    ("deepspeed.runtime.swap_tensor.partitioned_param_swapper", ["AsyncPartitionedParameterSwapper",
+                                                                 "PartitionedParamStatus"]),
+    ("deepspeed.profiling.constants", ["FLOPS_PROFILER_PROFILE_STEP_DEFAULT"]),
+    ("deepspeed.profiling.config", ["DeepSpeedFlopsProfilerConfig"]),
+    ("deepspeed.module_inject.inject", ["module_inject"]),
+    ("deepspeed.ops.module_inject", ["replace_transformer_layer", "revert_transformer_layer"]),
+    ("deepspeed.ops.adam.multi_tensor_apply", ["MultiTensorApply"]),
+    ("deepspeed.runtime.compression.cupy", ["CupyBackend"]),
+    ("deepspeed.runtime.comm.compressed_ar", ["compressed_all_reduce", "decompose", "reconstruct"]),
 ]
+
+
+def test_constants_match_parser_defaults():
+    """Generated key constants are the ones the config parsers read."""
+    from deeperspeed_amd.runtime import constants as c
+    from deeperspeed_amd.runtime.zero import constants as z
+    from deeperspeed_amd.runtime.zero.config import _SCALARS
+    assert c.STEPS_PER_PRINT_DEFAULT == 10 and c.FP16_INITIAL_SCALE_POWER_DEFAULT == 32
+    for stem, key in [("ZERO_OPTIMIZATION_REDUCE_BUCKET_SIZE", "reduce_bucket_size"),
+                      ("ZERO_OPTIMIZATION_MAX_LIVE_PARAMETERS", "stage3_max_live_parameters"),
+                      ("ZERO_OPTIMIZATION_PARAM_PERSISTENCE_THRESHOLD", "stage3_param_persistence_threshold")]:
+        assert getattr(z, stem) == key and getattr(z, stem + "_DEFAULT") == _SCALARS[key]
 
 
 @pytest.mark.parametrize("mod,names", PATHS, ids=[p[0] for p in PATHS])
