@@ -14,15 +14,10 @@ import sys
 
 _TARGET = "deeperspeed_amd"
 _RENAMES = {
-    "deepspeed.runtime.zero.stage1": "deeperspeed_amd.runtime.zero.stage_1_and_2",
-    "deepspeed.runtime.zero.stage2": "deeperspeed_amd.runtime.zero.stage_1_and_2",
-    "deepspeed.runtime.zero.constants": "deeperspeed_amd.runtime.zero.config",
-    "deepspeed.runtime.zero.offload_config": "deeperspeed_amd.runtime.zero.config",
     "deepspeed.runtime.pipe.topology": "deeperspeed_amd.runtime.pipe.topology",
-    "deepspeed.runtime.constants": "deeperspeed_amd.runtime.config",
     "deepspeed.ops.op_builder": "deeperspeed_amd.ops.op_builder",
     "deepspeed.op_builder": "deeperspeed_amd.ops.op_builder",
-    "deepspeed.git_version_info": "deeperspeed_amd.version",
+    "deepspeed.git_version_info": "deeperspeed_amd.git_version_info",
 }
 
 
