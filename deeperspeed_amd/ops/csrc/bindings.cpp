@@ -281,6 +281,45 @@ Tensor transpose2d(Tensor x, OptT colsum_out, bool accum) {
   return y;
 }
 
+// BERT head layout moves (16-bit, head dim % 8 == 0)
+std::vector<Tensor> heads_split(Tensor qkv, int64_t NH) {
+  check_dev(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) % (3 * NH) == 0 && qkv.element_size() == 2, "heads_split: qkv [B,S,3*NH*HD] 16-bit");
+  const int64_t B = qkv.size(0), S = qkv.size(1), HD = qkv.size(2) / (3 * NH);
+  TORCH_CHECK(HD % 8 == 0 && aligned16(qkv.data_ptr()), "heads_split: head dim % 8, 16-byte aligned");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  auto o = qkv.options();
+  Tensor q = at::empty({B, NH, S, HD}, o), k = at::empty({B, NH, S, HD}, o), v = at::empty({B, NH, S, HD}, o);
+  dsa::launch_heads_split(qkv.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), (int)B, (int)S, (int)NH, (int)HD,
+                          cur_stream());
+  return {q, k, v};
+}
+
+Tensor heads_merge(Tensor q, Tensor k, Tensor v) {
+  check_dev(q, "q"); check_dev(k, "k"); check_dev(v, "v");
+  TORCH_CHECK(q.dim() == 4 && q.sizes() == k.sizes() && q.sizes() == v.sizes() && q.element_size() == 2,
+              "heads_merge: q,k,v [B,NH,S,HD] 16-bit");
+  const int64_t B = q.size(0), NH = q.size(1), S = q.size(2), HD = q.size(3);
+  TORCH_CHECK(HD % 8 == 0, "heads_merge: head dim % 8");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  Tensor qkv = at::empty({B, S, 3 * NH * HD}, q.options());
+  dsa::launch_heads_merge(q.data_ptr(), k.data_ptr(), v.data_ptr(), qkv.data_ptr(), (int)B, (int)S, (int)NH, (int)HD,
+                          cur_stream());
+  return qkv;
+}
+
+// x [A,P,Q,D] -> contiguous [A,Q,P,D]
+Tensor swap12(Tensor x) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.element_size() == 2 && x.size(3) % 8 == 0 && aligned16(x.data_ptr()),
+              "swap12: 4-D 16-bit, last dim % 8");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor y = at::empty({x.size(0), x.size(2), x.size(1), x.size(3)}, x.options());
+  dsa::launch_swap12(x.data_ptr(), y.data_ptr(), x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3),
+                     cur_stream());
+  return y;
+}
+
 // ----------------------------------------------------------------------------- attention elementwise
 // qkv [B,S,NH*3*HD] (NeoX per-head q|k|v) -> q,k,v [B,NH,S,HD]; cs [S, ROT/2, 2] fp32
 std::vector<Tensor> rotary_split_fwd(Tensor qkv, Tensor cs, int64_t NH, int64_t HD, int64_t ROT, double qscale) {
@@ -604,5 +643,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("colsum", &colsum);
+  m.def("heads_split", &heads_split);
+  m.def("heads_merge", &heads_merge);
+  m.def("swap12", &swap12);
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("colsum_out") = py::none(), py::arg("accum") = false);
 }

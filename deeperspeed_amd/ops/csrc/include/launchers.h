@@ -68,6 +68,11 @@ void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const f
                              int HD, int ROT, float qscale, int dt, hipStream_t s);
 void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, void* dqkv, const float* cs, int B,
                              int S, int NH, int HD, int ROT, float qscale, int dt, hipStream_t s);
+// 16-bit layout moves (HD, D multiples of 8): qkv [B,S,3,NH,HD] <-> q,k,v [B,NH,S,HD]; x [A,P,Q,D] -> [A,Q,P,D]
+void launch_heads_split(const void* qkv, void* q, void* k, void* v, int B, int S, int NH, int HD, hipStream_t s);
+void launch_heads_merge(const void* q, const void* k, const void* v, void* qkv, int B, int S, int NH, int HD,
+                        hipStream_t s);
+void launch_swap12(const void* x, void* y, int64_t A, int P, int Q, int D, hipStream_t s);
 int softmax_max_cols();
 void launch_softmax_fwd(const void* x, void* y, const void* mask, int64_t R, int C, int Sq, int heads, float scale,
                         int causal, int mask_rows, int dt, hipStream_t s);

@@ -535,4 +535,84 @@ void launch_softmax_bwd(const void* dy, const void* y, void* dx, int64_t R, int 
                        (const T*)y, (T*)dx, R, C, scale)));
 }
 
+// --------------------------------------------------------------------------------------
+// BERT attention layout moves (reference transform_kernels.cu: bias_add_transform_0213,
+// transform4d_0213): one 16-byte vector per thread, reads and writes both coalesced along the
+// head dimension.
+//   heads_split:  qkv [B, S, 3, NH, HD] -> q, k, v [B, NH, S, HD]   (and heads_merge, its inverse)
+//   swap12:       x [A, P, Q, D] -> y [A, Q, P, D]                   (context merge and its backward)
+// --------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) heads_split_kernel(const uint4* __restrict__ qkv, uint4* __restrict__ q,
+                                                          uint4* __restrict__ k, uint4* __restrict__ v, int64_t total,
+                                                          int S, int NH, int HV) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int dv = (int)(t % HV);
+    int64_t r = t / HV;
+    const int h = (int)(r % NH); r /= NH;
+    const int which = (int)(r % 3); r /= 3;
+    const int s = (int)(r % S);
+    const int64_t b = r / S;
+    uint4* dst = which == 0 ? q : (which == 1 ? k : v);
+    dst[((b * NH + h) * S + s) * HV + dv] = qkv[t];
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) heads_merge_kernel(const uint4* __restrict__ q, const uint4* __restrict__ k,
+                                                          const uint4* __restrict__ v, uint4* __restrict__ qkv,
+                                                          int64_t total, int S, int NH, int HV) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int dv = (int)(t % HV);
+    int64_t r = t / HV;
+    const int h = (int)(r % NH); r /= NH;
+    const int which = (int)(r % 3); r /= 3;
+    const int s = (int)(r % S);
+    const int64_t b = r / S;
+    const uint4* src = which == 0 ? q : (which == 1 ? k : v);
+    qkv[t] = src[((b * NH + h) * S + s) * HV + dv];
+  }
+}
+
+__global__ void __launch_bounds__(256) swap12_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int64_t total,
+                                                     int P, int Q, int DV) {
+  // t enumerates the OUTPUT [A, Q, P, DV] so writes are contiguous
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int dv = (int)(t % DV);
+    int64_t r = t / DV;
+    const int p = (int)(r % P); r /= P;
+    const int q = (int)(r % Q);
+    const int64_t a = r / Q;
+    y[t] = x[((a * P + p) * Q + q) * DV + dv];
+  }
+}
+
+static int move_grid(int64_t vecs) {
+  int64_t g = (vecs + 255) / 256;
+  if (g > 65536) g = 65536;
+  return (int)(g < 1 ? 1 : g);
+}
+
+void launch_heads_split(const void* qkv, void* q, void* k, void* v, int B, int S, int NH, int HD, hipStream_t s) {
+  const int HV = HD / 8;
+  const int64_t total = (int64_t)B * S * 3 * NH * HV;
+  hipLaunchKernelGGL((heads_split_kernel<bf16_t>), dim3(move_grid(total)), dim3(256), 0, s, (const uint4*)qkv,
+                     (uint4*)q, (uint4*)k, (uint4*)v, total, S, NH, HV);
+}
+
+void launch_heads_merge(const void* q, const void* k, const void* v, void* qkv, int B, int S, int NH, int HD,
+                        hipStream_t s) {
+  const int HV = HD / 8;
+  const int64_t total = (int64_t)B * S * 3 * NH * HV;
+  hipLaunchKernelGGL((heads_merge_kernel<bf16_t>), dim3(move_grid(total)), dim3(256), 0, s, (const uint4*)q,
+                     (const uint4*)k, (const uint4*)v, (uint4*)qkv, total, S, NH, HV);
+}
+
+void launch_swap12(const void* x, void* y, int64_t A, int P, int Q, int D, hipStream_t s) {
+  const int DV = D / 8;
+  const int64_t total = A * P * Q * DV;
+  hipLaunchKernelGGL(swap12_kernel, dim3(move_grid(total)), dim3(256), 0, s, (const uint4*)x, (uint4*)y, total, P, Q,
+                     DV);
+}
+
 }  // namespace dsa

@@ -76,6 +76,39 @@ class DeepSpeedTransformerConfig(TransformerConfig):
             return cls.from_dict(json.loads(reader.read()))
 
 
+class _SplitHeads(torch.autograd.Function):
+    """qkv [B,S,3H] -> contiguous q,k,v [B,nh,S,hd] in one HIP pass (reference
+    bias_add_transform_0213); backward merges dq,dk,dv back into dqkv in one pass."""
+
+    @staticmethod
+    def forward(ctx, qkv, nh):
+        q, k, v = native.hip_ops().heads_split(qkv.contiguous(), nh)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        return native.hip_ops().heads_merge(dq.contiguous(), dk.contiguous(), dv.contiguous()), None
+
+
+class _MergeHeads(torch.autograd.Function):
+    """ctx [B,nh,S,hd] -> [B,S,nh*hd] (reference transform4d_0213) and back."""
+
+    @staticmethod
+    def forward(ctx, x):
+        B, nh, S, hd = x.shape
+        ctx.nh, ctx.hd = nh, hd
+        return native.hip_ops().swap12(x.contiguous()).view(B, S, nh * hd)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, S, _ = g.shape
+        return native.hip_ops().swap12(g.contiguous().view(B, S, ctx.nh, ctx.hd))
+
+
+def _use_head_kernels(x, hd):
+    return x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and hd % 8 == 0
+
+
 def _gelu_tanh(x, b):
     return native.bias_gelu(x, b, approximate=True)
 
@@ -96,7 +129,11 @@ class DeepSpeedTransformerFunction:
         x = input
         inp = native.layer_norm(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
         qkv = F.linear(inp, attn_qkvw, attn_qkvb)
-        q, k, v = qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, hd]
+        fast = _use_head_kernels(qkv, hd)
+        if fast:
+            q, k, v = _SplitHeads.apply(qkv, nh)  # contiguous [B, nh, S, hd]: batched GEMMs without copies
+        else:
+            q, k, v = qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, hd]
         scores = torch.matmul(q, k.transpose(-1, -2))
         mask = None
         if input_mask is not None:
@@ -106,7 +143,8 @@ class DeepSpeedTransformerFunction:
             mask = mask.reshape(B, 1, -1, S).contiguous()
         probs = masked_softmax(scores, mask, 1.0 / math.sqrt(hd), False, nh)
         probs = native.dropout(probs, cfg.attn_dropout_ratio, training, gen)
-        ctx = torch.matmul(probs, v).transpose(1, 2).reshape(B, S, Hd)
+        ctx = torch.matmul(probs, v)
+        ctx = _MergeHeads.apply(ctx) if fast else ctx.transpose(1, 2).reshape(B, S, Hd)
         attn_out = F.linear(ctx, attn_ow)
         add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen)
         ff1_inp = native.layer_norm(add_res, attn_nw, attn_nb, eps)

@@ -33,9 +33,11 @@ def _train(out_dir):
     pos = torch.stack([torch.randperm(32, generator=g)[:5].sort().values for _ in range(4)])
     lab = torch.randint(0, cfg.vocab_size, (4, 5), generator=g)
     nsp = torch.randint(0, 2, (4,), generator=g)
+    dev = engine.device
+    ids, pos, lab, nsp = ids.to(dev), pos.to(dev), lab.to(dev), nsp.to(dev)
     losses = []
     for _ in range(8):
-        loss = engine(ids, None, torch.ones(4, 32, dtype=torch.long), pos, lab, nsp)
+        loss = engine(ids, None, torch.ones(4, 32, dtype=torch.long, device=dev), pos, lab, nsp)
         engine.backward(loss)
         engine.step()
         losses.append(float(loss))
