@@ -510,19 +510,20 @@ def test_multi_tensor_lamb_matches_per_tensor(gdt):
     torch.testing.assert_close(torch.tensor(res[True][3]), torch.tensor(res[False][3]), atol=1e-5, rtol=1e-4)
 
 
-def test_bert_head_layout_kernels():
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_bert_head_layout_kernels(dt):
     """heads_split / heads_merge / swap12 equal the torch permute copies exactly (fwd and bwd)."""
     from deeperspeed_amd.ops import native
     torch.manual_seed(6)
     B, S, nh, hd = 3, 40, 4, 64
-    qkv = torch.randn(B, S, 3 * nh * hd, device=_dev(), dtype=torch.bfloat16)
+    qkv = torch.randn(B, S, 3 * nh * hd, device=_dev(), dtype=dt)
     q, k, v = native.hip_ops().heads_split(qkv, nh)
     ref = qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4)
     for i, t in enumerate((q, k, v)):
         torch.testing.assert_close(t, ref[i].contiguous(), atol=0, rtol=0)
     back = native.hip_ops().heads_merge(q, k, v)
     torch.testing.assert_close(back, qkv, atol=0, rtol=0)
-    x = torch.randn(B, nh, S, hd, device=_dev(), dtype=torch.bfloat16)
+    x = torch.randn(B, nh, S, hd, device=_dev(), dtype=dt)
     torch.testing.assert_close(native.hip_ops().swap12(x), x.transpose(1, 2).contiguous(), atol=0, rtol=0)
 
 
