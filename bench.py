@@ -62,6 +62,12 @@ def parse():
     p.add_argument("--optimizer", type=str, default="adam", choices=["adam", "onebitadam", "onebitlamb", "lamb"],
                    help="1-bit optimizers run without ZeRO (reference restriction)")
     p.add_argument("--freeze-step", type=int, default=2, help="1-bit optimizers: full-precision warm-up steps")
+    p.add_argument("--force-sharded", action="store_true",
+                   help="ZeRO-3 on one GPU: run the gather / reduce-scatter unit path over a world-1 RCCL "
+                        "communicator instead of binding parameters to their shards")
+    p.add_argument("--resident-grads", type=str, default="auto", choices=["auto", "on", "off"],
+                   help="keep gradients resident across micro-batches, one reduce-scatter per step "
+                        "(auto: when the spare HBM holds a bf16 copy of the gradients)")
     p.add_argument("--dist-backend", type=str, default="nccl",
                    help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU")
     return p.parse_args()
@@ -171,10 +177,22 @@ def main():
     live = int(max(0.0, min(spare / 2, cfg.num_params() * 1.0)))  # bf16 elements
     if args.max_live is not None:
         live = int(args.max_live)
-    zcfg = {"stage": args.zero, "overlap_comm": True, "reduce_bucket_size": int(2e8),
+    # resident gradients (one reduce-scatter per optimizer step instead of one per
+    # micro-batch): a bf16 copy of the full gradients, planned after parameter retention
+    sharded = world > 1 or args.force_sharded
+    resident = args.resident_grads == "on" or (
+        args.resident_grads == "auto" and sharded and ga > 1 and world > 1 and
+        spare - 2 * live >= 2 * cfg.num_params() + reserve)
+    zcfg = {"stage": args.zero, "overlap_comm": True, "reduce_scatter": True, "reduce_bucket_size": int(2e8),
             "stage3_prefetch_bucket_size": int(5e8), "stage3_param_persistence_threshold": int(1e6),
             "stage3_unit_max_numel": int(2e8), "stage3_max_live_parameters": live,
             "stage3_max_reuse_distance": int(2 * cfg.num_params())}
+    if args.force_sharded:
+        # the bypass accumulates micro-batch gradients in bf16 in the bound shard; the forced
+        # sharded path does the same (an fp32 shard would not fit next to 20B's states)
+        zcfg.update(stage3_force_sharded=True, grad_accum_dtype="param")
+    if resident:
+        zcfg["resident_grads"] = True
     if offload == "compact":
         zcfg["compact_master"] = True
     elif offload == "nvme":
@@ -195,7 +213,8 @@ def main():
         "wall_clock_breakdown": False,
     }
     log(f"model={args.model} params={cfg.num_params() / 1e9:.2f}B world={world} mb={mb} ga={ga} seq={args.seq} "
-        f"zero={args.zero} offload={offload} ckpt={ckpt} live={live / 1e9:.1f}B hbm={hbm / 2**30:.0f} GiB "
+        f"zero={args.zero} offload={offload} ckpt={ckpt} live={live / 1e9:.1f}B resident_grads={resident} "
+        f"force_sharded={args.force_sharded} hbm={hbm / 2**30:.0f} GiB "
         f"planned={plan_memory(cfg, mb, args.seq, world, offload, ckpt == 'on', ga) / 2**30:.0f} GiB")
     if args.pipe > 1:
         return run_pipeline(args, cfg, mb, ga, world, rank, dev)
@@ -336,6 +355,8 @@ def main():
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
                    "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) / 2**30, 1),
                    "max_live_parameters": live, "stashed_attention_layers": stashed,
+                   "zero3_path": "sharded" if (world > 1 or args.force_sharded) else "bound-single-rank",
+                   "resident_grads": resident,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N), BASELINE.md derived target"},
     }
     if rank == 0:

@@ -195,15 +195,24 @@ class NeoXAttention(nn.Module):
         # of a checkpointed block keeps q, k, v and the attention output + LSE (4 s*b*h + LSE),
         # and the recompute in backward reuses them, skipping the QKV GEMM, the rotary split and
         # the flash forward (~1.8 ms per 20B layer and micro-batch of 4x2048 on MI355X).
+        # Stashes are keyed by the checkpointed block's input (its storage is held by the
+        # checkpoint until that block's backward, and the recompute sees a detached view of the
+        # same storage), so several forwards in flight before their backwards (pipeline 1F1B,
+        # forward-forward-backward loops) each recompute with their own tensors.
         self.stash_outputs = False
-        self._stash = None
+        self._stash = {}
+        self._stash_key = None  # set by the enclosing layer around each block call
+
+    _STASH_LIMIT = 16  # in-flight checkpointed forwards per layer (pipeline depth bound)
 
     def forward(self, x):
         cfg = self.cfg
         B, S, H = x.shape
         qs = 1.0 / math.sqrt(cfg.head_dim)
-        if self._stash is not None and torch.is_grad_enabled() and ds_ckpt.is_recomputing():
-            stash, self._stash = self._stash, None
+        key = self._stash_key
+        stash = self._stash.pop(key, None) if (key is not None and self._stash and torch.is_grad_enabled()
+                                               and ds_ckpt.is_recomputing()) else None
+        if stash is not None:
             self.query_key_value.grad_only_next = True  # gradient handle only: q, k, v are kept
             qkv = self.query_key_value(x)
             q, k, v = rotary_split(qkv, cfg.num_heads, cfg.head_dim, cfg.rotary_dim, cfg.rotary_base, qscale=qs,
@@ -218,7 +227,11 @@ class NeoXAttention(nn.Module):
             if (self.stash_outputs and ds_ckpt.is_checkpoint_forward() and cfg.attention_dropout == 0.0
                     and native.has_flash_attention(q)):
                 ctx, lse = native.flash_attention_fwd_lse(q, k, v, True, 1.0, out_layout="bshd")
-                self._stash = (q, k, v, ctx, lse)
+                if key is not None:
+                    if key in self._stash or len(self._stash) >= self._STASH_LIMIT:
+                        raise RuntimeError(f"layer {self.layer_number}: selective-recompute stash for this input "
+                                           f"was never consumed (forward without backward?)")
+                    self._stash[key] = (q, k, v, ctx, lse)
             else:
                 ctx = attention(q, k, v, causal=True, softmax_scale=1.0, dropout_p=cfg.attention_dropout,
                                 training=self.training, out_layout="bshd")
@@ -281,10 +294,14 @@ class NeoXTransformerLayer(nn.Module):
         return residual_sum(x, self.mlp(self.post_attention_layernorm(x)))
 
     def _block_ckpt(self, x):
-        if ds_ckpt.is_recomputing():
-            with skip_unread_outputs():
-                return self._block(x)
-        return self._block(x)
+        self.attention._stash_key = (x.untyped_storage().data_ptr(), x.storage_offset(), tuple(x.shape))
+        try:
+            if ds_ckpt.is_recomputing():
+                with skip_unread_outputs():
+                    return self._block(x)
+            return self._block(x)
+        finally:
+            self.attention._stash_key = None
 
     def forward(self, x):
         if self.cfg.checkpoint_activations and self.training and torch.is_grad_enabled():

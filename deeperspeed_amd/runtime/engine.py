@@ -620,11 +620,16 @@ class DeepSpeedEngine(Module):
             from .zero.stage_1_and_2 import DeepSpeedZeroOptimizer
             return DeepSpeedZeroOptimizer(optimizer, stage=stage, reduce_bucket_size=zc.reduce_bucket_size,
                                           allgather_bucket_size=zc.allgather_bucket_size, overlap_comm=zc.overlap_comm,
-                                          reduce_scatter=zc.reduce_scatter, **common)
+                                          reduce_scatter=zc.reduce_scatter, resident_grads=bool(zc.resident_grads),
+                                          sub_group_size=zc.sub_group_size, **common)
         if stage == ZERO_OPTIMIZATION_WEIGHTS:
             from .zero.stage3 import DeepSpeedZeroOptimizer_Stage3
-            unit = zc._raw.get("stage3_unit_max_numel", int(2e8))
+            unit = zc.stage3_unit_max_numel
             return DeepSpeedZeroOptimizer_Stage3(self.module, optimizer,
+                                                 force_sharded=bool(zc.stage3_force_sharded),
+                                                 resident_grads=bool(zc.resident_grads),
+                                                 grad_accum_dtype=zc.grad_accum_dtype,
+                                                 reduce_scatter=zc.reduce_scatter,
                                                  prefetch_bucket_size=zc.stage3_prefetch_bucket_size,
                                                  max_live_parameters=zc.stage3_max_live_parameters,
                                                  max_reuse_distance=zc.stage3_max_reuse_distance,
@@ -1065,11 +1070,24 @@ class DeepSpeedEngine(Module):
 
     @staticmethod
     def _load_file(path, map_location="cpu"):
+        """Weights-only load.  Types this framework itself writes into checkpoints, plus
+        argparse.Namespace (GPT-NeoX client state), are allow-listed; anything else in the
+        file is refused unless DSA_ALLOW_UNSAFE_CHECKPOINT_LOAD=1 explicitly opts into full
+        unpickling of a trusted file."""
+        import argparse
+        import pickle
+        safe = [argparse.Namespace, set, OrderedDict]
         try:
-            return torch.load(path, map_location=map_location, weights_only=True)
-        except Exception:
-            # files written by this framework may carry client objects (e.g. argparse.Namespace)
-            return torch.load(path, map_location=map_location, weights_only=False)
+            with torch.serialization.safe_globals(safe):
+                return torch.load(path, map_location=map_location, weights_only=True)
+        except pickle.UnpicklingError as e:
+            if os.environ.get("DSA_ALLOW_UNSAFE_CHECKPOINT_LOAD", "0") == "1":
+                logger.warning(f"{path}: not loadable weights-only ({e}); DSA_ALLOW_UNSAFE_CHECKPOINT_LOAD=1 set, "
+                               f"unpickling the full file")
+                return torch.load(path, map_location=map_location, weights_only=False)
+            raise RuntimeError(f"{path} holds objects outside the weights-only allow-list: {e}. Register the "
+                               f"types with torch.serialization.add_safe_globals, or set "
+                               f"DSA_ALLOW_UNSAFE_CHECKPOINT_LOAD=1 for a file you trust.") from e
 
     def load_checkpoint(self, load_dir, tag=None, load_module_strict=True, load_optimizer_states=True,
                         load_lr_scheduler_states=True):
@@ -1100,7 +1118,7 @@ class DeepSpeedEngine(Module):
         logger.info(f"rank: {self.global_rank} loading checkpoint: {load_path}")
         checkpoint = self._load_file(load_path)
         if self.zero_optimization_partition_weights():
-            self._load_zero3_module(checkpoint["module"])
+            self._load_zero3_module(checkpoint["module"], load_path)
         elif checkpoint.get("module") is not None or getattr(self, "_loads_module_from_dir", False):
             self.load_module_state_dict(state_dict=checkpoint.get("module"), strict=load_module_strict)
             if hasattr(self.optimizer, "refresh_from_params") and (not load_optimizer_states or
@@ -1122,15 +1140,35 @@ class DeepSpeedEngine(Module):
         client_state = {k: v for k, v in checkpoint.items() if k not in deepspeed_states}
         return load_path, client_state
 
-    def _load_zero3_module(self, payload):
+    def _load_zero3_module(self, payload, load_path=None):
+        """Restore this rank's ZeRO-3 bf16 parameter shards.  Same layout and DP world: the
+        saved shard as is.  Otherwise the low-precision parameters are rebuilt from every
+        saved rank's shard (zero_pp_rank_*_model_states.pt) and re-partitioned, so that a
+        load with load_from_fp32_weights=false still restores the weights."""
         opt = self.optimizer
         if payload is None or "zero3_param_shards" not in payload:
             return
-        from .zero.layout import layout_signature
+        from .zero.layout import layout_signature, params_to_shard, shards_to_params
         if payload.get("layout") == layout_signature(opt.groups) and payload.get("dp_world_size") == opt.dp_world:
             for g, s in zip(opt.groups, payload["zero3_param_shards"]):
                 opt.load_param_shard(g, s)
             opt._post_step()
+            return
+        old_world = int(payload.get("dp_world_size") or 1)
+        folder = os.path.dirname(load_path) if load_path else None
+        mp = os.path.basename(load_path).split("_mp_rank_")[1] if load_path else "00_model_states.pt"
+        files = [os.path.join(folder, f"zero_pp_rank_{r}_mp_rank_{mp}") for r in range(old_world)] if folder else []
+        if not files or not all(os.path.exists(f) for f in files):
+            logger.warning("ZeRO-3 checkpoint: layout / DP world changed and not every rank's model-states file is "
+                           "present; parameters are restored from the fp32 masters only")
+            return
+        payloads = [self._load_file(f)["module"] for f in files]
+        sigs = payloads[0]["layout"]
+        for gi, g in enumerate(opt.groups):
+            full = shards_to_params([pl["zero3_param_shards"][gi] for pl in payloads], sigs[gi])
+            opt.load_param_shard(g, params_to_shard(full, g, opt.dp_rank, g.dtype))
+        logger.info(f"ZeRO-3 checkpoint: re-partitioned bf16 parameters from {old_world} to {opt.dp_world} ranks")
+        opt._post_step()
 
     def _load_zero_checkpoint(self, load_dir, tag, load_optimizer_states=True):
         dp_world = self.loaded_checkpoint_dp_world_size or self.dp_world_size

@@ -43,6 +43,15 @@ _SCALARS = {
     # MI355X extension: hold the fp32 master exactly as bf16 weight + int16 residual
     # (runtime/zero/compact_master.py), 14 instead of 16 B/param of model state.
     "compact_master": False,
+    # MI355X extensions (ZeRO-3): run the gather / reduce-scatter path even on one rank;
+    # keep gradients resident across micro-batches and reduce once per step (ZeRO-2 / 3); dtype the
+    # reduced gradient shard accumulates in ("auto": fp32 when it accumulates GA>1 reductions
+    # over dp>1, else the parameter dtype; "fp32"; "param").  `stage3_unit_max_numel` bounds
+    # the module subtree that forms one gather/reduce unit.
+    "stage3_force_sharded": False,
+    "resident_grads": False,
+    "grad_accum_dtype": "auto",
+    "stage3_unit_max_numel": int(2e8),
 }
 
 _OFFLOAD_PARAM_DEFAULTS = dict(device=None, nvme_path=None, buffer_count=5, buffer_size=int(1e8),
@@ -88,6 +97,8 @@ class DeepSpeedZeroConfig(DeepSpeedConfigObject):
         self._raw = dict(zd)
         for k, v in _SCALARS.items():
             setattr(self, k, zd.get(k, v))
+        if "stage3_resident_grads" in zd and "resident_grads" not in zd:
+            self.resident_grads = zd["stage3_resident_grads"]
         if "allgather_size" in zd:  # deprecated alias
             self.allgather_bucket_size = zd["allgather_size"]
         if self.overlap_comm is None:

@@ -52,8 +52,12 @@ class ShardedOptimizerBase:
     def __init__(self, init_optimizer, dp_process_group=None, mpu=None, clip_grad=0.0, static_loss_scale=1.0,
                  dynamic_loss_scale=False, dynamic_loss_args=None, fp32_reduce=False, gradient_predivide_factor=1.0,
                  gradient_accumulation_steps=1, offload_optimizer=None, timers=None, verbose=False,
-                 compact_master=False):
+                 compact_master=False, sub_group_size=None):
         self.optimizer = init_optimizer
+        # reference stage3.py:1332-1356: the optimizer steps over sub-groups of at most this
+        # many elements (bounds the step's temporaries / host staging); here a sub-group is a
+        # contiguous range of a group's shard, never larger than one bucket chunk
+        self.sub_group_size = int(sub_group_size) if sub_group_size else 0
         self.compact_master = bool(compact_master)
         self.dp_group = dp_process_group
         self.mpu = mpu
@@ -219,6 +223,13 @@ class ShardedOptimizerBase:
 
         self._swapper.update(keys, update)
 
+    def _step_pieces(self, b):
+        """(lo, hi) shard ranges of bucket b, each at most sub_group_size elements."""
+        lo, hi = b.shard_offset, b.shard_offset + b.chunk
+        step = self.sub_group_size if 0 < self.sub_group_size < b.chunk else b.chunk
+        step = max(step, 64)  # keep pieces vector-aligned and non-degenerate
+        return [(s, min(s + step, hi)) for s in range(lo, hi, step)] or [(lo, hi)]
+
     def _inner_group(self, g: FlatGroup):
         return self.optimizer.param_groups[g.group_index]
 
@@ -321,10 +332,11 @@ class ShardedOptimizerBase:
             for g in self.groups:
                 grp = self._inner_group(g)
                 for b in g.buckets:
-                    lo, hi = b.shard_offset, b.shard_offset + b.chunk
                     out = self._bucket_out(g, b)
-                    self.optimizer.update_flat(grp, g.master, g.master, g.shard_grad, out=out, grad_scale=grad_scale,
-                                               lo=lo, hi=hi)
+                    for lo, hi in self._step_pieces(b):
+                        o = None if out is None else out[lo - b.shard_offset: hi - b.shard_offset]
+                        self.optimizer.update_flat(grp, g.master, g.master, g.shard_grad, out=o,
+                                                   grad_scale=grad_scale, lo=lo, hi=hi)
                     self._after_bucket_update(g, b)
             return
         # generic torch optimizer over the fp32 master shards
@@ -488,6 +500,10 @@ class ShardedOptimizerBase:
                 else:
                     g.master.copy_(m.to(g.master.device))
             self._refresh_params_from_master()
+        else:
+            # reference stage2.py:1877-1880 (_restore_from_fp16_weights): the low-precision
+            # weights just loaded with the module become the masters
+            self._masters_from_low_precision()
         if load_optimizer_states:
             self._load_moments(moments)
 
@@ -538,6 +554,23 @@ class ShardedOptimizerBase:
                                  else "cpu").clone()
                 else:
                     st[k] = v
+
+    def _low_precision_shard(self, g: FlatGroup) -> torch.Tensor:
+        return g.shard_param
+
+    def _masters_from_low_precision(self):
+        """fp32 masters <- this rank's low-precision parameter shards (compact: the bf16 shard
+        is the master's high half, the residual restarts at zero)."""
+        for gi, g in enumerate(self.groups):
+            src = self._low_precision_shard(g)
+            if src is None:
+                continue
+            if self.compact_master:
+                g.master.zero_()
+            elif self.nvme:
+                self._nvme_write_group(gi, "master", src.float())
+            elif g.master.data_ptr() != src.data_ptr():
+                g.master.copy_(src.float().to(g.master.device))
 
     def master_fp32(self, g: FlatGroup) -> torch.Tensor:
         """This rank's fp32 master shard of group g as a host tensor (checkpoints, tests)."""

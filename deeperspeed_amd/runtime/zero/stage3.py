@@ -97,16 +97,31 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                  param_persistence_threshold=int(1e5), unit_max_numel=int(2e8), fp32_reduce=False,
                  gradient_predivide_factor=1.0, gradient_accumulation_steps=1, offload_optimizer=None,
                  offload_param=None, timers=None, overlap_comm=True, sub_group_size=int(1e12), verbose=False,
-                 compact_master=False):
+                 compact_master=False, force_sharded=False, resident_grads=False, grad_accum_dtype="auto",
+                 reduce_scatter=True):
         super().__init__(init_optimizer, dp_process_group=dp_process_group, mpu=mpu, clip_grad=clip_grad,
                          static_loss_scale=static_loss_scale, dynamic_loss_scale=dynamic_loss_scale,
                          dynamic_loss_args=dynamic_loss_args, fp32_reduce=fp32_reduce,
                          gradient_predivide_factor=gradient_predivide_factor,
                          gradient_accumulation_steps=gradient_accumulation_steps,
                          offload_optimizer=offload_optimizer, timers=timers, verbose=verbose,
-                         compact_master=compact_master)
+                         compact_master=compact_master, sub_group_size=sub_group_size)
         self.module = module
         self.stage = 3
+        # overlap_comm=False (reference stage3.py:706,826): collectives are waited for right
+        # where they are issued and nothing is prefetched
+        self.overlap_comm = True if overlap_comm is None else bool(overlap_comm)
+        # reduce_scatter=False (reference stage3.py:1948): gradients are all-reduced per bucket
+        # and each rank keeps its chunk -- twice the traffic, kept for parity only
+        self.use_reduce_scatter = bool(reduce_scatter)
+        # MI355X extension: run the sharded gather / reduce-scatter machinery even on a world of
+        # one (the real RCCL code path of N>1, on one GPU) instead of binding params to shards
+        self.force_sharded = bool(force_sharded)
+        # MI355X extension: keep each unit's full gradient buffer resident across the
+        # micro-batches of one optimizer step and reduce-scatter once, at the accumulation
+        # boundary (GA x fewer reduce-scatters; costs one bf16 copy of the model's gradients)
+        self.resident_grads = bool(resident_grads)
+        self.grad_accum_dtype = str(grad_accum_dtype or "auto")
         self.prefetch_bucket_size = int(prefetch_bucket_size)
         self.max_live_parameters = int(max_live_parameters)
         self.max_reuse_distance = int(max_reuse_distance)
@@ -129,7 +144,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self._pswap = None
         self._pkey: Dict[int, tuple] = {}
         self.compute_device = self.device
-        self.single = self.dp_world == 1 and not self.param_offload
+        self.single = self.dp_world == 1 and not self.param_offload and not self.force_sharded
+        if self.single:
+            self.resident_grads = False  # gradients accumulate in the bound shard already
         self._pending = []
         self._fwd_trace: List[int] = []
         self._bwd_trace: List[int] = []
@@ -295,11 +312,25 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         return torch.zeros(g.shard_numel, dtype=g.dtype, pin_memory=pin)
 
     def _grad_dtype(self, g):
+        """dtype of the reduced gradient shard (where micro-batch reductions accumulate)."""
         if self.single:
             return g.dtype  # accumulate in place (p.grad views need the param dtype)
-        if self.fp32_reduce or self.gradient_accumulation_steps > 1 or g.dtype == torch.float32:
+        if self.fp32_reduce or g.dtype == torch.float32 or self.grad_accum_dtype in ("fp32", "float32"):
+            return torch.float32
+        if self.grad_accum_dtype != "auto":
+            return g.dtype
+        # auto: with resident unit grads the shard receives one reduction per step
+        if self.gradient_accumulation_steps > 1 and not self.resident_grads:
             return torch.float32
         return g.dtype
+
+    def _unit_grad_dtype(self, g):
+        """dtype of a unit's full (pre-reduction) gradient buffer: autograd accumulates into it
+        through the p.grad views, so it is the parameter dtype (resident micro-batch sums too)."""
+        return g.dtype
+
+    def _collective(self):
+        return _dist_ready() and (self.dp_world > 1 or self.force_sharded)
 
     # ------------------------------------------------------------------ gather / release
     def _fetch(self, u: ZeroUnit):
@@ -317,9 +348,13 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                 chunk = g.shard_param[b.shard_offset: b.shard_offset + b.chunk]
                 if self.param_offload:
                     chunk = chunk.to(self.compute_device, non_blocking=chunk.is_pinned())
-            if _dist_ready() and self.dp_world > 1:
-                u.works.append(comm.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True,
-                                                           tag=f"zero3.gather.u{u.uid}"))
+            if self._collective():
+                w = comm.all_gather_into_tensor(full, chunk, group=self.dp_group, async_op=True,
+                                                tag=f"zero3.gather.u{u.uid}")
+                if self.overlap_comm:
+                    u.works.append(w)
+                else:
+                    w.wait()
             else:
                 full.copy_(chunk)
             u.fulls.append(full)
@@ -421,7 +456,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             self._fwd_pos = 0
 
     def _prefetch(self, trace, pos):
-        if not self._trace_frozen or pos < 0:
+        if not self._trace_frozen or pos < 0 or not self.overlap_comm:
             return
         budget = self.prefetch_bucket_size
         k = pos + 1
@@ -488,12 +523,12 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self._fetch(u)
         self._wait(u)
         u.in_backward = True
-        u.grad_fulls = []
         u.bw_expected = sum(1 for p in u.params if p.requires_grad)
         u.bw_ready = 0
-        for g, b in u.buckets:
-            gf = torch.zeros(b.numel, dtype=g.dtype, device=self.compute_device)
-            u.grad_fulls.append(gf)
+        if not u.grad_fulls:  # resident buffers of earlier micro-batches accumulate on
+            u.grad_fulls = [torch.zeros(b.numel, dtype=self._unit_grad_dtype(g), device=self.compute_device)
+                            for g, b in u.buckets]
+        for (g, b), gf in zip(u.buckets, u.grad_fulls):
             for i, p in enumerate(b.params):
                 if p.requires_grad:
                     p.grad = gf[b.offsets[i]: b.offsets[i] + b.numels[i]].view(p.ds_shape)
@@ -504,6 +539,13 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
 
     def _grad_ready(self, p):
         u = self._unit_of_param[id(p)]
+        if u.reduced:
+            # the unit's buffers were already reduced (reference stage3.py asserts the same:
+            # a gradient computed twice in one backward, e.g. a parameter used both inside and
+            # outside a reentrant-checkpointed region)
+            raise RuntimeError(f"ZeRO-3: gradient of a parameter of unit {u.uid} ({type(u.module).__name__}) "
+                               f"arrived after the unit was reduced; a parameter was used by two separate "
+                               f"backward graph tasks")
         if not u.in_backward:
             # grad produced without the output hook firing (e.g. params used outside the
             # unit's forward): materialise the unit's grad buffers now and fold it in
@@ -521,30 +563,44 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             return
         u.reduced = True
         u.in_backward = False
-        accumulate_needed = True
-        for (g, b), gf in zip(u.buckets, u.grad_fulls):
+        for g, b in u.buckets:
             for p in b.params:
                 p.grad = None
+        if self.resident_grads and not self.is_gradient_accumulation_boundary:
+            # keep accumulating into the unit's full buffers; reduce once at the boundary
+            if u.active == 0:
+                self._maybe_release(u, "b")
+            return
+        for (g, b), gf in zip(u.buckets, u.grad_fulls):
             src = gf
             if g.dtype == torch.float16:
                 src.mul_(1.0 / self.dp_world)
             if self.fp32_reduce and src.dtype != torch.float32:
                 src = src.float()
             out_slice = g.shard_grad[b.shard_offset: b.shard_offset + b.chunk]
-            direct = (out_slice.dtype == src.dtype) and self.gradient_accumulation_steps == 1 and \
-                not self._grads_nonzero
+            direct = out_slice.dtype == src.dtype and not self._grads_nonzero
             out = out_slice if direct else torch.empty(b.chunk, dtype=src.dtype, device=src.device)
-            work = comm.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True,
-                                              tag=f"zero3.reduce.u{u.uid}")
-            if direct:
-                self._pending.append((work, None))
+            if self.use_reduce_scatter:
+                work = comm.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True,
+                                                  tag=f"zero3.reduce.u{u.uid}")
+                fin = None if direct else functools.partial(_accum, out_slice, out)
             else:
-                self._pending.append((work, functools.partial(_accum, out_slice, out)))
+                work = comm.all_reduce(src, group=self.dp_group, async_op=True, tag=f"zero3.allreduce.u{u.uid}")
+                mine = src[self.dp_rank * b.chunk: (self.dp_rank + 1) * b.chunk]
+                fin = functools.partial(_copy if direct else _accum, out_slice, mine)
+            self._reduced_this_pass = True
+            if self.overlap_comm:
+                self._pending.append((work, fin))
+            else:
+                work.wait()
+                if fin is not None:
+                    fin()
         u.grad_fulls = []
         if u.active == 0:
             self._maybe_release(u, "b")
 
     _grads_nonzero = False
+    _reduced_this_pass = False
 
     def reduce_epilogue(self):
         if self.single:
@@ -552,6 +608,10 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         for u in self._units:
             if u.in_backward and not u.reduced:
                 self._reduce_unit(u)
+        if self.resident_grads and self.is_gradient_accumulation_boundary:
+            for u in self._units:  # accumulated in earlier micro-batches, unused in this one
+                if u.grad_fulls and not u.reduced:
+                    self._reduce_unit(u)
         for work, fin in self._pending:
             if work is not None:
                 work.wait()
@@ -563,7 +623,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             u.in_backward = False
             if u.active == 0 and u.status != ZeroParamStatus.NOT_AVAILABLE:
                 self._maybe_release(u, "b")
-        self._grads_nonzero = True
+        if self._reduced_this_pass:
+            self._grads_nonzero = True
+        self._reduced_this_pass = False
         if not self._trace_frozen and self._fwd_trace:
             self._trace_frozen = True
             self._compute_reuse()
@@ -598,6 +660,11 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             return out
         return g.shard_param.detach().cpu()
 
+    def _low_precision_shard(self, g):
+        if self.param_nvme and g.shard_param is None:
+            return self.param_shard_host(g)
+        return g.shard_param
+
     def load_param_shard(self, g, shard: torch.Tensor):
         if self.param_nvme and g.shard_param is None:
             for b in g.buckets:
@@ -625,6 +692,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         for g in self.groups:
             g.shard_grad.zero_()
         self._grads_nonzero = False
+        for u in self._units:  # an overflow-skipped step drops resident micro-batch grads too
+            u.grad_fulls = []
 
     def _zero_stage(self):
         return 3
@@ -702,6 +771,10 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
 
 def _accum(dst, src):
     dst.add_(src.to(dst.dtype))
+
+
+def _copy(dst, src):
+    dst.copy_(src)
 
 
 FP16_DeepSpeedZeroOptimizer_Stage3 = DeepSpeedZeroOptimizer_Stage3

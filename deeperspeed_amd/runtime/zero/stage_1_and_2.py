@@ -46,19 +46,32 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
                  static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None, reduce_bucket_size=int(5e8),
                  allgather_bucket_size=int(5e8), overlap_comm=True, reduce_scatter=True, fp32_reduce=False,
                  gradient_predivide_factor=1.0, gradient_accumulation_steps=1, offload_optimizer=None, timers=None,
-                 postscale_gradients=True, verbose=False, compact_master=False):
+                 postscale_gradients=True, verbose=False, compact_master=False, resident_grads=False,
+                 sub_group_size=None, prebind_window=2):
         super().__init__(init_optimizer, dp_process_group=dp_process_group, mpu=mpu, clip_grad=clip_grad,
                          static_loss_scale=static_loss_scale, dynamic_loss_scale=dynamic_loss_scale,
                          dynamic_loss_args=dynamic_loss_args, fp32_reduce=fp32_reduce,
                          gradient_predivide_factor=gradient_predivide_factor,
                          gradient_accumulation_steps=gradient_accumulation_steps,
                          offload_optimizer=offload_optimizer, timers=timers, verbose=verbose,
-                         compact_master=compact_master)
+                         compact_master=compact_master, sub_group_size=sub_group_size)
         assert stage in (0, 1, 2)
         self.stage = stage
         self.sharded = stage >= 1
         self.layout_world = self.dp_world if self.sharded else 1
-        self.overlap_comm = overlap_comm
+        # overlap_comm=False (reference stage2.py:680-686): each bucket's reduction is waited
+        # for where it is issued instead of at the end of backward
+        self.overlap_comm = True if overlap_comm is None else bool(overlap_comm)
+        # reduce_scatter=False (reference stage2.py:687): all-reduce each bucket, keep the chunk
+        self.use_reduce_scatter = bool(reduce_scatter)
+        # MI355X extension for ZeRO-2: hold a full gradient arena (like stage 1) so micro-batch
+        # gradients accumulate in place and every bucket is reduce-scattered once per optimizer
+        # step; on 288 GB parts this usually fits next to the full bf16 parameter arena
+        self.resident = stage == 2 and bool(resident_grads)
+        # ZeRO-2 without a resident arena: the next `prebind_window` buckets (backward order)
+        # get pooled buffers bound as p.grad before their gradients arrive, so autograd
+        # accumulates straight into the bucket instead of a copy per parameter
+        self.prebind_window = max(1, int(prebind_window))
         self.reduce_bucket_size = max(int(reduce_bucket_size), ALIGN * max(1, self.dp_world))
         self.groups = self._split_groups()
         for g in self.groups:
@@ -120,14 +133,18 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
     def _grad_dtype(self, g):
         if self.fp32_reduce or g.dtype == torch.float32:
             return torch.float32
-        if self.stage == 2 and self.gradient_accumulation_steps > 1:
-            return torch.float32
+        if self._bucketed() and self.gradient_accumulation_steps > 1:
+            return torch.float32  # GA reductions accumulate in the shard
         return g.dtype
+
+    def _bucketed(self):
+        """ZeRO-2 proper: gradients live in pooled bucket buffers during backward only."""
+        return self.stage == 2 and not self.resident
 
     def _build_grad_storage(self):
         for g in self.groups:
             dev = g.arena.device
-            if self.stage in (0, 1):
+            if not self._bucketed():
                 g.grad_arena = torch.zeros(g.arena_numel, dtype=g.dtype, device=dev)
                 for b in g.buckets:
                     for p, off, n in zip(b.params, b.offsets, b.numels):
@@ -163,7 +180,7 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
 
     # ------------------------------------------------------------------ backward hooks
     def _hooks_active(self):
-        return self.stage == 2 or self.is_gradient_accumulation_boundary
+        return self._bucketed() or self.is_gradient_accumulation_boundary
 
     def _acquire_buffer(self, g, b):
         pool = self._buf_pool.setdefault(g.dtype, [])
@@ -173,17 +190,32 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
         view.zero_()
         return buf, view
 
+    def _prebind(self, k):
+        """Bind bucket k (launch order) to a pooled buffer: its params' .grad become views."""
+        if k >= len(self._launch_seq):
+            return
+        g, b = self._launch_seq[k]
+        st = self._bstate[id(b)]
+        if st.buffer is not None or st.launched:
+            return
+        st.buffer = self._acquire_buffer(g, b)
+        for i, p in enumerate(b.params):
+            if p.requires_grad and p.grad is None:
+                off = b.offsets[i]
+                p.grad = st.buffer[1][off: off + b.numels[i]].view(p.shape)
+
     def _grad_ready(self, p):
         if not self._hooks_active():
             return
         g, b, i = self._pos[p]
         st = self._bstate[id(b)]
-        if self.stage == 2:
+        if self._bucketed():
             if st.buffer is None:
                 st.buffer = self._acquire_buffer(g, b)
             off = b.offsets[i]
-            if p.grad is not None:
-                st.buffer[1][off: off + b.numels[i]].copy_(p.grad.reshape(-1))
+            dst = st.buffer[1][off: off + b.numels[i]]
+            if p.grad is not None and p.grad.data_ptr() != dst.data_ptr():
+                dst.copy_(p.grad.reshape(-1))  # arrived before its bucket was pre-bound
                 p.grad = None
         st.ready += 1
         if st.ready >= st.expected:
@@ -201,10 +233,13 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
     def _launch_bucket(self, g: FlatGroup, b, st: _BucketState):
         st.launched = True
         world = self.dp_world
-        if self.stage == 2:
+        if self._bucketed():
             if st.buffer is None:  # no grads at all arrived (unused params)
                 st.buffer = self._acquire_buffer(g, b)
             src = st.buffer[1]
+            for p in b.params:
+                p.grad = None  # the buffer goes to the collective and back to the pool
+            self._prebind(st.order + self.prebind_window)
         else:
             src = g.grad_arena[b.arena_offset: b.arena_offset + b.numel]
         dst_full = g.shard_grad
@@ -221,16 +256,19 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
                 target.copy_(src)
             work = comm.all_reduce(target, group=self.dp_group, async_op=True, tag="zero.allreduce") if (_dist_ready() and world > 1) \
                 else None
-            self._pending.append((work, None))
+            self._queue(work, None)
             return
         out_slice = dst_full[b.shard_offset: b.shard_offset + b.chunk]
-        accumulate = self.stage == 2 and self.gradient_accumulation_steps > 1
-        if accumulate or out_slice.dtype != src.dtype:
+        accumulate = self._bucketed() and self.gradient_accumulation_steps > 1
+        if accumulate or out_slice.dtype != src.dtype or not self.use_reduce_scatter:
             out = torch.empty(b.chunk, dtype=src.dtype, device=src.device)
         else:
             out = out_slice
-        if _dist_ready() and world > 1:
+        if _dist_ready() and world > 1 and self.use_reduce_scatter:
             work = comm.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True, tag="zero.reduce")
+        elif _dist_ready() and world > 1:
+            work = comm.all_reduce(src, group=self.dp_group, async_op=True, tag="zero.allreduce")
+            out = src[self.dp_rank * b.chunk: (self.dp_rank + 1) * b.chunk]
         else:
             out.copy_(src[: b.chunk])
             work = None
@@ -245,7 +283,16 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
                 self._buf_pool.setdefault(g.dtype, []).append(st.buffer[0])
                 st.buffer = None
 
-        self._pending.append((work, finish))
+        self._queue(work, finish)
+
+    def _queue(self, work, fin):
+        if self.overlap_comm:
+            self._pending.append((work, fin))
+            return
+        if work is not None:
+            work.wait()
+        if fin is not None:
+            fin()
 
     def reduce_epilogue(self):
         """Flush all buckets and complete their reductions (end of backward)."""
@@ -269,6 +316,9 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
 
     # ------------------------------------------------------------------ forward/backward API
     def backward(self, loss, retain_graph=False):
+        if self._bucketed():
+            for k in range(self.prebind_window):
+                self._prebind(k)
         self.loss_scaler.backward(loss.float(), retain_graph=retain_graph)
 
     def _grads_are_sharded(self):
@@ -303,16 +353,18 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
 
     def refresh_from_params(self):
         """Re-derive shards and fp32 masters from the (just loaded) model parameters."""
-        for g in self.groups:
-            if self.sharded:
+        if self.sharded:
+            for g in self.groups:
                 for b in g.buckets:
                     c0 = b.arena_offset + self.dp_rank * b.chunk
                     g.shard_param[b.shard_offset: b.shard_offset + b.chunk].copy_(g.arena[c0: c0 + b.chunk])
-            src = g.shard_param if g.shard_param is not None else g.arena
-            if self.compact_master:
-                g.master.zero_()  # bf16 shard is now the exact master
-            elif g.master.data_ptr() != src.data_ptr():
-                g.master.copy_(src.float().to(g.master.device))
+        super()._masters_from_low_precision()
+
+    def _low_precision_shard(self, g):
+        return g.shard_param if g.shard_param is not None else g.arena
+
+    def _masters_from_low_precision(self):
+        self.refresh_from_params()  # arena (loaded module weights) -> shard -> master
 
     def zero_grad(self, set_to_none=True):
         for g in self.groups:

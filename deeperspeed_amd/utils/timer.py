@@ -126,39 +126,57 @@ class SynchronizedWallClockTimer:
 
 
 class ThroughputTimer:
-    """Samples/sec after `start_step` warm-up steps (reference timer.py:105-182)."""
+    """Samples/sec over the steps after a warm-up (behaviour of reference timer.py:105-182).
+
+    No host synchronisation on the hot path: each micro-step brackets itself with two HIP
+    events on the current stream; the events are only resolved (one event wait) when a rate
+    is reported or read, i.e. every `steps_per_output` steps.  On CPU wall clock is used.
+    """
 
     def __init__(self, batch_size, num_workers=1, start_step=2, steps_per_output=50, monitor_memory=False,
                  logging_fn=None):
-        self.start_time = 0
-        self.end_time = 0
-        self.started = False
-        self.batch_size = batch_size if batch_size is not None else 1
+        self.batch_size = 1 if batch_size is None else batch_size
         self.num_workers = num_workers
         self.start_step = start_step
-        self.epoch_count = 0
-        self.local_step_count = 0
-        self.total_step_count = 0
-        self.total_elapsed_time = 0
         self.steps_per_output = steps_per_output
         self.monitor_memory = monitor_memory
         self.logging = logging_fn or (lambda msg: log_dist(msg, ranks=[0]))
+        self.epoch_count = 0
+        self.local_step_count = 0
+        self.total_step_count = 0
+        self.total_elapsed_time = 0.0
+        self.started = False
         self.initialized = False
+        self._open = None  # start marker of the interval being measured
+        self._closed = []  # finished (start, end) markers not yet folded into total_elapsed_time
 
     def update_epoch_count(self):
         self.epoch_count += 1
         self.local_step_count = 0
 
-    def _init_timer(self):
-        self.initialized = True
+    @staticmethod
+    def _mark():
+        if _gpu():
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.time()
+
+    def _fold(self, keep=0):
+        """Fold finished intervals into the total; `keep` most recent ones stay pending (their
+        end events may still be in flight, the older ones have long completed)."""
+        done, self._closed = self._closed[:len(self._closed) - keep], self._closed[len(self._closed) - keep:]
+        for a, b in done:
+            if isinstance(a, float):
+                self.total_elapsed_time += b - a
+            else:
+                b.synchronize()
+                self.total_elapsed_time += a.elapsed_time(b) / 1000.0
 
     def start(self):
-        self._init_timer()
+        self.initialized = True
         self.started = True
-        if self.total_step_count >= self.start_step:
-            if _gpu():
-                torch.cuda.synchronize()
-            self.start_time = time.time()
+        self._open = self._mark() if self.total_step_count >= self.start_step else None
 
     def stop(self, report_speed=True):
         if not self.started:
@@ -166,25 +184,21 @@ class ThroughputTimer:
         self.started = False
         self.total_step_count += 1
         self.local_step_count += 1
-        if self.total_step_count > self.start_step:
-            if _gpu():
-                torch.cuda.synchronize()
-            self.end_time = time.time()
-            duration = self.end_time - self.start_time
-            self.total_elapsed_time += duration
-            if self.local_step_count % self.steps_per_output == 0 and report_speed:
-                self.logging("{}/{}, SamplesPerSec={}".format(self.epoch_count, self.local_step_count,
-                                                             self.avg_samples_per_sec()))
-                if self.monitor_memory and PSUTILS_INSTALLED:
-                    virt_mem = psutil.virtual_memory()
-                    swap = psutil.swap_memory()
-                    self.logging("{}/{}, vm percent: {}, swap percent: {}".format(
-                        self.epoch_count, self.local_step_count, virt_mem.percent, swap.percent))
+        if self._open is not None and self.total_step_count > self.start_step:
+            self._closed.append((self._open, self._mark()))
+            if len(self._closed) > 64:  # bound the pending list on ranks that never report
+                self._fold(keep=8)
+        self._open = None
+        if report_speed and self.local_step_count % self.steps_per_output == 0:
+            self.logging(f"{self.epoch_count}/{self.local_step_count}, SamplesPerSec={self.avg_samples_per_sec()}")
+            if self.monitor_memory and PSUTILS_INSTALLED:
+                vm, sw = psutil.virtual_memory(), psutil.swap_memory()
+                self.logging(f"{self.epoch_count}/{self.local_step_count}, vm percent: {vm.percent}, "
+                             f"swap percent: {sw.percent}")
 
     def avg_samples_per_sec(self):
-        if self.total_step_count > self.start_step and self.total_elapsed_time > 0:
-            samples_per_step = self.batch_size * self.num_workers
-            total_step_offset = self.total_step_count - self.start_step
-            avg_time_per_step = self.total_elapsed_time / total_step_offset
-            return samples_per_step / avg_time_per_step
-        return float("-inf")
+        self._fold()
+        measured = self.total_step_count - self.start_step
+        if measured <= 0 or self.total_elapsed_time <= 0:
+            return float("-inf")
+        return self.batch_size * self.num_workers * measured / self.total_elapsed_time

@@ -28,7 +28,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world_size, port, fn, args, kwargs, errq):
+def _worker(rank, world_size, port, fn, args, kwargs, errq, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     os.environ["RANK"] = str(rank)
@@ -38,7 +38,9 @@ def _worker(rank, world_size, port, fn, args, kwargs, errq):
     torch.set_num_threads(2)
     try:
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world_size)
+        if backend == "nccl":  # RCCL: one rank per visible GPU
+            torch.cuda.set_device(rank % torch.cuda.device_count())
+        dist.init_process_group(backend, rank=rank, world_size=world_size)
         fn(*args, **kwargs)
         dist.barrier()
         dist.destroy_process_group()
@@ -47,11 +49,12 @@ def _worker(rank, world_size, port, fn, args, kwargs, errq):
         sys.exit(1)
 
 
-def run_distributed(fn, world_size, *args, timeout=DEFAULT_TIMEOUT, **kwargs):
+def run_distributed(fn, world_size, *args, timeout=DEFAULT_TIMEOUT, backend="gloo", **kwargs):
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world_size, port, fn, args, kwargs, errq)) for r in range(world_size)]
+    procs = [ctx.Process(target=_worker, args=(r, world_size, port, fn, args, kwargs, errq, backend))
+             for r in range(world_size)]
     for p in procs:
         p.start()
     deadline = time.time() + timeout

@@ -170,3 +170,42 @@ def test_zero_to_fp32(tmp_path):
     for k, v in ref.items():
         assert sd[k].dtype == torch.float32
         assert torch.allclose(sd[k].to(v.dtype).float(), v.float(), atol=1e-2), k
+
+
+def _fp16_weights_resume_body(save_dir, stage):
+    """load_from_fp32_weights=false: the masters must be rebuilt from the loaded bf16 weights
+    (reference stage2.py:1877-1880 _restore_from_fp16_weights), so a resumed engine keeps
+    training exactly like one restarted from a checkpoint whose masters equal its weights."""
+    import deeperspeed_amd as ds
+    e1 = _engine(stage, sched=False)
+    _train(e1, 3, 0)
+    e1.save_checkpoint(save_dir)
+    p1 = _params(e1)
+
+    def fresh():
+        torch.manual_seed(11)
+        model = SimpleModel(32)
+        z = {"reduce_bucket_size": 400, "stage3_unit_max_numel": 600, "stage3_param_persistence_threshold": 10,
+             "load_from_fp32_weights": False}
+        cfg = base_config(stage=stage, mb=2, **z)
+        return ds.initialize(model=model, model_parameters=model.parameters(), config_params=cfg)[0]
+
+    e2 = fresh()
+    e2.load_checkpoint(save_dir)
+    p2 = _params(e2)
+    for k in p1:
+        assert torch.equal(p1[k], p2[k]), k
+    # masters == bf16 weights (upcast), shard for shard
+    for g in e2.optimizer.groups:
+        src = e2.optimizer._low_precision_shard(g)
+        assert torch.equal(e2.optimizer.master_fp32(g).float(), src.detach().float().cpu())
+    _train(e2, 1, 5)
+    p3 = _params(e2)
+    moved = [k for k in p1 if not torch.equal(p1[k], p3[k])]
+    diffs = max((p1[k].float() - p3[k].float()).abs().max().item() for k in p1)
+    assert moved and diffs < 0.05, (moved, diffs)  # one Adam step (lr 1e-2) away, not back at init
+
+
+@pytest.mark.parametrize("stage", [1, 2, 3])
+def test_resume_from_fp16_weights(tmp_path, stage):
+    run_distributed(_fp16_weights_resume_body, 2, str(tmp_path), stage)

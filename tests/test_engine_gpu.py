@@ -118,3 +118,56 @@ def test_engine_param_offload(dev):
     base = _run(3, "all", steps=3, ga=1)
     off = _run(3, "all", steps=3, ga=1, offload_param=dev)
     assert abs(base[-1] - off[-1]) < 5e-2 * max(1.0, abs(base[-1]))
+
+
+def _sharded_body(out_dir, tag, zero_extra, ga):
+    """Rank body on RCCL (world 1): GPT-NeoX 2 layers, ZeRO-3, 3 optimizer steps."""
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = get_config("gpt-neox-125m", num_layers=2, max_seq_len=128)
+    model = GPTNeoX(cfg, device=dev, dtype=torch.bfloat16)
+    z = {"stage": 3, "stage3_unit_max_numel": int(5e6), "stage3_param_persistence_threshold": int(1e4),
+         "reduce_scatter": True}
+    z.update(zero_extra)
+    conf = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": ga,
+            "optimizer": {"type": "Adam", "params": {"lr": 3e-4}}, "fp16": {"enabled": True, "type": "bfloat16"},
+            "fp32_allreduce": False, "gradient_clipping": 1.0, "zero_optimization": z}
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    batches = [torch.randint(0, cfg.vocab_size, (2, 128), device=dev, generator=g) for _ in range(ga)]
+    losses = []
+    for _ in range(3):
+        for ids in batches:
+            loss = engine(ids, labels=ids)
+            engine.backward(loss)
+            engine.step()
+        losses.append(float(loss.detach()))
+    sd = engine.optimizer.gathered_state_dict(engine.module)
+    torch.save({"losses": losses, "sd": sd, "sharded": not engine.optimizer.single},
+               os.path.join(out_dir, f"{tag}.pt"))
+
+
+@pytest.mark.parametrize("ga", [1, 2])
+def test_zero3_force_sharded_rccl_matches_bypass(tmp_path, ga):
+    """The sharded ZeRO-3 path (unit hooks, all_gather_into_tensor / reduce_scatter_tensor on
+    a world-1 RCCL communicator, prefetch, resident gradients) reproduces the single-rank
+    bind-to-shard bypass over 3 optimizer steps."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from common import run_distributed
+    run_distributed(_sharded_body, 1, str(tmp_path), "bypass", {}, ga, backend="nccl", timeout=400)
+    extra = {"stage3_force_sharded": True, "grad_accum_dtype": "param"}
+    if ga > 1:
+        extra["resident_grads"] = True
+    run_distributed(_sharded_body, 1, str(tmp_path), "sharded", extra, ga, backend="nccl", timeout=400)
+    a = torch.load(tmp_path / "bypass.pt", weights_only=True)
+    b = torch.load(tmp_path / "sharded.pt", weights_only=True)
+    assert b["sharded"] and not a["sharded"]
+    for x, y in zip(a["losses"], b["losses"]):
+        assert abs(x - y) <= 2e-3 * max(1.0, abs(x)), (a["losses"], b["losses"])
+    for k in a["sd"]:
+        d = (a["sd"][k].float() - b["sd"][k].float()).abs().max().item()
+        assert d <= 2e-3, (k, d)
