@@ -300,7 +300,9 @@ def main():
         log(f"warmup {i} loss={float(loss.detach()):.4f} {time.time() - ts:.2f}s "
             + " ".join(f"{k}={v:.2f}s" for k, v in ph.items())
             + f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB"
-            + f" reserved={torch.cuda.max_memory_reserved() / 2**30:.1f} GiB")
+            + f" reserved={torch.cuda.max_memory_reserved() / 2**30:.1f} GiB"
+            + (f" zero3_pool={engine.optimizer._pool.held * 2 / 2**30:.1f} GiB"
+               if hasattr(engine.optimizer, "_pool") else ""))
         if i == 0 and args.warmup >= 2:
             stashed = plan_stash()
 

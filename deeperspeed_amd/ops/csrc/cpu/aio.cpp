@@ -1,26 +1,40 @@
 // Asynchronous file I/O engine for ZeRO-Infinity NVMe offload (module `_cpu_ops`).
 //
-// Reference parity: csrc/aio (deepspeed_aio_common.cpp, deepspeed_py_aio_handle.cpp,
-// deepspeed_aio_thread.cpp, deepspeed_py_copy.cpp): an `aio_handle(block_size,
-// queue_depth, single_submit, overlap_events, thread_count)` with read/write,
-// pread/pwrite (sync or async) and wait(); module functions aio_read/aio_write and a
-// parallel deepspeed_memcpy.  The reference drives libaio io_submit/io_getevents; this
-// image has no libaio, so the engine here is a native thread pool issuing O_DIRECT
-// pread/pwrite of `block_size` pieces, each worker keeping up to `queue_depth` pieces
-// of its slice in flight through sequential submission (the kernel's NVMe queue does the
-// parallelism across workers).  Buffers are the caller's pinned host tensors, which the
-// swappers then move to HBM with hipMemcpyAsync (no extra bounce copy).
+// Reference parity: csrc/aio (deepspeed_aio_common.cpp:69-160,265 io_submit/io_getevents
+// with queue depth, single vs block submit, overlapped completion; deepspeed_aio_thread.cpp
+// request split across worker threads; deepspeed_py_aio_handle.cpp Python handle;
+// deepspeed_py_copy.cpp parallel memcpy).  API: `aio_handle(block_size, queue_depth,
+// single_submit, overlap_events, thread_count)` with read/write, pread/pwrite (sync or
+// async), sync_*/async_* and wait(); module functions aio_read/aio_write/deepspeed_memcpy.
+//
+// Engine: io_uring through raw syscalls (no liburing/libaio in the image).  Every worker
+// thread owns one ring of `queue_depth` entries; a request is cut into `block_size` pieces
+// and split into one contiguous slice per worker.  A worker keeps up to `queue_depth`
+// pieces in flight:
+//   * single_submit=true  -> one io_uring_enter per piece (reference: one iocb per
+//     io_submit call); false -> the whole batch of free slots in one enter.
+//   * overlap_events=true -> a freed slot is refilled as soon as its completion is reaped
+//     (reference: overlapped submit/reap); false -> a batch is reaped completely before
+//     the next batch is submitted (reference: lock-step submit/wait).
+// O_DIRECT is used when buffer, length and file offset are 4 KiB aligned (pinned tensors
+// from the swappers are page aligned) and the filesystem supports it; otherwise buffered.
+// Where the kernel refuses io_uring (seccomp, old kernel) the same workers fall back to
+// positional pread/pwrite ("psync" engine) -- get_engine() reports which one runs.
 #include <torch/extension.h>
+#include <errno.h>
 #include <fcntl.h>
+#include <linux/io_uring.h>
 #include <omp.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
-#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -28,103 +42,320 @@
 
 namespace {
 
-struct IoJob {
+constexpr int64_t kAlign = 4096;
+
+// ------------------------------------------------------------------------------ io_uring
+class Ring {
+ public:
+  ~Ring() { close_ring(); }
+
+  bool open_ring(unsigned entries) {
+    io_uring_params p;
+    std::memset(&p, 0, sizeof(p));
+    fd_ = (int)syscall(__NR_io_uring_setup, entries, &p);
+    if (fd_ < 0) return false;
+    sq_sz_ = p.sq_off.array + p.sq_entries * sizeof(unsigned);
+    cq_sz_ = p.cq_off.cqes + p.cq_entries * sizeof(io_uring_cqe);
+    const bool single = p.features & IORING_FEAT_SINGLE_MMAP;
+    if (single) sq_sz_ = cq_sz_ = std::max(sq_sz_, cq_sz_);
+    sq_ptr_ = mmap(nullptr, sq_sz_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd_, IORING_OFF_SQ_RING);
+    if (sq_ptr_ == MAP_FAILED) return fail();
+    cq_ptr_ = single ? sq_ptr_
+                     : mmap(nullptr, cq_sz_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd_, IORING_OFF_CQ_RING);
+    if (cq_ptr_ == MAP_FAILED) return fail();
+    sqe_sz_ = p.sq_entries * sizeof(io_uring_sqe);
+    sqes_ = (io_uring_sqe*)mmap(nullptr, sqe_sz_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd_,
+                                IORING_OFF_SQES);
+    if (sqes_ == MAP_FAILED) return fail();
+    char* sq = (char*)sq_ptr_;
+    char* cq = (char*)cq_ptr_;
+    sq_tail_ = (unsigned*)(sq + p.sq_off.tail);
+    sq_mask_ = *(unsigned*)(sq + p.sq_off.ring_mask);
+    sq_array_ = (unsigned*)(sq + p.sq_off.array);
+    cq_head_ = (unsigned*)(cq + p.cq_off.head);
+    cq_tail_ = (unsigned*)(cq + p.cq_off.tail);
+    cq_mask_ = *(unsigned*)(cq + p.cq_off.ring_mask);
+    cqes_ = (io_uring_cqe*)(cq + p.cq_off.cqes);
+    entries_ = p.sq_entries;
+    return true;
+  }
+
+  unsigned entries() const { return entries_; }
+
+  // Queue one read/write SQE (not yet visible to the kernel until enter()).
+  void prep(bool read, int fd, void* buf, unsigned len, int64_t off, uint64_t tag) {
+    const unsigned tail = local_tail_;
+    const unsigned idx = tail & sq_mask_;
+    io_uring_sqe* s = &sqes_[idx];
+    std::memset(s, 0, sizeof(*s));
+    s->opcode = read ? IORING_OP_READ : IORING_OP_WRITE;
+    s->fd = fd;
+    s->addr = (uint64_t)(uintptr_t)buf;
+    s->len = len;
+    s->off = (uint64_t)off;
+    s->user_data = tag;
+    sq_array_[idx] = idx;
+    local_tail_ = tail + 1;
+    ++unsubmitted_;
+  }
+
+  // Publish queued SQEs and optionally wait for `min_complete` completions.
+  int enter(unsigned min_complete) {
+    __atomic_store_n(sq_tail_, local_tail_, __ATOMIC_RELEASE);
+    unsigned flags = min_complete ? IORING_ENTER_GETEVENTS : 0;
+    int r;
+    do {
+      r = (int)syscall(__NR_io_uring_enter, fd_, unsubmitted_, min_complete, flags, nullptr, 0);
+    } while (r < 0 && errno == EINTR);
+    if (r >= 0) unsubmitted_ -= std::min<unsigned>(unsubmitted_, (unsigned)r);
+    return r;
+  }
+
+  // Reap one completion if available: returns false when the CQ is empty.
+  bool reap(uint64_t* tag, int* res) {
+    const unsigned head = *cq_head_;
+    const unsigned tail = __atomic_load_n(cq_tail_, __ATOMIC_ACQUIRE);
+    if (head == tail) return false;
+    const io_uring_cqe* c = &cqes_[head & cq_mask_];
+    *tag = c->user_data;
+    *res = c->res;
+    __atomic_store_n(cq_head_, head + 1, __ATOMIC_RELEASE);
+    return true;
+  }
+
+ private:
+  bool fail() {
+    close_ring();
+    return false;
+  }
+  void close_ring() {
+    if (sqes_ && sqes_ != MAP_FAILED) munmap(sqes_, sqe_sz_);
+    if (cq_ptr_ && cq_ptr_ != MAP_FAILED && cq_ptr_ != sq_ptr_) munmap(cq_ptr_, cq_sz_);
+    if (sq_ptr_ && sq_ptr_ != MAP_FAILED) munmap(sq_ptr_, sq_sz_);
+    if (fd_ >= 0) close(fd_);
+    sqes_ = nullptr;
+    cq_ptr_ = sq_ptr_ = nullptr;
+    fd_ = -1;
+  }
+  int fd_ = -1;
+  void *sq_ptr_ = nullptr, *cq_ptr_ = nullptr;
+  size_t sq_sz_ = 0, cq_sz_ = 0, sqe_sz_ = 0;
+  io_uring_sqe* sqes_ = nullptr;
+  io_uring_cqe* cqes_ = nullptr;
+  unsigned *sq_tail_ = nullptr, *sq_array_ = nullptr, *cq_head_ = nullptr, *cq_tail_ = nullptr;
+  unsigned sq_mask_ = 0, cq_mask_ = 0, entries_ = 0;
+  unsigned local_tail_ = 0, unsubmitted_ = 0;
+};
+
+bool io_uring_usable() {
+  static const bool ok = [] {
+    if (const char* e = std::getenv("DSA_AIO_ENGINE")) {
+      if (std::string(e) == "psync") return false;
+    }
+    Ring r;
+    return r.open_ring(2);
+  }();
+  return ok;
+}
+
+// ------------------------------------------------------------------------------ requests
+struct Request {
   char* buf;
   int64_t nbytes;
-  int64_t file_offset;
   std::string path;
   bool read;
   bool validate;
+  std::atomic<int> slices_left{0};
+  std::atomic<bool> failed{false};
 };
 
-bool is_aligned(const void* p, int64_t n, int64_t a) {
-  return (reinterpret_cast<uintptr_t>(p) % a == 0) && (n % a == 0);
+struct Slice {
+  std::shared_ptr<Request> req;
+  int64_t off, len;  // byte range of the buffer (== file offset)
+};
+
+int open_for(const Request& r, bool direct) {
+  int flags = r.read ? O_RDONLY : O_WRONLY;
+  if (direct) flags |= O_DIRECT;
+  return open(r.path.c_str(), flags, 0644);
 }
 
-// Performs one slice of a job: [off, off+len) of the buffer <-> file.
-int64_t do_slice(const IoJob& j, int64_t off, int64_t len, int64_t block) {
-  if (len <= 0) return 0;
-  int flags = j.read ? O_RDONLY : (O_WRONLY | O_CREAT);
-  const bool direct = is_aligned(j.buf + off, len, 4096) && ((j.file_offset + off) % 4096 == 0);
-#ifdef O_DIRECT
-  if (direct) flags |= O_DIRECT;
-#endif
-  int fd = open(j.path.c_str(), flags, 0644);
-  if (fd < 0 && direct) {  // filesystem without O_DIRECT (tmpfs): retry buffered
-    fd = open(j.path.c_str(), j.read ? O_RDONLY : (O_WRONLY | O_CREAT), 0644);
-  }
-  if (fd < 0) return -1;
+bool slice_direct_ok(const Slice& s) {
+  return (reinterpret_cast<uintptr_t>(s.req->buf + s.off) % kAlign == 0) && (s.off % kAlign == 0) &&
+         (s.len % kAlign == 0);
+}
+
+// psync engine / fallback: positional I/O of `block`-sized pieces.
+bool run_psync(int fd, const Slice& s, int64_t block) {
   int64_t done = 0;
-  while (done < len) {
-    const int64_t n = std::min(block, len - done);
-    ssize_t r = j.read ? pread(fd, j.buf + off + done, n, j.file_offset + off + done)
-                       : pwrite(fd, j.buf + off + done, n, j.file_offset + off + done);
-    if (r <= 0) {
-      close(fd);
-      return -1;
-    }
+  while (done < s.len) {
+    const int64_t n = std::min(block, s.len - done);
+    char* p = s.req->buf + s.off + done;
+    const int64_t o = s.off + done;
+    const ssize_t r = s.req->read ? ::pread(fd, p, n, o) : ::pwrite(fd, p, n, o);
+    if (r <= 0) return false;
     done += r;
   }
-  close(fd);
-  return done;
+  return true;
 }
 
-class ThreadPool {
+class Worker {
  public:
-  explicit ThreadPool(int n) : stop_(false) {
-    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  Worker(int64_t block, int64_t qd, bool single_submit, bool overlap)
+      : block_(block), qd_(std::max<int64_t>(1, qd)), single_(single_submit), overlap_(overlap) {
+    uring_ = io_uring_usable() && ring_.open_ring((unsigned)qd_);
+    thread_ = std::thread([this] { loop(); });
   }
-  ~ThreadPool() {
+  ~Worker() {
     {
       std::lock_guard<std::mutex> g(mu_);
       stop_ = true;
     }
     cv_.notify_all();
-    for (auto& t : workers_) t.join();
+    thread_.join();
   }
-  void submit(std::function<void()> f) {
+  bool uring() const { return uring_; }
+
+  void push(Slice s, std::function<void(const Slice&, bool)> done) {
     {
       std::lock_guard<std::mutex> g(mu_);
-      q_.push_back(std::move(f));
+      q_.emplace_back(std::move(s), std::move(done));
     }
     cv_.notify_one();
   }
-  int size() const { return (int)workers_.size(); }
 
  private:
   void loop() {
     for (;;) {
-      std::function<void()> f;
+      std::pair<Slice, std::function<void(const Slice&, bool)>> job;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
         if (stop_ && q_.empty()) return;
-        f = std::move(q_.front());
+        job = std::move(q_.front());
         q_.pop_front();
       }
-      f();
+      job.second(job.first, run(job.first));
     }
   }
-  std::vector<std::thread> workers_;
-  std::deque<std::function<void()>> q_;
+
+  bool run(const Slice& s) {
+    if (s.len <= 0) return true;
+    bool direct = slice_direct_ok(s);
+    int fd = open_for(*s.req, direct);
+    if (fd < 0 && direct) {  // tmpfs & co. refuse O_DIRECT: buffered
+      direct = false;
+      fd = open_for(*s.req, false);
+    }
+    if (fd < 0) return false;
+    bool ok = uring_ ? run_uring(fd, s) : run_psync(fd, s, block_);
+    close(fd);
+    return ok;
+  }
+
+  // Pieces of `block_` bytes, up to qd_ in flight on this worker's ring.
+  bool run_uring(int fd, const Slice& s) {
+    const int64_t npieces = (s.len + block_ - 1) / block_;
+    const int64_t depth = std::min<int64_t>(qd_, ring_.entries());
+    int64_t next = 0, inflight = 0;
+    bool ok = true;
+    auto submit_one = [&](int64_t k, int64_t done_bytes) {
+      const int64_t lo = k * block_ + done_bytes;
+      const int64_t len = std::min(block_, s.len - k * block_) - done_bytes;
+      ring_.prep(s.req->read, fd, s.req->buf + s.off + lo, (unsigned)len, s.off + lo,
+                 ((uint64_t)k << 32) | (uint64_t)done_bytes);
+    };
+    std::vector<int64_t> progress(npieces, 0);
+    while ((next < npieces || inflight > 0) && ok) {
+      // fill free slots
+      int64_t to_fill = depth - inflight;
+      if (!overlap_ && inflight > 0) to_fill = 0;  // lock-step: drain the batch first
+      int64_t filled = 0;
+      while (filled < to_fill && next < npieces) {
+        submit_one(next++, 0);
+        ++filled;
+        ++inflight;
+        if (single_) {
+          if (ring_.enter(0) < 0) return false;
+        }
+      }
+      // submit the batch (block submit) and wait for at least one completion
+      if (ring_.enter(1) < 0) return false;
+      uint64_t tag;
+      int res;
+      while (ring_.reap(&tag, &res)) {
+        --inflight;
+        const int64_t k = (int64_t)(tag >> 32);
+        const int64_t done0 = (int64_t)(tag & 0xffffffffu);
+        const int64_t want = std::min(block_, s.len - k * block_) - done0;
+        if (res <= 0) {
+          ok = false;
+          continue;
+        }
+        if (res < want) {  // short transfer: resubmit the remainder of this piece
+          submit_one(k, done0 + res);
+          ++inflight;
+        }
+      }
+    }
+    // never leave SQEs referencing the buffer behind on error
+    while (inflight > 0) {
+      if (ring_.enter(1) < 0) break;
+      uint64_t tag;
+      int res;
+      while (ring_.reap(&tag, &res)) --inflight;
+    }
+    return ok;
+  }
+
+  int64_t block_, qd_;
+  bool single_, overlap_;
+  Ring ring_;
+  bool uring_ = false;
+  std::thread thread_;
   std::mutex mu_;
   std::condition_variable cv_;
-  bool stop_;
+  std::deque<std::pair<Slice, std::function<void(const Slice&, bool)>>> q_;
+  bool stop_ = false;
 };
+
+bool validate_request(const Request& r) {
+  // re-read the file range through the page cache and compare with the buffer
+  int fd = open(r.path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  std::vector<char> tmp(1 << 20);
+  int64_t off = 0;
+  bool same = true;
+  while (off < r.nbytes && same) {
+    const int64_t n = std::min<int64_t>((int64_t)tmp.size(), r.nbytes - off);
+    if (::pread(fd, tmp.data(), n, off) != n) {
+      same = false;
+      break;
+    }
+    same = std::memcmp(tmp.data(), r.buf + off, n) == 0;
+    off += n;
+  }
+  close(fd);
+  return same;
+}
 
 }  // namespace
 
 class AioHandle {
  public:
   AioHandle(int64_t block_size, int64_t queue_depth, bool single_submit, bool overlap_events, int64_t thread_count)
-      : block_(block_size), qd_(queue_depth), single_submit_(single_submit), overlap_(overlap_events),
-        threads_(std::max<int64_t>(1, thread_count)), pool_((int)std::max<int64_t>(1, thread_count)) {}
+      : block_(std::max<int64_t>(kAlign, block_size)), qd_(std::max<int64_t>(1, queue_depth)),
+        single_submit_(single_submit), overlap_(overlap_events), threads_(std::max<int64_t>(1, thread_count)) {
+    for (int64_t i = 0; i < threads_; ++i)
+      workers_.emplace_back(new Worker(block_, qd_, single_submit_, overlap_));
+  }
 
   int64_t get_block_size() const { return block_; }
   int64_t get_queue_depth() const { return qd_; }
   bool get_single_submit() const { return single_submit_; }
   bool get_overlap_events() const { return overlap_; }
   int64_t get_thread_count() const { return threads_; }
+  std::string get_engine() const { return workers_[0]->uring() ? "io_uring" : "psync"; }
 
   int64_t read(at::Tensor buffer, const std::string& filename, bool validate) {
     return sync_io(buffer, filename, true, validate);
@@ -143,13 +374,13 @@ class AioHandle {
   int64_t async_pread(at::Tensor b, const std::string& f) { return submit(b, f, true, false); }
   int64_t async_pwrite(at::Tensor b, const std::string& f) { return submit(b, f, false, false); }
 
-  // Wait for all outstanding async ops; returns how many completed (or -1 on error).
+  // Wait for all outstanding async requests; returns how many completed (-1 on any error).
   int64_t wait() {
     pybind11::gil_scoped_release nogil;
     std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [this] { return pending_slices_ == 0; });
-    const int64_t n = completed_ops_;
-    completed_ops_ = 0;
+    cv_.wait(lk, [this] { return pending_ == 0; });
+    const int64_t n = completed_;
+    completed_ = 0;
     if (failed_) {
       failed_ = false;
       return -1;
@@ -158,58 +389,71 @@ class AioHandle {
   }
 
  private:
-  void check(const at::Tensor& b) {
-    TORCH_CHECK(!b.is_cuda(), "aio: buffers must be host tensors (stage GPU tensors through pinned memory)");
-    TORCH_CHECK(b.is_contiguous(), "aio: contiguous buffer required");
-  }
-
   int64_t sync_io(at::Tensor buffer, const std::string& filename, bool read, bool validate) {
     submit(buffer, filename, read, validate);
     return wait() < 0 ? -1 : 1;
   }
 
   int64_t submit(at::Tensor buffer, const std::string& filename, bool read, bool validate) {
-    check(buffer);
-    IoJob job{reinterpret_cast<char*>(buffer.data_ptr()), (int64_t)buffer.nbytes(), 0, filename, read, validate};
-    if (!read) {  // create / size the file once before parallel slices write into it
+    TORCH_CHECK(!buffer.is_cuda(), "aio: buffers must be host tensors (stage GPU tensors through pinned memory)");
+    TORCH_CHECK(buffer.is_contiguous(), "aio: contiguous buffer required");
+    auto req = std::make_shared<Request>();
+    req->buf = reinterpret_cast<char*>(buffer.data_ptr());
+    req->nbytes = (int64_t)buffer.nbytes();
+    req->path = filename;
+    req->read = read;
+    req->validate = validate;
+    if (!read) {  // create the file before parallel slices write into it
       int fd = open(filename.c_str(), O_WRONLY | O_CREAT, 0644);
-      TORCH_CHECK(fd >= 0, "aio: cannot open ", filename);
+      TORCH_CHECK(fd >= 0, "aio: cannot open ", filename, " for writing");
       close(fd);
+    } else {
+      struct stat st;
+      TORCH_CHECK(stat(filename.c_str(), &st) == 0, "aio: cannot stat ", filename);
+      TORCH_CHECK(st.st_size >= req->nbytes, "aio: ", filename, " holds ", (int64_t)st.st_size,
+                  " bytes, read of ", req->nbytes, " requested");
     }
-    // split into `threads_` contiguous slices aligned to the block size
-    const int64_t nb = (job.nbytes + block_ - 1) / block_;
-    const int64_t per = (nb + threads_ - 1) / threads_;
-    std::vector<std::pair<int64_t, int64_t>> parts;
+    // one contiguous, block-aligned slice per worker (reference deepspeed_aio_thread.cpp)
+    const int64_t nb = (req->nbytes + block_ - 1) / block_;
+    const int64_t per = std::max<int64_t>(1, (nb + threads_ - 1) / threads_);
+    std::vector<Slice> parts;
     for (int64_t t = 0; t < threads_; ++t) {
       const int64_t off = t * per * block_;
-      if (off >= job.nbytes) break;
-      parts.emplace_back(off, std::min(job.nbytes - off, per * block_));
+      if (off >= req->nbytes) break;
+      parts.push_back(Slice{req, off, std::min(req->nbytes - off, per * block_)});
     }
+    if (parts.empty()) parts.push_back(Slice{req, 0, 0});
+    req->slices_left = (int)parts.size();
     {
       std::lock_guard<std::mutex> g(mu_);
-      pending_slices_ += (int64_t)parts.size();
+      ++pending_;
     }
-    auto remaining = std::make_shared<std::atomic<int64_t>>((int64_t)parts.size());
-    for (auto& pr : parts) {
-      pool_.submit([this, job, pr, remaining] {
-        const int64_t r = do_slice(job, pr.first, pr.second, block_);
-        std::lock_guard<std::mutex> g(mu_);
-        if (r < 0) failed_ = true;
-        if (--(*remaining) == 0) completed_ops_ += 1;
-        if (--pending_slices_ == 0) cv_.notify_all();
+    for (size_t i = 0; i < parts.size(); ++i) {
+      workers_[i % workers_.size()]->push(parts[i], [this](const Slice& s, bool ok) {
+        if (!ok) s.req->failed = true;
+        if (--s.req->slices_left == 0) finish(*s.req);
       });
     }
     return 0;
   }
 
+  void finish(Request& r) {
+    bool ok = !r.failed;
+    if (ok && r.validate) ok = validate_request(r);
+    std::lock_guard<std::mutex> g(mu_);
+    if (!ok) failed_ = true;
+    ++completed_;
+    if (--pending_ == 0) cv_.notify_all();
+  }
+
   int64_t block_, qd_;
   bool single_submit_, overlap_;
   int64_t threads_;
-  ThreadPool pool_;
+  std::vector<std::unique_ptr<Worker>> workers_;
   std::mutex mu_;
   std::condition_variable cv_;
-  int64_t pending_slices_ = 0;
-  int64_t completed_ops_ = 0;
+  int64_t pending_ = 0;
+  int64_t completed_ = 0;
   bool failed_ = false;
 };
 
@@ -239,10 +483,13 @@ int64_t deepspeed_memcpy(at::Tensor dest, at::Tensor src) {
   return 0;
 }
 
+std::string aio_engine() { return io_uring_usable() ? "io_uring" : "psync"; }
+
 void register_aio(pybind11::module& m) {
   m.def("aio_read", &aio_read);
   m.def("aio_write", &aio_write);
   m.def("deepspeed_memcpy", &deepspeed_memcpy);
+  m.def("aio_engine", &aio_engine);
   pybind11::class_<AioHandle>(m, "aio_handle")
       .def(pybind11::init<int64_t, int64_t, bool, bool, int64_t>(), pybind11::arg("block_size") = 1 << 20,
            pybind11::arg("queue_depth") = 128, pybind11::arg("single_submit") = false,
@@ -252,6 +499,7 @@ void register_aio(pybind11::module& m) {
       .def("get_single_submit", &AioHandle::get_single_submit)
       .def("get_overlap_events", &AioHandle::get_overlap_events)
       .def("get_thread_count", &AioHandle::get_thread_count)
+      .def("get_engine", &AioHandle::get_engine)
       .def("read", &AioHandle::read)
       .def("write", &AioHandle::write)
       .def("pread", &AioHandle::pread)

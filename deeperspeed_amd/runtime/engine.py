@@ -630,6 +630,7 @@ class DeepSpeedEngine(Module):
                                                  resident_grads=bool(zc.resident_grads),
                                                  grad_accum_dtype=zc.grad_accum_dtype,
                                                  reduce_scatter=zc.reduce_scatter,
+                                                 reduce_bucket_size=zc.reduce_bucket_size,
                                                  prefetch_bucket_size=zc.stage3_prefetch_bucket_size,
                                                  max_live_parameters=zc.stage3_max_live_parameters,
                                                  max_reuse_distance=zc.stage3_max_reuse_distance,

@@ -233,6 +233,43 @@ class ShardedOptimizerBase:
     def _inner_group(self, g: FlatGroup):
         return self.optimizer.param_groups[g.group_index]
 
+    # ------------------------------------------------------------------ in-flight reductions
+    # ProcessGroupNCCL keeps an async collective's tensors alive until its work is waited
+    # for, so an unbounded queue of gradient reductions would hold every bucket/unit gradient
+    # buffer of the backward at once (the whole model's gradients).  The queue is bounded by
+    # element count: once more than `max_inflight_numel` elements are in flight the oldest
+    # reductions are completed.  work.wait() on RCCL only makes the compute stream wait for
+    # the collective's stream (no host block), so draining early costs no CPU run-ahead.
+    max_inflight_numel = 0  # 0 = two of the largest reductions
+
+    def _queue_reduction(self, work, fin, numel=0, overlap=True):
+        if not overlap:
+            if work is not None:
+                work.wait()
+            if fin is not None:
+                fin()
+            return
+        pend = self.__dict__.setdefault("_pending", [])
+        pend.append((work, fin, int(numel)))
+        self._inflight = getattr(self, "_inflight", 0) + int(numel)
+        self._inflight_peak = max(getattr(self, "_inflight_peak", 0), int(numel))
+        cap = self.max_inflight_numel or 2 * self._inflight_peak
+        while len(pend) > 1 and self._inflight > cap:
+            self._complete_oldest()
+
+    def _complete_oldest(self):
+        work, fin, numel = self._pending.pop(0)
+        self._inflight -= numel
+        if work is not None:
+            work.wait()
+        if fin is not None:
+            fin()
+
+    def _drain_reductions(self):
+        while getattr(self, "_pending", None):
+            self._complete_oldest()
+        self._inflight = 0
+
     # ------------------------------------------------------------------ norm / overflow
     def _shard_grads_for_norm(self):
         """Yield (tensor, include) pairs whose sum of squares forms this rank's share."""

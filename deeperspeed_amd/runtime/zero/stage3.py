@@ -67,6 +67,50 @@ def _in_backward():
     return torch._C._current_graph_task_id() != -1
 
 
+class _BufferPool:
+    """Persistent device buffers for gathered units and unit gradients.
+
+    RCCL collectives record their tensors on the communicator's stream, so a buffer freed
+    back to the caching allocator only becomes reusable once that stream's event has
+    completed; with the host running ahead of the GPU the allocator keeps growing.  Buffers
+    returned here are reused immediately: later work on the compute stream is
+    stream-ordered after their last use, and ProcessGroupNCCL makes its stream wait for the
+    compute stream before each collective, so a reused buffer never races an earlier
+    reader.  Sizes are rounded up to `SIZE_CLASS` elements so units of nearly equal size
+    (GPT-NeoX attention / MLP-in / MLP-out are all ~151M elements at 20B) share buffers."""
+
+    SIZE_CLASS = 1 << 22
+
+    def __init__(self):
+        self.free: Dict[tuple, List[torch.Tensor]] = {}
+        self.held = 0  # elements owned by the pool (free + handed out)
+
+    def _cls(self, numel):
+        return -(-int(numel) // self.SIZE_CLASS) * self.SIZE_CLASS if numel > self.SIZE_CLASS else int(numel)
+
+    def get(self, numel, dtype, device, zero=False):
+        c = self._cls(numel)
+        lst = self.free.get((dtype, c, str(device)))
+        if lst:
+            base = lst.pop()
+        else:
+            self.held += c
+            base = torch.empty(c, dtype=dtype, device=device)
+        t = base[:numel] if c != numel else base
+        if zero:
+            t.zero_()
+        return t
+
+    def put(self, t):
+        base = t if t._base is None else t._base
+        self.free.setdefault((base.dtype, base.numel(), str(base.device)), []).append(base)
+
+    def clear(self):
+        for lst in self.free.values():
+            self.held -= sum(t.numel() for t in lst)
+        self.free = {}
+
+
 class ZeroUnit:
     def __init__(self, uid, module, params):
         self.uid = uid
@@ -98,7 +142,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                  gradient_predivide_factor=1.0, gradient_accumulation_steps=1, offload_optimizer=None,
                  offload_param=None, timers=None, overlap_comm=True, sub_group_size=int(1e12), verbose=False,
                  compact_master=False, force_sharded=False, resident_grads=False, grad_accum_dtype="auto",
-                 reduce_scatter=True):
+                 reduce_scatter=True, reduce_bucket_size=0):
         super().__init__(init_optimizer, dp_process_group=dp_process_group, mpu=mpu, clip_grad=clip_grad,
                          static_loss_scale=static_loss_scale, dynamic_loss_scale=dynamic_loss_scale,
                          dynamic_loss_args=dynamic_loss_args, fp32_reduce=fp32_reduce,
@@ -114,6 +158,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         # reduce_scatter=False (reference stage3.py:1948): gradients are all-reduced per bucket
         # and each rank keeps its chunk -- twice the traffic, kept for parity only
         self.use_reduce_scatter = bool(reduce_scatter)
+        # in-flight gradient reductions are bounded (sharded_base._queue_reduction): at most
+        # two reduce buckets' worth, or two units when units are larger
+        self.max_inflight_numel = 2 * int(reduce_bucket_size or 0)
         # MI355X extension: run the sharded gather / reduce-scatter machinery even on a world of
         # one (the real RCCL code path of N>1, on one GPU) instead of binding params to shards
         self.force_sharded = bool(force_sharded)
@@ -159,6 +206,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         # stage3_max_reuse_distance): live numel of non-persistent gathered units and the
         # per-trace-position distance (in elements) to each unit's next use
         self._live_numel = 0
+        self._pool = _BufferPool()
+        self.pool_skipped = 0  # released buffers still referenced elsewhere (left to the allocator)
         self.gathered_numel = 0  # elements all-gathered so far (stats / tests)
         self._reuse_f: Dict[int, int] = {}
         self._reuse_b: Dict[int, int] = {}
@@ -341,7 +390,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             self._live_numel += u.numel
         self.gathered_numel += u.numel
         for g, b in u.buckets:
-            full = torch.empty(b.numel, dtype=g.dtype, device=self.compute_device)
+            full = self._pool.get(b.numel, g.dtype, self.compute_device)
             if self.param_nvme and g.shard_param is None:
                 chunk = self._pswap.read_to_device(self._pkey[id(b)], self.compute_device)
             else:
@@ -387,6 +436,13 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             for p in b.params:
                 p.data = e
                 p.ds_status = ZeroParamStatus.NOT_AVAILABLE
+        for full in u.fulls:
+            # a gathered buffer still referenced elsewhere (e.g. a view autograd saved for
+            # backward) goes back to the allocator instead; it must not be overwritten
+            if _sole_owner(full):
+                self._pool.put(full)
+            else:
+                self.pool_skipped += 1
         u.fulls = []
         u.status = ZeroParamStatus.NOT_AVAILABLE
         if not u.persistent:
@@ -458,14 +514,21 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def _prefetch(self, trace, pos):
         if not self._trace_frozen or pos < 0 or not self.overlap_comm:
             return
+        # the window is the next `prefetch_bucket_size` elements of the trace, counting units
+        # already gathered or in flight: a budget charged only for new fetches would let every
+        # pre-forward hook push the frontier one unit further until the whole model is gathered
         budget = self.prefetch_bucket_size
         k = pos + 1
+        seen = set()
         while k < len(trace) and budget > 0:
             u = self._units[trace[k]]
+            k += 1
+            if u.persistent or u.uid in seen:
+                continue
+            seen.add(u.uid)
+            budget -= u.numel
             if u.status == ZeroParamStatus.NOT_AVAILABLE:
                 self._fetch(u)
-                budget -= u.numel
-            k += 1
 
     def _pre_forward(self, u: ZeroUnit, module, inputs):
         u.active += 1
@@ -526,7 +589,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         u.bw_expected = sum(1 for p in u.params if p.requires_grad)
         u.bw_ready = 0
         if not u.grad_fulls:  # resident buffers of earlier micro-batches accumulate on
-            u.grad_fulls = [torch.zeros(b.numel, dtype=self._unit_grad_dtype(g), device=self.compute_device)
+            u.grad_fulls = [self._pool.get(b.numel, self._unit_grad_dtype(g), self.compute_device, zero=True)
                             for g, b in u.buckets]
         for (g, b), gf in zip(u.buckets, u.grad_fulls):
             for i, p in enumerate(b.params):
@@ -579,22 +642,20 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                 src = src.float()
             out_slice = g.shard_grad[b.shard_offset: b.shard_offset + b.chunk]
             direct = out_slice.dtype == src.dtype and not self._grads_nonzero
-            out = out_slice if direct else torch.empty(b.chunk, dtype=src.dtype, device=src.device)
+            out = out_slice if direct else self._pool.get(b.chunk, src.dtype, src.device)
             if self.use_reduce_scatter:
                 work = comm.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True,
                                                   tag=f"zero3.reduce.u{u.uid}")
-                fin = None if direct else functools.partial(_accum, out_slice, out)
+                done = None if direct else functools.partial(_accum, out_slice, out)
             else:
                 work = comm.all_reduce(src, group=self.dp_group, async_op=True, tag=f"zero3.allreduce.u{u.uid}")
                 mine = src[self.dp_rank * b.chunk: (self.dp_rank + 1) * b.chunk]
-                fin = functools.partial(_copy if direct else _accum, out_slice, mine)
+                done = functools.partial(_copy if direct else _accum, out_slice, mine)
+            # buffers go back to the pool once the reduction has been waited for
+            back = [gf] if direct else [gf, out]
+            fin = functools.partial(_finish_reduce, done, self._pool, back)
             self._reduced_this_pass = True
-            if self.overlap_comm:
-                self._pending.append((work, fin))
-            else:
-                work.wait()
-                if fin is not None:
-                    fin()
+            self._queue_reduction(work, fin, b.numel, overlap=self.overlap_comm)
         u.grad_fulls = []
         if u.active == 0:
             self._maybe_release(u, "b")
@@ -612,12 +673,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             for u in self._units:  # accumulated in earlier micro-batches, unused in this one
                 if u.grad_fulls and not u.reduced:
                     self._reduce_unit(u)
-        for work, fin in self._pending:
-            if work is not None:
-                work.wait()
-            if fin is not None:
-                fin()
-        self._pending = []
+        self._drain_reductions()
         for u in self._units:
             u.reduced = False
             u.in_backward = False
@@ -693,6 +749,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             g.shard_grad.zero_()
         self._grads_nonzero = False
         for u in self._units:  # an overflow-skipped step drops resident micro-batch grads too
+            for t in u.grad_fulls:
+                self._pool.put(t)
             u.grad_fulls = []
 
     def _zero_stage(self):
@@ -767,6 +825,26 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         for name, bfr in module.named_buffers(prefix=prefix.rstrip(".")):
             out[name] = bfr.detach().cpu()
         return out
+
+
+def _sole_owner(t) -> bool:
+    """True when nothing but `t` (and its pool base) references its storage (the temporary
+    storage handle of this query counts one)."""
+    try:
+        own = 2 if t._base is None else 3
+        return torch._C._storage_Use_Count(t.untyped_storage()._cdata) <= own
+    except Exception:  # noqa: BLE001 - private API; without it nothing is pooled
+        return False
+
+
+def _finish_reduce(done, pool, bufs):
+    if done is not None:
+        done()
+    seen = set()
+    for t in bufs:
+        if id(t) not in seen:
+            seen.add(id(t))
+            pool.put(t)
 
 
 def _accum(dst, src):

@@ -73,6 +73,7 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
         # accumulates straight into the bucket instead of a copy per parameter
         self.prebind_window = max(1, int(prebind_window))
         self.reduce_bucket_size = max(int(reduce_bucket_size), ALIGN * max(1, self.dp_world))
+        self.max_inflight_numel = 2 * self.reduce_bucket_size
         self.groups = self._split_groups()
         for g in self.groups:
             build_size_buckets(g, self.layout_world, self.reduce_bucket_size)
@@ -256,7 +257,7 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
                 target.copy_(src)
             work = comm.all_reduce(target, group=self.dp_group, async_op=True, tag="zero.allreduce") if (_dist_ready() and world > 1) \
                 else None
-            self._queue(work, None)
+            self._queue(work, None, b.numel)
             return
         out_slice = dst_full[b.shard_offset: b.shard_offset + b.chunk]
         accumulate = self._bucketed() and self.gradient_accumulation_steps > 1
@@ -283,28 +284,17 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
                 self._buf_pool.setdefault(g.dtype, []).append(st.buffer[0])
                 st.buffer = None
 
-        self._queue(work, finish)
+        self._queue(work, finish, b.numel)
 
-    def _queue(self, work, fin):
-        if self.overlap_comm:
-            self._pending.append((work, fin))
-            return
-        if work is not None:
-            work.wait()
-        if fin is not None:
-            fin()
+    def _queue(self, work, fin, numel=0):
+        self._queue_reduction(work, fin, numel, overlap=self.overlap_comm)
 
     def reduce_epilogue(self):
         """Flush all buckets and complete their reductions (end of backward)."""
         if not self._hooks_active():
             return
         self._launch_ready_in_order(force=True)
-        for work, fin in self._pending:
-            if work is not None:
-                work.wait()
-            if fin is not None:
-                fin()
-        self._pending = []
+        self._drain_reductions()
         self._reset_bucket_states()
 
     # reference method names

@@ -1,31 +1,74 @@
-"""Turn a rocprofv3 `*_kernel_stats.csv` into the markdown table committed under profiles/.
+"""Turn a rocprofv3 kernel trace into the markdown table committed under profiles/.
 
-usage: python scripts/prof_summary.py <kernel_stats.csv> <title> <command> [note] > profiles/<name>.md
+Accepts either a `*_kernel_stats.csv` (--output-format csv) or the default SQLite output
+(`*_results.db`, aggregated from its `kernels` view).  Besides the per-kernel table it
+prints a category breakdown (hipBLASLt GEMMs, RCCL, own HIP kernels, torch elementwise,
+fills / copies) so the non-GEMM share can be tracked across rounds.
+
+usage: python scripts/prof_summary.py <stats.csv|results.db> <title> <command> [note] > profiles/<name>.md
 """
 
 import csv
+import sqlite3
 import sys
+from collections import defaultdict
+
+
+def load(path):
+    """[(name, calls, total_ns)]"""
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        rows = c.execute("select name, count(*), sum(duration) from kernels group by name").fetchall()
+        return [(n, int(k), float(t)) for n, k, t in rows]
+    return [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"])) for r in csv.DictReader(open(path))]
+
+
+def category(name):
+    n = name.lower()
+    if "cijk_" in n or "gemm" in n and "dsa::" not in n:
+        return "GEMM (hipBLASLt/rocBLAS)"
+    if "nccl" in n or "rccl" in n:
+        return "RCCL collectives"
+    if "dsa::fa::" in n:
+        return "flash attention (own HIP)"
+    if "dsa::" in n:
+        return "other own HIP kernels"
+    if "fill" in n:
+        return "fills / memset"
+    if "copy" in n or "memcpy" in n:
+        return "copies"
+    if "at::native" in n:
+        return "torch elementwise / reductions"
+    return "other"
 
 
 def main():
     path, title, cmd = sys.argv[1:4]
     note = sys.argv[4] if len(sys.argv) > 4 else ""
-    rows = list(csv.DictReader(open(path)))
-    total_ns = sum(float(r["TotalDurationNs"]) for r in rows)
+    rows = load(path)
+    total_ns = sum(t for _, _, t in rows)
     print(f"# {title}\n")
     print(f"Command: `{cmd}`")
     if note:
         print(f"\n{note}")
     print(f"\nTotal kernel time: {total_ns / 1e6:.1f} ms\n")
-    print("| total ms | % | calls | avg us | kernel |")
+    cats = defaultdict(lambda: [0, 0.0])
+    for n, k, t in rows:
+        c = cats[category(n)]
+        c[0] += k
+        c[1] += t
+    print("| category | total ms | % | calls |")
+    print("|---|---|---|---|")
+    for name, (k, t) in sorted(cats.items(), key=lambda kv: -kv[1][1]):
+        print(f"| {name} | {t / 1e6:.1f} | {100 * t / total_ns:.1f} | {k} |")
+    print("\n| total ms | % | calls | avg us | kernel |")
     print("|---|---|---|---|---|")
-    rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
-    for r in rows[:45]:
-        name = r["Name"].replace("|", "/")
+    rows.sort(key=lambda r: -r[2])
+    for n, k, t in rows[:45]:
+        name = n.replace("|", "/")
         if len(name) > 120:
             name = name[:117] + "..."
-        print(f"| {float(r['TotalDurationNs']) / 1e6:.1f} | {100 * float(r['TotalDurationNs']) / total_ns:.1f} | "
-              f"{r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | `{name}` |")
+        print(f"| {t / 1e6:.1f} | {100 * t / total_ns:.1f} | {k} | {t / k / 1e3:.1f} | `{name}` |")
 
 
 if __name__ == "__main__":
