@@ -30,7 +30,11 @@ from typing import Dict, List, Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(_HERE, "csrc")
-BUILD_DIR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "build", "ops")
+_ROOT = os.path.dirname(os.path.dirname(_HERE))
+# object files: build/ops of a source checkout; next to the package when installed
+BUILD_DIR = os.environ.get("DSA_BUILD_DIR") or (
+    os.path.join(_ROOT, "build", "ops") if os.path.exists(os.path.join(_ROOT, "setup.py"))
+    else os.path.join(_HERE, "_build"))
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
