@@ -9,6 +9,10 @@ Semantics kept: hysteresis (`delayed_shift`) before each scale decrease, growth 
 import torch
 
 
+class LossScaleUnderflowError(Exception):
+    """Raised when gradients overflow although the dynamic loss scale is at its minimum."""
+
+
 class LossScalerBase:
     def __init__(self, cur_scale):
         self.cur_scale = cur_scale
@@ -79,23 +83,29 @@ class DynamicLossScaler(LossScalerBase):
         return s != s or s in (float("inf"), float("-inf"))
 
     def update_scale(self, overflow):
+        """Advance one iteration.  An overflow first spends the hysteresis budget
+        (`delayed_shift - 1` tolerated overflows), then divides the scale (never below
+        `min_scale`; overflowing AT the minimum is fatal when raise_error_at_min_scale).
+        Every `scale_window` iterations after the last overflow the scale grows by
+        `scale_factor` and the budget refills (consecutive_hysteresis refills it on every
+        clean iteration)."""
+        it = self.cur_iter
+        self.cur_iter = it + 1
         if overflow:
-            if self.delayed_shift == 1 or self.cur_hysteresis == 1:
-                if self.cur_scale == self.min_scale and self.raise_error_at_min_scale:
-                    raise Exception("Current loss scale already at minimum - cannot decrease scale anymore. "
-                                    "Exiting run.")
-                self.cur_scale = max(self.cur_scale / self.scale_factor, self.min_scale)
-            else:
+            self.last_overflow_iter = it
+            if self.delayed_shift > 1 and self.cur_hysteresis > 1:
                 self.cur_hysteresis -= 1
-            self.last_overflow_iter = self.cur_iter
-        else:
-            if self.consecutive_hysteresis:
-                self.cur_hysteresis = self.delayed_shift
-            if (self.cur_iter - self.last_overflow_iter) % self.scale_window == 0:
-                if not self.consecutive_hysteresis:
-                    self.cur_hysteresis = self.delayed_shift
-                self.cur_scale *= self.scale_factor
-        self.cur_iter += 1
+                return
+            if self.raise_error_at_min_scale and self.cur_scale == self.min_scale:
+                raise LossScaleUnderflowError(
+                    f"gradients overflow at the minimum loss scale ({self.min_scale}); the run cannot continue")
+            self.cur_scale = max(self.min_scale, self.cur_scale / self.scale_factor)
+            return
+        grow = (it - self.last_overflow_iter) % self.scale_window == 0
+        if grow or self.consecutive_hysteresis:
+            self.cur_hysteresis = self.delayed_shift
+        if grow:
+            self.cur_scale *= self.scale_factor
 
     def state_dict(self):
         sd = super().state_dict()

@@ -71,9 +71,9 @@ class PipelineEngine(DeepSpeedEngine):
 
         num_params = sum(p.numel() for p in self.module.parameters() if p.requires_grad)
         unique = num_params
-        for key, d in self.module.tied_comms.items():
-            if self.global_rank != min(d["ranks"]):
-                unique -= sum(p.numel() for p in d["module"].parameters())
+        for tie in self.module.tied_comms.values():
+            if self.global_rank != min(tie.ranks):
+                unique -= sum(p.numel() for p in tie.module.parameters())
         t = torch.LongTensor([num_params, unique]).to(self.device)
         dist.all_reduce(t, group=self.grid.get_model_parallel_group())
         total, uniq = t.tolist()

@@ -1,19 +1,31 @@
-"""PipelineModule: a model expressed as a sequence of layers partitioned over pipeline stages.
+"""PipelineModule: a model written as a list of layers, each pipeline stage owning a slice.
 
-Reference parity: deepspeed/runtime/pipe/module.py:19-589 -- `LayerSpec` (lazy construction so
-each stage only builds its own layers), `TiedLayerSpec` (weights shared across stages, e.g.
-embedding / LM head, with gradient all-reduce and initial broadcast), partition methods
-`uniform`, `parameters`, `type:<regex>`, per-stage activation checkpointing at
-`activation_checkpoint_interval` layers (DeeperSpeed `checkpointable_layers`), per-layer
-checkpoint files `layer_XX[-model_YY]-model_states.pt` written by data-parallel rank 0,
-and `seed_layers` deterministic per-layer seeding.
+Behavioural parity with deepspeed/runtime/pipe/module.py:19-589:
+* `LayerSpec(cls, *args, **kw)` defers construction so a stage builds only its own layers;
+  `TiedLayerSpec(key, cls, ..., forward_fn, tied_weight_attr)` shares one module between
+  the stages that use `key` (embedding / LM head): weights broadcast from the lowest stage
+  at construction, gradients all-reduced over the stages by `allreduce_tied_weight_gradients`.
+* partition methods `uniform`, `parameters` (balanced by trainable parameter count) and
+  `type:<regex>` (balanced by the number of layers whose class name matches).
+* `activation_checkpoint_interval` recomputes groups of that many consecutive layers; the
+  DeeperSpeed `checkpointable_layers` list restricts which groups qualify.
+* `seed_layers` seeds each layer's construction and each forward deterministically.
+* checkpoints: one file per layer, `layer_XX[-<rank repr>]-model_states.pt`, written by
+  data-parallel rank 0; `ckpt_prefix` for the stage's engine state.
+
+Structure here: the stage plan (partition boundaries) is computed once by `_plan_stages`;
+the local layers are `_Slot` records (callable + owning module or tie key); the forward is a
+precomputed list of `_Segment`s (range + whether it is recomputed), run by one loop, so no
+closures are rebuilt per micro-batch.
 """
 
 from __future__ import annotations
 
 import os
 import re
+from dataclasses import dataclass, field
 from functools import partial
+from typing import Callable, Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -30,15 +42,15 @@ class PipelineError(Exception):
 
 
 class LayerSpec:
-    """Deferred construction of a layer: `LayerSpec(nn.Linear, 8, 4)` builds `nn.Linear(8, 4)`
-    only on the stage that owns it."""
+    """A layer to be built later: `LayerSpec(nn.Linear, 8, 4)` -> `nn.Linear(8, 4)` on the
+    owning stage only."""
 
     def __init__(self, typename, *module_args, **module_kwargs):
+        if not (isinstance(typename, type) and issubclass(typename, nn.Module)):
+            raise RuntimeError("LayerSpec only supports torch.nn.Module types.")
         self.typename = typename
         self.module_args = module_args
         self.module_kwargs = module_kwargs
-        if not issubclass(typename, nn.Module):
-            raise RuntimeError("LayerSpec only supports torch.nn.Module types.")
         self.global_rank = dist.get_rank() if dist.is_initialized() else -1
 
     def __repr__(self):
@@ -46,16 +58,82 @@ class LayerSpec:
 
     def build(self, log=False):
         if log:
-            logger.info(f"RANK={self.global_rank} building {repr(self)}")
+            logger.info(f"RANK={self.global_rank} building {self!r}")
         return self.typename(*self.module_args, **self.module_kwargs)
 
 
 class TiedLayerSpec(LayerSpec):
+    """A layer whose module (and `tied_weight_attr` parameter) is shared by every position
+    using the same `key`; `forward_fn(module, x)` lets a position use it differently (e.g.
+    the LM head reading the embedding matrix)."""
+
     def __init__(self, key, typename, *module_args, forward_fn=None, tied_weight_attr="weight", **module_kwargs):
         super().__init__(typename, *module_args, **module_kwargs)
         self.key = key
         self.forward_fn = forward_fn
         self.tied_weight_attr = tied_weight_attr
+
+
+@dataclass
+class _Slot:
+    index: int                      # global layer index
+    fn: Callable                    # what forward calls
+    module: Optional[nn.Module]     # registered submodule (None for tied layers / plain callables)
+    tie_key: Optional[str] = None
+
+
+@dataclass
+class _Segment:
+    start: int
+    stop: int
+    recompute: bool
+
+
+@dataclass
+class _TieGroup:
+    ranks: List[int]
+    group: object
+    weight_attr: str
+    module: nn.Module = field(repr=False)
+
+    def __getitem__(self, k):  # dict-style access kept for callers written against the reference
+        return {"ranks": self.ranks, "group": self.group, "weight_attr": self.weight_attr, "module": self.module}[k]
+
+
+def _layer_name(layer) -> Optional[str]:
+    if isinstance(layer, LayerSpec):
+        return layer.typename.__name__
+    if isinstance(layer, nn.Module):
+        return type(layer).__name__
+    return getattr(layer, "__name__", None)
+
+
+def _trainable_numel(layer) -> int:
+    if isinstance(layer, LayerSpec):
+        mod = layer.build()
+        n = sum(p.numel() for p in mod.parameters() if p.requires_grad)
+        del mod
+        return n
+    if isinstance(layer, nn.Module):
+        return sum(p.numel() for p in layer.parameters() if p.requires_grad)
+    return 0
+
+
+def _plan_stages(specs, num_stages: int, method: str) -> List[int]:
+    """Stage boundaries (len num_stages + 1) for the layer list under a partition method."""
+    method = method.lower()
+    n = len(specs)
+    if method == "uniform":
+        return ds_utils.partition_uniform(num_items=n, num_parts=num_stages)
+    if method == "parameters":
+        return ds_utils.partition_balanced(weights=[_trainable_numel(s) for s in specs], num_parts=num_stages)
+    if method.startswith("type:"):
+        rx = re.compile(method.split(":", 1)[1], re.IGNORECASE)
+        hits = [1 if (_layer_name(s) is not None and rx.search(_layer_name(s))) else 0 for s in specs]
+        if not any(hits):
+            raise RuntimeError(f"Partitioning '{method[5:]}' found no valid layers to partition.")
+        return ds_utils.partition_balanced(weights=hits, num_parts=num_stages)
+    raise NotImplementedError(f"Partitioning method {method} not implemented.")
 
 
 class PipelineModule(nn.Module):
@@ -65,209 +143,179 @@ class PipelineModule(nn.Module):
         super().__init__()
         if num_stages is None and topology is None:
             raise RuntimeError("must provide num_stages or topology")
-        self.micro_offset = 0
+        if checkpointable_layers is not None and not isinstance(checkpointable_layers, list):
+            raise TypeError("checkpointable_layers must be a list of class names")
+        if not dist.is_initialized():
+            from ...utils.distributed import init_distributed
+            init_distributed()
         self.loss_fn = loss_fn
         self.seed_layers = seed_layers
         self.seed_fn = seed_fn
         self.base_seed = base_seed
-        if not dist.is_initialized():
-            from ...utils.distributed import init_distributed
-            init_distributed()
+        self.micro_offset = 0
+        self.curr_layer = -1
+        self.activation_checkpoint_func = activation_checkpoint_func
+        self.checkpointable_layers = checkpointable_layers
+
         self.world_group = dist.new_group(ranks=range(dist.get_world_size()))
         self.global_rank = dist.get_rank(group=self.world_group)
         self.world_size = dist.get_world_size(group=self.world_group)
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        if topology:
-            self._topo = topology
-            self.num_stages = self._topo.get_dim("pipe")
-        else:
-            self.num_stages = num_stages
-            if self.world_size % self.num_stages != 0:
-                raise RuntimeError(f"num_stages ({self.num_stages}) must divide distributed world size "
-                                   f"({self.world_size})")
-            self._topo = PipeDataParallelTopology(num_pp=num_stages, num_dp=self.world_size // num_stages)
-        self._grid = PipelineParallelGrid(process_group=self.world_group, topology=self._topo)
-        self.stage_id = self._topo.get_coord(self.global_rank).pipe
+        if topology is None:
+            if self.world_size % num_stages:
+                raise RuntimeError(f"num_stages ({num_stages}) must divide distributed world size ({self.world_size})")
+            topology = PipeDataParallelTopology(num_pp=num_stages, num_dp=self.world_size // num_stages)
+        self._topo = topology
+        self.num_stages = topology.get_dim("pipe")
+        self._grid = PipelineParallelGrid(process_group=self.world_group, topology=topology)
+        self.stage_id = topology.get_coord(self.global_rank).pipe
+
         self._layer_specs = list(layers)
         self._num_layers = len(self._layer_specs)
-        self._local_start = 0
-        self._local_stop = None
-        self._partition_layers(method=partition_method)
-        self.forward_funcs = []
-        self.tied_modules = nn.ModuleDict()
-        self.tied_weight_attrs = {}
-        self._build()
-        if torch.cuda.is_available():
-            self.to(f"cuda:{self.local_rank % max(1, torch.cuda.device_count())}")
-        self.tied_comms = self._index_tied_modules()
-        self._synchronize_tied_weights()
-        self.activation_checkpoint_interval = activation_checkpoint_interval
-        self.activation_checkpoint_func = activation_checkpoint_func
-        if checkpointable_layers is not None:
-            assert isinstance(checkpointable_layers, list)
-        self.checkpointable_layers = checkpointable_layers
+        self.parts = _plan_stages(self._layer_specs, self.num_stages, partition_method)
+        self._local_start, self._local_stop = self.parts[self.stage_id], self.parts[self.stage_id + 1]
+        if self.global_rank == 0:
+            for s in range(self.num_stages):
+                logger.info(f"stage={s} layers={self.parts[s + 1] - self.parts[s]}")
 
-    def _build(self):
-        for local_idx, layer in enumerate(self._layer_specs[self._local_start:self._local_stop]):
-            layer_idx = local_idx + self._local_start
-            if self.seed_layers:
-                (self.seed_fn or ds_utils.set_random_seed)(self.base_seed + layer_idx)
-            if isinstance(layer, PipelineModule):
-                raise NotImplementedError("RECURSIVE BUILD NOT YET IMPLEMENTED")
-            elif isinstance(layer, nn.Module):
-                self.forward_funcs.append(layer)
-                self.add_module(str(layer_idx), layer)
-            elif isinstance(layer, TiedLayerSpec):
-                if layer.key not in self.tied_modules:
-                    self.tied_modules[layer.key] = layer.build()
-                    self.tied_weight_attrs[layer.key] = layer.tied_weight_attr
-                mod = self.tied_modules[layer.key]
-                self.forward_funcs.append(mod if layer.forward_fn is None else partial(layer.forward_fn, mod))
-            elif isinstance(layer, LayerSpec):
-                module = layer.build()
-                self.forward_funcs.append(module)
-                self.add_module(str(layer_idx), module)
-            else:
-                self.forward_funcs.append(layer)
-        # pipeline params are distinct per stage: "model parallel" for the norm reductions
+        self.tied_modules = nn.ModuleDict()
+        self.tied_weight_attrs: Dict[str, str] = {}
+        self._slots: List[_Slot] = [self._materialize(i) for i in range(self._local_start, self._local_stop)]
+        # a stage's parameters are its own: norms / overflow checks reduce over the pipe group
         for p in self.parameters():
             p.model_parallel = True
+        if torch.cuda.is_available():
+            self.to(f"cuda:{self.local_rank % max(1, torch.cuda.device_count())}")
+        self.tied_comms = self._make_tie_groups()
+        self._synchronize_tied_weights()
+        self.activation_checkpoint_interval = activation_checkpoint_interval
 
-    def _count_layer_params(self):
-        counts = [0] * len(self._layer_specs)
-        for idx, layer in enumerate(self._layer_specs):
-            if isinstance(layer, LayerSpec):
-                mod = layer.build()
-                counts[idx] = sum(p.numel() for p in mod.parameters() if p.requires_grad)
-                del mod
-            elif isinstance(layer, nn.Module):
-                counts[idx] = sum(p.numel() for p in layer.parameters() if p.requires_grad)
-        return counts
+    # ------------------------------------------------------------------ construction
+    def _seed(self, value):
+        (self.seed_fn or ds_utils.set_random_seed)(value)
 
-    def _find_layer_type(self, layername):
-        rx = re.compile(layername, re.IGNORECASE)
-        idxs = []
-        for idx, layer in enumerate(self._layer_specs):
-            if isinstance(layer, LayerSpec):
-                name = layer.typename.__name__
-            elif isinstance(layer, nn.Module):
-                name = layer.__class__.__name__
-            else:
-                name = getattr(layer, "__name__", None)
-                if name is None:
-                    continue
-            if rx.search(name):
-                idxs.append(idx)
-        if not idxs:
-            raise RuntimeError(f"Partitioning '{layername}' found no valid layers to partition.")
-        return idxs
+    def _materialize(self, idx) -> _Slot:
+        spec = self._layer_specs[idx]
+        if self.seed_layers:
+            self._seed(self.base_seed + idx)
+        if isinstance(spec, PipelineModule):
+            raise NotImplementedError("nested PipelineModule layers are not supported")
+        if isinstance(spec, TiedLayerSpec):
+            if spec.key not in self.tied_modules:
+                self.tied_modules[spec.key] = spec.build()
+                self.tied_weight_attrs[spec.key] = spec.tied_weight_attr
+            mod = self.tied_modules[spec.key]
+            fn = mod if spec.forward_fn is None else partial(spec.forward_fn, mod)
+            return _Slot(idx, fn, None, spec.key)
+        if isinstance(spec, LayerSpec):
+            spec = spec.build()
+        if isinstance(spec, nn.Module):
+            self.add_module(str(idx), spec)
+            return _Slot(idx, spec, spec)
+        return _Slot(idx, spec, None)  # plain callable (e.g. a lambda reshaping the activations)
+
+    @property
+    def forward_funcs(self) -> List[Callable]:
+        return [s.fn for s in self._slots]
+
+    def _make_tie_groups(self) -> Dict[str, _TieGroup]:
+        """One process group per (tie key, data-parallel / model-parallel coordinate) spanning
+        the stages that hold the key; every rank creates every group (collective)."""
+        out: Dict[str, _TieGroup] = {}
+        if self.num_stages == 1:
+            return out
+        keys = sorted({s.key for s in self._layer_specs if isinstance(s, TiedLayerSpec)})
+        g = self._grid
+        for key in keys:
+            stages = sorted({self.stage_owner(i) for i, s in enumerate(self._layer_specs)
+                             if isinstance(s, TiedLayerSpec) and s.key == key})
+            for dp in range(g.data_parallel_size):
+                for mp in range(g.model_parallel_size):
+                    coord = {"data": dp, "model": mp} if g.model_parallel_size > 1 else {"data": dp}
+                    ranks = [g.stage_to_global(stage_id=s, **coord) for s in stages]
+                    pg = dist.new_group(ranks=ranks)
+                    if self.global_rank not in ranks:
+                        continue
+                    out[key] = _TieGroup(ranks, pg, self.tied_weight_attrs[key], self.tied_modules[key])
+                    if self.global_rank != ranks[0]:
+                        # replicated copy: counted once (on the first stage) in grad norms
+                        for p in self.tied_modules[key].parameters():
+                            p.model_parallel = False
+        return out
+
+    def _synchronize_tied_weights(self):
+        for t in self.tied_comms.values():
+            dist.broadcast(getattr(t.module, t.weight_attr).data, src=min(t.ranks), group=t.group)
+
+    def allreduce_tied_weight_gradients(self):
+        for t in self.tied_comms.values():
+            w = getattr(t.module, t.weight_attr)
+            if w.grad is not None:
+                dist.all_reduce(w.grad, group=t.group)
+
+    # ------------------------------------------------------------------ forward
+    @property
+    def activation_checkpoint_interval(self):
+        return self._ckpt_interval
+
+    @activation_checkpoint_interval.setter
+    def activation_checkpoint_interval(self, interval):
+        if interval < 0:
+            raise ValueError("activation_checkpoint_interval must be >= 0")
+        self._ckpt_interval = int(interval)
+        self._segments = self._make_segments()
+
+    def set_checkpoint_interval(self, interval):
+        self.checkpoint_interval = interval
+        self.activation_checkpoint_interval = interval
+
+    def _make_segments(self) -> List[_Segment]:
+        n = len(self._slots)
+        k = self._ckpt_interval
+        if k == 0:
+            return [_Segment(0, n, False)] if n else []
+        return [_Segment(s, min(s + k, n), self._is_checkpointable(self.forward_funcs[s:min(s + k, n)]))
+                for s in range(0, n, k)]
+
+    def _is_checkpointable(self, funcs):
+        if self.checkpointable_layers is not None:
+            return all(type(f).__name__ in self.checkpointable_layers for f in funcs)
+        if type(self).__name__ == "GPT2ModelPipe":  # DeeperSpeed special case for GPT-NeoX
+            return all("ParallelTransformerLayerPipe" in type(f).__name__ for f in funcs)
+        return any(any(True for _ in f.parameters()) for f in funcs if isinstance(f, nn.Module))
+
+    def _run_range(self, seg: _Segment, micro: int, *inputs):
+        x = inputs[0] if len(inputs) == 1 else inputs
+        for slot in self._slots[seg.start:seg.stop]:
+            self.curr_layer = slot.index
+            if self.seed_layers:
+                self._seed(self.base_seed * micro + slot.index)
+            x = slot.fn(x)
+        return x
 
     def forward(self, forward_input):
         self.micro_offset += 1
-
-        def exec_range_func(start, end):
-            local_micro_offset = self.micro_offset + 1
-
-            def exec_func(*inputs):
-                if len(inputs) == 1:
-                    inputs = inputs[0]
-                for idx, layer in enumerate(self.forward_funcs[start:end]):
-                    self.curr_layer = idx + self._local_start
-                    if self.seed_layers:
-                        (self.seed_fn or ds_utils.set_random_seed)(self.base_seed * local_micro_offset +
-                                                                    self.curr_layer)
-                    inputs = layer(inputs)
-                return inputs
-
-            return exec_func
-
-        if self.activation_checkpoint_interval == 0:
-            return exec_range_func(0, len(self.forward_funcs))(forward_input)
+        micro = self.micro_offset + 1
         x = forward_input
-        n = len(self.forward_funcs)
-        for s in range(0, n, self.activation_checkpoint_interval):
-            e = min(s + self.activation_checkpoint_interval, n)
-            if not isinstance(x, tuple):
-                x = (x,)
-            if self._is_checkpointable(self.forward_funcs[s:e]):
-                x = self.activation_checkpoint_func(exec_range_func(s, e), *x)
+        for seg in self._segments:
+            args = x if isinstance(x, tuple) else (x,)
+            if seg.recompute:
+                x = self.activation_checkpoint_func(partial(self._run_range, seg, micro), *args)
             else:
-                x = exec_range_func(s, e)(*x)
+                x = self._run_range(seg, micro, *args)
         return x
 
-    def _partition_layers(self, method="uniform"):
-        num_stages = self._topo.get_dim("pipe")
-        stage_id = self._topo.get_coord(self.global_rank).pipe
-        method = method.lower()
-        if method == "uniform":
-            self.parts = ds_utils.partition_uniform(num_items=len(self._layer_specs), num_parts=num_stages)
-        elif method == "parameters":
-            self.parts = ds_utils.partition_balanced(weights=self._count_layer_params(), num_parts=num_stages)
-        elif method.startswith("type:"):
-            weights = [0] * len(self._layer_specs)
-            for idx in self._find_layer_type(method.split(":", 1)[1]):
-                weights[idx] = 1
-            self.parts = ds_utils.partition_balanced(weights=weights, num_parts=num_stages)
-        else:
-            raise NotImplementedError(f"Partitioning method {method} not implemented.")
-        if self.global_rank == 0:
-            for stage in range(num_stages):
-                start, stop = self.parts[stage], self.parts[stage + 1]
-                logger.info(f"stage={stage} layers={stop - start}")
-        self._set_bounds(start=self.parts[stage_id], stop=self.parts[stage_id + 1])
-
-    def allreduce_tied_weight_gradients(self):
-        for key, comm in self.tied_comms.items():
-            weight = getattr(self.tied_modules[key], comm["weight_attr"])
-            if weight.grad is not None:
-                dist.all_reduce(weight.grad, group=comm["group"])
-
-    def _synchronize_tied_weights(self):
-        for key, comm in self.tied_comms.items():
-            dist.broadcast(getattr(comm["module"], comm["weight_attr"]).data, src=min(comm["ranks"]),
-                           group=comm["group"])
-
-    def _index_tied_modules(self):
-        tied_comms = {}
-        if self._topo.get_dim("pipe") == 1:
-            return tied_comms
-        specs = self._layer_specs
-        for key in sorted(set(s.key for s in specs if isinstance(s, TiedLayerSpec))):
-            tied_layers = [i for i, s in enumerate(specs) if isinstance(s, TiedLayerSpec) and s.key == key]
-            tied_stages = sorted(set(self.stage_owner(i) for i in tied_layers))
-            for dp in range(self._grid.data_parallel_size):
-                for mp in range(self._grid.model_parallel_size):
-                    kw = dict(data=dp, model=mp) if self._grid.model_parallel_size > 1 else dict(data=dp)
-                    ranks = [self._grid.stage_to_global(stage_id=s, **kw) for s in tied_stages]
-                    group = dist.new_group(ranks=ranks)
-                    if self.global_rank in ranks:
-                        assert key in self.tied_modules
-                        tied_comms[key] = {"ranks": ranks, "group": group,
-                                           "weight_attr": self.tied_weight_attrs[key],
-                                           "module": self.tied_modules[key]}
-                        if self.global_rank != ranks[0]:
-                            for p in self.tied_modules[key].parameters():
-                                p.model_parallel = False
-        return tied_comms
-
+    # ------------------------------------------------------------------ topology queries
     def partitions(self):
         return self.parts
 
     def stage_owner(self, layer_idx):
-        assert 0 <= layer_idx < self._num_layers
-        for stage in range(self._topo.get_dim("pipe")):
-            if self.parts[stage] <= layer_idx < self.parts[stage + 1]:
-                return stage
+        if not 0 <= layer_idx < self._num_layers:
+            raise IndexError(f"layer {layer_idx} out of range [0, {self._num_layers})")
+        for s in range(self.num_stages):
+            if self.parts[s] <= layer_idx < self.parts[s + 1]:
+                return s
         raise RuntimeError(f"Layer {layer_idx} not owned? parts={self.parts}")
-
-    def _set_bounds(self, start=None, stop=None):
-        self._local_start = start
-        self._local_stop = stop
-
-    def set_checkpoint_interval(self, interval):
-        assert interval >= 0
-        self.checkpoint_interval = interval
-        self.activation_checkpoint_interval = interval
 
     def topology(self):
         return self._topo
@@ -276,46 +324,38 @@ class PipelineModule(nn.Module):
         return self._grid
 
     def num_pipeline_stages(self):
-        return self._topo.get_dim("pipe")
+        return self.num_stages
 
+    # ------------------------------------------------------------------ checkpoints
     def ckpt_prefix(self, checkpoints_path, tag):
-        rank_name = "module"
-        coord = self._grid._topo.get_coord(rank=self.global_rank)
-        for dim in [a for a in self._grid._topo.get_axis_names() if a != "data"]:
-            rank_name += f"-{dim}_{getattr(coord, dim):02d}"
-        return os.path.join(checkpoints_path, str(tag), rank_name)
+        coord = self._topo.get_coord(rank=self.global_rank)
+        parts = [f"{a}_{getattr(coord, a):02d}" for a in self._topo.get_axis_names() if a != "data"]
+        return os.path.join(checkpoints_path, str(tag), "-".join(["module"] + parts))
 
     def ckpt_layer_path(self, ckpt_dir, local_layer_idx):
-        idx = local_layer_idx + self._local_start
-        path = os.path.join(ckpt_dir, f"layer_{idx:02d}")
-        rank_repr = self._grid._topo.get_rank_repr(rank=self.global_rank)
-        if rank_repr != "":
-            path += f"-{rank_repr}"
-        return path + "-model_states.pt"
+        rank_repr = self._topo.get_rank_repr(rank=self.global_rank)
+        name = f"layer_{local_layer_idx + self._local_start:02d}" + (f"-{rank_repr}" if rank_repr else "")
+        return os.path.join(ckpt_dir, name + "-model_states.pt")
+
+    def _stateful(self):
+        for local, slot in enumerate(self._slots):
+            obj = slot.module if slot.module is not None else (
+                self.tied_modules[slot.tie_key] if slot.tie_key is not None else slot.fn)
+            if hasattr(obj, "state_dict") and hasattr(obj, "load_state_dict"):
+                yield local, obj
 
     def save_state_dict(self, save_dir):
         if self._grid.data_parallel_id != 0:
             return
         os.makedirs(save_dir, exist_ok=True)
-        for idx, layer in enumerate(self.forward_funcs):
-            if not hasattr(layer, "state_dict"):
-                continue
-            torch.save({k: (v.detach().cpu().clone() if torch.is_tensor(v) else v)
-                        for k, v in layer.state_dict().items()}, self.ckpt_layer_path(save_dir, idx))
+        for local, obj in self._stateful():
+            host = {k: v.detach().cpu().clone() if torch.is_tensor(v) else v for k, v in obj.state_dict().items()}
+            torch.save(host, self.ckpt_layer_path(save_dir, local))
 
     def load_state_dir(self, load_dir, strict=True):
-        for idx, layer in enumerate(self.forward_funcs):
-            if not hasattr(layer, "load_state_dict"):
-                continue
-            path = self.ckpt_layer_path(load_dir, idx)
-            layer.load_state_dict(torch.load(path, map_location="cpu", weights_only=True), strict=strict)
+        for local, obj in self._stateful():
+            path = self.ckpt_layer_path(load_dir, local)
+            obj.load_state_dict(torch.load(path, map_location="cpu", weights_only=True), strict=strict)
             if self._grid.data_parallel_id == 0:
-                logger.info(f"RANK={self.global_rank} Loaded layer={idx + self._local_start} file={path}")
+                logger.info(f"RANK={self.global_rank} Loaded layer={local + self._local_start} file={path}")
         self._synchronize_tied_weights()
-
-    def _is_checkpointable(self, funcs):
-        if self.checkpointable_layers is not None:
-            return all(f.__class__.__name__ in self.checkpointable_layers for f in funcs)
-        if self.__class__.__name__ == "GPT2ModelPipe":
-            return all("ParallelTransformerLayerPipe" in f.__class__.__name__ for f in funcs)
-        return any(len(list(f.parameters())) > 0 for f in funcs if isinstance(f, nn.Module))

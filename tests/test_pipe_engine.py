@@ -147,3 +147,38 @@ def _infer_body():
 
 def test_inference_batch_returns_logits_and_presents():
     run_distributed(_infer_body, 2)
+
+
+def _module_plan(out):
+    import torch.nn as nn
+    from deeperspeed_amd.runtime.pipe.module import LayerSpec, PipelineModule, _plan_stages
+
+    class Block(nn.Module):
+        def __init__(self, d):
+            super().__init__()
+            self.lin = nn.Linear(d, d)
+
+        def forward(self, x):
+            return self.lin(x)
+
+    specs = [LayerSpec(nn.Linear, 8, 64), LayerSpec(Block, 64), LayerSpec(Block, 64), LayerSpec(Block, 64),
+             LayerSpec(Block, 64), LayerSpec(nn.Linear, 64, 8)]
+    # type: balances the matching layers only; parameters balances trainable numel
+    assert _plan_stages(specs, 2, "type:block") == [0, 3, 6]
+    assert _plan_stages(specs, 2, "uniform") == [0, 3, 6]
+    p = _plan_stages(specs, 3, "parameters")
+    assert p[0] == 0 and p[-1] == 6 and len(p) == 4
+    m = PipelineModule(layers=specs, num_stages=1, partition_method="type:Block", activation_checkpoint_interval=2,
+                       checkpointable_layers=["Block"])
+    # segments of 2: [Linear, Block] not checkpointable, [Block, Block] yes, [Block, Linear] no
+    assert [(s.start, s.stop, s.recompute) for s in m._segments] == [(0, 2, False), (2, 4, True), (4, 6, False)]
+    x = torch.randn(3, 8, requires_grad=True)
+    y = m(x)
+    y.sum().backward()
+    assert y.shape == (3, 8) and x.grad is not None
+    m.set_checkpoint_interval(0)
+    assert [(s.start, s.stop, s.recompute) for s in m._segments] == [(0, 6, False)]
+
+
+def test_pipeline_module_partition_and_segments():
+    run_distributed(_module_plan, 1, None)
