@@ -1077,7 +1077,12 @@ class DeepSpeedEngine(Module):
         unpickling of a trusted file."""
         import argparse
         import pickle
-        safe = [argparse.Namespace, set, OrderedDict]
+        from .fp16.loss_scaler import DynamicLossScaler, LossScaler
+        # reference checkpoints pickle their loss-scaler object: the same attribute set as
+        # ours, reconstructed without running any code from the file
+        safe = [argparse.Namespace, set, OrderedDict,
+                (DynamicLossScaler, "deepspeed.runtime.fp16.loss_scaler.DynamicLossScaler"),
+                (LossScaler, "deepspeed.runtime.fp16.loss_scaler.LossScaler")]
         try:
             with torch.serialization.safe_globals(safe):
                 return torch.load(path, map_location=map_location, weights_only=True)

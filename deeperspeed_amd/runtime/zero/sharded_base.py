@@ -34,6 +34,7 @@ from ...utils.logging import logger
 from ..fp16.loss_scaler import DynamicLossScaler, LossScaler
 from . import compact_master as cm
 from .layout import FlatGroup, layout_signature, params_to_shard, shards_to_params
+from .ref_layout import LAYOUT_VERSION, is_reference_layout, merge_reference_shards
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
 
@@ -122,6 +123,8 @@ class ShardedOptimizerBase:
         """Split each inner param group into (dtype, model-parallel) flat groups."""
         from .layout import split_param_group
         out = []
+        # registration order of every param group (reference-layout checkpoint import)
+        self._orig_group_params = [list(pg["params"]) for pg in self.optimizer.param_groups]
         for gi, pg in enumerate(self.optimizer.param_groups):
             for si, (dt, mp, plist) in enumerate(split_param_group(pg["params"], _is_mp_param)):
                 out.append(FlatGroup(group_index=gi, sub_index=si, dtype=dt, model_parallel=mp, params=plist))
@@ -500,20 +503,29 @@ class ShardedOptimizerBase:
             "zero_stage": self._zero_stage(),
             "partition_count": self.dp_world,
             "layout": layout_signature(self.groups),
+            "dsa_layout_version": LAYOUT_VERSION,
             "fp32_groups_key": self._fp32_key(),
             self._fp32_key(): [self.master_fp32(g) for g in self.groups],
         }
         return sd
 
     def _fp32_key(self):
-        return "single_partition_of_fp32_groups"
+        # NOT the reference's key names (single_partition_of_fp32_groups / fp32_flat_groups):
+        # these shards are interleaved per bucket, and reference tools must fail on them
+        # rather than silently mis-read them (ref_layout.py)
+        return "dsa_flat_fp32_shards"
 
     def load_state_dict(self, state_dict_list, load_optimizer_states=True, load_from_fp32_weights=True):
         if isinstance(state_dict_list, dict):
             state_dict_list = [state_dict_list]
         sd0 = state_dict_list[0]
-        if "loss_scaler" in sd0 and isinstance(sd0["loss_scaler"], dict):
-            self.loss_scaler.load_state_dict(sd0["loss_scaler"])
+        ls = sd0.get("loss_scaler")
+        if isinstance(ls, dict):
+            self.loss_scaler.load_state_dict(ls)
+        elif ls is not None and hasattr(ls, "cur_scale"):  # reference checkpoints pickle the scaler object
+            self.loss_scaler.load_state_dict({k: getattr(ls, k) for k in
+                                              ("cur_scale", "cur_iter", "last_overflow_iter", "cur_hysteresis")
+                                              if hasattr(ls, k)})
         self.dynamic_loss_scale = sd0.get("dynamic_loss_scale", self.dynamic_loss_scale)
         self.overflow = sd0.get("overflow", False)
         key = sd0.get("fp32_groups_key", self._fp32_key())
@@ -521,7 +533,9 @@ class ShardedOptimizerBase:
         if sd0.get("zero_stage", 0) == 0:
             state_dict_list = state_dict_list[:1]  # unsharded: every rank saved the same full state
         same_layout = (len(state_dict_list) == lw and sd0.get("layout") == layout_signature(self.groups))
-        if same_layout:
+        if is_reference_layout(sd0):
+            masters, moments = self._import_reference_layout(state_dict_list)
+        elif same_layout:
             mine = state_dict_list[lr]
             masters = mine[key]
             moments = mine["base_optimizer_state"]
@@ -567,6 +581,29 @@ class ShardedOptimizerBase:
             st_new["step"] = step
             moments_state[gi] = st_new
         return masters, {"state": moments_state, "param_groups": old_base[0]["param_groups"]}
+
+    def _import_reference_layout(self, sds):
+        """Masters + moments of a reference (contiguous per-group) ZeRO checkpoint, re-partitioned
+        into this rank's shards of the current layout (any saved world size)."""
+        numels = [[p.ds_numel if hasattr(p, "ds_numel") else p.numel() for p in plist]
+                  for plist in self._orig_group_params]
+        ref_masters, ref_moments = merge_reference_shards(sds, numels)
+        _, my_rank = self._layout_world_rank()
+        masters, state = [], {}
+        for gi, g in enumerate(self.groups):
+            pos = {id(p): j for j, p in enumerate(self._orig_group_params[g.group_index])}
+            mine = [pos[id(p)] for p in g.params]
+            masters.append(params_to_shard({i: ref_masters[g.group_index][j] for i, j in enumerate(mine)}, g,
+                                           my_rank, torch.float32))
+            mom = ref_moments[g.group_index]
+            st = {"step": mom.get("step", 0)}
+            for k in ("exp_avg", "exp_avg_sq"):
+                if k in mom:
+                    st[k] = params_to_shard({i: mom[k][j] for i, j in enumerate(mine)}, g, my_rank, torch.float32)
+            state[gi] = st
+        logger.info(f"imported a reference-layout ZeRO-{sds[0].get('zero_stage')} checkpoint saved by "
+                    f"{len(sds)} ranks into {self._layout_world_rank()[0]} ranks")
+        return masters, {"state": state, "param_groups": []}
 
     def _load_moments(self, base_sd):
         # param groups hyper-params (lr etc.) restored; state tensors copied in place

@@ -756,9 +756,6 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def _zero_stage(self):
         return 3
 
-    def _fp32_key(self):
-        return "fp32_flat_groups"
-
     # ------------------------------------------------------------------ model state helpers
     def register_external_parameter(self, module, param):
         owner = self.unit_of(param)

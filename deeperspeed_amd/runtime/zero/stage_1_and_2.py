@@ -370,7 +370,7 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
         return (self.dp_world, self.dp_rank) if self.sharded else (1, 0)
 
     def _fp32_key(self):
-        return "single_partition_of_fp32_groups" if self.sharded else "fp32_groups_flat"
+        return super()._fp32_key() if self.sharded else "fp32_groups_flat"
 
 
 # reference class names
