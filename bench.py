@@ -45,10 +45,12 @@ def parse():
     p.add_argument("--grad-accum", type=int, default=None)
     p.add_argument("--seq", type=int, default=2048)
     p.add_argument("--zero", type=int, default=3)
-    p.add_argument("--offload", type=str, default="auto", choices=["auto", "none", "compact", "master", "all", "nvme"])
+    p.add_argument("--offload", type=str, default="auto", choices=["auto", "none", "compact", "master", "all", "nvme", "moments"],
+                   help="moments: Adam moments in pinned host memory, compact master + grads in HBM (6 B/param)")
     p.add_argument("--ckpt", type=str, default="auto", choices=["auto", "on", "off"],
                    help="activation checkpointing; auto = off when activations fit in HBM next to the shards")
     p.add_argument("--layers", type=int, default=None, help="override depth (memory experiments only)")
+    p.add_argument("--hidden", type=int, default=None, help="override width (peak-params runs; heads = hidden/128)")
     p.add_argument("--sparse", type=str, default=None,
                    help="block-sparse attention mode (bigbird|fixed|bslongformer|variable|local) - BASELINE config 5")
     p.add_argument("--block", type=int, default=64, help="sparse attention block size")
@@ -87,7 +89,7 @@ def plan_memory(cfg, mb, seq, world, offload, ckpt, ga=1):
     fused HIP cross-entropy) and allocator slack."""
     p = cfg.num_params()
     grad = 4 if (world > 1 and ga > 1) else 2
-    per_param = {"none": 14, "compact": 12, "master": 10, "all": 2, "nvme": 2}[offload] + grad
+    per_param = {"none": 14, "compact": 12, "master": 10, "all": 2, "nvme": 2, "moments": 4}[offload] + grad
     states = p * per_param / world
     sbh = seq * mb * cfg.hidden_size
     act_layer = 2 * sbh if ckpt else 34 * sbh
@@ -132,6 +134,8 @@ def main():
     native.hip_ops()  # fail loudly if the HIP extension is missing
 
     over = {"num_layers": args.layers} if args.layers else {}
+    if args.hidden:
+        over.update(hidden_size=args.hidden, num_heads=args.hidden // 128)
     if args.sparse:
         over["sparse_attention"] = {"mode": args.sparse, "block": args.block}
     cfg = get_config(args.model, max_seq_len=args.seq, checkpoint_activations=True, **over)
@@ -195,6 +199,9 @@ def main():
         zcfg["resident_grads"] = True
     if offload == "compact":
         zcfg["compact_master"] = True
+    elif offload == "moments":
+        zcfg["compact_master"] = True
+        zcfg["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": "moments"}
     elif offload == "nvme":
         zcfg["offload_optimizer"] = {"device": "nvme", "nvme_path": args.nvme_path, "pin_memory": True,
                                      "states": "all"}
@@ -335,8 +342,10 @@ def main():
     flops_tok = cfg.flops_per_token(args.seq, recompute=False)
     ms_step = elapsed / args.steps * 1000.0
     out = {
-        "metric": ("tokens/sec (node) GPT-NeoX-20B ZeRO-3" if args.model == "gpt-neox-20b" else
-                   f"tokens/sec {args.model}") + (f" block-sparse {args.sparse} seq{args.seq}" if args.sparse else ""),
+        "metric": ("tokens/sec (node) GPT-NeoX-20B ZeRO-3" if args.model == "gpt-neox-20b" and not (args.hidden or args.layers)
+                   else f"tokens/sec {args.model}" + (f" reshaped to {cfg.num_params() / 1e9:.1f}B (hidden {cfg.hidden_size},"
+                                                      f" {cfg.num_layers} layers)" if (args.hidden or args.layers) else ""))
+                  + (f" block-sparse {args.sparse} seq{args.seq}" if args.sparse else ""),
         "value": round(tps, 2),
         "unit": "tokens/s",
         "n_gpus": world,

@@ -57,8 +57,10 @@ _STAGING = _Staging()
 def cpu_adam_update_flat(master, grad, exp_avg, exp_avg_sq, group, step, grad_scale, adamw, out_device=None):
     """Update host fp32 `master` in place; optionally refresh a device low-precision copy."""
     b1, b2 = group["betas"]
-    if grad.dtype != torch.float32 or grad.device.type != "cpu":
-        grad = grad.to("cpu", torch.float32)
+    if grad.device.type != "cpu":
+        grad = grad.to("cpu")
+    if grad.dtype not in (torch.float32, torch.bfloat16):  # the kernel widens bf16 itself
+        grad = grad.float()
     out_host = None
     key = None
     if out_device is not None and out_device.device.type == "cuda":

@@ -609,9 +609,81 @@ std::vector<Tensor> flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Te
   return {dq, dk, dv};
 }
 
+// Block-sparse flash attention.  q,k,v [B, H, S, D] (S % 64 == 0); LUT tensors int32 on the
+// device (see flash_attn.hip): rowptr [Hl * S/64 + 1], cols / masks [nnz]; the transposed LUT
+// colptr / rows / masks_t for the backward.  `shift` = min(6, log2(layout block)).
+static void check_lut(const Tensor& ptr, const Tensor& idx, const Tensor& msk, int64_t Hl, int64_t ntiles,
+                      const char* what) {
+  check_dev(ptr, what); check_dev(idx, what); check_dev(msk, what);
+  TORCH_CHECK(ptr.scalar_type() == at::kInt && idx.scalar_type() == at::kInt && msk.scalar_type() == at::kInt &&
+                  ptr.is_contiguous() && idx.is_contiguous() && msk.is_contiguous(),
+              what, ": int32 contiguous LUT tensors");
+  TORCH_CHECK(ptr.numel() == Hl * ntiles + 1, what, ": pointer array must hold Hl * S/64 + 1 entries");
+  TORCH_CHECK(idx.numel() == msk.numel(), what, ": index / mask length mismatch");
+}
+
+std::vector<Tensor> sparse_flash_fwd(Tensor q, Tensor k, Tensor v, Tensor rowptr, Tensor cols, Tensor masks,
+                                     int64_t Hl, bool causal, double scale, int64_t shift, bool out_bshd) {
+  check_dev(q, "q"); check_dev(k, "k"); check_dev(v, "v");
+  TORCH_CHECK(q.dim() == 4 && q.sizes() == k.sizes() && q.sizes() == v.sizes(), "sparse_flash: q/k/v shape mismatch");
+  TORCH_CHECK(q.scalar_type() != at::kFloat && q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(),
+              "sparse_flash: 16-bit q/k/v of one dtype");
+  TORCH_CHECK(q.is_contiguous() && k.is_contiguous() && v.is_contiguous(), "sparse_flash: contiguous inputs");
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
+  TORCH_CHECK(dsa::flash_supported((int)D), "sparse_flash: head dim must be 64, 96 or 128");
+  TORCH_CHECK(S % 64 == 0 && S > 0, "sparse_flash: sequence length must be a multiple of 64");
+  TORCH_CHECK(Hl == 1 || Hl == H, "sparse_flash: layout heads must be 1 or H");
+  TORCH_CHECK(shift >= 0 && shift <= 6, "sparse_flash: shift in [0, 6]");
+  check_lut(rowptr, cols, masks, Hl, S / 64, "sparse_flash rowptr/cols/masks");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  Tensor o = out_bshd ? at::empty({B, S, H, D}, q.options()) : at::empty_like(q);
+  Tensor lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  dsa::launch_sparse_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                               rowptr.data_ptr<int>(), cols.data_ptr<int>(),
+                               reinterpret_cast<const uint32_t*>(masks.data_ptr<int>()), (int)(B * H), (int)H, (int)Hl,
+                               (int)S, (int)D, causal, (float)scale, (int)shift, dcode(q), cur_stream(),
+                               out_bshd ? (int)H : 0);
+  return {o, lse};
+}
+
+std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor rowptr,
+                                     Tensor cols, Tensor masks, Tensor colptr, Tensor rows, Tensor masks_t,
+                                     int64_t Hl, bool causal, double scale, int64_t shift, bool o_bshd) {
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
+  for (auto* t : {&q, &k, &v}) {
+    check_dev(*t, "sparse_flash_bwd");
+    TORCH_CHECK(t->sizes() == q.sizes() && t->scalar_type() == q.scalar_type() && t->is_contiguous(),
+                "sparse_flash_bwd: q/k/v must match");
+  }
+  const std::vector<int64_t> oshape = o_bshd ? std::vector<int64_t>{B, S, H, D} : std::vector<int64_t>{B, H, S, D};
+  for (auto* t : {&dout, &o}) {
+    check_dev(*t, "sparse_flash_bwd");
+    TORCH_CHECK(t->sizes() == at::IntArrayRef(oshape) && t->scalar_type() == q.scalar_type() && t->is_contiguous(),
+                "sparse_flash_bwd: dout/o must be contiguous in the forward's output layout");
+  }
+  TORCH_CHECK(dsa::flash_supported((int)D) && S % 64 == 0 && (Hl == 1 || Hl == H) && shift >= 0 && shift <= 6,
+              "sparse_flash_bwd: unsupported shape");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * S, "sparse_flash_bwd: lse");
+  check_lut(rowptr, cols, masks, Hl, S / 64, "sparse_flash_bwd rowptr/cols/masks");
+  check_lut(colptr, rows, masks_t, Hl, S / 64, "sparse_flash_bwd colptr/rows/masks_t");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  Tensor dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  Tensor delta = at::empty_like(lse);
+  dsa::launch_sparse_flash_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                               lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
+                               dv.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(),
+                               reinterpret_cast<const uint32_t*>(masks.data_ptr<int>()), colptr.data_ptr<int>(),
+                               rows.data_ptr<int>(), reinterpret_cast<const uint32_t*>(masks_t.data_ptr<int>()),
+                               (int)(B * H), (int)H, (int)Hl, (int)S, (int)D, causal, (float)scale, (int)shift,
+                               dcode(q), cur_stream(), o_bshd ? (int)H : 0);
+  return {dq, dk, dv};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("sparse_flash_fwd", &sparse_flash_fwd);
+  m.def("sparse_flash_bwd", &sparse_flash_bwd);
   m.def("onebit_worker_compress", &onebit_worker_compress);
   m.def("onebit_server_compress", &onebit_server_compress);
   m.def("onebit_unpack", &onebit_unpack);

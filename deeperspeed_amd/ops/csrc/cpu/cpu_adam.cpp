@@ -37,10 +37,23 @@ inline uint16_t f32_to_f16(float f) {
 }
 
 // ---------------------------------------------------------------- scalar tail / fallback
-inline void adam_scalar(float* p, const float* g, float* m, float* v, uint16_t* out, OutKind ok, int64_t i0,
+inline float bf16_to_f32(uint16_t b) {
+  uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+inline float load_g(const float* g, int64_t i) { return g[i]; }
+inline float load_g(const uint16_t* g, int64_t i) { return bf16_to_f32(g[i]); }
+
+// Gradients arrive as fp32 or as bf16 (the reduced HBM shard copied to host as is: half the
+// PCIe bytes of an fp32 copy; widened here, in registers).
+template <typename GT>
+inline void adam_scalar(float* p, const GT* g, float* m, float* v, uint16_t* out, OutKind ok, int64_t i0,
                         int64_t i1, const AdamHP& h) {
   for (int64_t i = i0; i < i1; ++i) {
-    float gr = g[i] * h.gscale;
+    float gr = load_g(g, i) * h.gscale;
     float w = p[i];
     if (!h.adamw && h.wd != 0.f) gr += h.wd * w;
     float mm = h.b1 * m[i] + (1.f - h.b1) * gr;
@@ -57,7 +70,16 @@ inline void adam_scalar(float* p, const float* g, float* m, float* v, uint16_t* 
 }
 
 // ---------------------------------------------------------------- AVX2 + FMA (8 lanes)
-__attribute__((target("avx2,fma,f16c"))) void adam_avx2(float* p, const float* g, float* m, float* v,
+__attribute__((target("avx2,fma,f16c"))) inline __m256 load8(const float* g, int64_t i) {
+  return _mm256_loadu_ps(g + i);
+}
+__attribute__((target("avx2,fma,f16c"))) inline __m256 load8(const uint16_t* g, int64_t i) {
+  __m256i w = _mm256_cvtepu16_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(g + i)));
+  return _mm256_castsi256_ps(_mm256_slli_epi32(w, 16));
+}
+
+template <typename GT>
+__attribute__((target("avx2,fma,f16c"))) void adam_avx2(float* p, const GT* g, float* m, float* v,
                                                         uint16_t* out, OutKind ok, int64_t i0, int64_t i1,
                                                         const AdamHP& h) {
   const __m256 b1 = _mm256_set1_ps(h.b1), b2 = _mm256_set1_ps(h.b2);
@@ -69,7 +91,7 @@ __attribute__((target("avx2,fma,f16c"))) void adam_avx2(float* p, const float* g
   int64_t i = i0;
   for (; i + 8 <= i1; i += 8) {
     __m256 w = _mm256_loadu_ps(p + i);
-    __m256 gr = _mm256_mul_ps(_mm256_loadu_ps(g + i), gs);
+    __m256 gr = _mm256_mul_ps(load8(g, i), gs);
     if (l2) gr = _mm256_fmadd_ps(wd, w, gr);
     __m256 mm = _mm256_fmadd_ps(b1, _mm256_loadu_ps(m + i), _mm256_mul_ps(ob1, gr));
     __m256 vv = _mm256_fmadd_ps(b2, _mm256_loadu_ps(v + i), _mm256_mul_ps(ob2, _mm256_mul_ps(gr, gr)));
@@ -94,7 +116,16 @@ __attribute__((target("avx2,fma,f16c"))) void adam_avx2(float* p, const float* g
 }
 
 // ---------------------------------------------------------------- AVX-512 (16 lanes)
-__attribute__((target("avx512f,avx512bw,avx512vl,fma,f16c"))) void adam_avx512(float* p, const float* g, float* m,
+__attribute__((target("avx512f,avx512bw,avx512vl,fma,f16c"))) inline __m512 load16(const float* g, int64_t i) {
+  return _mm512_loadu_ps(g + i);
+}
+__attribute__((target("avx512f,avx512bw,avx512vl,fma,f16c"))) inline __m512 load16(const uint16_t* g, int64_t i) {
+  __m512i w = _mm512_cvtepu16_epi32(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(g + i)));
+  return _mm512_castsi512_ps(_mm512_slli_epi32(w, 16));
+}
+
+template <typename GT>
+__attribute__((target("avx512f,avx512bw,avx512vl,fma,f16c"))) void adam_avx512(float* p, const GT* g, float* m,
                                                                                float* v, uint16_t* out, OutKind ok,
                                                                                int64_t i0, int64_t i1,
                                                                                const AdamHP& h) {
@@ -107,7 +138,7 @@ __attribute__((target("avx512f,avx512bw,avx512vl,fma,f16c"))) void adam_avx512(f
   int64_t i = i0;
   for (; i + 16 <= i1; i += 16) {
     __m512 w = _mm512_loadu_ps(p + i);
-    __m512 gr = _mm512_mul_ps(_mm512_loadu_ps(g + i), gs);
+    __m512 gr = _mm512_mul_ps(load16(g, i), gs);
     if (l2) gr = _mm512_fmadd_ps(wd, w, gr);
     __m512 mm = _mm512_fmadd_ps(b1, _mm512_loadu_ps(m + i), _mm512_mul_ps(ob1, gr));
     __m512 vv = _mm512_fmadd_ps(b2, _mm512_loadu_ps(v + i), _mm512_mul_ps(ob2, _mm512_mul_ps(gr, gr)));
@@ -149,7 +180,8 @@ Isa detect_isa() {
 
 constexpr int64_t kTile = 1 << 16;  // elements per OpenMP work item (256 KB of fp32)
 
-void adam_run(float* p, const float* g, float* m, float* v, uint16_t* out, OutKind ok, int64_t n, const AdamHP& h) {
+template <typename GT>
+void adam_run(float* p, const GT* g, float* m, float* v, uint16_t* out, OutKind ok, int64_t n, const AdamHP& h) {
   const Isa isa = detect_isa();
   const int64_t tiles = (n + kTile - 1) / kTile;
 #pragma omp parallel for schedule(static)
@@ -168,8 +200,9 @@ void cpu_adam_update(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, dou
                      double eps, double wd, int64_t step, bool bias_correction, double grad_scale, bool adamw,
                      c10::optional<at::Tensor> out) {
   TORCH_CHECK(!p.is_cuda() && !g.is_cuda() && !m.is_cuda() && !v.is_cuda(), "cpu_adam: host tensors required");
-  TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat &&
-                  v.scalar_type() == at::kFloat, "cpu_adam: fp32 tensors required");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "cpu_adam: fp32 master / moments required");
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "cpu_adam: fp32 or bf16 gradients");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "cpu_adam: contiguous");
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "cpu_adam: size mismatch");
@@ -186,7 +219,11 @@ void cpu_adam_update(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, dou
            bias_correction ? (float)(1.0 - std::pow(b2, (double)step)) : 1.f, (float)grad_scale, adamw};
   {
     pybind11::gil_scoped_release nogil;
-    adam_run(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), optr, ok, n, h);
+    if (g.scalar_type() == at::kBFloat16)
+      adam_run(p.data_ptr<float>(), reinterpret_cast<const uint16_t*>(g.data_ptr()), m.data_ptr<float>(),
+               v.data_ptr<float>(), optr, ok, n, h);
+    else
+      adam_run(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), optr, ok, n, h);
   }
 }
 

@@ -119,5 +119,15 @@ void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, floa
 void launch_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                       float* delta, void* dq, void* dk, void* dv, int BH, int S, int D, bool causal, float scale,
                       int dt, hipStream_t s, int onh = 0);
+// block-sparse flash attention (S % 64 == 0): LUTs per layout head (Hl = 1 or H), shift =
+// min(6, log2(layout block))
+void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
+                             const int* cols, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
+                             float scale, int shift, int dt, hipStream_t s, int onh = 0);
+void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
+                             const float* lse, float* delta, void* dq, void* dk, void* dv, const int* rowptr,
+                             const int* cols, const uint32_t* masks, const int* colptr, const int* rows,
+                             const uint32_t* masks_t, int BH, int H, int Hl, int S, int D, bool causal, float scale,
+                             int shift, int dt, hipStream_t s, int onh = 0);
 
 }  // namespace dsa

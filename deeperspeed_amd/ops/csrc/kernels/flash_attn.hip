@@ -905,6 +905,453 @@ template <int D> constexpr int fwd_lds() { return (2 * BN * (D + 8) + 4 * 16 * (
 template <int D> constexpr int dkdv_lds() { return (2 * BN * (D + 8)) * 2 + 2 * BN * 4 + 4 * 2 * 16 * (BN + 8) * 2; }
 template <int D> constexpr int dq_lds() { return (2 * BN * (D + 8) + 4 * 16 * (BN + 8)) * 2; }
 
+// ======================================================================== block-sparse (LUT-driven)
+// Flash attention restricted to the active blocks of a block-sparse layout (reference:
+// deepspeed/ops/sparse_attention matmul.py SDD/DSD + softmax.py, fused here into one pass per
+// query tile so the sparse score matrix is never written).  Granularity: 64-query x 64-key
+// tiles, 2 waves (32 queries or keys each) per workgroup.  The host builds, per layout head,
+//   fwd / dQ LUT : rowptr[nqt + 1], cols[e] = key tile, masks[e] = active layout sub-blocks
+//   dK / dV LUT  : colptr[nkt + 1], rows[e] = query tile, masks_t[e] (same bit convention)
+// For layout blocks smaller than 64 (16 / 32), a tile holds nsub x nsub sub-blocks; bit
+// (qsub << log2 nsub) + ksub of the mask says whether sub-block (qsub, ksub) is active, and
+// only tiles whose mask is not full are masked element-wise.  `shift` = log2(block) capped at
+// 6.  S must be a multiple of 64.  Causal masking (GPT) is applied on top of the layout.
+constexpr int STILE = 64;
+
+template <int D, int NT>
+__device__ __forceinline__ void stile_load(uint4 (&r)[8 * D / NT], const uint16_t* __restrict__ g, int r0, int S,
+                                           int ld = D) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int k = 0; k < 8 * D / NT; ++k) {
+    const int c = threadIdx.x + NT * k;
+    const int row = c / CH, ch = c - row * CH;
+    r[k] = (r0 + row < S) ? *reinterpret_cast<const uint4*>(g + (int64_t)(r0 + row) * ld + ch * 8)
+                          : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int D, int NT>
+__device__ __forceinline__ void stile_store(uint16_t* lds, const uint4 (&r)[8 * D / NT]) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int k = 0; k < 8 * D / NT; ++k) {
+    const int c = threadIdx.x + NT * k;
+    const int row = c / CH, ch = c - row * CH;
+    *reinterpret_cast<uint4*>(lds + row * (D + 8) + ch * 8) = r[k];
+  }
+}
+
+__device__ __forceinline__ uint32_t full_mask(int nsub_l2) {
+  const int bits = 1 << (2 * nsub_l2);
+  return bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
+}
+
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(128, 2) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                      const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
+                                                      float* __restrict__ LSE, const int* __restrict__ rowptr,
+                                                      const int* __restrict__ cols, const uint32_t* __restrict__ masks,
+                                                      int S, float scale, int onh, int H, int Hl, int shift) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int TS = STILE * (D + 8);
+  constexpr int NT = 128;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  const int nqt = S / STILE;
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int64_t bh = task / nqt;
+  const int qt = task - (int)bh * nqt;
+  const int lh = Hl == 1 ? 0 : (int)(bh % H);
+  const int e0 = rowptr[lh * nqt + qt], e1 = rowptr[lh * nqt + qt + 1];
+  const int qrow = 32 * w + c32;  // row inside the tile
+  const int myq = qt * STILE + qrow;
+  const int nsub_l2 = 6 - shift;
+  const uint32_t full = full_mask(nsub_l2);
+  const int qsub = qrow >> shift;
+  const uint16_t* Qb = Q + bh * (int64_t)S * D;
+  const uint16_t* Kb = K + bh * (int64_t)S * D;
+  const uint16_t* Vb = V + bh * (int64_t)S * D;
+
+  s16x8 qf[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) qf[ks] = *reinterpret_cast<const s16x8*>(Qb + (int64_t)myq * D + 16 * ks + 8 * h);
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const float sl2 = scale * 1.4426950408889634f;
+
+  uint4 kr[8 * D / NT], vr[8 * D / NT];
+  if (e0 < e1) {
+    stile_load<D, NT>(kr, Kb, cols[e0] * STILE, S);
+    stile_load<D, NT>(vr, Vb, cols[e0] * STILE, S);
+    stile_store<D, NT>(smem, kr);
+    stile_store<D, NT>(smem + TS, vr);
+  }
+  __syncthreads();
+  for (int e = e0; e < e1; ++e) {
+    const int it = e - e0;
+    const int j0 = cols[e] * STILE;
+    const uint32_t mask = masks[e];
+    const bool has_next = e + 1 < e1;
+    if (has_next) {
+      stile_load<D, NT>(kr, Kb, cols[e + 1] * STILE, S);
+      stile_load<D, NT>(vr, Vb, cols[e + 1] * STILE, S);
+    }
+    const uint16_t* Ks = smem + (it & 1) * 2 * TS;
+    const uint16_t* Vs = Ks + TS;
+    float sv[32];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks)
+        acc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), qf[ks], acc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[16 * t + r] = acc[r];
+    }
+    // wave-uniform: a partially active tile, or keys past this wave's first query
+    if (mask != full || (CAUSAL && j0 + STILE - 1 > qt * STILE + 32 * w)) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kc = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);  // key column inside the tile
+          const int bit = (qsub << nsub_l2) + (kc >> shift);
+          if (!((mask >> bit) & 1u) || (CAUSAL && j0 + kc > myq)) sv[16 * t + r] = -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) mx = fmaxf(mx, sv[i]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mt = mx * sl2;
+    if (__any(mt > m + LAZY_TH)) {
+      const float mn = fmaxf(m, mt);
+      const float alpha = fast_exp2(m - ((mn == -INFINITY) ? 0.f : mn));
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    }
+    const float mu = (m == -INFINITY) ? 0.f : m;
+    float ps = 0.f, ps1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; i += 2) {
+      sv[i] = fast_exp2(fmaf(sv[i], sl2, -mu));
+      sv[i + 1] = fast_exp2(fmaf(sv[i + 1], sl2, -mu));
+      ps += sv[i];
+      ps1 += sv[i + 1];
+    }
+    ps += ps1;
+    ps += __shfl_xor(ps, 32, 64);
+    l += ps;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const s16x8 pf = __is_same(T, bf16_t) ? pack8(sv, 8 * ks) : pack8_h(sv, 8 * ks);
+      const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const uint16_t* a0 = Vs + row1 * (D + 8) + 32 * dt + 16 * (g16 & 1) + 4 * pc;
+        const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * (D + 8)));
+        o[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, pf, o[dt]);
+      }
+    }
+    if (has_next) {
+      uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
+      stile_store<D, NT>(nxt, kr);
+      stile_store<D, NT>(nxt + TS, vr);
+    }
+    __syncthreads();
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh);
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      ushort4 v4;
+      v4.x = to16<T>(o[dt][4 * rb + 0] * inv);
+      v4.y = to16<T>(o[dt][4 * rb + 1] * inv);
+      v4.z = to16<T>(o[dt][4 * rb + 2] * inv);
+      v4.w = to16<T>(o[dt][4 * rb + 3] * inv);
+      *reinterpret_cast<ushort4*>(orow + 32 * dt + 8 * rb + 4 * h) = v4;
+    }
+  if (h == 0) LSE[bh * (int64_t)S + myq] = (l > 0.f) ? (m + log2f(l)) * 0.6931471805599453f : -INFINITY;
+}
+
+// dK / dV over the query tiles listed for this key tile (transposed LUT)
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(128, 2) sdkdv_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                       const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
+                                                       const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                       uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
+                                                       const int* __restrict__ colptr, const int* __restrict__ rows,
+                                                       const uint32_t* __restrict__ masks, int S, float scale, int onh,
+                                                       int H, int Hl, int shift) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int TS = STILE * (D + 8);
+  constexpr int NT = 128;
+  float* stats = reinterpret_cast<float*>(smem + 4 * TS);  // [2 stages][LSE 64 | DELTA 64]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  const int nkt = S / STILE;
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int64_t bh = task / nkt;
+  const int kt = task - (int)bh * nkt;
+  const int lh = Hl == 1 ? 0 : (int)(bh % H);
+  const int e0 = colptr[lh * nkt + kt], e1 = colptr[lh * nkt + kt + 1];
+  const int kcol = 32 * w + c32;
+  const int mykey = kt * STILE + kcol;
+  const int nsub_l2 = 6 - shift;
+  const uint32_t full = full_mask(nsub_l2);
+  const int ksub = kcol >> shift;
+  const int64_t base = bh * (int64_t)S * D;
+  const int64_t obase = o_base<D>(bh, S, onh);
+  const float sl2 = scale * 1.4426950408889634f;
+
+  s16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) {
+    kf[ks] = *reinterpret_cast<const s16x8*>(K + base + (int64_t)mykey * D + 16 * ks + 8 * h);
+    vf[ks] = *reinterpret_cast<const s16x8*>(V + base + (int64_t)mykey * D + 16 * ks + 8 * h);
+  }
+  f32x16 dk[D / 32], dv[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+
+  uint4 qr[8 * D / NT], orr[8 * D / NT];
+  float st_l = 0.f, st_d = 0.f;
+  auto load_tile = [&](int i0) {
+    stile_load<D, NT>(qr, Q + base, i0, S);
+    stile_load<D, NT>(orr, dO + obase, i0, S, o_ld<D>(onh));
+    if (threadIdx.x < STILE) {
+      st_l = LSE[bh * (int64_t)S + i0 + threadIdx.x] * 1.4426950408889634f;
+      st_d = DELTA[bh * (int64_t)S + i0 + threadIdx.x];
+    }
+  };
+  auto store_tile = [&](int stage) {
+    uint16_t* b = smem + stage * 2 * TS;
+    stile_store<D, NT>(b, qr);
+    stile_store<D, NT>(b + TS, orr);
+    if (threadIdx.x < STILE) {
+      stats[stage * 2 * STILE + threadIdx.x] = st_l;
+      stats[stage * 2 * STILE + STILE + threadIdx.x] = st_d;
+    }
+  };
+  if (e0 < e1) {
+    load_tile(rows[e0] * STILE);
+    store_tile(0);
+  }
+  __syncthreads();
+  for (int e = e0; e < e1; ++e) {
+    const int it = e - e0;
+    const int i0 = rows[e] * STILE;
+    const uint32_t mask = masks[e];
+    const bool has_next = e + 1 < e1;
+    if (has_next) load_tile(rows[e + 1] * STILE);
+    const uint16_t* Qs = smem + (it & 1) * 2 * TS;
+    const uint16_t* Os = Qs + TS;
+    const float* lse_s = stats + (it & 1) * 2 * STILE;
+    const float* del_s = lse_s + STILE;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), kf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), vf[ks], pacc);
+      }
+      float pv[16], dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+        pv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse_s[qi]));
+      }
+      if (mask != full || (CAUSAL && kt * STILE + 32 * w + 31 > i0 + 32 * t)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          const int bit = ((qi >> shift) << nsub_l2) + ksub;
+          if (!((mask >> bit) & 1u) || (CAUSAL && mykey > i0 + qi)) pv[r] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+        dsv[r] = pv[r] * (pacc[r] - del_s[qi]);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ks = 2 * t + kk;
+        const s16x8 pf = __is_same(T, bf16_t) ? pack8(pv, 8 * kk) : pack8_h(pv, 8 * kk);
+        const s16x8 sf = __is_same(T, bf16_t) ? pack8(dsv, 8 * kk) : pack8_h(dsv, 8 * kk);
+        const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
+          const s16x4 ox = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + row1 * (D + 8) + col));
+          const s16x4 oy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (row1 + 8) * (D + 8) + col));
+          dv[dt] = Mfma32<T>::run(s16x8{ox[0], ox[1], ox[2], ox[3], oy[0], oy[1], oy[2], oy[3]}, pf, dv[dt]);
+          const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + row1 * (D + 8) + col));
+          const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * (D + 8) + col));
+          dk[dt] = Mfma32<T>::run(s16x8{qx[0], qx[1], qx[2], qx[3], qy[0], qy[1], qy[2], qy[3]}, sf, dk[dt]);
+        }
+      }
+    }
+    if (has_next) store_tile((it + 1) & 1);
+    __syncthreads();
+  }
+  uint16_t* dkr = dK + base + (int64_t)mykey * D;
+  uint16_t* dvr = dV + base + (int64_t)mykey * D;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      ushort4 a4, b4;
+      a4.x = to16<T>(dk[dt][4 * rb + 0] * scale); a4.y = to16<T>(dk[dt][4 * rb + 1] * scale);
+      a4.z = to16<T>(dk[dt][4 * rb + 2] * scale); a4.w = to16<T>(dk[dt][4 * rb + 3] * scale);
+      b4.x = to16<T>(dv[dt][4 * rb + 0]); b4.y = to16<T>(dv[dt][4 * rb + 1]);
+      b4.z = to16<T>(dv[dt][4 * rb + 2]); b4.w = to16<T>(dv[dt][4 * rb + 3]);
+      *reinterpret_cast<ushort4*>(dkr + 32 * dt + 8 * rb + 4 * h) = a4;
+      *reinterpret_cast<ushort4*>(dvr + 32 * dt + 8 * rb + 4 * h) = b4;
+    }
+}
+
+// dQ over the key tiles listed for this query tile (forward LUT)
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(128, 2) sdq_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                     const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
+                                                     const float* __restrict__ LSE, const float* __restrict__ DELTA,
+                                                     uint16_t* __restrict__ dQ, const int* __restrict__ rowptr,
+                                                     const int* __restrict__ cols, const uint32_t* __restrict__ masks,
+                                                     int S, float scale, int onh, int H, int Hl, int shift) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int TS = STILE * (D + 8);
+  constexpr int NT = 128;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  const int nqt = S / STILE;
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int64_t bh = task / nqt;
+  const int qt = task - (int)bh * nqt;
+  const int lh = Hl == 1 ? 0 : (int)(bh % H);
+  const int e0 = rowptr[lh * nqt + qt], e1 = rowptr[lh * nqt + qt + 1];
+  const int qrow = 32 * w + c32;
+  const int myq = qt * STILE + qrow;
+  const int nsub_l2 = 6 - shift;
+  const uint32_t full = full_mask(nsub_l2);
+  const int qsub = qrow >> shift;
+  const int64_t base = bh * (int64_t)S * D;
+  const float sl2 = scale * 1.4426950408889634f;
+
+  s16x8 qf[D / 16], of[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) {
+    qf[ks] = *reinterpret_cast<const s16x8*>(Q + base + (int64_t)myq * D + 16 * ks + 8 * h);
+    of[ks] = *reinterpret_cast<const s16x8*>(dO + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh) + 16 * ks + 8 * h);
+  }
+  const float lse2 = LSE[bh * (int64_t)S + myq] * 1.4426950408889634f;
+  const float dl = DELTA[bh * (int64_t)S + myq];
+  f32x16 dq[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+
+  uint4 kr[8 * D / NT], vr[8 * D / NT];
+  if (e0 < e1) {
+    stile_load<D, NT>(kr, K + base, cols[e0] * STILE, S);
+    stile_load<D, NT>(vr, V + base, cols[e0] * STILE, S);
+    stile_store<D, NT>(smem, kr);
+    stile_store<D, NT>(smem + TS, vr);
+  }
+  __syncthreads();
+  for (int e = e0; e < e1; ++e) {
+    const int it = e - e0;
+    const int j0 = cols[e] * STILE;
+    const uint32_t mask = masks[e];
+    const bool has_next = e + 1 < e1;
+    if (has_next) {
+      stile_load<D, NT>(kr, K + base, cols[e + 1] * STILE, S);
+      stile_load<D, NT>(vr, V + base, cols[e + 1] * STILE, S);
+    }
+    const uint16_t* Ks = smem + (it & 1) * 2 * TS;
+    const uint16_t* Vs = Ks + TS;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        sacc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), qf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), of[ks], pacc);
+      }
+      float dsv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dsv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse2));
+      if (mask != full || (CAUSAL && j0 + 32 * t + 31 > qt * STILE + 32 * w)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kc = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          const int bit = (qsub << nsub_l2) + (kc >> shift);
+          if (!((mask >> bit) & 1u) || (CAUSAL && j0 + kc > myq)) dsv[r] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dsv[r] = dsv[r] * (pacc[r] - dl);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ks = 2 * t + kk;
+        const s16x8 sf = __is_same(T, bf16_t) ? pack8(dsv, 8 * kk) : pack8_h(dsv, 8 * kk);
+        const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
+#pragma unroll
+        for (int dt = 0; dt < D / 32; ++dt) {
+          const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
+          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * (D + 8) + col));
+          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * (D + 8) + col));
+          dq[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, sf, dq[dt]);
+        }
+      }
+    }
+    if (has_next) {
+      uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
+      stile_store<D, NT>(nxt, kr);
+      stile_store<D, NT>(nxt + TS, vr);
+    }
+    __syncthreads();
+  }
+  uint16_t* dqr = dQ + base + (int64_t)myq * D;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      ushort4 v4;
+      v4.x = to16<T>(dq[dt][4 * rb + 0] * scale); v4.y = to16<T>(dq[dt][4 * rb + 1] * scale);
+      v4.z = to16<T>(dq[dt][4 * rb + 2] * scale); v4.w = to16<T>(dq[dt][4 * rb + 3] * scale);
+      *reinterpret_cast<ushort4*>(dqr + 32 * dt + 8 * rb + 4 * h) = v4;
+    }
+}
+
+template <int D> constexpr int sfwd_lds() { return 2 * 2 * STILE * (D + 8) * 2; }
+template <int D> constexpr int sdkdv_lds() { return 2 * 2 * STILE * (D + 8) * 2 + 2 * 2 * STILE * 4; }
+
 }  // namespace fa
 
 #define FA_DISPATCH(dt, D, causal, ...)                                                              \
@@ -975,6 +1422,34 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
                          fa::dq_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                          (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale);
     });
+}
+
+void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
+                             const int* cols, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
+                             float scale, int shift, int dt, hipStream_t s, int onh) {
+  const unsigned grid = (unsigned)(BH * (S / fa::STILE));
+  FA_DISPATCH(dt, D, causal,
+    hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(), s,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
+                       masks, S, scale, onh, H, Hl, shift));
+}
+
+void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
+                             const float* lse, float* delta, void* dq, void* dk, void* dv, const int* rowptr,
+                             const int* cols, const uint32_t* masks, const int* colptr, const int* rows,
+                             const uint32_t* masks_t, int BH, int H, int Hl, int S, int D, bool causal, float scale,
+                             int shift, int dt, hipStream_t s, int onh) {
+  const int64_t nrows = (int64_t)BH * S;
+  const unsigned grid = (unsigned)(BH * (S / fa::STILE));
+  FA_DISPATCH(dt, D, causal,
+    hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((nrows * 8 + 255) / 256)), dim3(256), 0, s,
+                       (const uint16_t*)dout, (const uint16_t*)o, delta, nrows, S, onh);
+    hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC>), dim3(grid), dim3(128), fa::sdkdv_lds<DD>(), s,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                       (uint16_t*)dk, (uint16_t*)dv, colptr, rows, masks_t, S, scale, onh, H, Hl, shift);
+    hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(), s,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                       (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift));
 }
 
 }  // namespace dsa

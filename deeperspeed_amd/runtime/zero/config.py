@@ -60,7 +60,9 @@ _OFFLOAD_OPT_DEFAULTS = dict(device=None, nvme_path=None, buffer_count=4, pin_me
                              pipeline_write=False, fast_init=False,
                              # MI355X extension: "all" = fp32 master + Adam moments on host (reference
                              # ZeRO-Offload); "master" = only the fp32 master on host, moments stay in HBM
-                             # and the step streams the master through pinned buffers.
+                             # and the step streams the master through pinned buffers; "moments" = the
+                             # Adam moments on host, the master in HBM (compact: bf16 + int16 residual,
+                             # 6 B/param of HBM in all), the GPU step streams the moments.
                              states="all")
 
 

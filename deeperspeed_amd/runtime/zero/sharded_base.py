@@ -16,7 +16,9 @@ MI355X design:
 * Offload ("cpu"): `states="all"` keeps master+moments in pinned host memory and steps with
   the native AVX-512 CPU Adam; `states="master"` (MI355X extension for 288 GB HBM) keeps
   the moments in HBM and streams the fp32 master through pinned staging buffers with
-  H2D / kernel / D2H overlapped on separate HIP streams.
+  H2D / kernel / D2H overlapped on separate HIP streams; `states="moments"` is the mirror
+  image (moments on the host, master in HBM -- with compact_master only 6 B/param of HBM:
+  the largest model one GPU trains, bounded by host memory at 8 B/param).
 """
 
 from __future__ import annotations
@@ -37,6 +39,63 @@ from .layout import FlatGroup, layout_signature, params_to_shard, shards_to_para
 from .ref_layout import LAYOUT_VERSION, is_reference_layout, merge_reference_shards
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
+CPU_STEP_PIECE = int(16 * 1024 * 1024)  # elements per CPU-Adam piece of the pipelined offload step
+
+
+def _pipelined_offload() -> bool:
+    """DSA_OFFLOAD_PIPELINE=0 restores the serial D2H -> CPU Adam -> H2D offload step (A/B)."""
+    import os
+    return torch.cuda.is_available() and os.environ.get("DSA_OFFLOAD_PIPELINE", "1") != "0"
+
+
+class HostGradStream:
+    """Reduced gradient pieces streamed to pinned host memory ahead of the CPU optimizer
+    (reference: the async per-parameter D2H gradient copies of stage2.py:782-880).
+
+    `get(k)` returns piece k on the host; before that it has issued the device-to-host
+    copies of pieces k+1 .. k+depth on a dedicated HIP stream, so PCIe transfers of the next
+    pieces overlap the CPU Adam of this one (and the H2D of the previous one's parameters).
+    Gradients travel in their HBM dtype (bf16 shards: half the bytes of an fp32 copy); the
+    CPU kernel widens them.  Slots are reused round-robin per dtype: piece k+depth takes
+    the slot of a piece at least one position before k, which the CPU has finished."""
+
+    def __init__(self, pieces, stream, depth=2):
+        self.pieces = list(pieces)
+        self.stream = stream
+        self.depth = max(1, int(depth))
+        self.slot_of = []
+        seq, maxn = {}, {}
+        for t in self.pieces:
+            n = seq.get(t.dtype, 0)
+            self.slot_of.append(n % (self.depth + 1))
+            seq[t.dtype] = n + 1
+            maxn[t.dtype] = max(maxn.get(t.dtype, 0), t.numel())
+        self.slots = {dt: [torch.empty(n, dtype=dt, pin_memory=True) for _ in range(self.depth + 1)]
+                      for dt, n in maxn.items()}
+        self.ready = torch.cuda.Event()
+        self.ready.record()  # gradients are final on the compute stream
+        self.events = [None] * len(self.pieces)
+        self.issued = 0
+
+    def _issue(self, k):
+        src = self.pieces[k]
+        dst = self.slots[src.dtype][self.slot_of[k]][: src.numel()]
+        with torch.cuda.stream(self.stream):
+            if k == 0:
+                self.stream.wait_event(self.ready)
+            dst.copy_(src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.events[k] = (ev, dst)
+
+    def get(self, k):
+        while self.issued < min(len(self.pieces), k + self.depth + 1):
+            self._issue(self.issued)
+            self.issued += 1
+        ev, dst = self.events[k]
+        ev.synchronize()
+        self.events[k] = None
+        return dst
 
 
 def _is_mp_param(p):
@@ -135,9 +194,14 @@ class ShardedOptimizerBase:
         right device, rebind inner optimizer param groups to the masters."""
         host = self.offload is not None and self.offload.get("device") in ("cpu", "nvme")
         pin = bool(self.offload and self.offload.get("pin_memory", True)) and torch.cuda.is_available()
+        moments_only = self.offload is not None and self.offload_states == "moments"
+        if moments_only and (self.offload.get("device") != "cpu" or not self.fused or not torch.cuda.is_available()):
+            raise ValueError("offload_optimizer states='moments' needs device 'cpu', the fused Adam optimizer and a GPU")
+        host = host and not moments_only  # the master stays in HBM
         if self.compact_master:
-            if self.offload is not None or not self.fused:
-                raise ValueError("compact_master needs the fused Adam optimizer and no optimizer offload")
+            if (self.offload is not None and not moments_only) or not self.fused:
+                raise ValueError("compact_master needs the fused Adam optimizer and no optimizer offload "
+                                 "(or offload_optimizer states='moments')")
             for g in self.groups:
                 if g.dtype != torch.bfloat16 or g.shard_param is None:
                     raise ValueError("compact_master needs bf16 model parameters")
@@ -165,8 +229,8 @@ class ShardedOptimizerBase:
             for g in self.groups:
                 st = self.optimizer.state[g.master]
                 st["step"] = 0
-                on_host = host and self.offload_states == "all"
-                kw = dict(dtype=torch.float32, pin_memory=on_host and pin)
+                on_host = (host and self.offload_states == "all") or moments_only
+                kw = dict(dtype=torch.float32, pin_memory=on_host and (pin or moments_only))
                 if on_host:
                     st["exp_avg"] = torch.zeros(g.shard_numel, **kw)
                     st["exp_avg_sq"] = torch.zeros(g.shard_numel, **kw)
@@ -213,13 +277,20 @@ class ShardedOptimizerBase:
         from ...ops.adam.cpu_adam import cpu_adam_update_flat
         adamw = bool(getattr(self.optimizer, "adam_w_mode", getattr(self.optimizer, "adamw_mode", True)))
         keys = [(gi, bi) for gi, g in enumerate(self.groups) for bi in range(len(g.buckets))]
+        stream = None
+        if _pipelined_offload() and any(g.shard_grad.is_cuda for g in self.groups):
+            stream = HostGradStream([self.groups[gi].shard_grad[self.groups[gi].buckets[bi].shard_offset:
+                                                                 self.groups[gi].buckets[bi].shard_offset +
+                                                                 self.groups[gi].buckets[bi].chunk]
+                                     for gi, bi in keys], self._streams()[0])
+        order = {k: i for i, k in enumerate(keys)}
 
         def update(key, t):
             gi, bi = key
             g = self.groups[gi]
             b = g.buckets[bi]
             lo, hi = b.shard_offset, b.shard_offset + b.chunk
-            grad_host = g.shard_grad[lo:hi].to("cpu", dtype=torch.float32, non_blocking=False)
+            grad_host = stream.get(order[key]) if stream is not None else g.shard_grad[lo:hi]
             cpu_adam_update_flat(t["master"], grad_host, t["exp_avg"], t["exp_avg_sq"], self._inner_group(g),
                                  grp_steps[id(g)], grad_scale, adamw, out_device=self._bucket_out(g, b))
             self._after_bucket_update(g, b)
@@ -409,6 +480,8 @@ class ShardedOptimizerBase:
             return self._offload_nvme_step(grad_scale, grp_steps)
         if self.offload_states == "master" and torch.cuda.is_available():
             return self._offload_master_step(grad_scale, grp_steps)
+        if self.offload_states == "moments":
+            return self._offload_moments_step(grad_scale, grp_steps)
         return self._offload_all_step(grad_scale, grp_steps)
 
     def _offload_master_step(self, grad_scale, grp_steps):
@@ -457,19 +530,94 @@ class ShardedOptimizerBase:
         d2h.synchronize()
         del stages
 
-    def _offload_all_step(self, grad_scale, grp_steps):
-        """Reference ZeRO-Offload: master + moments on host, native CPU Adam."""
-        from ...ops.adam.cpu_adam import cpu_adam_update_flat
+    def _offload_moments_step(self, grad_scale, grp_steps):
+        """Adam moments in pinned host memory, master (compact or fp32) and gradients in HBM.
+        Per piece: H2D of m, v (stream A) -> fused Adam on the compute stream -> D2H of m, v
+        (stream B); three device staging slots keep both copy engines and the kernel busy."""
+        h2d, d2h = self._streams()
+        cur = torch.cuda.current_stream()
+        nbuf = 3
+        piece = min(OFFLOAD_SUBCHUNK // 2, max(b.chunk for g in self.groups for b in g.buckets))
+        stages = [(torch.empty(piece, dtype=torch.float32, device=self.device),
+                   torch.empty(piece, dtype=torch.float32, device=self.device)) for _ in range(nbuf)]
+        free_ev = [None] * nbuf
+        start = torch.cuda.Event()
+        start.record(cur)  # gradients are final
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+        k = 0
         for g in self.groups:
             grp = self._inner_group(g)
+            b1, b2 = grp["betas"]
             st = self.optimizer.state[g.master]
             for b in g.buckets:
-                lo, hi = b.shard_offset, b.shard_offset + b.chunk
-                grad_host = g.shard_grad[lo:hi].to("cpu", dtype=torch.float32, non_blocking=False)
-                out = self._bucket_out(g, b)
-                cpu_adam_update_flat(g.master[lo:hi], grad_host, st["exp_avg"][lo:hi], st["exp_avg_sq"][lo:hi], grp,
-                                     grp_steps[id(g)], grad_scale, bool(getattr(self.optimizer, "adam_w_mode", True)),
-                                     out_device=out)
+                out_full = self._bucket_out(g, b)
+                for s in range(0, b.chunk, piece):
+                    e = min(s + piece, b.chunk)
+                    lo, hi, n = b.shard_offset + s, b.shard_offset + e, e - s
+                    i = k % nbuf
+                    k += 1
+                    m_dev, v_dev = stages[i][0][:n], stages[i][1][:n]
+                    with torch.cuda.stream(h2d):
+                        h2d.wait_event(start)
+                        if free_ev[i] is not None:
+                            h2d.wait_event(free_ev[i])
+                        m_dev.copy_(st["exp_avg"][lo:hi], non_blocking=True)
+                        v_dev.copy_(st["exp_avg_sq"][lo:hi], non_blocking=True)
+                        ev_in = torch.cuda.Event()
+                        ev_in.record(h2d)
+                    cur.wait_event(ev_in)
+                    o = None if out_full is None else out_full[s:e]
+                    if self.compact_master:
+                        native.adam_compact_(o, g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, grp["lr"], b1, b2,
+                                             grp["eps"], grp["weight_decay"], grp_steps[id(g)],
+                                             grp.get("bias_correction", True), grad_scale, adamw)
+                    else:
+                        native.adam_flat_(g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, o, grp["lr"], b1, b2,
+                                          grp["eps"], grp["weight_decay"], grp_steps[id(g)],
+                                          grp.get("bias_correction", True), grad_scale, adamw)
+                    ev_done = torch.cuda.Event()
+                    ev_done.record(cur)
+                    with torch.cuda.stream(d2h):
+                        d2h.wait_event(ev_done)
+                        st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
+                        st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
+                        ev_free = torch.cuda.Event()
+                        ev_free.record(d2h)
+                    free_ev[i] = ev_free
+                self._after_bucket_update(g, b)
+        # host moments final before a checkpoint or the next step reads them; staging buffers
+        # are released only after the copies that use them
+        cur.wait_stream(d2h)
+        d2h.synchronize()
+        del stages
+
+    def _offload_all_step(self, grad_scale, grp_steps):
+        """Reference ZeRO-Offload: master + moments on host, native CPU Adam.  Pipelined over
+        pieces of at most CPU_STEP_PIECE elements: D2H of the next gradient pieces (copy
+        stream) and H2D of the previous piece's bf16 parameters (double-buffered pinned
+        staging) run while the CPU updates the current piece."""
+        from ...ops.adam.cpu_adam import cpu_adam_update_flat
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+        work = []  # (group, bucket, lo, hi, last piece of the bucket)
+        for g in self.groups:
+            for b in g.buckets:
+                lo0, hi0 = b.shard_offset, b.shard_offset + b.chunk
+                cuts = list(range(lo0, hi0, CPU_STEP_PIECE)) or [lo0]
+                for i, lo in enumerate(cuts):
+                    work.append((g, b, lo, min(lo + CPU_STEP_PIECE, hi0), i == len(cuts) - 1))
+        stream = None
+        if _pipelined_offload() and any(g.shard_grad.is_cuda for g in self.groups):
+            stream = HostGradStream([g.shard_grad[lo:hi] for g, _, lo, hi, _ in work], self._streams()[0])
+        bucket_out = None
+        for k, (g, b, lo, hi, last) in enumerate(work):
+            grad_host = stream.get(k) if stream is not None else g.shard_grad[lo:hi]
+            st = self.optimizer.state[g.master]
+            if lo == b.shard_offset:  # once per bucket (NVMe params: acquires one staging buffer)
+                bucket_out = self._bucket_out(g, b)
+            out = None if bucket_out is None else bucket_out[lo - b.shard_offset: hi - b.shard_offset]
+            cpu_adam_update_flat(g.master[lo:hi], grad_host, st["exp_avg"][lo:hi], st["exp_avg_sq"][lo:hi],
+                                 self._inner_group(g), grp_steps[id(g)], grad_scale, adamw, out_device=out)
+            if last:
                 self._after_bucket_update(g, b)
 
     # ------------------------------------------------------------------ grads

@@ -16,7 +16,7 @@ def _env():
     os.environ.setdefault("WORLD_SIZE", "1")
 
 
-def _run(stage, offload=None, steps=4, ga=2, offload_param=None):
+def _run(stage, offload=None, steps=4, ga=2, offload_param=None, compact=False):
     _env()
     import deeperspeed_amd as ds
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
@@ -29,6 +29,8 @@ def _run(stage, offload=None, steps=4, ga=2, offload_param=None):
         z["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": offload}
     if offload_param:
         z["offload_param"] = {"device": offload_param, "pin_memory": True, "nvme_path": "/tmp/dsa_pnvme"}
+    if compact:
+        z["compact_master"] = True
     conf = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": ga,
             "optimizer": {"type": "Adam", "params": {"lr": 3e-4}}, "fp16": {"enabled": True, "type": "bfloat16"},
             "fp32_allreduce": False, "gradient_clipping": 1.0, "zero_optimization": z}
@@ -53,11 +55,20 @@ def test_engine_loss_decreases(stage):
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize("offload", ["master", "all"])
+@pytest.mark.parametrize("offload", ["master", "all", "moments"])
 def test_engine_offload(offload):
     base = _run(3, None, steps=3, ga=1)
     off = _run(3, offload, steps=3, ga=1)
     assert abs(base[-1] - off[-1]) < 5e-2 * max(1.0, abs(base[-1]))
+
+
+@pytest.mark.parametrize("stage", [2, 3])
+def test_moments_offload_compact_matches_compact(stage):
+    """Moments on the host + compact master in HBM (6 B/param of HBM) steps exactly like the
+    all-in-HBM compact master: the streamed moments are bit-identical copies."""
+    base = _run(stage, None, steps=3, ga=2, compact=True)
+    off = _run(stage, "moments", steps=3, ga=2, compact=True)
+    assert base == off
 
 
 def _mr_body(out_dir, stage, compact, world):
