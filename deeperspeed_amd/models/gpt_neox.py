@@ -223,6 +223,8 @@ class NeoXAttention(nn.Module):
         q, k, v = rotary_split(qkv, cfg.num_heads, cfg.head_dim, cfg.rotary_dim, cfg.rotary_base, qscale=qs)
         if self._sparsity is not None:
             ctx = self._sparse_attention(q, k, v)
+            if ctx.shape[1] == S:  # fused kernel wrote the token-major [B, S, H, D] layout
+                return self.dense(ctx.reshape(B, S, H))
         else:
             if (self.stash_outputs and ds_ckpt.is_checkpoint_forward() and cfg.attention_dropout == 0.0
                     and native.has_flash_attention(q)):
@@ -249,13 +251,23 @@ class NeoXAttention(nn.Module):
             layout = self._sparsity.make_layout(S)
             random.setstate(state)
             blk = self._sparsity.block
+            from ..ops.sparse_attention.flash import SparseFlashLUT
+            try:  # fused LUT-walk kernel (ops/sparse_attention/flash.py); else SDD / softmax / DSD
+                lut = SparseFlashLUT(layout, blk, causal=True)
+            except ValueError:
+                lut = None
             self._sp_ops[S] = (MatMul(layout, blk, "sdd", trans_b=True), MatMul(layout, blk, "dsd"),
-                               Softmax(layout, blk))
+                               Softmax(layout, blk), lut)
         return self._sp_ops[S]
 
     def _sparse_attention(self, q, k, v):
-        """Block-sparse causal attention (q is pre-scaled): SDD -> causal sparse softmax -> DSD."""
-        sdd, dsd, softmax = self._sparse_ops(q.shape[2])
+        """Block-sparse causal attention (q is pre-scaled).  On the GPU one fused kernel walks the
+        layout's active tiles and returns [B, S, H, D]; otherwise SDD -> causal sparse softmax ->
+        DSD returns [B, H, S, D]."""
+        sdd, dsd, softmax, lut = self._sparse_ops(q.shape[2])
+        from ..ops.sparse_attention import flash as sflash
+        if self.cfg.attention_dropout == 0.0 and sflash.supported(q, lut):
+            return sflash.sparse_flash_attention(q, k, v, lut, 1.0, out_bshd=True)
         w = softmax(sdd(q, k), scale=1.0, causal=True)
         return dsd(w, v)
 

@@ -646,9 +646,12 @@ std::vector<Tensor> sparse_flash_fwd(Tensor q, Tensor k, Tensor v, Tensor rowptr
   return {o, lse};
 }
 
+// tasks int32 [Hl, ntask, 4] = (key tile or -1, entry begin, entry end, partial slot or -1) over
+// rows / masks_t (the transposed LUT); fin int32 [Hl, nfin, 4] = (key tile or -1, first slot, chunks, 0);
+// nslot = partial slots per (batch, head).
 std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor rowptr,
-                                     Tensor cols, Tensor masks, Tensor colptr, Tensor rows, Tensor masks_t,
-                                     int64_t Hl, bool causal, double scale, int64_t shift, bool o_bshd) {
+                                     Tensor cols, Tensor masks, Tensor rows, Tensor masks_t, Tensor tasks, Tensor fin,
+                                     int64_t nslot, int64_t Hl, bool causal, double scale, int64_t shift, bool o_bshd) {
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
   for (auto* t : {&q, &k, &v}) {
     check_dev(*t, "sparse_flash_bwd");
@@ -665,15 +668,24 @@ std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, 
               "sparse_flash_bwd: unsupported shape");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * S, "sparse_flash_bwd: lse");
   check_lut(rowptr, cols, masks, Hl, S / 64, "sparse_flash_bwd rowptr/cols/masks");
-  check_lut(colptr, rows, masks_t, Hl, S / 64, "sparse_flash_bwd colptr/rows/masks_t");
+  check_dev(rows, "rows"); check_dev(masks_t, "masks_t"); check_dev(tasks, "tasks"); check_dev(fin, "fin");
+  TORCH_CHECK(rows.scalar_type() == at::kInt && masks_t.scalar_type() == at::kInt && rows.numel() == masks_t.numel(),
+              "sparse_flash_bwd: transposed LUT");
+  TORCH_CHECK(tasks.scalar_type() == at::kInt && tasks.dim() == 3 && tasks.size(0) == Hl && tasks.size(2) == 4 &&
+                  tasks.is_contiguous(), "sparse_flash_bwd: tasks [Hl, ntask, 4]");
+  TORCH_CHECK(fin.scalar_type() == at::kInt && fin.dim() == 3 && fin.size(0) == Hl && fin.size(2) == 4 &&
+                  fin.is_contiguous(), "sparse_flash_bwd: fin [Hl, nfin, 4]");
+  const int64_t ntask = tasks.size(1), nfin = fin.size(1);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
   Tensor dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
   Tensor delta = at::empty_like(lse);
+  Tensor ws = at::empty({std::max<int64_t>(1, B * H * nslot * 2 * 64 * D)}, q.options().dtype(at::kFloat));
   dsa::launch_sparse_flash_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
                                lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
                                dv.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(),
-                               reinterpret_cast<const uint32_t*>(masks.data_ptr<int>()), colptr.data_ptr<int>(),
-                               rows.data_ptr<int>(), reinterpret_cast<const uint32_t*>(masks_t.data_ptr<int>()),
+                               reinterpret_cast<const uint32_t*>(masks.data_ptr<int>()), rows.data_ptr<int>(),
+                               reinterpret_cast<const uint32_t*>(masks_t.data_ptr<int>()), tasks.data_ptr<int>(),
+                               (int)ntask, fin.data_ptr<int>(), (int)nfin, ws.data_ptr<float>(), (int)nslot,
                                (int)(B * H), (int)H, (int)Hl, (int)S, (int)D, causal, (float)scale, (int)shift,
                                dcode(q), cur_stream(), o_bshd ? (int)H : 0);
   return {dq, dk, dv};

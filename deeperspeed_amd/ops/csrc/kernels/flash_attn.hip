@@ -947,8 +947,8 @@ __device__ __forceinline__ uint32_t full_mask(int nsub_l2) {
   return bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
 }
 
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(128, 2) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+template <typename T, int D, bool CAUSAL, bool RP>
+__global__ void __launch_bounds__(128, RP ? 2 : 3) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                       const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                       float* __restrict__ LSE, const int* __restrict__ rowptr,
                                                       const int* __restrict__ cols, const uint32_t* __restrict__ masks,
@@ -986,7 +986,7 @@ __global__ void __launch_bounds__(128, 2) sfwd_kernel(const uint16_t* __restrict
   const float sl2 = scale * 1.4426950408889634f;
 
   uint4 kr[8 * D / NT], vr[8 * D / NT];
-  if (e0 < e1) {
+  if (RP && e0 < e1) {
     stile_load<D, NT>(kr, Kb, cols[e0] * STILE, S);
     stile_load<D, NT>(vr, Vb, cols[e0] * STILE, S);
     stile_store<D, NT>(smem, kr);
@@ -998,11 +998,19 @@ __global__ void __launch_bounds__(128, 2) sfwd_kernel(const uint16_t* __restrict
     const int j0 = cols[e] * STILE;
     const uint32_t mask = masks[e];
     const bool has_next = e + 1 < e1;
-    if (has_next) {
+    if (RP && has_next) {
       stile_load<D, NT>(kr, Kb, cols[e + 1] * STILE, S);
       stile_load<D, NT>(vr, Vb, cols[e + 1] * STILE, S);
     }
-    const uint16_t* Ks = smem + (it & 1) * 2 * TS;
+    if (!RP) {  // single LDS stage: more workgroups per CU hide the load instead
+      stile_load<D, NT>(kr, Kb, j0, S);
+      stile_load<D, NT>(vr, Vb, j0, S);
+      if (it > 0) __syncthreads();
+      stile_store<D, NT>(smem, kr);
+      stile_store<D, NT>(smem + TS, vr);
+      __syncthreads();
+    }
+    const uint16_t* Ks = smem + (RP ? (it & 1) * 2 * TS : 0);
     const uint16_t* Vs = Ks + TS;
     float sv[32];
 #pragma unroll
@@ -1066,12 +1074,14 @@ __global__ void __launch_bounds__(128, 2) sfwd_kernel(const uint16_t* __restrict
         o[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, pf, o[dt]);
       }
     }
-    if (has_next) {
-      uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
-      stile_store<D, NT>(nxt, kr);
-      stile_store<D, NT>(nxt + TS, vr);
+    if (RP) {
+      if (has_next) {
+        uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
+        stile_store<D, NT>(nxt, kr);
+        stile_store<D, NT>(nxt + TS, vr);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   const float inv = l > 0.f ? 1.f / l : 0.f;
   uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh);
@@ -1090,27 +1100,32 @@ __global__ void __launch_bounds__(128, 2) sfwd_kernel(const uint16_t* __restrict
 }
 
 // dK / dV over the query tiles listed for this key tile (transposed LUT)
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(128, 2) sdkdv_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+template <typename T, int D, bool CAUSAL, bool RP>
+__global__ void __launch_bounds__(128, RP ? 2 : 3) sdkdv_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                        const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
                                                        const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                        uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
-                                                       const int* __restrict__ colptr, const int* __restrict__ rows,
-                                                       const uint32_t* __restrict__ masks, int S, float scale, int onh,
+                                                       const int* __restrict__ rows,
+                                                       const uint32_t* __restrict__ masks,
+                                                       const int4* __restrict__ tasks, int ntask,
+                                                       float* __restrict__ ws, int nslot, int S, float scale, int onh,
                                                        int H, int Hl, int shift) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = STILE * (D + 8);
   constexpr int NT = 128;
-  float* stats = reinterpret_cast<float*>(smem + 4 * TS);  // [2 stages][LSE 64 | DELTA 64]
+  float* stats = reinterpret_cast<float*>(smem + (RP ? 4 : 2) * TS);  // [stages][LSE 64 | DELTA 64]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
-  const int nkt = S / STILE;
+  // task = (key tile, entry range of its query-tile list, partial slot or -1): key tiles whose
+  // list is long (the global columns of BigBird / Longformer layouts) are split into chunks
+  // that write fp32 partials, summed by sdkdv_finish_kernel -- no single workgroup walks them all
   const int task = xcd_task(blockIdx.x, gridDim.x);
-  const int64_t bh = task / nkt;
-  const int kt = task - (int)bh * nkt;
+  const int64_t bh = task / ntask;
   const int lh = Hl == 1 ? 0 : (int)(bh % H);
-  const int e0 = colptr[lh * nkt + kt], e1 = colptr[lh * nkt + kt + 1];
+  const int4 tk = tasks[lh * ntask + (task - (int)bh * ntask)];
+  const int kt = tk.x, e0 = tk.y, e1 = tk.z, slot = tk.w;
+  if (kt < 0) return;  // padding task (whole workgroup, before any barrier)
   const int kcol = 32 * w + c32;
   const int mykey = kt * STILE + kcol;
   const int nsub_l2 = 6 - shift;
@@ -1151,7 +1166,7 @@ __global__ void __launch_bounds__(128, 2) sdkdv_kernel(const uint16_t* __restric
       stats[stage * 2 * STILE + STILE + threadIdx.x] = st_d;
     }
   };
-  if (e0 < e1) {
+  if (RP && e0 < e1) {
     load_tile(rows[e0] * STILE);
     store_tile(0);
   }
@@ -1161,10 +1176,16 @@ __global__ void __launch_bounds__(128, 2) sdkdv_kernel(const uint16_t* __restric
     const int i0 = rows[e] * STILE;
     const uint32_t mask = masks[e];
     const bool has_next = e + 1 < e1;
-    if (has_next) load_tile(rows[e + 1] * STILE);
-    const uint16_t* Qs = smem + (it & 1) * 2 * TS;
+    if (RP && has_next) load_tile(rows[e + 1] * STILE);
+    if (!RP) {
+      load_tile(i0);
+      if (it > 0) __syncthreads();
+      store_tile(0);
+      __syncthreads();
+    }
+    const uint16_t* Qs = smem + (RP ? (it & 1) * 2 * TS : 0);
     const uint16_t* Os = Qs + TS;
-    const float* lse_s = stats + (it & 1) * 2 * STILE;
+    const float* lse_s = stats + (RP ? (it & 1) * 2 * STILE : 0);
     const float* del_s = lse_s + STILE;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1213,8 +1234,25 @@ __global__ void __launch_bounds__(128, 2) sdkdv_kernel(const uint16_t* __restric
         }
       }
     }
-    if (has_next) store_tile((it + 1) & 1);
-    __syncthreads();
+    if (RP) {
+      if (has_next) store_tile((it + 1) & 1);
+      __syncthreads();
+    }
+  }
+  if (slot >= 0) {  // partial of a split key tile: fp32 [bh][slot][dK | dV][64][D]
+    float* pk = ws + ((bh * nslot + slot) * 2 * STILE + kcol) * (int64_t)D;
+    float* pv = pk + STILE * D;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int c = 32 * dt + 8 * rb + 4 * h;
+        *reinterpret_cast<float4*>(pk + c) = make_float4(dk[dt][4 * rb], dk[dt][4 * rb + 1], dk[dt][4 * rb + 2],
+                                                         dk[dt][4 * rb + 3]);
+        *reinterpret_cast<float4*>(pv + c) = make_float4(dv[dt][4 * rb], dv[dt][4 * rb + 1], dv[dt][4 * rb + 2],
+                                                         dv[dt][4 * rb + 3]);
+      }
+    return;
   }
   uint16_t* dkr = dK + base + (int64_t)mykey * D;
   uint16_t* dvr = dV + base + (int64_t)mykey * D;
@@ -1232,9 +1270,38 @@ __global__ void __launch_bounds__(128, 2) sdkdv_kernel(const uint16_t* __restric
     }
 }
 
+// Sum the fp32 partials of each split key tile and write its bf16/fp16 dK (scaled) and dV.
+// fin[lh][j] = (key tile, first slot, chunk count, -), padded with key tile -1.
+template <typename T, int D>
+__global__ void __launch_bounds__(256) sdkdv_finish_kernel(const float* __restrict__ ws, const int4* __restrict__ fin,
+                                                           int nfin, int nslot, uint16_t* __restrict__ dK,
+                                                           uint16_t* __restrict__ dV, int S, float scale, int H,
+                                                           int Hl) {
+  const int64_t bh = blockIdx.x / nfin;
+  const int lh = Hl == 1 ? 0 : (int)(bh % H);
+  const int4 f = fin[lh * nfin + (blockIdx.x - (int)bh * nfin)];
+  if (f.x < 0) return;
+  const int64_t base = bh * (int64_t)S * D;
+  for (int i = threadIdx.x; i < 2 * STILE * D / 4; i += blockDim.x) {  // float4 granules of dK | dV
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = 0; c < f.z; ++c) {
+      const float4 v = reinterpret_cast<const float4*>(ws + (bh * nslot + f.y + c) * 2 * STILE * (int64_t)D)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    const int e = 4 * i;
+    const bool is_k = e < STILE * D;
+    const int off = is_k ? e : e - STILE * D;
+    const float sc = is_k ? scale : 1.f;
+    ushort4 o4;
+    o4.x = to16<T>(acc.x * sc); o4.y = to16<T>(acc.y * sc); o4.z = to16<T>(acc.z * sc); o4.w = to16<T>(acc.w * sc);
+    uint16_t* dst = (is_k ? dK : dV) + base + (int64_t)f.x * STILE * D + off;
+    *reinterpret_cast<ushort4*>(dst) = o4;
+  }
+}
+
 // dQ over the key tiles listed for this query tile (forward LUT)
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(128, 2) sdq_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+template <typename T, int D, bool CAUSAL, bool RP>
+__global__ void __launch_bounds__(128, RP ? 2 : 3) sdq_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                      const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                      uint16_t* __restrict__ dQ, const int* __restrict__ rowptr,
@@ -1275,7 +1342,7 @@ __global__ void __launch_bounds__(128, 2) sdq_kernel(const uint16_t* __restrict_
     for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
 
   uint4 kr[8 * D / NT], vr[8 * D / NT];
-  if (e0 < e1) {
+  if (RP && e0 < e1) {
     stile_load<D, NT>(kr, K + base, cols[e0] * STILE, S);
     stile_load<D, NT>(vr, V + base, cols[e0] * STILE, S);
     stile_store<D, NT>(smem, kr);
@@ -1287,11 +1354,19 @@ __global__ void __launch_bounds__(128, 2) sdq_kernel(const uint16_t* __restrict_
     const int j0 = cols[e] * STILE;
     const uint32_t mask = masks[e];
     const bool has_next = e + 1 < e1;
-    if (has_next) {
+    if (RP && has_next) {
       stile_load<D, NT>(kr, K + base, cols[e + 1] * STILE, S);
       stile_load<D, NT>(vr, V + base, cols[e + 1] * STILE, S);
     }
-    const uint16_t* Ks = smem + (it & 1) * 2 * TS;
+    if (!RP) {
+      stile_load<D, NT>(kr, K + base, j0, S);
+      stile_load<D, NT>(vr, V + base, j0, S);
+      if (it > 0) __syncthreads();
+      stile_store<D, NT>(smem, kr);
+      stile_store<D, NT>(smem + TS, vr);
+      __syncthreads();
+    }
+    const uint16_t* Ks = smem + (RP ? (it & 1) * 2 * TS : 0);
     const uint16_t* Vs = Ks + TS;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1330,12 +1405,14 @@ __global__ void __launch_bounds__(128, 2) sdq_kernel(const uint16_t* __restrict_
         }
       }
     }
-    if (has_next) {
-      uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
-      stile_store<D, NT>(nxt, kr);
-      stile_store<D, NT>(nxt + TS, vr);
+    if (RP) {
+      if (has_next) {
+        uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
+        stile_store<D, NT>(nxt, kr);
+        stile_store<D, NT>(nxt + TS, vr);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   uint16_t* dqr = dQ + base + (int64_t)myq * D;
 #pragma unroll
@@ -1349,8 +1426,8 @@ __global__ void __launch_bounds__(128, 2) sdq_kernel(const uint16_t* __restrict_
     }
 }
 
-template <int D> constexpr int sfwd_lds() { return 2 * 2 * STILE * (D + 8) * 2; }
-template <int D> constexpr int sdkdv_lds() { return 2 * 2 * STILE * (D + 8) * 2 + 2 * 2 * STILE * 4; }
+template <int D> constexpr int sfwd_lds(bool rp) { return (rp ? 2 : 1) * 2 * STILE * (D + 8) * 2; }
+template <int D> constexpr int sdkdv_lds(bool rp) { return (rp ? 2 : 1) * (2 * STILE * (D + 8) * 2 + 2 * STILE * 4); }
 
 }  // namespace fa
 
@@ -1424,32 +1501,65 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     });
 }
 
+// DSA_SPARSE_FLASH_RP=1: register prefetch + double-buffered LDS (2 workgroups / CU);
+// default: one LDS stage, 3 workgroups / CU (the short per-row tile lists of block-sparse
+// layouts leave little to pipeline inside one workgroup)
+static bool sparse_rp() {
+  static const bool rp = getenv("DSA_SPARSE_FLASH_RP") && getenv("DSA_SPARSE_FLASH_RP")[0] == '1';
+  return rp;
+}
+
 void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
                              const int* cols, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
                              float scale, int shift, int dt, hipStream_t s, int onh) {
   const unsigned grid = (unsigned)(BH * (S / fa::STILE));
+  const bool rp = sparse_rp();
   FA_DISPATCH(dt, D, causal,
-    hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(), s,
-                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
-                       masks, S, scale, onh, H, Hl, shift));
+    if (rp)
+      hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
+                         masks, S, scale, onh, H, Hl, shift);
+    else
+      hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, false>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(false), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
+                         masks, S, scale, onh, H, Hl, shift));
 }
 
 void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
                              const float* lse, float* delta, void* dq, void* dk, void* dv, const int* rowptr,
-                             const int* cols, const uint32_t* masks, const int* colptr, const int* rows,
-                             const uint32_t* masks_t, int BH, int H, int Hl, int S, int D, bool causal, float scale,
-                             int shift, int dt, hipStream_t s, int onh) {
+                             const int* cols, const uint32_t* masks, const int* rows, const uint32_t* masks_t,
+                             const int* tasks, int ntask, const int* fin, int nfin, float* ws, int nslot, int BH,
+                             int H, int Hl, int S, int D, bool causal, float scale, int shift, int dt, hipStream_t s,
+                             int onh) {
   const int64_t nrows = (int64_t)BH * S;
   const unsigned grid = (unsigned)(BH * (S / fa::STILE));
+  const unsigned tgrid = (unsigned)(BH * ntask);
+  const bool rp = sparse_rp();
+  const int4* tk = reinterpret_cast<const int4*>(tasks);
   FA_DISPATCH(dt, D, causal,
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((nrows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const uint16_t*)dout, (const uint16_t*)o, delta, nrows, S, onh);
-    hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC>), dim3(grid), dim3(128), fa::sdkdv_lds<DD>(), s,
-                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                       (uint16_t*)dk, (uint16_t*)dv, colptr, rows, masks_t, S, scale, onh, H, Hl, shift);
-    hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(), s,
-                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                       (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift));
+    if (rp) {
+      hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, true>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
+                         shift);
+      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift);
+    } else {
+      hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, false>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(false), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
+                         shift);
+      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, false>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(false), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift);
+    }
+    if (nfin > 0)
+      hipLaunchKernelGGL((fa::sdkdv_finish_kernel<T, DD>), dim3((unsigned)(BH * nfin)), dim3(256), 0, s, ws,
+                         reinterpret_cast<const int4*>(fin), nfin, nslot, (uint16_t*)dk, (uint16_t*)dv, S, scale, H,
+                         Hl));
 }
 
 }  // namespace dsa

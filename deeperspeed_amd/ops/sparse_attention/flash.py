@@ -59,7 +59,45 @@ class SparseFlashLUT:
         self.density = float(act.sum()) / act.size
         self.tiles = int(act.sum())
         self._host = self._csr(act, masks) + self._csr(act.transpose(0, 2, 1), masks.transpose(0, 2, 1))
+        self._host += self._split_tasks(self._host[3], nt)
+        self.nslot = self._nslot
         self._dev: Dict[torch.device, tuple] = {}
+
+    # query tiles per dK / dV workgroup: longer key-tile lists (global columns) are split into
+    # chunks whose fp32 partials are summed by a finish kernel
+    CHUNK = 8
+
+    def _split_tasks(self, colptr, nt):
+        per_head, fins, slots = [], [], []
+        for h in range(self.heads):
+            heavy, light, fin, nslot = [], [], [], 0
+            for kt in range(nt):
+                e0, e1 = int(colptr[h * nt + kt]), int(colptr[h * nt + kt + 1])
+                if e1 - e0 <= self.CHUNK:
+                    if e1 > e0:
+                        light.append((kt, e0, e1, -1))
+                    continue
+                n = -(-(e1 - e0) // self.CHUNK)
+                fin.append((kt, nslot, n, 0))
+                for c in range(n):
+                    heavy.append((kt, e0 + c * self.CHUNK, min(e1, e0 + (c + 1) * self.CHUNK), nslot + c))
+                nslot += n
+            per_head.append(heavy + light)  # split (long) tiles launch first
+            fins.append(fin)
+            slots.append(nslot)
+        ntask = max(1, max(len(t) for t in per_head))
+        nfin = max(len(f) for f in fins)
+        tasks = np.full((self.heads, ntask, 4), -1, dtype=np.int32)
+        fin = np.full((self.heads, max(1, nfin), 4), -1, dtype=np.int32)
+        for h in range(self.heads):
+            if per_head[h]:
+                tasks[h, :len(per_head[h])] = per_head[h]
+            if fins[h]:
+                fin[h, :len(fins[h])] = fins[h]
+        self._nslot = max(slots) if slots else 0
+        if nfin == 0:
+            fin = fin[:, :0]
+        return (tasks, fin)
 
     @staticmethod
     def _csr(act, masks):
@@ -75,7 +113,7 @@ class SparseFlashLUT:
     def device_tensors(self, device):
         t = self._dev.get(device)
         if t is None:
-            t = tuple(torch.from_numpy(a).to(device) for a in self._host)
+            t = tuple(torch.from_numpy(np.ascontiguousarray(a)).to(device) for a in self._host)
             self._dev[device] = t
         return t
 
@@ -87,7 +125,8 @@ def supported(q: torch.Tensor, lut: Optional[SparseFlashLUT]) -> bool:
     if D not in (64, 96, 128) or S != lut.seq or (lut.heads not in (1, H)):
         return False
     from .. import native
-    return native.has_hip()
+    native.hip_ops()  # fails loudly when the extension is missing on a GPU box
+    return True
 
 
 class _SparseFlash(torch.autograd.Function):
@@ -95,7 +134,7 @@ class _SparseFlash(torch.autograd.Function):
     def forward(ctx, q, k, v, lut, scale, out_bshd):
         from .. import native
         ops = native.hip_ops()
-        rp, cols, masks, cp, rows, masks_t = lut.device_tensors(q.device)
+        rp, cols, masks = lut.device_tensors(q.device)[:3]
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         o, lse = ops.sparse_flash_fwd(q, k, v, rp, cols, masks, lut.heads, lut.causal, float(scale), lut.shift,
                                       bool(out_bshd))
@@ -108,10 +147,10 @@ class _SparseFlash(torch.autograd.Function):
         from .. import native
         q, k, v, o, lse = ctx.saved_tensors
         lut = ctx.lut
-        rp, cols, masks, cp, rows, masks_t = lut.device_tensors(q.device)
-        dq, dk, dv = native.hip_ops().sparse_flash_bwd(do.contiguous(), q, k, v, o, lse, rp, cols, masks, cp, rows,
-                                                       masks_t, lut.heads, lut.causal, ctx.scale, lut.shift,
-                                                       ctx.out_bshd)
+        rp, cols, masks, _cp, rows, masks_t, tasks, fin = lut.device_tensors(q.device)
+        dq, dk, dv = native.hip_ops().sparse_flash_bwd(do.contiguous(), q, k, v, o, lse, rp, cols, masks, rows,
+                                                       masks_t, tasks, fin, lut.nslot, lut.heads, lut.causal,
+                                                       ctx.scale, lut.shift, ctx.out_bshd)
         return dq, dk, dv, None, None, None
 
 

@@ -10,6 +10,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from . import flash
 from .matmul import MatMul
 from .softmax import Softmax
 from .sparsity_config import SparsityConfig
@@ -48,6 +49,17 @@ class SparseSelfAttention(nn.Module):
                            MatMul(layout, block, "dsd", trans_a=False, trans_b=False), Softmax(layout, block))
         return self.ops[L]
 
+    def get_lut(self, L):
+        """LUT of the fused kernel for sequence length L (None when the layout is outside its
+        domain: block not in 16/32/64/128 or L not a multiple of 64)."""
+        luts = self.__dict__.setdefault("_luts", {})
+        if L not in luts:
+            try:
+                luts[L] = flash.SparseFlashLUT(self.get_layout(L), self.sparsity_config.block)
+            except ValueError:
+                luts[L] = None
+        return luts[L]
+
     def transpose_key_for_scores(self, x, L):
         bsz, num_heads, seq_len, head_dim = x.size()
         if seq_len != L:
@@ -74,8 +86,12 @@ class SparseSelfAttention(nn.Module):
                 key_padding_mask = key_padding_mask.unsqueeze(0)
         if attn_mask is not None:
             attn_mask = self.transpose_mask_for_sparse(query.dtype, attn_mask)
-        sdd_nt, dsd_nn, softmax = self.get_ops(num_heads, tgt_len)
         scaling = float(head_dim) ** -0.5
+        if rpe is None and key_padding_mask is None and attn_mask is None:
+            lut = self.get_lut(tgt_len)
+            if flash.supported(query, lut):  # one fused kernel per query tile (ops/sparse_attention/flash.py)
+                return flash.sparse_flash_attention(query, key, value, lut, scaling)
+        sdd_nt, dsd_nn, softmax = self.get_ops(num_heads, tgt_len)
         w = sdd_nt(query, key)
         w = softmax(w, scale=scaling, rpe=rpe, key_padding_mask=key_padding_mask, attn_mask=attn_mask,
                     key_padding_mask_mode=self.key_padding_mask_mode, attn_mask_mode=self.attn_mask_mode)
