@@ -53,7 +53,8 @@ def _ext_specs() -> Dict[str, dict]:
     return {
         "_hip_ops": dict(
             kind="hip",
-            sources=[os.path.join(CSRC, "bindings.cpp")] + sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))),
+            sources=[os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "gemm_lt.cpp")] +
+            sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))),
             headers=sorted(glob.glob(os.path.join(CSRC, "include", "*.h"))),
         ),
         "_cpu_ops": dict(
@@ -108,7 +109,7 @@ def _link_cmd(kind: str, objs: List[str], out: str) -> List[str]:
     libs = [f"-L{tlib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python"]
     if kind == "hip":
         return [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + \
-            ["-o", out] + libs + ["-lc10_hip", "-ltorch_hip", f"-Wl,-rpath,{tlib}"]
+            ["-o", out] + libs + ["-lc10_hip", "-ltorch_hip", "-lhipblaslt", f"-Wl,-rpath,{tlib}"]
     return ["g++", "-shared", "-fPIC", "-fopenmp"] + objs + ["-o", out] + libs + \
         [f"-L{os.path.join(ROCM, 'lib')}", "-lamdhip64", f"-Wl,-rpath,{tlib}", "-lpthread"]
 

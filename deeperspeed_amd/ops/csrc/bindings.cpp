@@ -693,7 +693,10 @@ std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, 
 
 }  // namespace
 
+void register_gemm_lt(pybind11::module& m);  // gemm_lt.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  register_gemm_lt(m);
   m.def("sparse_flash_fwd", &sparse_flash_fwd);
   m.def("sparse_flash_bwd", &sparse_flash_bwd);
   m.def("onebit_worker_compress", &onebit_worker_compress);

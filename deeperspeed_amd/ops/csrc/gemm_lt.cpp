@@ -1,0 +1,275 @@
+// hipBLASLt GEMMs with fused epilogues for the transformer MLP / residual projections
+// (module `_hip_ops`).
+//
+// Reference counterparts: the cuBLAS GEMMs of csrc/transformer (cublas_wrappers.cu:3-90,
+// feed_forward.h:26-93) followed by separate bias+GeLU (gelu_kernels.cu:94), GeLU-backward
+// (gelu_kernels.cu:176) and bias+residual kernels (normalize_kernels.cu:16, general_kernels.cu:89).
+// On gfx950 hipBLASLt applies these in the GEMM epilogue, so the activation never makes an
+// extra HBM round trip:
+//   linear_lt      Y = X W^T (+ b) (+ R)              epilogue BIAS, C = R with beta = 1
+//                  Y = gelu(X W^T + b)                  epilogue GELU_BIAS (tanh GeLU)
+//                  Y = gelu(.), AUX = X W^T + b         epilogue GELU_AUX_BIAS (where the build has it)
+//   dgrad_dgelu_lt dP = (dY W) * gelu'(AUX), db = sum_rows(dP)   epilogue DGELU_BGRAD
+// Row-major tensors are passed as their column-major transposes: Y^T[N,M] = W[N,K] . X^T[K,M]
+// ("TN"), so the bias runs along D's rows as hipBLASLt requires.  Per (shape, epilogue) the
+// top heuristic algorithms are timed once on the first call and the fastest is cached.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+namespace {
+
+#define LT_CHECK(x)                                                                               \
+  do {                                                                                            \
+    hipblasStatus_t _s = (x);                                                                     \
+    TORCH_CHECK(_s == HIPBLAS_STATUS_SUCCESS, "hipBLASLt call failed (", (int)_s, "): " #x);      \
+  } while (0)
+
+constexpr size_t kWorkspace = 64ull << 20;
+
+struct Ctx {
+  hipblasLtHandle_t handle = nullptr;
+  at::Tensor workspace;
+};
+
+Ctx& ctx_for(int device) {
+  static std::mutex mu;
+  static std::map<int, Ctx> ctxs;
+  std::lock_guard<std::mutex> g(mu);
+  Ctx& c = ctxs[device];
+  if (!c.handle) {
+    LT_CHECK(hipblasLtCreate(&c.handle));
+    c.workspace = at::empty({(int64_t)kWorkspace}, at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device));
+  }
+  return c;
+}
+
+hipDataType dtype_of(const at::Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return HIP_R_16BF;
+  if (t.scalar_type() == at::kHalf) return HIP_R_16F;
+  if (t.scalar_type() == at::kFloat) return HIP_R_32F;
+  TORCH_CHECK(false, "gemm_lt: unsupported dtype ", t.scalar_type());
+}
+
+// One column-major GEMM D[m,n] = epi(op(A)[m,k] . op(B)[k,n] + beta C) with descriptors.
+struct Gemm {
+  hipblasOperation_t ta, tb;
+  int64_t m, n, k, lda, ldb, ldd;
+  hipDataType ab_type, d_type;
+  hipblasLtEpilogue_t epi;
+  const void* A;
+  const void* B;
+  const void* C;  // nullptr -> beta = 0
+  void* D;
+  const void* bias;  // BIAS pointer (input) or bias-grad output for BGRAD
+  hipDataType bias_type;
+  void* aux;
+  int64_t ld_aux;
+};
+
+using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int, bool>;
+
+struct Algo {
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws;
+};
+
+std::map<Key, Algo>& algo_cache() {
+  static std::map<Key, Algo> c;
+  return c;
+}
+
+void run(const Gemm& g, int device, hipStream_t stream) {
+  Ctx& c = ctx_for(device);
+  hipblasLtMatmulDesc_t op;
+  LT_CHECK(hipblasLtMatmulDescCreate(&op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_TRANSA, &g.ta, sizeof(g.ta)));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_TRANSB, &g.tb, sizeof(g.tb)));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &g.epi, sizeof(g.epi)));
+  if (g.bias) {
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &g.bias, sizeof(void*)));
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &g.bias_type,
+                                             sizeof(g.bias_type)));
+  }
+  if (g.aux) {
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &g.aux, sizeof(void*)));
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &g.ld_aux, sizeof(int64_t)));
+    const hipDataType at = g.d_type;
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &at, sizeof(at)));
+  }
+  hipblasLtMatrixLayout_t la, lb, ld;
+  const int64_t ar = g.ta == HIPBLAS_OP_N ? g.m : g.k, ac = g.ta == HIPBLAS_OP_N ? g.k : g.m;
+  const int64_t br = g.tb == HIPBLAS_OP_N ? g.k : g.n, bc = g.tb == HIPBLAS_OP_N ? g.n : g.k;
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&la, g.ab_type, ar, ac, g.lda));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&lb, g.ab_type, br, bc, g.ldb));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&ld, g.d_type, g.m, g.n, g.ldd));
+  const float alpha = 1.f, beta = g.C ? 1.f : 0.f;
+  const Key key{device, (int)g.epi, g.m, g.n, g.k, (int)g.ta, (int)g.tb, (int)g.ab_type, g.C != nullptr};
+  auto& cache = algo_cache();
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    hipblasLtMatmulPreference_t pref;
+    LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+    uint64_t wsz = kWorkspace;
+    LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz)));
+    hipblasLtMatmulHeuristicResult_t res[8];
+    int nres = 0;
+    LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(c.handle, op, la, lb, ld, ld, pref, 8, res, &nres));
+    hipblasLtMatmulPreferenceDestroy(pref);
+    TORCH_CHECK(nres > 0, "gemm_lt: hipBLASLt has no algorithm for this GEMM / epilogue");
+    // time the candidates once (each 3 launches after one warm-up); the output buffers are
+    // scratch until the real launch below overwrites them
+    int best = 0;
+    if (nres > 1) {
+      hipEvent_t e0, e1;
+      hipEventCreate(&e0);
+      hipEventCreate(&e1);
+      float best_ms = 1e30f;
+      for (int i = 0; i < nres; ++i) {
+        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
+        if (hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, g.C ? g.C : g.D, ld, g.D, ld, &res[i].algo,
+                            c.workspace.data_ptr(), kWorkspace, stream) != HIPBLAS_STATUS_SUCCESS)
+          continue;
+        hipEventRecord(e0, stream);
+        for (int r = 0; r < 3; ++r)
+          hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, g.C ? g.C : g.D, ld, g.D, ld, &res[i].algo,
+                          c.workspace.data_ptr(), kWorkspace, stream);
+        hipEventRecord(e1, stream);
+        hipEventSynchronize(e1);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best_ms) {
+          best_ms = ms;
+          best = i;
+        }
+      }
+      hipEventDestroy(e0);
+      hipEventDestroy(e1);
+    }
+    it = cache.emplace(key, Algo{res[best].algo, res[best].workspaceSize}).first;
+  }
+  LT_CHECK(hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, g.C ? g.C : g.D, ld, g.D, ld,
+                           &it->second.algo, c.workspace.data_ptr(), kWorkspace, stream));
+  hipblasLtMatrixLayoutDestroy(la);
+  hipblasLtMatrixLayoutDestroy(lb);
+  hipblasLtMatrixLayoutDestroy(ld);
+  hipblasLtMatmulDescDestroy(op);
+}
+
+void check2d(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.is_contiguous(), "gemm_lt: ", what, " must be a contiguous 2-D device tensor");
+}
+
+}  // namespace
+
+// Y[M,N] = X[M,K] W[N,K]^T (+ bias[N]) (+ residual[M,N]); with gelu_aux: Y = gelu(.), aux_out = pre-act.
+at::Tensor linear_lt(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> residual,
+                     bool gelu, c10::optional<at::Tensor> aux_out) {
+  check2d(x, "x");
+  check2d(w, "w");
+  TORCH_CHECK(x.scalar_type() == w.scalar_type() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "linear_lt: bf16/fp16 x and w of one dtype");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "linear_lt: x [M,K] . w[N,K]^T shape mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor y = at::empty({M, N}, x.options());
+  Gemm g{HIPBLAS_OP_T, HIPBLAS_OP_N, N, M, K, K, K, N, dtype_of(x), dtype_of(y), HIPBLASLT_EPILOGUE_DEFAULT,
+         w.data_ptr(), x.data_ptr(), nullptr, y.data_ptr(), nullptr, dtype_of(x), nullptr, 0};
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->is_cuda() && bias->numel() == N && bias->is_contiguous() && bias->scalar_type() == x.scalar_type(),
+                "linear_lt: bias [N] of the input dtype");
+    g.bias = bias->data_ptr();
+    g.epi = HIPBLASLT_EPILOGUE_BIAS;
+  }
+  if (residual.has_value()) {
+    check2d(*residual, "residual");
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N && residual->scalar_type() == x.scalar_type(),
+                "linear_lt: residual [M,N]");
+    g.C = residual->data_ptr();
+  }
+  if (gelu) {
+    TORCH_CHECK(bias.has_value() && !residual.has_value(), "linear_lt: gelu needs bias (and no residual)");
+    g.epi = HIPBLASLT_EPILOGUE_GELU_BIAS;
+    if (aux_out.has_value()) {  // pre-activation for a later backward (GELU_AUX_BIAS: not in every build)
+      check2d(*aux_out, "aux_out");
+      TORCH_CHECK(aux_out->size(0) == M && aux_out->size(1) == N && aux_out->scalar_type() == x.scalar_type(),
+                  "linear_lt: aux_out [M,N]");
+      g.epi = HIPBLASLT_EPILOGUE_GELU_AUX_BIAS;
+      g.aux = aux_out->data_ptr();
+      g.ld_aux = N;
+    }
+  }
+  run(g, x.get_device(), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  return y;
+}
+
+// dP[M,I] = (dY[M,N] W[N,I]) * gelu'(aux[M,I]); bias_grad[I] = sum over M of dP (written, not accumulated).
+at::Tensor dgrad_dgelu_lt(at::Tensor dy, at::Tensor w, at::Tensor aux, at::Tensor bias_grad) {
+  check2d(dy, "dy");
+  check2d(w, "w");
+  check2d(aux, "aux");
+  const int64_t M = dy.size(0), N = dy.size(1), I = w.size(1);
+  TORCH_CHECK(w.size(0) == N && aux.size(0) == M && aux.size(1) == I, "dgrad_dgelu_lt: shape mismatch");
+  TORCH_CHECK(dy.scalar_type() == w.scalar_type() && aux.scalar_type() == dy.scalar_type(), "dgrad_dgelu_lt: dtypes");
+  TORCH_CHECK(bias_grad.is_cuda() && bias_grad.numel() == I && bias_grad.is_contiguous() &&
+                  bias_grad.scalar_type() == dy.scalar_type(), "dgrad_dgelu_lt: bias_grad [I] of the input dtype");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  at::Tensor dp = at::empty({M, I}, dy.options());
+  // dP^T[I,M] = W^T[I,N] . dY^T[N,M]: W row-major [N,I] is column-major [I,N] (ld I), no transpose
+  Gemm g{HIPBLAS_OP_N, HIPBLAS_OP_N, I, M, N, I, N, I, dtype_of(dy), dtype_of(dp), HIPBLASLT_EPILOGUE_DGELU_BGRAD,
+         w.data_ptr(), dy.data_ptr(), nullptr, dp.data_ptr(), bias_grad.data_ptr(), dtype_of(bias_grad),
+         aux.data_ptr(), I};
+  run(g, dy.get_device(), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  return dp;
+}
+
+// Number of heuristic algorithms hipBLASLt offers for a bf16 TN GEMM [m,n,k] with epilogue
+// code `epi` (diagnostics: epilogue availability differs between hipBLASLt builds).
+int64_t lt_algo_count(int64_t m, int64_t n, int64_t k, int64_t epi, bool with_aux) {
+  Ctx& c = ctx_for(0);
+  hipblasLtMatmulDesc_t op;
+  LT_CHECK(hipblasLtMatmulDescCreate(&op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+  const hipblasLtEpilogue_t e = (hipblasLtEpilogue_t)epi;
+  hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e));
+  const hipDataType bt = HIP_R_16BF;
+  void* dummy = c.workspace.data_ptr();
+  hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &dummy, sizeof(void*));
+  hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  if (with_aux) {
+    hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &dummy, sizeof(void*));
+    hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &m, sizeof(int64_t));
+    hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &bt, sizeof(bt));
+  }
+  hipblasLtMatrixLayout_t la, lb, ld;
+  hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, k, m, k);
+  hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, k, n, k);
+  hipblasLtMatrixLayoutCreate(&ld, HIP_R_16BF, m, n, m);
+  hipblasLtMatmulPreference_t pref;
+  hipblasLtMatmulPreferenceCreate(&pref);
+  uint64_t wsz = kWorkspace;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz));
+  hipblasLtMatmulHeuristicResult_t res[8];
+  int nres = 0;
+  hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(c.handle, op, la, lb, ld, ld, pref, 8, res, &nres);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  hipblasLtMatrixLayoutDestroy(la);
+  hipblasLtMatrixLayoutDestroy(lb);
+  hipblasLtMatrixLayoutDestroy(ld);
+  hipblasLtMatmulDescDestroy(op);
+  return st == HIPBLAS_STATUS_SUCCESS ? nres : -(int64_t)st;
+}
+
+void register_gemm_lt(pybind11::module& m) {
+  m.def("lt_algo_count", &lt_algo_count);
+  m.def("linear_lt", &linear_lt);
+  m.def("dgrad_dgelu_lt", &dgrad_dgelu_lt);
+}

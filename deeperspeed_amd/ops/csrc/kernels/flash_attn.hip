@@ -1501,11 +1501,11 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     });
 }
 
-// DSA_SPARSE_FLASH_RP=1: register prefetch + double-buffered LDS (2 workgroups / CU);
-// default: one LDS stage, 3 workgroups / CU (the short per-row tile lists of block-sparse
-// layouts leave little to pipeline inside one workgroup)
+// default: register prefetch + double-buffered LDS (2 workgroups / CU, measured faster);
+// DSA_SPARSE_FLASH_RP=0: one LDS stage, 3 workgroups / CU (the short per-row tile lists of
+// block-sparse layouts leave little to pipeline inside one workgroup)
 static bool sparse_rp() {
-  static const bool rp = getenv("DSA_SPARSE_FLASH_RP") && getenv("DSA_SPARSE_FLASH_RP")[0] == '1';
+  static const bool rp = !(getenv("DSA_SPARSE_FLASH_RP") && getenv("DSA_SPARSE_FLASH_RP")[0] == '0');
   return rp;
 }
 
