@@ -84,6 +84,50 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tenso
     return _LayerNormFn.apply(x, weight, bias, eps)
 
 
+class _InvertibleLayerNormFn(torch.autograd.Function):
+    """LayerNorm that keeps only its OUTPUT for backward (reference `normalize_invertible`,
+    csrc/transformer/normalize_kernels.cu invertible variants): x_hat = (y - beta) / gamma is
+    recovered from y, so the layer input is not stored -- when y is saved anyway by the next
+    GEMM, one [tokens, hidden] activation per LayerNorm less is held until backward.  The
+    backward is the regular fused LN backward on x_hat (mean 0, rstd 1) scaled by the saved
+    per-row rstd.  Needs gamma != 0 (as the reference)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        x = x.contiguous()
+        if x.is_cuda:
+            y, mean, rstd, _ = hip_ops().ln_fwd(x, gamma, beta, eps, None, None)
+        else:
+            y, mean, rstd = _ln_ref(x, gamma, beta, eps)
+        ctx.save_for_backward(y, gamma, beta if beta is not None else gamma.new_zeros(gamma.shape), rstd)
+        ctx.has_beta = beta is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, gamma, beta, rstd = ctx.saved_tensors
+        H = y.shape[-1]
+        xhat = ((y.float() - beta.float()) / gamma.float()).to(y.dtype).reshape(-1, H)
+        rows = xhat.shape[0]
+        zero = torch.zeros(rows, dtype=torch.float32, device=y.device)
+        one = torch.ones(rows, dtype=torch.float32, device=y.device)
+        dyc = dy.contiguous().reshape(-1, H)
+        if y.is_cuda:
+            dx, dg, db = hip_ops().ln_bwd(dyc, xhat, gamma, zero, one, ctx.has_beta, None)
+        else:
+            xf, g = xhat.float(), dyc.float()
+            gw = g * gamma.float()
+            dx = (gw - gw.mean(-1, keepdim=True) - xf * (gw * xf).mean(-1, keepdim=True)).to(dy.dtype)
+            dg = (g * xf).sum(0).to(gamma.dtype)
+            db = g.sum(0).to(gamma.dtype) if ctx.has_beta else None
+        dx = (dx.float() * rstd.reshape(-1, 1).float()).to(dy.dtype).reshape(dy.shape)
+        return dx, dg, (db if ctx.has_beta else None), None
+
+
+def layer_norm_invertible(x, weight, bias, eps: float = 1e-5):
+    return _InvertibleLayerNormFn.apply(x, weight, bias, eps)
+
+
 class FusedLayerNorm(torch.nn.Module):
     """LayerNorm on the HIP kernel (wave64 row reductions, fp32 statistics)."""
 
@@ -463,6 +507,49 @@ def dropout(x, p, training=True, generator=None):
     if not training or p <= 0:
         return x
     return _DropoutFn.apply(x, float(p), _draw_seed(generator))
+
+
+class _DropoutMatmulFn(torch.autograd.Function):
+    """out = dropout(probs) @ v without storing the dropped probabilities (reference
+    `attn_dropout_checkpoint`, ds_transformer_cuda.cpp:185-193): backward re-applies the saved
+    1-byte mask to the saved probs, so one [B, heads, S, S] activation per layer is not held."""
+
+    @staticmethod
+    def forward(ctx, probs, v, p, seed):
+        if probs.is_cuda:
+            pd, mask = hip_ops().dropout_fwd(probs.contiguous(), p, seed, 0)
+        else:
+            g = torch.Generator().manual_seed(seed)
+            mask = (torch.rand(probs.shape, generator=g) >= p).to(torch.uint8)
+            pd = (probs.float() * mask / (1 - p)).to(probs.dtype)
+        v = v.contiguous()  # a view of a fused qkv buffer would keep all of it alive
+        out = torch.matmul(pd, v)
+        ctx.save_for_backward(probs, mask, v)
+        ctx.p = p
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        probs, mask, v = ctx.saved_tensors
+        p = ctx.p
+        if probs.is_cuda:  # mask * probs / (1 - p): the dropout-backward kernel applied to probs
+            pd = hip_ops().dropout_bwd(probs.contiguous(), mask, p)
+        else:
+            pd = (probs.float() * mask / (1 - p)).to(probs.dtype)
+        dv = torch.matmul(pd.transpose(-1, -2), dout)
+        dpd = torch.matmul(dout, v.transpose(-1, -2))
+        if dpd.is_cuda:
+            dprobs = hip_ops().dropout_bwd(dpd.contiguous(), mask, p)
+        else:
+            dprobs = (dpd.float() * mask / (1 - p)).to(dpd.dtype)
+        return dprobs, dv, None, None
+
+
+def dropout_matmul(probs, v, p, training=True, generator=None):
+    """dropout(probs, p) @ v, recomputing the dropped probabilities in backward."""
+    if not training or p <= 0:
+        return torch.matmul(probs, v)
+    return _DropoutMatmulFn.apply(probs, v, float(p), _draw_seed(generator))
 
 
 class _BiasDropoutResidualFn(torch.autograd.Function):

@@ -8,10 +8,14 @@ post-LN, tanh GeLU, additive attention mask [B,1,1,S], attention-prob and hidden
 Built from the framework's HIP kernels + hipBLASLt GEMMs instead of one monolithic C++
 layer: fused LayerNorm, bias+tanh-GeLU, row softmax with a broadcast additive mask, Philox
 dropout, and bias+dropout+residual fusion, composed under autograd (so ZeRO-3 hooks,
-activation checkpointing and mixed precision work unchanged).  Memory flags:
-`gelu_checkpoint` is inherent (the GeLU kernel keeps only its input), `attn_dropout_checkpoint`
-stores the 1-byte dropout mask instead of the dropped probabilities, `normalize_invertible` and
-`stochastic_mode` are accepted for config compatibility (deterministic kernels either way).
+activation checkpointing and mixed precision work unchanged).  Memory flags (reference
+ds_transformer_cuda.cpp:185-193): `gelu_checkpoint` is inherent (the GeLU kernel keeps only its
+input); `attn_dropout_checkpoint` keeps the softmax output + the 1-byte dropout mask and
+re-applies the mask in backward instead of holding the dropped probabilities
+(native.dropout_matmul); `normalize_invertible` keeps LayerNorm outputs only and recovers the
+normalised input from them in backward (native.layer_norm_invertible).  `stochastic_mode` is
+accepted for config compatibility: the kernels here are deterministic and already take the
+reference's fast path.
 """
 
 import json
@@ -127,7 +131,8 @@ class DeepSpeedTransformerFunction:
         gen = layer._generator if layer is not None else None
         eps = cfg.layer_norm_eps
         x = input
-        inp = native.layer_norm(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
+        ln = native.layer_norm_invertible if getattr(cfg, "normalize_invertible", False) else native.layer_norm
+        inp = ln(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
         qkv = F.linear(inp, attn_qkvw, attn_qkvb)
         fast = _use_head_kernels(qkv, hd)
         if fast:
@@ -142,19 +147,22 @@ class DeepSpeedTransformerFunction:
                 mask = mask[:, None, None, :]
             mask = mask.reshape(B, 1, -1, S).contiguous()
         probs = masked_softmax(scores, mask, 1.0 / math.sqrt(hd), False, nh)
-        probs = native.dropout(probs, cfg.attn_dropout_ratio, training, gen)
-        ctx = torch.matmul(probs, v)
+        if getattr(cfg, "attn_dropout_checkpoint", False):
+            ctx = native.dropout_matmul(probs, v, cfg.attn_dropout_ratio, training, gen)
+        else:
+            probs = native.dropout(probs, cfg.attn_dropout_ratio, training, gen)
+            ctx = torch.matmul(probs, v)
         ctx = _MergeHeads.apply(ctx) if fast else ctx.transpose(1, 2).reshape(B, S, Hd)
         attn_out = F.linear(ctx, attn_ow)
         add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen)
-        ff1_inp = native.layer_norm(add_res, attn_nw, attn_nb, eps)
+        ff1_inp = ln(add_res, attn_nw, attn_nb, eps)
         inter = _gelu_tanh(F.linear(ff1_inp, inter_w), inter_b)
         out = F.linear(inter, output_w)
         if cfg.pre_layer_norm:
             out = native.bias_dropout_residual(out, output_b, add_res, cfg.hidden_dropout_ratio, training, gen)
         else:
             out = native.bias_dropout_residual(out, output_b, ff1_inp, cfg.hidden_dropout_ratio, training, gen)
-            out = native.layer_norm(out, norm_w, norm_b, eps)
+            out = ln(out, norm_w, norm_b, eps)
         if grads is not None:  # reference test hook: collect gradients of the intermediates
             for t in (out, add_res, ff1_inp):
                 if t.requires_grad:

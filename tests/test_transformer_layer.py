@@ -100,3 +100,68 @@ def test_dropout_training_reproducible():
     ya, yb = a(x), b(x)
     assert torch.equal(ya, yb)
     assert not torch.allclose(ya, a.eval()(x))
+
+
+def _saved_bytes(fn):
+    """Bytes of distinct storages autograd saves while running fn()."""
+    seen = {}
+
+    def pack(t):
+        seen[t.untyped_storage().data_ptr()] = t.untyped_storage().nbytes()
+        return t
+
+    with torch.autograd.graph.saved_tensors_hooks(pack, lambda t: t):
+        out = fn()
+    return out, sum(seen.values())
+
+
+@pytest.mark.parametrize("pre_ln", [True, False])
+def test_memory_modes_same_gradients_less_saved(pre_ln):
+    """normalize_invertible + attn_dropout_checkpoint (reference ds_transformer_cuda.cpp:185-193):
+    identical forward / gradients (same dropout masks), fewer bytes held for backward."""
+    torch.manual_seed(3)
+    B, S, H = 2, 16, 64
+    outs = {}
+    for flags in (False, True):
+        cfg = DeepSpeedTransformerConfig(batch_size=B, hidden_size=H, heads=4, attn_dropout_ratio=0.1,
+                                         hidden_dropout_ratio=0.1, num_hidden_layers=2, initializer_range=0.02,
+                                         seed=11, pre_layer_norm=pre_ln, normalize_invertible=flags,
+                                         attn_dropout_checkpoint=flags, layer_norm_eps=1e-12)
+        torch.manual_seed(5)
+        DeepSpeedTransformerLayer.layer_id = 0  # same per-layer dropout seed stream in both runs
+        layer = DeepSpeedTransformerLayer(cfg).train()
+        x = torch.randn(B, S, H, requires_grad=True, generator=torch.Generator().manual_seed(7))
+        y, nbytes = _saved_bytes(lambda: layer(x, _mask(B, S)))
+        y.sum().backward()
+        outs[flags] = (y.detach(), x.grad.clone(), {n: p.grad.clone() for n, p in layer.named_parameters()},
+                       nbytes)
+    (y0, gx0, gp0, b0), (y1, gx1, gp1, b1) = outs[False], outs[True]
+    assert torch.allclose(y0, y1, atol=1e-6)
+    assert torch.allclose(gx0, gx1, atol=1e-4, rtol=1e-3)
+    for n in gp0:
+        assert torch.allclose(gp0[n], gp1[n], atol=1e-4, rtol=1e-3), n
+    assert b1 < b0, (b0, b1)
+
+
+@pytest.mark.gpu
+def test_memory_modes_gpu_kernels():
+    """Same equivalence on the HIP kernels (bf16): invertible LayerNorm backward through the
+    fused LN-backward kernel, dropout mask re-applied with the dropout-backward kernel."""
+    torch.manual_seed(3)
+    B, S, H = 4, 64, 256
+    dev = torch.device("cuda")
+    res = {}
+    for flags in (False, True):
+        cfg = DeepSpeedTransformerConfig(batch_size=B, hidden_size=H, heads=4, attn_dropout_ratio=0.1,
+                                         hidden_dropout_ratio=0.1, num_hidden_layers=2, initializer_range=0.02,
+                                         seed=11, pre_layer_norm=True, normalize_invertible=flags,
+                                         attn_dropout_checkpoint=flags, layer_norm_eps=1e-12, bf16=True)
+        torch.manual_seed(5)
+        DeepSpeedTransformerLayer.layer_id = 0
+        layer = DeepSpeedTransformerLayer(cfg).to(dev).train()
+        x = torch.randn(B, S, H, generator=torch.Generator().manual_seed(7)).to(dev, torch.bfloat16).requires_grad_(True)
+        y = layer(x, _mask(B, S).to(dev, torch.bfloat16))
+        y.float().sum().backward()
+        res[flags] = (y.detach().float(), x.grad.float(), layer.attn_qkvw.grad.float(), layer.norm_w.grad.float())
+    for a, b in zip(res[False], res[True]):
+        assert (a - b).abs().max().item() <= 3e-2 * max(1.0, a.abs().max().item())
