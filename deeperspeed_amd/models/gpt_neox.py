@@ -142,6 +142,8 @@ def residual_sum(*xs):
     whose output only seeds backward) the two full-tensor adds are skipped."""
     if _SKIP_OUTPUTS and torch.is_grad_enabled():
         return _GradOnlySum.apply(*xs)
+    if len(xs) <= 3:
+        return native.add3(*xs)  # one fused HIP pass on the GPU
     out = xs[0] + xs[1]
     for x in xs[2:]:
         out = out + x

@@ -207,6 +207,21 @@ std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tenso
 }
 
 // ----------------------------------------------------------------------------- bias + gelu
+Tensor add3(Tensor a, Tensor b, OptT c) {
+  check_dev(a, "add3"); check_dev(b, "add3");
+  TORCH_CHECK(a.sizes() == b.sizes() && a.scalar_type() == b.scalar_type() && a.is_contiguous() && b.is_contiguous(),
+              "add3: a and b must match and be contiguous");
+  if (c.has_value())
+    TORCH_CHECK(c->sizes() == a.sizes() && c->scalar_type() == a.scalar_type() && c->is_contiguous(), "add3: c");
+  const int vn = a.scalar_type() == at::kFloat ? 4 : 8;
+  TORCH_CHECK(a.numel() % vn == 0, "add3: numel must be a multiple of 16 bytes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  Tensor y = at::empty_like(a);
+  dsa::launch_add3(a.data_ptr(), b.data_ptr(), c.has_value() ? c->data_ptr() : nullptr, y.data_ptr(), a.numel(),
+                   dcode(a), cur_stream());
+  return y;
+}
+
 Tensor bias_gelu_fwd(Tensor x, OptT b, bool approx) {
   check_dev(x, "x");
   const int64_t C = x.size(-1);
@@ -697,6 +712,7 @@ void register_gemm_lt(pybind11::module& m);  // gemm_lt.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_gemm_lt(m);
+  m.def("add3", &add3, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c") = pybind11::none());
   m.def("sparse_flash_fwd", &sparse_flash_fwd);
   m.def("sparse_flash_bwd", &sparse_flash_bwd);
   m.def("onebit_worker_compress", &onebit_worker_compress);

@@ -232,6 +232,30 @@ __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict_
   }
 }
 
+// y = a + b (+ c): the residual sums of a transformer block in one pass (reference fused_add2 /
+// fused_add3 / fused_add4, general_kernels.cu:89-292), fp32 accumulation, 16-byte vectors.
+template <typename T>
+__global__ void __launch_bounds__(256) add3_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                                                   const T* __restrict__ c, T* __restrict__ y, int64_t n) {
+  constexpr int VN = Vec16<T>::N;
+  const int64_t nvec = n / VN;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    float va[VN], vb[VN], vc[VN];
+    Vec16<T>::load(a + i * VN, va);
+    Vec16<T>::load(b + i * VN, vb);
+    if (c) {
+      Vec16<T>::load(c + i * VN, vc);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) va[j] += vb[j] + vc[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) va[j] += vb[j];
+    }
+    Vec16<T>::store(y + i * VN, va);
+  }
+}
+
 // dx = dy * gelu'(x + b); per-block column partials of dx for the bias gradient.
 // grid: (ceil(C / (256*VN)), row_chunks); each thread owns VN consecutive columns.
 template <typename T>
@@ -311,6 +335,17 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
                        (T*)dgamma, 0);
     if (dbeta) hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, s,
                                   partial + (int64_t)grid * H, grid, H, (T*)dbeta, 0));
+}
+
+void launch_add3(const void* a, const void* b, const void* c, void* y, int64_t n, int dt, hipStream_t s) {
+  if (n <= 0) return;
+  const int vn = dt == kF32 ? 4 : 8;
+  int64_t g = (n / vn + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((add3_kernel<T>), dim3((unsigned)g), dim3(256), 0, s, (const T*)a, (const T*)b, (const T*)c,
+                       (T*)y, n));
 }
 
 void launch_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, int C, int approx, int dt,

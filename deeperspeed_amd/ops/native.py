@@ -184,6 +184,28 @@ def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool =
     return _BiasGeluFn.apply(x, bias, approximate)
 
 
+class _Add3Fn(torch.autograd.Function):
+    """a + b (+ c) in one HIP pass (residual sums); the gradient passes to every summand."""
+
+    @staticmethod
+    def forward(ctx, a, b, c):
+        ctx.n = 2 if c is None else 3
+        return hip_ops().add3(a.contiguous(), b.contiguous(), None if c is None else c.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g, g, g if ctx.n == 3 else None)
+
+
+def add3(a: torch.Tensor, b: torch.Tensor, c: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused residual sum on the GPU (one read of each input, one write); plain adds elsewhere."""
+    vn = 4 if a.dtype == torch.float32 else 8
+    if (a.is_cuda and a.shape == b.shape and a.dtype == b.dtype and a.numel() % vn == 0
+            and (c is None or (c.shape == a.shape and c.dtype == a.dtype))):
+        return _Add3Fn.apply(a, b, c)
+    return a + b if c is None else a + b + c
+
+
 # --------------------------------------------------------------------------- reductions
 _WS = {}
 

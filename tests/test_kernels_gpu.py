@@ -550,3 +550,17 @@ def test_transformer_layer_head_kernels_match_permute_path(monkeypatch):
         res[fast] = [out.detach().float(), xi.grad.float()] + [p.grad.float() for p in layer.parameters()]
     for a, b in zip(res[True], res[False]):
         torch.testing.assert_close(a, b, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_add3_matches_reference(dtype):
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    a, b, c = (torch.randn(4, 512, 768, device=dev, dtype=dtype) for _ in range(3))
+    ref = a.float() + b.float() + c.float()
+    assert (native.hip_ops().add3(a, b, c).float() - ref).abs().max().item() <= (1e-5 if dtype == torch.float32 else 3e-2)
+    assert torch.allclose(native.hip_ops().add3(a, b).float(), a.float() + b.float(), atol=3e-2)
+    xs = [t.clone().requires_grad_(True) for t in (a, b, c)]
+    native.add3(*xs).float().sum().backward()
+    assert all(torch.equal(x.grad, torch.ones_like(x)) for x in xs)
