@@ -624,6 +624,67 @@ std::vector<Tensor> flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Te
   return {dq, dk, dv};
 }
 
+// Encoder (non-causal) flash attention with an optional additive per-key bias kbias [B, S] fp32
+// (the [B,1,1,S] padding mask) and in-kernel attention dropout p_drop, whose keep mask is a hash
+// of (seed, b*H+h, query, key) regenerated by the backward.  S % 8 == 0, head dim 64 or 128.
+static void check_ex(const Tensor& q, const c10::optional<Tensor>& kbias, double p_drop, const char* what) {
+  const int64_t B = q.size(0), S = q.size(2), D = q.size(3);
+  TORCH_CHECK(S % 8 == 0 && (D == 64 || D == 128), what, ": S % 8 == 0 and head dim 64 or 128");
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, what, ": dropout probability in [0, 1)");
+  TORCH_CHECK(kbias.has_value() || p_drop > 0.0, what, ": needs a key bias or dropout (use flash_attn_fwd)");
+  if (kbias.has_value()) {
+    check_dev(*kbias, what);
+    TORCH_CHECK(kbias->scalar_type() == at::kFloat && kbias->is_contiguous() && kbias->numel() == B * S, what,
+                ": kbias must be contiguous fp32 [B, S]");
+  }
+}
+
+std::vector<Tensor> flash_attn_fwd_ex(Tensor q, Tensor k, Tensor v, c10::optional<Tensor> kbias, double scale,
+                                      double p_drop, int64_t seed, bool out_bshd) {
+  check_dev(q, "q"); check_dev(k, "k"); check_dev(v, "v");
+  TORCH_CHECK(q.dim() == 4 && q.sizes() == k.sizes() && q.sizes() == v.sizes(), "flash_attn_ex: q/k/v shape mismatch");
+  TORCH_CHECK(q.scalar_type() != at::kFloat && q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(),
+              "flash_attn_ex: 16-bit q/k/v of one dtype");
+  TORCH_CHECK(q.is_contiguous() && k.is_contiguous() && v.is_contiguous(), "flash_attn_ex: contiguous inputs");
+  check_ex(q, kbias, p_drop, "flash_attn_fwd_ex");
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  Tensor o = out_bshd ? at::empty({B, S, H, D}, q.options()) : at::empty_like(q);
+  Tensor lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  dsa::launch_flash_fwd_ex(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)(B * H),
+                           (int)S, (int)D, (float)scale, kbias ? kbias->data_ptr<float>() : nullptr, (int)H,
+                           (float)p_drop, (uint64_t)seed, dcode(q), cur_stream(), out_bshd ? (int)H : 0);
+  return {o, lse};
+}
+
+std::vector<Tensor> flash_attn_bwd_ex(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse,
+                                      c10::optional<Tensor> kbias, double scale, double p_drop, int64_t seed,
+                                      bool o_bshd) {
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
+  for (auto* t : {&q, &k, &v}) {
+    check_dev(*t, "flash_attn_bwd_ex");
+    TORCH_CHECK(t->sizes() == q.sizes() && t->scalar_type() == q.scalar_type() && t->is_contiguous(),
+                "flash_attn_bwd_ex: q/k/v must match");
+  }
+  const std::vector<int64_t> oshape = o_bshd ? std::vector<int64_t>{B, S, H, D} : std::vector<int64_t>{B, H, S, D};
+  for (auto* t : {&dout, &o}) {
+    check_dev(*t, "flash_attn_bwd_ex");
+    TORCH_CHECK(t->sizes() == at::IntArrayRef(oshape) && t->scalar_type() == q.scalar_type() && t->is_contiguous(),
+                "flash_attn_bwd_ex: dout/o must be contiguous in the forward's output layout");
+  }
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * S,
+              "flash_attn_bwd_ex: lse");
+  check_ex(q, kbias, p_drop, "flash_attn_bwd_ex");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
+  Tensor dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  Tensor delta = at::empty_like(lse);
+  dsa::launch_flash_bwd_ex(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                           lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                           (int)(B * H), (int)S, (int)D, (float)scale, kbias ? kbias->data_ptr<float>() : nullptr,
+                           (int)H, (float)p_drop, (uint64_t)seed, dcode(q), cur_stream(), o_bshd ? (int)H : 0);
+  return {dq, dk, dv};
+}
+
 // Block-sparse flash attention.  q,k,v [B, H, S, D] (S % 64 == 0); LUT tensors int32 on the
 // device (see flash_attn.hip): rowptr [Hl * S/64 + 1], cols / masks [nnz]; the transposed LUT
 // colptr / rows / masks_t for the backward.  `shift` = min(6, log2(layout block)).
@@ -714,6 +775,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_gemm_lt(m);
   m.def("add3", &add3, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c") = pybind11::none());
   m.def("sparse_flash_fwd", &sparse_flash_fwd);
+  m.def("flash_attn_fwd_ex", &flash_attn_fwd_ex);
+  m.def("flash_attn_bwd_ex", &flash_attn_bwd_ex);
   m.def("sparse_flash_bwd", &sparse_flash_bwd);
   m.def("onebit_worker_compress", &onebit_worker_compress);
   m.def("onebit_server_compress", &onebit_server_compress);

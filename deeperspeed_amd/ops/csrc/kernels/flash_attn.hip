@@ -498,10 +498,43 @@ __device__ __forceinline__ s16x8 pack8_h(const float* v, int base) {
 // O / l rescale (D/32*16 + 1 multiplies per lane) and alpha's exp.  Exact up to rounding.
 constexpr float LAZY_TH = 8.0f;
 
-template <typename T, int D, bool CAUSAL, bool LAZY = true>
+// ---- encoder (BERT) extras, compiled in by the EX template bits of the v2 kernels
+//   EX_BIAS: additive per-key bias kbias[b][key] (the [B,1,1,S] padding mask), b = bh / hdiv
+//   EX_DROP: dropout on the probabilities (reference attn_dropout after the softmax).  The
+//            keep mask is a counter-based hash of (seed, bh, query, key), so the backward
+//            kernels regenerate it in their own register layouts and nothing S x S is stored:
+//            one 32-bit hash yields the 16-bit draws of keys 2j and 2j+1 of a query row.
+//            The normaliser l / LSE stays the undropped one; O = (P * Z) V / (1 - p).
+constexpr int EX_BIAS = 1, EX_DROP = 2;
+struct Extra {
+  const float* kbias = nullptr;
+  int hdiv = 1;
+  uint32_t seed = 0;
+  uint32_t thresh = 0;  // a draw below thresh (of 65536) drops the element
+  float rscale = 1.f;   // 1 / (1 - p)
+};
+constexpr float LOG2E = 1.4426950408889634f;
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_head(uint32_t seed, int64_t bh) {
+  return drop_mix(seed ^ drop_mix((uint32_t)bh * 0x9e3779b1u + 0x632be5abu));
+}
+// draws of (q, 2j) in the low and (q, 2j+1) in the high 16 bits
+__device__ __forceinline__ uint32_t drop_pair(uint32_t hb, int q, int half_s, int j) {
+  return drop_mix(((uint32_t)q * (uint32_t)half_s + (uint32_t)j) * 0x85ebca6bu ^ hb);
+}
+
+template <typename T, int D, bool CAUSAL, bool LAZY = true, int EX = 0>
 __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
-                                                        float* __restrict__ LSE, int S, float scale, int onh) {
+                                                        float* __restrict__ LSE, int S, float scale, int onh,
+                                                        Extra ex = Extra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -516,6 +549,9 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   const uint16_t* Qb = Q + bh * (int64_t)S * D;
   const uint16_t* Kb = K + bh * (int64_t)S * D;
   const uint16_t* Vb = V + bh * (int64_t)S * D;
+  constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
+  const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
+  const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
 
   s16x8 qf[D / 16];
 #pragma unroll
@@ -569,13 +605,28 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
           if (key >= S || (CAUSAL && key > myq)) sv[16 * t + r] = -INFINITY;
         }
     }
+    if constexpr (BIAS) {  // scores to the log2 domain with the key bias folded in (S % 8 == 0)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const int key0 = j0 + 32 * t + 8 * rb + 4 * h;
+          const float4 b4 = key0 < S ? *reinterpret_cast<const float4*>(kbrow + key0) : make_float4(0, 0, 0, 0);
+          float* s4 = sv + 16 * t + 4 * rb;
+          s4[0] = fmaf(s4[0], sl2, b4.x * LOG2E);
+          s4[1] = fmaf(s4[1], sl2, b4.y * LOG2E);
+          s4[2] = fmaf(s4[2], sl2, b4.z * LOG2E);
+          s4[3] = fmaf(s4[3], sl2, b4.w * LOG2E);
+        }
+    }
+    const float a2 = BIAS ? 1.f : sl2;
     // running max on raw scores (scale > 0 preserves order), exponent in the log2 domain:
     // p = 2^(s * scale*log2e - m) as one packed FMA + one v_exp_f32 per element
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 32; ++i) mx = fmaxf(mx, sv[i]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mt = mx * sl2;
+    const float mt = mx * a2;
     if (!LAZY || __any(mt > m + LAZY_TH)) {  // wave-uniform
       const float mn = fmaxf(m, mt);
       const float alpha = fast_exp2(m - ((mn == -INFINITY) ? 0.f : mn));
@@ -591,14 +642,23 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     float ps = 0.f, ps1 = 0.f;
 #pragma unroll
     for (int i = 0; i < 32; i += 2) {
-      sv[i] = fast_exp2(fmaf(sv[i], sl2, -mu));
-      sv[i + 1] = fast_exp2(fmaf(sv[i + 1], sl2, -mu));
+      sv[i] = fast_exp2(fmaf(sv[i], a2, -mu));
+      sv[i + 1] = fast_exp2(fmaf(sv[i + 1], a2, -mu));
       ps += sv[i];
       ps1 += sv[i + 1];
     }
     ps += ps1;
     ps += __shfl_xor(ps, 32, 64);
     l += ps;
+    if constexpr (DROP) {  // values 2i, 2i+1 of a lane are keys 2j, 2j+1 of its query row
+#pragma unroll
+      for (int i = 0; i < 32; i += 2) {
+        const int key = j0 + 32 * (i >> 4) + 8 * ((i & 15) >> 2) + 4 * h + (i & 3);
+        const uint32_t x = drop_pair(hb, myq, S >> 1, key >> 1);
+        if ((x & 0xffffu) < ex.thresh) sv[i] = 0.f;
+        if ((x >> 16) < ex.thresh) sv[i + 1] = 0.f;
+      }
+    }
     // O^T += V^T P^T over the 64 keys (4 steps of 16)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -620,7 +680,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     __syncthreads();
   }
   if (myq < S) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const float inv = l > 0.f ? (DROP ? ex.rscale : 1.f) / l : 0.f;
     uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh);
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt)
@@ -634,7 +694,8 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
         *reinterpret_cast<ushort4*>(orow + 32 * dt + 8 * rb + 4 * h) = v4;
       }
     if (h == 0)
-      LSE[bh * (int64_t)S + myq] = (m == -INFINITY) ? -INFINITY : (m + log2f(l)) * 0.6931471805599453f;
+      // a row with every key masked out stores +inf so the backward recomputes P = 0 for it
+      LSE[bh * (int64_t)S + myq] = (m == -INFINITY) ? INFINITY : (m + log2f(l)) * 0.6931471805599453f;
   }
 }
 
@@ -644,7 +705,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
 // index per value from the C layout, LSE/Delta broadcast from LDS), then
 //   dV^T += dO^T P   (A = dO^T via tr reads, B = P from registers)
 //   dK^T += Q^T dS   (A = Q^T via tr reads,  B = dS from registers)
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, int EX = 0>
 __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(const uint16_t* __restrict__ Q,
                                                              const uint16_t* __restrict__ K,
                                                              const uint16_t* __restrict__ V,
@@ -652,7 +713,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
                                                              const float* __restrict__ LSE,
                                                              const float* __restrict__ DELTA,
                                                              uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
-                                                             int S, float scale, int onh) {
+                                                             int S, float scale, int onh, Extra ex = Extra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   float* stats = reinterpret_cast<float*>(smem + 4 * TS);  // [2 stages][LSE 64 | DELTA 64]
@@ -667,6 +728,11 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   const int64_t base = bh * (int64_t)S * D;
   const int64_t obase = o_base<D>(bh, S, onh);
   const float sl2 = scale * 1.4426950408889634f;
+  constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
+  // this lane's key bias (log2 units) and which 16-bit half of a pair draw is its key's
+  const float kb2 = (BIAS && mykey < S) ? ex.kbias[(bh / ex.hdiv) * (int64_t)S + mykey] * LOG2E : 0.f;
+  const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
+  const int dshift = (mykey & 1) * 16;
 
   s16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
@@ -729,7 +795,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-        pv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse_s[qi]));
+        pv[r] = fast_exp2(fmaf(sacc[r], sl2, BIAS ? kb2 - lse_s[qi] : -lse_s[qi]));
       }
       // wave-uniform: ragged tail or a query of this sub-tile before the wave's last key
       if ((i0 + 32 * t + 32 > S) || (kb + 32 * w + 32 > S) || (CAUSAL && kb + 32 * w + 31 > i0 + 32 * t)) {
@@ -739,10 +805,21 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
           if (q >= S || mykey >= S || (CAUSAL && mykey > q)) pv[r] = 0.f;
         }
       }
+      if constexpr (DROP) {  // dV from the dropped P; dP = dP_dropped * Z / (1 - p)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-        dsv[r] = pv[r] * (pacc[r] - del_s[qi]);
+        for (int r = 0; r < 16; ++r) {
+          const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          const uint32_t x = drop_pair(hb, i0 + qi, S >> 1, mykey >> 1);
+          const float zr = ((x >> dshift) & 0xffffu) < ex.thresh ? 0.f : ex.rscale;
+          dsv[r] = pv[r] * fmaf(pacc[r], zr, -del_s[qi]);
+          pv[r] *= zr;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          dsv[r] = pv[r] * (pacc[r] - del_s[qi]);
+        }
       }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -786,14 +863,14 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
 // dQ: one wave = 32 queries (lane = query column of S^T = K Q^T); Q and dO are B operands in
 // registers; per 64-key tile: S^T, dP^T (A = K / V rows from LDS), dS^T in registers, then
 //   dQ^T += K^T dS^T   (A = K^T via tr reads, B = dS^T from registers)
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, int EX = 0>
 __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __restrict__ Q,
                                                            const uint16_t* __restrict__ K,
                                                            const uint16_t* __restrict__ V,
                                                            const uint16_t* __restrict__ dO,
                                                            const float* __restrict__ LSE,
                                                            const float* __restrict__ DELTA, uint16_t* __restrict__ dQ,
-                                                           int S, float scale, int onh) {
+                                                           int S, float scale, int onh, Extra ex = Extra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -806,6 +883,9 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
   const int myq = qb + 32 * w + c32;
   const int64_t base = bh * (int64_t)S * D;
   const float sl2 = scale * 1.4426950408889634f;
+  constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
+  const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
+  const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
 
   s16x8 qf[D / 16], of[D / 16];
 #pragma unroll
@@ -851,8 +931,20 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
         pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), of[ks], pacc);
       }
       float dsv[16];
+      if constexpr (BIAS) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dsv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse2));
+        for (int rb = 0; rb < 4; ++rb) {
+          const int key0 = j0 + 32 * t + 8 * rb + 4 * h;
+          const float4 b4 = key0 < S ? *reinterpret_cast<const float4*>(kbrow + key0) : make_float4(0, 0, 0, 0);
+          dsv[4 * rb + 0] = fast_exp2(fmaf(sacc[4 * rb + 0], sl2, fmaf(b4.x, LOG2E, -lse2)));
+          dsv[4 * rb + 1] = fast_exp2(fmaf(sacc[4 * rb + 1], sl2, fmaf(b4.y, LOG2E, -lse2)));
+          dsv[4 * rb + 2] = fast_exp2(fmaf(sacc[4 * rb + 2], sl2, fmaf(b4.z, LOG2E, -lse2)));
+          dsv[4 * rb + 3] = fast_exp2(fmaf(sacc[4 * rb + 3], sl2, fmaf(b4.w, LOG2E, -lse2)));
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dsv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse2));
+      }
       if ((j0 + 32 * t + 32 > S) || (qb + 32 * w + 32 > S) || (CAUSAL && j0 + 32 * t + 31 > qb + 32 * w)) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -860,8 +952,20 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
           if (key >= S || myq >= S || (CAUSAL && key > myq)) dsv[r] = 0.f;
         }
       }
+      if constexpr (DROP) {  // values r, r+1 are keys 2j, 2j+1 of this lane's query
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dsv[r] = dsv[r] * (pacc[r] - dl);
+        for (int r = 0; r < 16; r += 2) {
+          const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          const uint32_t x = drop_pair(hb, myq, S >> 1, key >> 1);
+          const float z0 = (x & 0xffffu) < ex.thresh ? 0.f : ex.rscale;
+          const float z1 = (x >> 16) < ex.thresh ? 0.f : ex.rscale;
+          dsv[r] = dsv[r] * fmaf(pacc[r], z0, -dl);
+          dsv[r + 1] = dsv[r + 1] * fmaf(pacc[r + 1], z1, -dl);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dsv[r] = dsv[r] * (pacc[r] - dl);
+      }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ks = 2 * t + kk;
@@ -1499,6 +1603,67 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
                          fa::dq_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                          (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale);
     });
+}
+
+// Encoder attention (non-causal) with a per-key additive bias and/or in-kernel dropout.
+// kbias: [BH / hdiv, S] fp32 or null; p_drop in [0, 1); S % 8 == 0; D in {64, 128}.
+#define FA_EX_DISPATCH(dt, D, kbias, pdrop, ...)                                                     \
+  do {                                                                                               \
+    auto _go = [&](auto tt, auto dd, auto ee) {                                                      \
+      using T = decltype(tt);                                                                        \
+      constexpr int DD = decltype(dd)::value;                                                        \
+      constexpr int EE = decltype(ee)::value;                                                        \
+      __VA_ARGS__;                                                                                   \
+    };                                                                                               \
+    auto _e = [&](auto tt, auto dd) {                                                                \
+      if (kbias && pdrop > 0.f) _go(tt, dd, std::integral_constant<int, fa::EX_BIAS | fa::EX_DROP>{}); \
+      else if (kbias) _go(tt, dd, std::integral_constant<int, fa::EX_BIAS>{});                      \
+      else _go(tt, dd, std::integral_constant<int, fa::EX_DROP>{});                                 \
+    };                                                                                               \
+    auto _d = [&](auto tt) {                                                                         \
+      if (D == 64) _e(tt, std::integral_constant<int, 64>{});                                       \
+      else _e(tt, std::integral_constant<int, 128>{});                                              \
+    };                                                                                               \
+    if (dt == kBF16) _d(bf16_t{}); else _d(f16_t{});                                                 \
+  } while (0)
+
+static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t seed) {
+  fa::Extra ex;
+  ex.kbias = kbias;
+  ex.hdiv = hdiv;
+  ex.seed = (uint32_t)(seed ^ (seed >> 32));
+  ex.thresh = pdrop > 0.f ? (uint32_t)fminf(65536.f, rintf(pdrop * 65536.f)) : 0u;
+  ex.rscale = pdrop > 0.f ? 1.f / (1.f - pdrop) : 1.f;
+  return ex;
+}
+
+void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
+                         float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
+                         int onh) {
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed);
+  const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
+  FA_EX_DISPATCH(dt, D, kbias, pdrop,
+    hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, false, true, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale, onh,
+                       ex));
+}
+
+void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const void* v, const void* o,
+                         const float* lse, float* delta, void* dq, void* dk, void* dv, int BH, int S, int D,
+                         float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
+                         int onh) {
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed);
+  const int64_t rows = (int64_t)BH * S;
+  const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
+  FA_EX_DISPATCH(dt, D, kbias, pdrop,
+    hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
+                       (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
+    hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::dkdv_v2_lds<DD>(), s,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                       (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex);
+    hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                       (uint16_t*)dq, S, scale, onh, ex));
 }
 
 // default: register prefetch + double-buffered LDS (2 workgroups / CU, measured faster);

@@ -363,6 +363,71 @@ def flash_attention(q, k, v, causal=True, scale=1.0, out_layout="bhsd", stash=No
     return _FlashAttnFn.apply(q, k, v, causal, scale, out_layout == "bshd")
 
 
+class _FlashAttnExFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, kbias, scale, p, seed, out_bshd):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        B, H, S, D = q.shape
+        _macs(2 * B * H * S * S * D)
+        o, lse = hip_ops().flash_attn_fwd_ex(q, k, v, kbias, scale, p, seed, out_bshd)
+        ctx.save_for_backward(q, k, v, o, lse, kbias)
+        ctx.scale, ctx.p, ctx.seed, ctx.out_bshd = scale, p, seed, out_bshd
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, kbias = ctx.saved_tensors
+        dq, dk, dv = hip_ops().flash_attn_bwd_ex(do.contiguous(), q, k, v, o, lse, kbias, ctx.scale, ctx.p, ctx.seed,
+                                                 ctx.out_bshd)
+        return dq, dk, dv, None, None, None, None, None
+
+
+def encoder_flash_supported(q: torch.Tensor, key_bias_ok: bool = True) -> bool:
+    """Shapes the encoder flash kernel (key bias + in-kernel dropout) handles."""
+    return (key_bias_ok and q.is_cuda and q.dtype in (torch.bfloat16, torch.float16) and q.dim() == 4
+            and q.shape[-1] in (64, 128) and q.shape[2] % 8 == 0)
+
+
+def flash_attention_encoder(q, k, v, key_bias=None, scale=1.0, dropout_p=0.0, training=True, generator=None,
+                            out_layout="bhsd"):
+    """Non-causal attention softmax(scale * q k^T + key_bias[b, None, :]) with dropout on the
+    probabilities, fused in one MFMA kernel per direction (no S x S tensor is stored; the keep mask
+    is a hash of (seed, head, query, key) regenerated in backward).  q, k, v [B, H, S, D];
+    key_bias [B, S] (any float dtype; the reference's additive [B,1,1,S] mask squeezed)."""
+    assert out_layout in ("bhsd", "bshd")
+    p = float(dropout_p) if training else 0.0
+    if key_bias is not None:
+        key_bias = key_bias.reshape(q.shape[0], q.shape[2]).float().contiguous()
+    if key_bias is None and p <= 0.0:
+        return flash_attention(q, k, v, False, scale, out_layout)
+    seed = _draw_seed(generator) if p > 0.0 else 0
+    return _FlashAttnExFn.apply(q, k, v, key_bias, float(scale), p, int(seed) & ((1 << 63) - 1),
+                                out_layout == "bshd")
+
+
+def flash_dropout_keep_mask(B, H, S, p, seed, device=None):
+    """Host/torch re-implementation of the kernel's keep mask ([B, H, S, S] bool), for tests."""
+    M = 0xFFFFFFFF
+
+    def mix(x):
+        x = x ^ (x >> 16)
+        x = (x * 0x7FEB352D) & M
+        x = x ^ (x >> 15)
+        x = (x * 0x846CA68B) & M
+        return x ^ (x >> 16)
+
+    s32 = (int(seed) ^ (int(seed) >> 32)) & M
+    thresh = min(65536, int(round(p * 65536))) if p > 0 else 0
+    bh = torch.arange(B * H, dtype=torch.int64, device=device)
+    hb = mix(s32 ^ mix((bh * 0x9E3779B1 + 0x632BE5AB) & M))  # [BH]
+    q = torch.arange(S, dtype=torch.int64, device=device)
+    j = torch.arange(S // 2, dtype=torch.int64, device=device)
+    idx = (q[:, None] * (S // 2) + j[None, :]) & M  # [S, S/2]
+    x = mix(((idx * 0x85EBCA6B) & M)[None] ^ hb[:, None, None])  # [BH, S, S/2]
+    draws = torch.stack([x & 0xFFFF, x >> 16], dim=-1).reshape(B, H, S, S)
+    return draws >= thresh
+
+
 def flash_attention_fwd_lse(q, k, v, causal=True, scale=1.0, out_layout="bhsd"):
     """Forward only (no autograd): (o, lse) with lse [B*H, S] fp32, for a later stashed backward."""
     q, k, v = q.contiguous(), k.contiguous(), v.contiguous()

@@ -20,6 +20,7 @@ reference's fast path.
 
 import json
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -109,6 +110,10 @@ class _MergeHeads(torch.autograd.Function):
         return native.hip_ops().swap12(g.contiguous().view(B, S, ctx.nh, ctx.hd))
 
 
+# DSA_ENCODER_FLASH=0 keeps the materialised scores -> softmax -> dropout -> P V path
+_ENCODER_FLASH = os.environ.get("DSA_ENCODER_FLASH", "1") != "0"
+
+
 def _use_head_kernels(x, hd):
     return x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and hd % 8 == 0
 
@@ -139,20 +144,29 @@ class DeepSpeedTransformerFunction:
             q, k, v = _SplitHeads.apply(qkv, nh)  # contiguous [B, nh, S, hd]: batched GEMMs without copies
         else:
             q, k, v = qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, hd]
-        scores = torch.matmul(q, k.transpose(-1, -2))
         mask = None
         if input_mask is not None:
-            mask = input_mask.to(scores.dtype)
+            mask = input_mask
             if mask.dim() == 2:
                 mask = mask[:, None, None, :]
-            mask = mask.reshape(B, 1, -1, S).contiguous()
-        probs = masked_softmax(scores, mask, 1.0 / math.sqrt(hd), False, nh)
-        if getattr(cfg, "attn_dropout_checkpoint", False):
-            ctx = native.dropout_matmul(probs, v, cfg.attn_dropout_ratio, training, gen)
+            mask = mask.reshape(B, 1, -1, S)
+        if fast and _ENCODER_FLASH and native.encoder_flash_supported(q, mask is None or mask.shape[2] == 1):
+            # one fused kernel per direction: scores, key-padding bias, softmax, dropout and P V
+            # stay on chip; the output is written token-major [B, S, nh, hd] for the projection
+            ctx = native.flash_attention_encoder(q, k, v, None if mask is None else mask.reshape(B, S),
+                                                 1.0 / math.sqrt(hd), cfg.attn_dropout_ratio, training, gen,
+                                                 out_layout="bshd").view(B, S, Hd)
         else:
-            probs = native.dropout(probs, cfg.attn_dropout_ratio, training, gen)
-            ctx = torch.matmul(probs, v)
-        ctx = _MergeHeads.apply(ctx) if fast else ctx.transpose(1, 2).reshape(B, S, Hd)
+            scores = torch.matmul(q, k.transpose(-1, -2))
+            if mask is not None:
+                mask = mask.to(scores.dtype).contiguous()
+            probs = masked_softmax(scores, mask, 1.0 / math.sqrt(hd), False, nh)
+            if getattr(cfg, "attn_dropout_checkpoint", False):
+                ctx = native.dropout_matmul(probs, v, cfg.attn_dropout_ratio, training, gen)
+            else:
+                probs = native.dropout(probs, cfg.attn_dropout_ratio, training, gen)
+                ctx = torch.matmul(probs, v)
+            ctx = _MergeHeads.apply(ctx) if fast else ctx.transpose(1, 2).reshape(B, S, Hd)
         attn_out = F.linear(ctx, attn_ow)
         add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen)
         ff1_inp = ln(add_res, attn_nw, attn_nb, eps)

@@ -144,9 +144,12 @@ def test_memory_modes_same_gradients_less_saved(pre_ln):
 
 
 @pytest.mark.gpu
-def test_memory_modes_gpu_kernels():
+def test_memory_modes_gpu_kernels(monkeypatch):
     """Same equivalence on the HIP kernels (bf16): invertible LayerNorm backward through the
-    fused LN-backward kernel, dropout mask re-applied with the dropout-backward kernel."""
+    fused LN-backward kernel, dropout mask re-applied with the dropout-backward kernel (the
+    materialised attention path, so the encoder flash kernel is switched off here)."""
+    from deeperspeed_amd.ops.transformer import transformer as tmod
+    monkeypatch.setattr(tmod, "_ENCODER_FLASH", False)
     torch.manual_seed(3)
     B, S, H = 4, 64, 256
     dev = torch.device("cuda")
@@ -165,3 +168,43 @@ def test_memory_modes_gpu_kernels():
         res[flags] = (y.detach().float(), x.grad.float(), layer.attn_qkvw.grad.float(), layer.norm_w.grad.float())
     for a, b in zip(res[False], res[True]):
         assert (a - b).abs().max().item() <= 3e-2 * max(1.0, a.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pre_ln", [True, False])
+def test_encoder_flash_matches_materialised_path(monkeypatch, pre_ln):
+    """Without attention dropout the fused encoder flash path (key-padding bias in the kernel,
+    token-major output) gives the materialised softmax path's outputs and gradients."""
+    from deeperspeed_amd.ops.transformer import transformer as tmod
+    B, S, H = 4, 128, 512
+    dev = torch.device("cuda")
+    res = {}
+    for flash in (False, True):
+        monkeypatch.setattr(tmod, "_ENCODER_FLASH", flash)
+        cfg = DeepSpeedTransformerConfig(batch_size=B, hidden_size=H, heads=8, attn_dropout_ratio=0.0,
+                                         hidden_dropout_ratio=0.0, num_hidden_layers=2, initializer_range=0.02,
+                                         seed=11, pre_layer_norm=pre_ln, layer_norm_eps=1e-12, bf16=True)
+        torch.manual_seed(5)
+        DeepSpeedTransformerLayer.layer_id = 0
+        layer = DeepSpeedTransformerLayer(cfg).to(dev).train()
+        x = torch.randn(B, S, H, generator=torch.Generator().manual_seed(7)).to(dev, torch.bfloat16).requires_grad_(True)
+        y = layer(x, _mask(B, S).to(dev, torch.bfloat16))
+        y.float().pow(2).sum().backward()
+        res[flash] = (y.detach().float(), x.grad.float(), layer.attn_qkvw.grad.float(), layer.attn_ow.grad.float())
+    for a, b in zip(res[False], res[True]):
+        assert (a - b).abs().max().item() <= 3e-2 * max(1.0, a.abs().max().item())
+
+
+def test_encoder_flash_keep_mask_statistics():
+    """The in-kernel attention-dropout mask (counter hash of seed, head, query, key): drop rate
+    matches p, heads and seeds give different masks, neighbouring keys are uncorrelated."""
+    from deeperspeed_amd.ops import native
+    keep = native.flash_dropout_keep_mask(2, 4, 256, 0.1, 99)
+    assert keep.shape == (2, 4, 256, 256)
+    assert abs(1.0 - keep.float().mean().item() - 0.1) < 0.005
+    assert not torch.equal(keep[0, 0], keep[0, 1]) and not torch.equal(keep[0, 0], keep[1, 0])
+    assert not torch.equal(keep, native.flash_dropout_keep_mask(2, 4, 256, 0.1, 100))
+    d = (~keep).float()
+    both = (d[..., 0::2] * d[..., 1::2]).mean().item()  # the two halves of one hash
+    assert abs(both - 0.01) < 0.003
+    assert native.flash_dropout_keep_mask(1, 1, 64, 0.0, 5).all()
