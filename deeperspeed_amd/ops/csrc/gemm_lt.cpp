@@ -32,6 +32,7 @@ namespace {
   } while (0)
 
 constexpr size_t kWorkspace = 64ull << 20;
+constexpr int kCandidates = 16;  // heuristic algorithms timed once per GEMM shape
 
 struct Ctx {
   hipblasLtHandle_t handle = nullptr;
@@ -73,7 +74,7 @@ struct Gemm {
   int64_t ld_aux;
 };
 
-using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int, bool>;
+using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int, int, bool>;
 
 struct Algo {
   hipblasLtMatmulAlgo_t algo;
@@ -110,7 +111,7 @@ void run(const Gemm& g, int device, hipStream_t stream) {
   LT_CHECK(hipblasLtMatrixLayoutCreate(&lb, g.ab_type, br, bc, g.ldb));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&ld, g.d_type, g.m, g.n, g.ldd));
   const float alpha = 1.f, beta = g.C ? 1.f : 0.f;
-  const Key key{device, (int)g.epi, g.m, g.n, g.k, (int)g.ta, (int)g.tb, (int)g.ab_type, g.C != nullptr};
+  const Key key{device, (int)g.epi, g.m, g.n, g.k, (int)g.ta, (int)g.tb, (int)g.ab_type, (int)g.d_type, g.C != nullptr};
   auto& cache = algo_cache();
   auto it = cache.find(key);
   if (it == cache.end()) {
@@ -118,27 +119,35 @@ void run(const Gemm& g, int device, hipStream_t stream) {
     LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
     uint64_t wsz = kWorkspace;
     LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz)));
-    hipblasLtMatmulHeuristicResult_t res[8];
+    hipblasLtMatmulHeuristicResult_t res[kCandidates];
     int nres = 0;
-    LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(c.handle, op, la, lb, ld, ld, pref, 8, res, &nres));
+    LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(c.handle, op, la, lb, ld, ld, pref, kCandidates, res, &nres));
     hipblasLtMatmulPreferenceDestroy(pref);
     TORCH_CHECK(nres > 0, "gemm_lt: hipBLASLt has no algorithm for this GEMM / epilogue");
     // time the candidates once (each 3 launches after one warm-up); the output buffers are
     // scratch until the real launch below overwrites them
     int best = 0;
     if (nres > 1) {
+      // when accumulating (C = D) the candidates write a scratch D so timing never disturbs
+      // the caller's output; otherwise D is overwritten by the final launch anyway
+      at::Tensor scratch;
+      if (g.C)
+        scratch = at::empty({g.m * g.n * (g.d_type == HIP_R_32F ? 4 : 2)},
+                            at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device));
+      void* sd = g.C ? scratch.data_ptr() : g.D;
+      const void* sc = g.C ? sd : nullptr;
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
       hipEventCreate(&e1);
       float best_ms = 1e30f;
       for (int i = 0; i < nres; ++i) {
         if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
-        if (hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, g.C ? g.C : g.D, ld, g.D, ld, &res[i].algo,
+        if (hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, sc ? sc : sd, ld, sd, ld, &res[i].algo,
                             c.workspace.data_ptr(), kWorkspace, stream) != HIPBLAS_STATUS_SUCCESS)
           continue;
         hipEventRecord(e0, stream);
         for (int r = 0; r < 3; ++r)
-          hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, g.C ? g.C : g.D, ld, g.D, ld, &res[i].algo,
+          hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, sc ? sc : sd, ld, sd, ld, &res[i].algo,
                           c.workspace.data_ptr(), kWorkspace, stream);
         hipEventRecord(e1, stream);
         hipEventSynchronize(e1);
@@ -229,6 +238,37 @@ at::Tensor dgrad_dgelu_lt(at::Tensor dy, at::Tensor w, at::Tensor aux, at::Tenso
   return dp;
 }
 
+// General row-major GEMM C[M,N] = op(A) op(B) (+ C when accumulate), op(A) = A or A^T.
+// A is [M,K] (or [K,M] with trans_a), B is [K,N] (or [N,K] with trans_b).  Passed to hipBLASLt
+// as the column-major product C^T = op(B)^T op(A)^T; the algorithm is autotuned per shape.
+at::Tensor gemm_lt(at::Tensor a, at::Tensor b, bool trans_a, bool trans_b, c10::optional<at::Tensor> out,
+                   bool accumulate) {
+  check2d(a, "a");
+  check2d(b, "b");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf),
+              "gemm_lt: bf16/fp16 operands of one dtype");
+  const int64_t M = trans_a ? a.size(1) : a.size(0), K = trans_a ? a.size(0) : a.size(1);
+  const int64_t N = trans_b ? b.size(0) : b.size(1);
+  TORCH_CHECK((trans_b ? b.size(1) : b.size(0)) == K, "gemm_lt: inner dimensions differ");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  at::Tensor c;
+  if (out.has_value()) {
+    c = *out;
+    check2d(c, "out");
+    TORCH_CHECK(c.size(0) == M && c.size(1) == N && (c.scalar_type() == a.scalar_type() || c.scalar_type() == at::kFloat),
+                "gemm_lt: out must be [M, N] of the operand dtype or fp32");
+  } else {
+    TORCH_CHECK(!accumulate, "gemm_lt: accumulate needs out");
+    c = at::empty({M, N}, a.options());
+  }
+  Gemm g{trans_b ? HIPBLAS_OP_T : HIPBLAS_OP_N, trans_a ? HIPBLAS_OP_T : HIPBLAS_OP_N, N, M, K,
+         trans_b ? K : N, trans_a ? M : K, N, dtype_of(a), dtype_of(c), HIPBLASLT_EPILOGUE_DEFAULT,
+         b.data_ptr(), a.data_ptr(), accumulate ? c.data_ptr() : nullptr, c.data_ptr(), nullptr, dtype_of(a),
+         nullptr, 0};
+  run(g, a.get_device(), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  return c;
+}
+
 // Number of heuristic algorithms hipBLASLt offers for a bf16 TN GEMM [m,n,k] with epilogue
 // code `epi` (diagnostics: epilogue availability differs between hipBLASLt builds).
 int64_t lt_algo_count(int64_t m, int64_t n, int64_t k, int64_t epi, bool with_aux) {
@@ -271,5 +311,7 @@ int64_t lt_algo_count(int64_t m, int64_t n, int64_t k, int64_t epi, bool with_au
 void register_gemm_lt(pybind11::module& m) {
   m.def("lt_algo_count", &lt_algo_count);
   m.def("linear_lt", &linear_lt);
+  m.def("gemm_lt", &gemm_lt, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("trans_a") = false,
+        pybind11::arg("trans_b") = false, pybind11::arg("out") = pybind11::none(), pybind11::arg("accumulate") = false);
   m.def("dgrad_dgelu_lt", &dgrad_dgelu_lt);
 }

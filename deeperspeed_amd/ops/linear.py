@@ -44,9 +44,24 @@ WGRAD_NT_MIN_NUMEL = int(float(os.environ.get("DSA_WGRAD_NT_MIN_NUMEL", "1e7")))
 # tokens (1.65 GB) keeps the token-major formulation instead of adding its copy to the peak
 WGRAD_NT_MAX_BYTES = int(float(os.environ.get("DSA_WGRAD_NT_MAX_BYTES", "1.2e9")))
 # input gradient dx = dy W from W^T [in, out] (reduction-contiguous, one HIP transpose of the
-# weight per use): hipBLASLt ~1.45 vs ~1.28 PF/s at the GPT-NeoX-20B shapes
+# weight per use): hipBLASLt ~1.45 vs ~1.28 PF/s at the GPT-NeoX-20B shapes, 1.05-1.2 vs
+# 0.98-1.03 PF/s at BERT-Large's (profiles/r2m_gemm_shapes_bert_neox.md)
 DGRAD_NT = os.environ.get("DSA_DGRAD_NT", "1") != "0"
+DGRAD_NT_MIN_NUMEL = int(float(os.environ.get("DSA_DGRAD_NT_MIN_NUMEL", "1e6")))
+# split-K weight gradient for small weights over many tokens: [out, in] gives too few 256x256
+# output tiles to fill 256 CUs (BERT-Large: 16-64 tiles at 8k tokens, 300-800 TF/s), so the
+# tokens are cut into WGRAD_SPLIT batches of one strided-batched GEMM whose partial products
+# are summed in fp32 (1.25-1.6x at the BERT-Large shapes, same profile).  DSA_WGRAD_SPLIT=1 off.
+WGRAD_SPLIT = int(os.environ.get("DSA_WGRAD_SPLIT", "4"))
+WGRAD_SPLIT_MAX_TILES = 128
+WGRAD_SPLIT_MIN_TOKENS = 4096
 
+
+# DSA_LINEAR_LT=1: forward GEMMs through the autotuned hipBLASLt wrapper (bias in the
+# epilogue).  Bias-free microbenchmarks favour it by up to 6 % at the GPT-NeoX-20B shapes, but
+# the whole 20B step measured 1.3 % slower with it (same box, profiles/r2n_linear_lt_ab.md), so
+# torch's F.linear stays the default.
+LINEAR_LT = os.environ.get("DSA_LINEAR_LT", "0") == "1"
 
 _count = [0]  # in-place accumulations performed (tests / diagnostics)
 _nt_count = [0]  # wgrads formed from transposed operands
@@ -83,9 +98,26 @@ def _nt_operands(g2, x2, bias_grad):
     return native.transpose2d(g2, bias_grad, accum=True), native.transpose2d(x2)
 
 
+def _split_k(g2, x2):
+    """Number of token batches for the split-K weight gradient (1 = one plain GEMM)."""
+    M, out, inp = g2.size(0), g2.size(1), x2.size(1)
+    if (WGRAD_SPLIT <= 1 or not g2.is_cuda or M < WGRAD_SPLIT_MIN_TOKENS or M % WGRAD_SPLIT
+            or not g2.is_contiguous() or not x2.is_contiguous()):
+        return 1
+    tiles = -(-out // 256) * -(-inp // 256)
+    return WGRAD_SPLIT if tiles <= WGRAD_SPLIT_MAX_TILES else 1
+
+
+def _wgrad_split(g2, x2, s):
+    """dy^T x as s strided-batched partial GEMMs over token slices, summed in fp32."""
+    M = g2.size(0)
+    part = torch.bmm(g2.view(s, M // s, g2.size(1)).transpose(1, 2), x2.view(s, M // s, x2.size(1)))
+    return part.sum(0, dtype=torch.float32)
+
+
 def input_grad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """dx = g2 @ W for g2 = dy [M, out], W [out, in]."""
-    if (DGRAD_NT and g2.is_cuda and g2.dtype == weight.dtype and weight.numel() >= WGRAD_NT_MIN_NUMEL
+    if (DGRAD_NT and g2.is_cuda and g2.dtype == weight.dtype and weight.numel() >= DGRAD_NT_MIN_NUMEL
             and g2.size(0) >= 1024):
         from . import native
         if native.transpose_supported(weight):
@@ -103,6 +135,18 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     has_b = bias is not None and need_b
     fuse = FUSE_WGRAD and need_w and (not has_b or _bound_grad(bias) is not None)
     gw = _bound_grad(weight) if fuse else None
+    split = _split_k(g2, x2) if need_w else 1
+    if split > 1:
+        dw32 = _wgrad_split(g2, x2, split)
+        if has_b:
+            db = g2.sum(0)
+        if gw is not None and gw.is_contiguous() and (not has_b or _bound_grad(bias) is not None):
+            gw.add_(dw32)
+            if has_b:
+                bias.grad.add_(db)
+            _count[0] += 1
+            return None, None
+        return dw32.to(weight.dtype), db
     if gw is not None and gw.is_contiguous():
         nt = _nt_operands(g2, x2, bias.grad if has_b else None)
         if nt is not None:
@@ -126,12 +170,23 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     return dw, db
 
 
+def forward_gemm(x, weight, bias=None):
+    """y = x W^T + b; on the GPU through the autotuned hipBLASLt wrapper."""
+    if (LINEAR_LT and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and weight.dtype == x.dtype
+            and weight.is_contiguous() and x.is_contiguous() and x.numel() > 0
+            and (bias is None or (bias.dtype == x.dtype and bias.is_contiguous()))):
+        from . import native
+        y = native.hip_ops().linear_lt(x.view(-1, x.shape[-1]), weight, bias, None, False, None)
+        return y.view(*x.shape[:-1], weight.shape[0])
+    return F.linear(x, weight, bias)
+
+
 class _AccumLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
-        return F.linear(x, weight, bias)
+        return forward_gemm(x, weight, bias)
 
     @staticmethod
     def backward(ctx, g):
@@ -173,7 +228,7 @@ def linear(x, weight, bias=None):
     """F.linear whose weight gradient accumulates in place when a gradient is bound."""
     if torch.is_grad_enabled() and weight.requires_grad:
         return _AccumLinear.apply(x, weight, bias)
-    return F.linear(x, weight, bias)
+    return forward_gemm(x, weight, bias)
 
 
 def grad_only_linear(x, weight, bias=None):

@@ -28,6 +28,7 @@ import torch.nn.functional as F
 
 from .. import native
 from ..attention import masked_softmax
+from ..linear import linear as _linear
 
 
 class TransformerConfig:
@@ -138,7 +139,7 @@ class DeepSpeedTransformerFunction:
         x = input
         ln = native.layer_norm_invertible if getattr(cfg, "normalize_invertible", False) else native.layer_norm
         inp = ln(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
-        qkv = F.linear(inp, attn_qkvw, attn_qkvb)
+        qkv = _linear(inp, attn_qkvw, attn_qkvb)
         fast = _use_head_kernels(qkv, hd)
         if fast:
             q, k, v = _SplitHeads.apply(qkv, nh)  # contiguous [B, nh, S, hd]: batched GEMMs without copies
@@ -167,11 +168,11 @@ class DeepSpeedTransformerFunction:
                 probs = native.dropout(probs, cfg.attn_dropout_ratio, training, gen)
                 ctx = torch.matmul(probs, v)
             ctx = _MergeHeads.apply(ctx) if fast else ctx.transpose(1, 2).reshape(B, S, Hd)
-        attn_out = F.linear(ctx, attn_ow)
+        attn_out = _linear(ctx, attn_ow)
         add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen)
         ff1_inp = ln(add_res, attn_nw, attn_nb, eps)
-        inter = _gelu_tanh(F.linear(ff1_inp, inter_w), inter_b)
-        out = F.linear(inter, output_w)
+        inter = _gelu_tanh(_linear(ff1_inp, inter_w), inter_b)
+        out = _linear(inter, output_w)
         if cfg.pre_layer_norm:
             out = native.bias_dropout_residual(out, output_b, add_res, cfg.hidden_dropout_ratio, training, gen)
         else:

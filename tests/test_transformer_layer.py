@@ -191,8 +191,8 @@ def test_encoder_flash_matches_materialised_path(monkeypatch, pre_ln):
         y = layer(x, _mask(B, S).to(dev, torch.bfloat16))
         y.float().pow(2).sum().backward()
         res[flash] = (y.detach().float(), x.grad.float(), layer.attn_qkvw.grad.float(), layer.attn_ow.grad.float())
-    for a, b in zip(res[False], res[True]):
-        assert (a - b).abs().max().item() <= 3e-2 * max(1.0, a.abs().max().item())
+    for a, b in zip(res[False], res[True]):  # bf16 activations: a few ulp of the largest entry
+        assert (a - b).abs().max().item() <= 5e-2 * max(1.0, a.abs().max().item())
 
 
 def test_encoder_flash_keep_mask_statistics():
