@@ -301,6 +301,28 @@ def main():
         torch.cuda.reset_peak_memory_stats()
         return n
 
+    def check_stash(n):
+        """Safety check after the first step WITH the stash: if the allocator's reserved peak
+        came within DSA_STASH_FLOOR_GIB (default 1.5) of the HBM budget, give stashed layers
+        back (first-stashed first) until the measured overshoot is covered, so allocator
+        variance on another box cannot push a timed step into an out-of-memory error."""
+        if n <= 0:
+            return n
+        layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
+        per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
+        floor = float(os.environ.get("DSA_STASH_FLOOR_GIB", "1.5")) * 2**30
+        over = torch.cuda.max_memory_reserved() - (hbm / share - floor)
+        if over <= 0:
+            return n
+        drop = min(n, int(-(-over // per_layer)))
+        for m in layers[len(layers) - n: len(layers) - n + drop]:
+            m.attention.stash_outputs = False
+            m.attention._stash.clear()
+        torch.cuda.empty_cache()
+        log(f"stash safety: reserved peak {torch.cuda.max_memory_reserved() / 2**30:.1f} GiB is within "
+            f"{floor / 2**30:.1f} GiB of the budget; {drop} layer(s) back to full recompute ({n - drop} stashed)")
+        return n - drop
+
     for i in range(args.warmup):
         ts = time.time()
         loss, ph = timed_step()
@@ -312,6 +334,8 @@ def main():
                if hasattr(engine.optimizer, "_pool") else ""))
         if i == 0 and args.warmup >= 2:
             stashed = plan_stash()
+        elif i == 1 and stashed:
+            stashed = check_stash(stashed)
 
     dist.barrier()
     torch.cuda.synchronize()
