@@ -207,6 +207,20 @@ std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tenso
 }
 
 // ----------------------------------------------------------------------------- bias + gelu
+// out (+)= part.sum(0) for part [S, ...] 16-bit contiguous; out of part's dtype or fp32, numel = part[0].numel()
+Tensor sum_slices(Tensor part, Tensor out, bool accumulate) {
+  check_dev(part, "sum_slices"); check_dev(out, "sum_slices");
+  TORCH_CHECK(part.is_contiguous() && out.is_contiguous() && part.dim() >= 2, "sum_slices: contiguous part [S, ...]");
+  TORCH_CHECK(part.scalar_type() == at::kBFloat16 || part.scalar_type() == at::kHalf, "sum_slices: 16-bit partials");
+  TORCH_CHECK(out.scalar_type() == part.scalar_type() || out.scalar_type() == at::kFloat, "sum_slices: out dtype");
+  const int64_t n = part.numel() / part.size(0);
+  TORCH_CHECK(out.numel() == n && n % 8 == 0, "sum_slices: out must hold one slice (numel % 8 == 0)");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
+  dsa::launch_sum_slices(part.data_ptr(), (int)part.size(0), n, out.data_ptr(), out.scalar_type() == at::kFloat,
+                         accumulate ? 1 : 0, dcode(part), cur_stream());
+  return out;
+}
+
 Tensor add3(Tensor a, Tensor b, OptT c) {
   check_dev(a, "add3"); check_dev(b, "add3");
   TORCH_CHECK(a.sizes() == b.sizes() && a.scalar_type() == b.scalar_type() && a.is_contiguous() && b.is_contiguous(),
@@ -257,17 +271,28 @@ std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, OptT b, bool approx) {
 }
 
 // Sum over all leading dims -> [C]
-Tensor colsum(Tensor x) {
+// out[C] (+)= column sums of x [..., C]; a fresh out when none is given
+Tensor colsum(Tensor x, OptT out_opt, bool accumulate) {
   check_dev(x, "x");
   const int64_t C = x.size(-1);
   const int64_t rows = x.numel() / C;
   const int dt = dcode(x);
   TORCH_CHECK(C % (dt == dsa::kCodeF32 ? 4 : 8) == 0, "colsum: last dim must be a multiple of 16 bytes");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  Tensor out = at::empty({C}, x.options());
+  Tensor out;
+  if (out_opt.has_value()) {
+    out = *out_opt;
+    check_dev(out, "colsum out");
+    TORCH_CHECK(out.numel() == C && out.is_contiguous() && out.scalar_type() == x.scalar_type(),
+                "colsum: out must be a contiguous [C] tensor of x's dtype");
+  } else {
+    TORCH_CHECK(!accumulate, "colsum: accumulate needs out");
+    out = at::empty({C}, x.options());
+  }
   Tensor partial =
       at::empty({(int64_t)dsa::bias_gelu_row_chunks(rows, (int)C, dt) * C}, x.options().dtype(at::kFloat));
-  dsa::launch_colsum(x.data_ptr(), out.data_ptr(), partial.data_ptr<float>(), rows, (int)C, 0, dt, cur_stream());
+  dsa::launch_colsum(x.data_ptr(), out.data_ptr(), partial.data_ptr<float>(), rows, (int)C, accumulate ? 1 : 0, dt,
+                     cur_stream());
   return out;
 }
 
@@ -773,6 +798,7 @@ void register_gemm_lt(pybind11::module& m);  // gemm_lt.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_gemm_lt(m);
+  m.def("sum_slices", &sum_slices);
   m.def("add3", &add3, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c") = pybind11::none());
   m.def("sparse_flash_fwd", &sparse_flash_fwd);
   m.def("flash_attn_fwd_ex", &flash_attn_fwd_ex);
@@ -808,7 +834,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
-  m.def("colsum", &colsum);
+  m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("heads_split", &heads_split);
   m.def("heads_merge", &heads_merge);
   m.def("swap12", &swap12);

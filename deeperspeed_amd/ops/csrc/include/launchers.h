@@ -47,6 +47,8 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
                    const void* dres, void* dx, void* dgamma, void* dbeta, float* partial, int64_t rows, int H,
                    int dt, hipStream_t s);
 // y = a + b (+ c), n % (16 B / elem) == 0
+void launch_sum_slices(const void* part, int S, int64_t n, void* out, bool out_f32, int accum, int dt,
+                       hipStream_t s);
 void launch_add3(const void* a, const void* b, const void* c, void* y, int64_t n, int dt, hipStream_t s);
 void launch_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, int C, int approx, int dt,
                           hipStream_t s);

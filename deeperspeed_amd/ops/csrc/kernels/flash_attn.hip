@@ -806,10 +806,21 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
         }
       }
       if constexpr (DROP) {  // dV from the dropped P; dP = dP_dropped * Z / (1 - p)
+        // lanes l and l^1 hold keys 2j and 2j+1 of the same 16 queries and need the same 16
+        // pair draws: each computes 8 and takes the other 8 from its neighbour (DPP quad_perm)
+        uint32_t own[8], nbr[8];
+        const int half = (mykey & 1) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = half + k;
+          own[k] = drop_pair(hb, i0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3), S >> 1, mykey >> 1);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nbr[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)own[k], 0xB1, 0xF, 0xF, true);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-          const uint32_t x = drop_pair(hb, i0 + qi, S >> 1, mykey >> 1);
+          const uint32_t x = ((r >> 3) == (mykey & 1)) ? own[r & 7] : nbr[r & 7];
           const float zr = ((x >> dshift) & 0xffffu) < ex.thresh ? 0.f : ex.rscale;
           dsv[r] = pv[r] * fmaf(pacc[r], zr, -del_s[qi]);
           pv[r] *= zr;

@@ -163,9 +163,16 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(const T* __restrict_
 
 // out[c] = sum_r partial[r][c] over R rows, C columns; written in dtype T
 // (optionally accumulated into existing out when `accum`).
+// blockIdx.y == 1 sums a second partial block (partial + second_off) into out2 in the same launch
+// (LayerNorm's gamma and beta gradients).
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ partial, int R, int C,
-                                                     T* __restrict__ out, int accum) {
+                                                     T* __restrict__ out, int accum, int64_t second_off = 0,
+                                                     T* __restrict__ out2 = nullptr) {
+  if (blockIdx.y == 1) {
+    partial += second_off;
+    out = out2;
+  }
   // 64 columns x 4 row-groups per block; lanes own columns -> coalesced reads.
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -331,10 +338,8 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
     DSA_DISPATCH_NV(nv, NV, hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(grid), dim3(LN_THREADS), 0, s,
                        (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
                        partial, rows, H));
-    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, s, partial, grid, H,
-                       (T*)dgamma, 0);
-    if (dbeta) hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64), dim3(256), 0, s,
-                                  partial + (int64_t)grid * H, grid, H, (T*)dbeta, 0));
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64, dbeta ? 2 : 1), dim3(256), 0, s, partial, grid, H,
+                       (T*)dgamma, 0, (int64_t)grid * H, (T*)dbeta));
 }
 
 void launch_add3(const void* a, const void* b, const void* c, void* y, int64_t n, int dt, hipStream_t s) {
@@ -407,6 +412,62 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const T* __restrict
   float* p = partial + (int64_t)blockIdx.y * C + c0;
 #pragma unroll
   for (int j = 0; j < VN; j += 4) *reinterpret_cast<float4*>(p + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+}
+
+// out[i] (+)= sum_s part[s][i]: the split-K weight-gradient partials folded in one pass with fp32
+// accumulation; out in the partials' dtype or fp32 (OUTF).  n % (16 / sizeof(T)) == 0.
+template <typename T, bool OUTF>
+__global__ void __launch_bounds__(256) sum_slices_kernel(const T* __restrict__ part, int S, int64_t n,
+                                                         void* __restrict__ out, int accum) {
+  constexpr int VN = Vec16<T>::N;
+  const int64_t nvec = n / VN;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    float acc[VN];
+    if (accum) {
+      if constexpr (OUTF) {
+#pragma unroll
+        for (int j = 0; j < VN; j += 4) {
+          const float4 o = *reinterpret_cast<const float4*>((const float*)out + i * VN + j);
+          acc[j] = o.x; acc[j + 1] = o.y; acc[j + 2] = o.z; acc[j + 3] = o.w;
+        }
+      } else {
+        Vec16<T>::load((const T*)out + i * VN, acc);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) acc[j] = 0.f;
+    }
+    for (int sl = 0; sl < S; ++sl) {
+      float v[VN];
+      Vec16<T>::load(part + sl * n + i * VN, v);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) acc[j] += v[j];
+    }
+    if constexpr (OUTF) {
+#pragma unroll
+      for (int j = 0; j < VN; j += 4)
+        *reinterpret_cast<float4*>((float*)out + i * VN + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+    } else {
+      Vec16<T>::store((T*)out + i * VN, acc);
+    }
+  }
+}
+
+void launch_sum_slices(const void* part, int S, int64_t n, void* out, bool out_f32, int accum, int dt,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  const int vn = dt == kF32 ? 4 : 8;
+  int64_t g = (n / vn + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  DSA_DISPATCH_T(dt, T,
+    if (out_f32)
+      hipLaunchKernelGGL((sum_slices_kernel<T, true>), dim3((unsigned)g), dim3(256), 0, s, (const T*)part, S, n, out,
+                         accum);
+    else
+      hipLaunchKernelGGL((sum_slices_kernel<T, false>), dim3((unsigned)g), dim3(256), 0, s, (const T*)part, S, n, out,
+                         accum));
 }
 
 void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s) {

@@ -108,11 +108,16 @@ def _split_k(g2, x2):
     return WGRAD_SPLIT if tiles <= WGRAD_SPLIT_MAX_TILES else 1
 
 
-def _wgrad_split(g2, x2, s):
-    """dy^T x as s strided-batched partial GEMMs over token slices, summed in fp32."""
+def _wgrad_split(g2, x2, s, out=None):
+    """dy^T x as s strided-batched partial GEMMs over token slices, folded with fp32 accumulation
+    by one HIP pass into `out` (accumulated: the bound gradient) or into a fresh tensor."""
     M = g2.size(0)
     part = torch.bmm(g2.view(s, M // s, g2.size(1)).transpose(1, 2), x2.view(s, M // s, x2.size(1)))
-    return part.sum(0, dtype=torch.float32)
+    from . import native
+    if out is not None:
+        return native.hip_ops().sum_slices(part, out, True)
+    return native.hip_ops().sum_slices(part, torch.empty(part.shape[1:], dtype=part.dtype, device=part.device),
+                                       False)
 
 
 def input_grad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
@@ -137,16 +142,14 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     gw = _bound_grad(weight) if fuse else None
     split = _split_k(g2, x2) if need_w else 1
     if split > 1:
-        dw32 = _wgrad_split(g2, x2, split)
-        if has_b:
-            db = g2.sum(0)
-        if gw is not None and gw.is_contiguous() and (not has_b or _bound_grad(bias) is not None):
-            gw.add_(dw32)
+        from . import native
+        if gw is not None and gw.is_contiguous() and (not has_b or bias.grad.is_contiguous()):
+            _wgrad_split(g2, x2, split, out=gw)
             if has_b:
-                bias.grad.add_(db)
+                native.colsum(g2, bias.grad, accumulate=True)
             _count[0] += 1
             return None, None
-        return dw32.to(weight.dtype), db
+        return _wgrad_split(g2, x2, split), (native.colsum(g2) if has_b else None)
     if gw is not None and gw.is_contiguous():
         nt = _nt_operands(g2, x2, bias.grad if has_b else None)
         if nt is not None:

@@ -233,10 +233,17 @@ def sumsq_accumulate(x: torch.Tensor, out: torch.Tensor):
     return out
 
 
-def colsum(x: torch.Tensor) -> torch.Tensor:
+def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False) -> torch.Tensor:
+    """Column sums of x [..., C] (fp32 accumulation) into a fresh [C] tensor, or into `out`
+    (added to it when `accumulate`)."""
     if x.is_cuda:
-        return hip_ops().colsum(x.contiguous())
-    return x.reshape(-1, x.shape[-1]).float().sum(0).to(x.dtype)
+        return hip_ops().colsum(x.contiguous(), out, accumulate)
+    r = x.reshape(-1, x.shape[-1]).float().sum(0)
+    if out is None:
+        return r.to(x.dtype)
+    if accumulate:
+        r += out.float()
+    return out.copy_(r)
 
 
 def transpose_supported(x: torch.Tensor) -> bool:

@@ -548,8 +548,10 @@ def test_transformer_layer_head_kernels_match_permute_path(monkeypatch):
         out = layer(xi, mask)
         out.float().pow(2).sum().backward()
         res[fast] = [out.detach().float(), xi.grad.float()] + [p.grad.float() for p in layer.parameters()]
+    # the fast path also takes the fused encoder attention: bf16 round-off differs from the
+    # materialised softmax path, so compare against each tensor's magnitude
     for a, b in zip(res[True], res[False]):
-        torch.testing.assert_close(a, b, atol=2e-2, rtol=2e-2)
+        assert (a - b).abs().max().item() <= 3e-2 * max(1.0, b.abs().max().item())
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
@@ -633,3 +635,25 @@ def test_encoder_flash_dropout_only_and_eval():
     o2 = native.flash_attention_encoder(q, k, v, None, 0.125, 0.1, True, generator=gen)
     assert torch.equal(o1, o2)  # same generator state -> same keep mask
     assert (o1.float() - ref).abs().max().item() > 1e-2  # dropout was applied
+
+
+@pytest.mark.parametrize("out_f32", [False, True])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_sum_slices_and_colsum_accumulate(out_f32, accumulate):
+    """Split-K fold (sum of bf16 partial slices, fp32 accumulation) and column sums into /
+    onto an existing output."""
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(0)
+    dev = _dev()
+    part = torch.randn(4, 384, 1024, device=dev, dtype=torch.bfloat16)
+    out = torch.randn(384, 1024, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    ref = part.float().sum(0) + (out.float() if accumulate else 0.0)
+    native.hip_ops().sum_slices(part, out, accumulate)
+    tol = 1e-5 if out_f32 else 2e-2
+    assert (out.float() - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item())
+    x = torch.randn(3000, 1024, device=dev, dtype=torch.bfloat16)
+    acc = torch.randn(1024, device=dev, dtype=torch.bfloat16)
+    want = x.float().sum(0) + (acc.float() if accumulate else 0.0)
+    got = native.colsum(x, acc, accumulate=accumulate)
+    assert got.data_ptr() == acc.data_ptr()
+    assert (got.float() - want).abs().max().item() <= 2e-2 * want.abs().max().item()
