@@ -710,6 +710,66 @@ std::vector<Tensor> flash_attn_bwd_ex(Tensor dout, Tensor q, Tensor k, Tensor v,
   return {dq, dk, dv};
 }
 
+// The same encoder attention reading q, k, v straight from the fused QKV projection output
+// qkv [B, S, 3, H, D] (contiguous) and writing o [B, S, H, D]; the backward writes dqkv in the
+// qkv layout, so no head split / merge copies are needed around the kernels.
+static void check_qkv(const Tensor& qkv, const char* what) {
+  check_dev(qkv, what);
+  TORCH_CHECK(qkv.dim() == 5 && qkv.size(2) == 3 && qkv.is_contiguous() && qkv.scalar_type() != at::kFloat, what,
+              ": qkv must be a contiguous 16-bit [B, S, 3, H, D] tensor");
+}
+
+std::vector<Tensor> flash_attn_qkv_fwd(Tensor qkv, c10::optional<Tensor> kbias, double scale, double p_drop,
+                                       int64_t seed) {
+  check_qkv(qkv, "flash_attn_qkv_fwd");
+  const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
+  TORCH_CHECK(S % 8 == 0 && (D == 64 || D == 128), "flash_attn_qkv_fwd: S % 8 == 0 and head dim 64 or 128");
+  TORCH_CHECK(p_drop >= 0.0 && p_drop < 1.0, "flash_attn_qkv_fwd: dropout probability in [0, 1)");
+  if (kbias.has_value()) {
+    check_dev(*kbias, "flash_attn_qkv_fwd");
+    TORCH_CHECK(kbias->scalar_type() == at::kFloat && kbias->is_contiguous() && kbias->numel() == B * S,
+                "flash_attn_qkv_fwd: kbias must be contiguous fp32 [B, S]");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  Tensor o = at::empty({B, S, H, D}, qkv.options());
+  Tensor lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+  const char* base = static_cast<const char*>(qkv.data_ptr());
+  const int64_t hd = H * D * qkv.element_size();
+  dsa::launch_flash_fwd_ex(base, base + hd, base + 2 * hd, o.data_ptr(), lse.data_ptr<float>(), (int)(B * H), (int)S,
+                           (int)D, (float)scale, kbias ? kbias->data_ptr<float>() : nullptr, (int)H, (float)p_drop,
+                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D);
+  return {o, lse};
+}
+
+Tensor flash_attn_qkv_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, c10::optional<Tensor> kbias, double scale,
+                          double p_drop, int64_t seed) {
+  check_qkv(qkv, "flash_attn_qkv_bwd");
+  const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
+  for (auto* t : {&dout, &o}) {
+    check_dev(*t, "flash_attn_qkv_bwd");
+    TORCH_CHECK(t->sizes() == at::IntArrayRef({B, S, H, D}) && t->scalar_type() == qkv.scalar_type() &&
+                    t->is_contiguous(), "flash_attn_qkv_bwd: dout/o must be contiguous [B, S, H, D]");
+  }
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * S,
+              "flash_attn_qkv_bwd: lse");
+  if (kbias.has_value()) {
+    check_dev(*kbias, "flash_attn_qkv_bwd");
+    TORCH_CHECK(kbias->scalar_type() == at::kFloat && kbias->is_contiguous() && kbias->numel() == B * S,
+                "flash_attn_qkv_bwd: kbias");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  Tensor dqkv = at::empty_like(qkv);
+  Tensor delta = at::empty_like(lse);
+  const char* base = static_cast<const char*>(qkv.data_ptr());
+  char* dbase = static_cast<char*>(dqkv.data_ptr());
+  const int64_t hd = H * D * qkv.element_size();
+  dsa::launch_flash_bwd_ex(dout.data_ptr(), base, base + hd, base + 2 * hd, o.data_ptr(), lse.data_ptr<float>(),
+                           delta.data_ptr<float>(), dbase, dbase + hd, dbase + 2 * hd, (int)(B * H), (int)S, (int)D,
+                           (float)scale, kbias ? kbias->data_ptr<float>() : nullptr, (int)H, (float)p_drop,
+                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D);
+  return dqkv;
+}
+
 // Block-sparse flash attention.  q,k,v [B, H, S, D] (S % 64 == 0); LUT tensors int32 on the
 // device (see flash_attn.hip): rowptr [Hl * S/64 + 1], cols / masks [nnz]; the transposed LUT
 // colptr / rows / masks_t for the backward.  `shift` = min(6, log2(layout block)).
@@ -803,6 +863,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sparse_flash_fwd", &sparse_flash_fwd);
   m.def("flash_attn_fwd_ex", &flash_attn_fwd_ex);
   m.def("flash_attn_bwd_ex", &flash_attn_bwd_ex);
+  m.def("flash_attn_qkv_fwd", &flash_attn_qkv_fwd);
+  m.def("flash_attn_qkv_bwd", &flash_attn_qkv_bwd);
   m.def("sparse_flash_bwd", &sparse_flash_bwd);
   m.def("onebit_worker_compress", &onebit_worker_compress);
   m.def("onebit_server_compress", &onebit_server_compress);

@@ -127,11 +127,11 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
 // min(6, log2(layout block))
 void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh);
+                         int onh, int inh = 0, int64_t ild = 0);
 void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const void* v, const void* o,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh);
+                         int onh, int inh = 0, int64_t ild = 0);
 void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
                              const int* cols, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
                              float scale, int shift, int dt, hipStream_t s, int onh = 0);

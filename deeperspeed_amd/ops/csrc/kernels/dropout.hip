@@ -3,6 +3,8 @@
 // (offset + i/4) under key = seed, so any launch is reproducible from (seed, offset) alone:
 // activation-checkpoint recomputation and the backward pass never need stored RNG state.
 // Masks are stored as uint8 (1 = keep); kept values are scaled by 1/(1-p).
+#include <initializer_list>
+
 #include "../include/dsa_common.h"
 #include "../include/launchers.h"
 
@@ -84,6 +86,118 @@ __global__ void __launch_bounds__(256) dropout_bwd_kernel(const T* __restrict__ 
     Conv<T>::store(dx, i, mask[i] ? Conv<T>::load(dy, i) * scale : 0.f);
 }
 
+// ---- 16-byte vector forms (VN = 8 for 16-bit types, 4 for fp32): the same element -> Philox
+// counter mapping as above, so masks and outputs are bit-identical to the scalar kernels; the
+// mask of a vector is stored as one 8- (or 4-) byte word.  Need n % VN == 0 (and C % VN == 0
+// for the bias) and 16-byte aligned tensors; the launchers fall back to the scalar kernels.
+template <int VN>
+__device__ __forceinline__ void draws(uint64_t seed, uint64_t offset, int64_t v, float (&u)[VN]) {
+#pragma unroll
+  for (int q = 0; q < VN / 4; ++q) {
+    float t[4];
+    uniform4(seed, offset, (uint64_t)v * (VN / 4) + q, t);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[4 * q + k] = t[k];
+  }
+}
+
+template <int VN>
+__device__ __forceinline__ void store_mask(uint8_t* m, const bool (&keep)[VN]) {
+  uint32_t w[2] = {0u, 0u};
+#pragma unroll
+  for (int k = 0; k < VN; ++k) w[k >> 2] |= (uint32_t)keep[k] << (8 * (k & 3));
+  if constexpr (VN == 8) *reinterpret_cast<uint2*>(m) = make_uint2(w[0], w[1]);
+  else *reinterpret_cast<uint32_t*>(m) = w[0];
+}
+
+template <int VN>
+__device__ __forceinline__ void load_mask(const uint8_t* m, bool (&keep)[VN]) {
+  uint32_t w[2];
+  if constexpr (VN == 8) {
+    const uint2 v = *reinterpret_cast<const uint2*>(m);
+    w[0] = v.x; w[1] = v.y;
+  } else {
+    w[0] = *reinterpret_cast<const uint32_t*>(m);
+    w[1] = 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < VN; ++k) keep[k] = ((w[k >> 2] >> (8 * (k & 3))) & 0xffu) != 0u;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_fwd_vec_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                              uint8_t* __restrict__ mask, int64_t n, float p,
+                                                              uint64_t seed, uint64_t offset) {
+  constexpr int VN = Vec16<T>::N;
+  const float scale = 1.f / (1.f - p);
+  const int64_t nvec = n / VN, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float u[VN], a[VN];
+    bool keep[VN];
+    draws<VN>(seed, offset, v, u);
+    Vec16<T>::load(x + v * VN, a);
+#pragma unroll
+    for (int k = 0; k < VN; ++k) {
+      keep[k] = u[k] >= p;
+      a[k] = keep[k] ? a[k] * scale : 0.f;
+    }
+    Vec16<T>::store(y + v * VN, a);
+    store_mask<VN>(mask + v * VN, keep);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bias_dropout_residual_vec_kernel(const T* __restrict__ x,
+                                                                        const T* __restrict__ b,
+                                                                        const T* __restrict__ res,
+                                                                        T* __restrict__ y, uint8_t* __restrict__ mask,
+                                                                        int64_t n, int C, float p, uint64_t seed,
+                                                                        uint64_t offset) {
+  constexpr int VN = Vec16<T>::N;
+  const float scale = 1.f / (1.f - p);
+  const int64_t nvec = n / VN, stride = (int64_t)gridDim.x * blockDim.x;
+  const int cvec = C / VN;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float u[VN], a[VN], bb[VN], r[VN];
+    bool keep[VN];
+    draws<VN>(seed, offset, v, u);
+    Vec16<T>::load(x + v * VN, a);
+    Vec16<T>::load(b + (int)(v % cvec) * VN, bb);
+    Vec16<T>::load(res + v * VN, r);
+#pragma unroll
+    for (int k = 0; k < VN; ++k) {
+      keep[k] = u[k] >= p;
+      a[k] = r[k] + (keep[k] ? (a[k] + bb[k]) * scale : 0.f);
+    }
+    Vec16<T>::store(y + v * VN, a);
+    store_mask<VN>(mask + v * VN, keep);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_bwd_vec_kernel(const T* __restrict__ dy,
+                                                              const uint8_t* __restrict__ mask, T* __restrict__ dx,
+                                                              int64_t n, float scale) {
+  constexpr int VN = Vec16<T>::N;
+  const int64_t nvec = n / VN, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float g[VN];
+    bool keep[VN];
+    Vec16<T>::load(dy + v * VN, g);
+    load_mask<VN>(mask + v * VN, keep);
+#pragma unroll
+    for (int k = 0; k < VN; ++k) g[k] = keep[k] ? g[k] * scale : 0.f;
+    Vec16<T>::store(dx + v * VN, g);
+  }
+}
+
+static inline bool vec_ok(int64_t n, int vn, std::initializer_list<const void*> ptrs) {
+  if (n % vn) return false;
+  for (const void* q : ptrs)
+    if (q && (reinterpret_cast<uintptr_t>(q) & 15)) return false;
+  return true;
+}
+
 static inline unsigned dgrid(int64_t work) {
   int64_t g = (work + 255) / 256;
   return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -92,6 +206,13 @@ static inline unsigned dgrid(int64_t work) {
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed, uint64_t offset,
                         int dt, hipStream_t s) {
   if (n <= 0) return;
+  const int vn = dt == kF32 ? 4 : 8;
+  if (vec_ok(n, vn, {x, y}) && (reinterpret_cast<uintptr_t>(mask) & 7) == 0) {
+    DSA_DISPATCH_T(dt, T,
+      hipLaunchKernelGGL((dropout_fwd_vec_kernel<T>), dim3(dgrid(n / vn)), dim3(256), 0, s, (const T*)x, (T*)y, mask,
+                         n, p, seed, offset));
+    return;
+  }
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((dropout_fwd_kernel<T>), dim3(dgrid((n + 3) / 4)), dim3(256), 0, s, (const T*)x, (T*)y, mask,
                        n, p, seed, offset));
@@ -102,6 +223,13 @@ void launch_bias_dropout_residual(const void* x, const void* bias, const void* r
                                   hipStream_t s) {
   const int64_t n = rows * C;
   if (n <= 0) return;
+  const int vn = dt == kF32 ? 4 : 8;
+  if (vec_ok(n, vn, {x, bias, res, y}) && C % vn == 0 && (reinterpret_cast<uintptr_t>(mask) & 7) == 0) {
+    DSA_DISPATCH_T(dt, T,
+      hipLaunchKernelGGL((bias_dropout_residual_vec_kernel<T>), dim3(dgrid(n / vn)), dim3(256), 0, s, (const T*)x,
+                         (const T*)bias, (const T*)res, (T*)y, mask, n, C, p, seed, offset));
+    return;
+  }
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((bias_dropout_residual_kernel<T>), dim3(dgrid((n + 3) / 4)), dim3(256), 0, s, (const T*)x,
                        (const T*)bias, (const T*)res, (T*)y, mask, n, C, p, seed, offset));
@@ -109,6 +237,13 @@ void launch_bias_dropout_residual(const void* x, const void* bias, const void* r
 
 void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, int dt, hipStream_t s) {
   if (n <= 0) return;
+  const int vn = dt == kF32 ? 4 : 8;
+  if (vec_ok(n, vn, {dy, dx}) && (reinterpret_cast<uintptr_t>(mask) & 7) == 0) {
+    DSA_DISPATCH_T(dt, T,
+      hipLaunchKernelGGL((dropout_bwd_vec_kernel<T>), dim3(dgrid(n / vn)), dim3(256), 0, s, (const T*)dy, mask, (T*)dx,
+                         n, 1.f / (1.f - p)));
+    return;
+  }
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((dropout_bwd_kernel<T>), dim3(dgrid(n)), dim3(256), 0, s, (const T*)dy, mask, (T*)dx, n,
                        1.f / (1.f - p)));

@@ -512,7 +512,18 @@ struct Extra {
   uint32_t seed = 0;
   uint32_t thresh = 0;  // a draw below thresh (of 65536) drops the element
   float rscale = 1.f;   // 1 / (1 - p)
+  // token-major q/k/v (and dq/dk/dv) with row stride ild elements, head h at column h*D, batch
+  // b = bh / inh (e.g. straight out of the fused QKV projection [B, S, 3, H, D]); inh == 0:
+  // the [B*H, S, D] layout
+  int inh = 0;
+  int64_t ild = 0;
 };
+template <int D>
+__device__ __forceinline__ int64_t in_base(const Extra& ex, int64_t bh, int S) {
+  return ex.inh ? (bh / ex.inh) * (int64_t)S * ex.ild + (bh % ex.inh) * D : bh * (int64_t)S * D;
+}
+template <int D>
+__device__ __forceinline__ int64_t in_ld(const Extra& ex) { return ex.inh ? ex.ild : D; }
 constexpr float LOG2E = 1.4426950408889634f;
 __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
   x ^= x >> 16;
@@ -546,9 +557,10 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   const int64_t bh = task / nqb;
   const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
   const int myq = qb + 32 * w + c32;
-  const uint16_t* Qb = Q + bh * (int64_t)S * D;
-  const uint16_t* Kb = K + bh * (int64_t)S * D;
-  const uint16_t* Vb = V + bh * (int64_t)S * D;
+  const int64_t ib = in_base<D>(ex, bh, S), ldi = in_ld<D>(ex);
+  const uint16_t* Qb = Q + ib;
+  const uint16_t* Kb = K + ib;
+  const uint16_t* Vb = V + ib;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
   const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
   const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
@@ -556,7 +568,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   s16x8 qf[D / 16];
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks)
-    qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Qb + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
+    qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Qb + (int64_t)myq * ldi + 16 * ks + 8 * h) : s16x8{};
   f32x16 o[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -568,8 +580,8 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   const int kend = CAUSAL ? min(S, qb + BM2) : S;
   const int ntiles = (kend + BN2 - 1) / BN2;
   uint4 kr[D / 32], vr[D / 32];
-  tile_load<D>(kr, Kb, 0, S);
-  tile_load<D>(vr, Vb, 0, S);
+  tile_load<D>(kr, Kb, 0, S, ldi);
+  tile_load<D>(vr, Vb, 0, S, ldi);
   tile_store<D>(smem, kr);
   tile_store<D>(smem + TS, vr);
   __syncthreads();
@@ -577,8 +589,8 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     const int j0 = it * BN2;
     const bool has_next = it + 1 < ntiles;
     if (has_next) {
-      tile_load<D>(kr, Kb, j0 + BN2, S);
-      tile_load<D>(vr, Vb, j0 + BN2, S);
+      tile_load<D>(kr, Kb, j0 + BN2, S, ldi);
+      tile_load<D>(vr, Vb, j0 + BN2, S, ldi);
     }
     const uint16_t* Ks = smem + (it & 1) * 2 * TS;
     const uint16_t* Vs = Ks + TS;
@@ -725,7 +737,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   const int64_t bh = task / nkb;
   const int kb = (task - (int)bh * nkb) * BM2;
   const int mykey = kb + 32 * w + c32;
-  const int64_t base = bh * (int64_t)S * D;
+  const int64_t base = in_base<D>(ex, bh, S), ldi = in_ld<D>(ex);
   const int64_t obase = o_base<D>(bh, S, onh);
   const float sl2 = scale * 1.4426950408889634f;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
@@ -737,8 +749,8 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   s16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) {
-    kf[ks] = mykey < S ? *reinterpret_cast<const s16x8*>(K + base + (int64_t)mykey * D + 16 * ks + 8 * h) : s16x8{};
-    vf[ks] = mykey < S ? *reinterpret_cast<const s16x8*>(V + base + (int64_t)mykey * D + 16 * ks + 8 * h) : s16x8{};
+    kf[ks] = mykey < S ? *reinterpret_cast<const s16x8*>(K + base + (int64_t)mykey * ldi + 16 * ks + 8 * h) : s16x8{};
+    vf[ks] = mykey < S ? *reinterpret_cast<const s16x8*>(V + base + (int64_t)mykey * ldi + 16 * ks + 8 * h) : s16x8{};
   }
   f32x16 dk[D / 32], dv[D / 32];
 #pragma unroll
@@ -751,7 +763,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   uint4 qr[D / 32], orr[D / 32];
   float st_l = 0.f, st_d = 0.f;
   auto load_tile = [&](int i0) {
-    tile_load<D>(qr, Q + base, i0, S);
+    tile_load<D>(qr, Q + base, i0, S, ldi);
     tile_load<D>(orr, dO + obase, i0, S, o_ld<D>(onh));
     if (threadIdx.x < BN2) {
       const int q = i0 + threadIdx.x;
@@ -854,8 +866,8 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
     __syncthreads();
   }
   if (mykey < S) {
-    uint16_t* dkr = dK + base + (int64_t)mykey * D;
-    uint16_t* dvr = dV + base + (int64_t)mykey * D;
+    uint16_t* dkr = dK + base + (int64_t)mykey * ldi;
+    uint16_t* dvr = dV + base + (int64_t)mykey * ldi;
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -892,7 +904,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
   const int64_t bh = task / nqb;
   const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
   const int myq = qb + 32 * w + c32;
-  const int64_t base = bh * (int64_t)S * D;
+  const int64_t base = in_base<D>(ex, bh, S), ldi = in_ld<D>(ex);
   const float sl2 = scale * 1.4426950408889634f;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
   const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
@@ -901,7 +913,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
   s16x8 qf[D / 16], of[D / 16];
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) {
-    qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Q + base + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
+    qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Q + base + (int64_t)myq * ldi + 16 * ks + 8 * h) : s16x8{};
     of[ks] = myq < S ? *reinterpret_cast<const s16x8*>(dO + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh) +
                                                          16 * ks + 8 * h)
                      : s16x8{};
@@ -917,8 +929,8 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
   const int kend = CAUSAL ? min(S, qb + BM2) : S;
   const int ntiles = (kend + BN2 - 1) / BN2;
   uint4 kr[D / 32], vr[D / 32];
-  tile_load<D>(kr, K + base, 0, S);
-  tile_load<D>(vr, V + base, 0, S);
+  tile_load<D>(kr, K + base, 0, S, ldi);
+  tile_load<D>(vr, V + base, 0, S, ldi);
   tile_store<D>(smem, kr);
   tile_store<D>(smem + TS, vr);
   __syncthreads();
@@ -926,8 +938,8 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
     const int j0 = it * BN2;
     const bool has_next = it + 1 < ntiles;
     if (has_next) {
-      tile_load<D>(kr, K + base, j0 + BN2, S);
-      tile_load<D>(vr, V + base, j0 + BN2, S);
+      tile_load<D>(kr, K + base, j0 + BN2, S, ldi);
+      tile_load<D>(vr, V + base, j0 + BN2, S, ldi);
     }
     const uint16_t* Ks = smem + (it & 1) * 2 * TS;
     const uint16_t* Vs = Ks + TS;
@@ -999,7 +1011,7 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
     __syncthreads();
   }
   if (myq < S) {
-    uint16_t* dqr = dQ + base + (int64_t)myq * D;
+    uint16_t* dqr = dQ + base + (int64_t)myq * ldi;
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
@@ -1618,6 +1630,7 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
 
 // Encoder attention (non-causal) with a per-key additive bias and/or in-kernel dropout.
 // kbias: [BH / hdiv, S] fp32 or null; p_drop in [0, 1); S % 8 == 0; D in {64, 128}.
+// inh > 0: q/k/v and dq/dk/dv are token-major with row stride ild (see fa::Extra).
 #define FA_EX_DISPATCH(dt, D, kbias, pdrop, ...)                                                     \
   do {                                                                                               \
     auto _go = [&](auto tt, auto dd, auto ee) {                                                      \
@@ -1629,7 +1642,8 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     auto _e = [&](auto tt, auto dd) {                                                                \
       if (kbias && pdrop > 0.f) _go(tt, dd, std::integral_constant<int, fa::EX_BIAS | fa::EX_DROP>{}); \
       else if (kbias) _go(tt, dd, std::integral_constant<int, fa::EX_BIAS>{});                      \
-      else _go(tt, dd, std::integral_constant<int, fa::EX_DROP>{});                                 \
+      else if (pdrop > 0.f) _go(tt, dd, std::integral_constant<int, fa::EX_DROP>{});                \
+      else _go(tt, dd, std::integral_constant<int, 0>{});                                           \
     };                                                                                               \
     auto _d = [&](auto tt) {                                                                         \
       if (D == 64) _e(tt, std::integral_constant<int, 64>{});                                       \
@@ -1638,8 +1652,11 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     if (dt == kBF16) _d(bf16_t{}); else _d(f16_t{});                                                 \
   } while (0)
 
-static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t seed) {
+static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t seed, int inh = 0,
+                            int64_t ild = 0) {
   fa::Extra ex;
+  ex.inh = inh;
+  ex.ild = ild;
   ex.kbias = kbias;
   ex.hdiv = hdiv;
   ex.seed = (uint32_t)(seed ^ (seed >> 32));
@@ -1650,8 +1667,8 @@ static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t 
 
 void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh) {
-  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed);
+                         int onh, int inh, int64_t ild) {
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild);
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
   FA_EX_DISPATCH(dt, D, kbias, pdrop,
     hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, false, true, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
@@ -1662,8 +1679,8 @@ void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, f
 void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const void* v, const void* o,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh) {
-  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed);
+                         int onh, int inh, int64_t ild) {
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild);
   const int64_t rows = (int64_t)BH * S;
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
   FA_EX_DISPATCH(dt, D, kbias, pdrop,

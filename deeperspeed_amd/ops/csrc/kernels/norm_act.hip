@@ -7,6 +7,9 @@
 // registers (16-byte vector loads), fp32 statistics, wave64 shuffles + one LDS hop;
 // weight/bias gradients are produced as per-block column partials in the same pass
 // and folded by a tiny column-reduce kernel (no atomics, deterministic).
+#include <algorithm>
+#include <cstdlib>
+
 #include "../include/dsa_common.h"
 #include "../include/launchers.h"
 
@@ -161,6 +164,153 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(const T* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-per-row LayerNorm for narrow rows (H <= 64 lanes x WV vectors, e.g. BERT's 1024): a
+// 256-thread block normalises 4 rows at once with wave-level shuffles only (no LDS hop, no block
+// barrier), where the block-per-row kernels would leave half the threads idle and serialise
+// every row behind a barrier.  Same math and outputs as ln_fwd_kernel / ln_bwd_kernel.
+// ---------------------------------------------------------------------------
+template <typename T, int WV>
+__global__ void __launch_bounds__(256) ln_fwd_wave_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                          const T* __restrict__ bias, T* __restrict__ sum_out,
+                                                          const T* __restrict__ gamma, const T* __restrict__ beta,
+                                                          T* __restrict__ y, float* __restrict__ mean_out,
+                                                          float* __restrict__ rstd_out, int64_t rows, int H,
+                                                          float eps) {
+  constexpr int VN = Vec16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;  // whole wave
+  const int nvec = H / VN;
+  const T* xr = x + row * H;
+  float vals[WV][VN];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < WV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nvec) {
+      Vec16<T>::load(xr + vi * VN, vals[k]);
+      if (res) {
+        float r[VN];
+        Vec16<T>::load(res + row * H + vi * VN, r);
+#pragma unroll
+        for (int j = 0; j < VN; ++j) vals[k][j] += r[j];
+        if (bias) {
+          float b[VN];
+          Vec16<T>::load(bias + vi * VN, b);
+#pragma unroll
+          for (int j = 0; j < VN; ++j) vals[k][j] += b[j];
+        }
+        if (sum_out) Vec16<T>::store(sum_out + row * H + vi * VN, vals[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < VN; ++j) s += vals[k][j];
+    }
+  }
+  const float mean = wave_sum(s) / H;
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < WV; ++k)
+    if (lane + 64 * k < nvec) {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) { const float d = vals[k][j] - mean; ss = fmaf(d, d, ss); }
+    }
+  const float rstd = rsqrtf(wave_sum(ss) / H + eps);
+#pragma unroll
+  for (int k = 0; k < WV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nvec) {
+      float gm[VN], bt[VN], o[VN];
+      Vec16<T>::load(gamma + vi * VN, gm);
+      if (beta) Vec16<T>::load(beta + vi * VN, bt);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) o[j] = (vals[k][j] - mean) * rstd * gm[j] + (beta ? bt[j] : 0.f);
+      Vec16<T>::store(y + row * H + vi * VN, o);
+    }
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// Each wave walks rows (4 * blockIdx.x + wave) + k * 4 * gridDim.x; gamma/beta partials of the
+// block's 4 waves are folded through LDS into partial[blockIdx.x] / [gridDim.x + blockIdx.x].
+template <typename T, int WV>
+__global__ void __launch_bounds__(256) ln_bwd_wave_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const T* __restrict__ gamma, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, const T* __restrict__ dres,
+                                                          T* __restrict__ dx, float* __restrict__ partial,
+                                                          int64_t rows, int H) {
+  extern __shared__ float fold[];  // [4 waves][2][H]
+  constexpr int VN = Vec16<T>::N;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nvec = H / VN;
+  float dg[WV][VN], db[WV][VN], gm[WV][VN];
+#pragma unroll
+  for (int k = 0; k < WV; ++k) {
+    const int vi = lane + 64 * k;
+#pragma unroll
+    for (int j = 0; j < VN; ++j) { dg[k][j] = 0.f; db[k][j] = 0.f; gm[k][j] = 0.f; }
+    if (vi < nvec) Vec16<T>::load(gamma + vi * VN, gm[k]);
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[WV][VN], g[WV][VN];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < WV; ++k) {
+      const int vi = lane + 64 * k;
+      if (vi < nvec) {
+        Vec16<T>::load(x + row * H + vi * VN, xh[k]);
+        Vec16<T>::load(dy + row * H + vi * VN, g[k]);
+#pragma unroll
+        for (int j = 0; j < VN; ++j) {
+          xh[k][j] = (xh[k][j] - mu) * rs;
+          dg[k][j] = fmaf(g[k][j], xh[k][j], dg[k][j]);
+          db[k][j] += g[k][j];
+          const float dxh = g[k][j] * gm[k][j];
+          a += dxh;
+          b = fmaf(dxh, xh[k][j], b);
+        }
+      }
+    }
+    a = wave_sum(a) / H;
+    b = wave_sum(b) / H;
+#pragma unroll
+    for (int k = 0; k < WV; ++k) {
+      const int vi = lane + 64 * k;
+      if (vi < nvec) {
+        float o[VN];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) o[j] = rs * (g[k][j] * gm[k][j] - a - xh[k][j] * b);
+        if (dres) {
+          float r[VN];
+          Vec16<T>::load(dres + row * H + vi * VN, r);
+#pragma unroll
+          for (int j = 0; j < VN; ++j) o[j] += r[j];
+        }
+        Vec16<T>::store(dx + row * H + vi * VN, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < WV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nvec) {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) {
+        fold[(w * 2) * H + vi * VN + j] = dg[k][j];
+        fold[(w * 2 + 1) * H + vi * VN + j] = db[k][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * H; c += 256) {
+    const int which = c / H, col = c - which * H;
+    const float v = fold[(0 * 2 + which) * H + col] + fold[(1 * 2 + which) * H + col] +
+                    fold[(2 * 2 + which) * H + col] + fold[(3 * 2 + which) * H + col];
+    partial[(int64_t)(which * gridDim.x + blockIdx.x) * H + col] = v;
+  }
+}
+
 // out[c] = sum_r partial[r][c] over R rows, C columns; written in dtype T
 // (optionally accumulated into existing out when `accum`).
 // blockIdx.y == 1 sums a second partial block (partial + second_off) into out2 in the same launch
@@ -173,30 +323,52 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
     partial += second_off;
     out = out2;
   }
-  // 64 columns x 4 row-groups per block; lanes own columns -> coalesced reads.
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;
-  float acc = 0.f;
+  // 16 columns x 64 row-groups per block: a lane reads 4 columns (float4) of every 64th row
+  // (loads issued 4 at a time, all independent), and C / 16 blocks spread the fold over the chip
+  // (C % 4 == 0).  The partials are usually L2-resident (written by the previous kernel).
+  // Row-groups are folded by shuffles inside each wave (lanes 4 apart share a column quad),
+  // then across the 4 waves through LDS.
+  __shared__ float4 red[4][4];
+  const int q = threadIdx.x & 3, rg = threadIdx.x >> 2;
+  const int c = blockIdx.x * 16 + 4 * q;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < C) {
-    // 8 independent loads in flight per thread (the partials are L2-resident; a serial
-    // load-add chain over R/4 rows is pure latency)
     int r = rg;
-    for (; r + 28 < R; r += 32) {
-      float v[8];
+    for (; r + 192 < R; r += 256) {
+      float4 v[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = partial[(int64_t)(r + 4 * j) * C + c];
+      for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(partial + (int64_t)(r + 64 * k) * C + c);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc += v[j];
+      for (int k = 0; k < 4; ++k) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
     }
-    for (; r < R; r += 4) acc += partial[(int64_t)r * C + c];
+    for (; r < R; r += 64) {
+      const float4 v = *reinterpret_cast<const float4*>(partial + (int64_t)r * C + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
   }
-  red[rg][threadIdx.x & 63] = acc;
+#pragma unroll
+  for (int off = 4; off < 64; off <<= 1) {
+    acc.x += __shfl_xor(acc.x, off, 64);
+    acc.y += __shfl_xor(acc.y, off, 64);
+    acc.z += __shfl_xor(acc.z, off, 64);
+    acc.w += __shfl_xor(acc.w, off, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < 4) red[wv][lane] = acc;
   __syncthreads();
-  if (rg == 0 && c < C) {
-    float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    if (accum) v += Conv<T>::load(out, c);
-    Conv<T>::store(out, c, v);
+  if (threadIdx.x < 16) {
+    const int qq = threadIdx.x >> 2, comp = threadIdx.x & 3;
+    const int col = blockIdx.x * 16 + 4 * qq + comp;
+    if (col < C) {
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 t = red[g][qq];
+        v += comp == 0 ? t.x : comp == 1 ? t.y : comp == 2 ? t.z : t.w;
+      }
+      if (accum) v += Conv<T>::load(out, col);
+      Conv<T>::store(out, col, v);
+    }
   }
 }
 
@@ -314,10 +486,24 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict_
 
 int ln_max_hidden(int dt) { return LN_THREADS * LN_MAXV * (dt == kF32 ? 4 : 8); }
 
+// rows of at most 64 lanes x 2 vectors (H <= 1024 for 16-bit, 512 for fp32) take the
+// wave-per-row kernels; DSA_LN_WAVE=0 keeps the block-per-row ones
+static bool ln_wave(int H, int dt) {
+  static const bool on = !(getenv("DSA_LN_WAVE") && getenv("DSA_LN_WAVE")[0] == '0');
+  return on && H <= 64 * 2 * (dt == kF32 ? 4 : 8);
+}
+
 void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_out, const void* gamma,
                    const void* beta, void* y, float* mean, float* rstd, int64_t rows, int H, float eps, int dt,
                    hipStream_t s) {
   if (rows <= 0) return;
+  if (ln_wave(H, dt)) {
+    DSA_DISPATCH_T(dt, T,
+      hipLaunchKernelGGL((ln_fwd_wave_kernel<T, 2>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s,
+                         (const T*)x, (const T*)res, (const T*)bias, (T*)sum_out, (const T*)gamma,
+                         (const T*)beta, (T*)y, mean, rstd, rows, H, eps));
+    return;
+  }
   const int nv = (H / (dt == kF32 ? 4 : 8) + LN_THREADS - 1) / LN_THREADS;
   DSA_DISPATCH_T(dt, T, DSA_DISPATCH_NV(nv, NV,
     hipLaunchKernelGGL((ln_fwd_kernel<T, NV>), dim3((unsigned)rows), dim3(LN_THREADS), 0, s,
@@ -332,13 +518,20 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
                    const void* dres, void* dx, void* dgamma, void* dbeta, float* partial, int64_t rows, int H,
                    int dt, hipStream_t s) {
   if (rows <= 0) return;
-  const int grid = ln_bwd_grid(rows);
+  const bool wave = ln_wave(H, dt);
+  // partial rows: one per block (<= ln_bwd_grid(rows), the caller's workspace)
+  const int grid = wave ? (int)std::min<int64_t>(ln_bwd_grid(rows), (rows + 3) / 4) : ln_bwd_grid(rows);
   const int nv = (H / (dt == kF32 ? 4 : 8) + LN_THREADS - 1) / LN_THREADS;
   DSA_DISPATCH_T(dt, T,
-    DSA_DISPATCH_NV(nv, NV, hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(grid), dim3(LN_THREADS), 0, s,
-                       (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
-                       partial, rows, H));
-    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 63) / 64, dbeta ? 2 : 1), dim3(256), 0, s, partial, grid, H,
+    if (wave)
+      hipLaunchKernelGGL((ln_bwd_wave_kernel<T, 2>), dim3(grid), dim3(256), 8 * H * sizeof(float), s,
+                         (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx, partial,
+                         rows, H);
+    else
+      DSA_DISPATCH_NV(nv, NV, hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(grid), dim3(LN_THREADS), 0, s,
+                         (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
+                         partial, rows, H));
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 15) / 16, dbeta ? 2 : 1), dim3(256), 0, s, partial, grid, H,
                        (T*)dgamma, 0, (int64_t)grid * H, (T*)dbeta));
 }
 
@@ -386,7 +579,7 @@ void launch_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((bias_gelu_bwd_kernel<T>), dim3(cblocks, rc), dim3(256), 0, s,
                        (const T*)dy, (const T*)x, (const T*)b, (T*)dx, db ? partial : nullptr, rows, C, approx);
-    if (db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 63) / 64), dim3(256), 0, s, partial, rc, C,
+    if (db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 15) / 16), dim3(256), 0, s, partial, rc, C,
                                (T*)db, 0));
 }
 
@@ -472,7 +665,7 @@ void launch_sum_slices(const void* part, int S, int64_t n, void* out, bool out_f
 
 void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s) {
   DSA_DISPATCH_T(dt, T,
-    hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 63) / 64), dim3(256), 0, s, partial, R, C, (T*)out, accum));
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 15) / 16), dim3(256), 0, s, partial, R, C, (T*)out, accum));
 }
 
 void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C, int accum, int dt,
@@ -484,7 +677,7 @@ void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((colsum_partial_kernel<T>), dim3(cblocks, rc), dim3(256), 0, s, (const T*)x, partial,
                        rows, C);
-    hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 63) / 64), dim3(256), 0, s, partial, rc, C, (T*)out,
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 15) / 16), dim3(256), 0, s, partial, rc, C, (T*)out,
                        accum));
 }
 

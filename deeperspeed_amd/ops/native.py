@@ -84,6 +84,40 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tenso
     return _LayerNormFn.apply(x, weight, bias, eps)
 
 
+class _LayerNormResidualFn(torch.autograd.Function):
+    """(LayerNorm(x), x) for a pre-LN block whose input also feeds the residual add: the second
+    output is x itself, so the residual branch's gradient reaches this node and the LN-backward
+    kernel adds it into dx in the same pass (reference LayerNormBackward*_fused_add,
+    normalize_kernels.cu:1350-1790) instead of autograd summing the two branches separately."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        x = x.contiguous()
+        _macs(5 * x.numel())
+        if x.is_cuda:
+            y, mean, rstd, _ = hip_ops().ln_fwd(x, gamma, beta, eps, None, None)
+        else:
+            y, mean, rstd = _ln_ref(x, gamma, beta, eps)
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.has_beta = beta is not None
+        return y, x
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        if not x.is_cuda:
+            dx, dg, db, _ = _LayerNormFn.backward(ctx, dy)
+            return (dx if dres is None else dx + dres), dg, db, None
+        dres = None if dres is None else dres.contiguous()
+        dx, dg, db = hip_ops().ln_bwd(dy.contiguous(), x, gamma, mean, rstd, ctx.has_beta, dres)
+        return dx, dg, (db if ctx.has_beta else None), None
+
+
+def layer_norm_residual(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float = 1e-5):
+    """(LayerNorm(x), x): use the second output for the residual path (fused backward add)."""
+    return _LayerNormResidualFn.apply(x, weight, bias, eps)
+
+
 class _InvertibleLayerNormFn(torch.autograd.Function):
     """LayerNorm that keeps only its OUTPUT for backward (reference `normalize_invertible`,
     csrc/transformer/normalize_kernels.cu invertible variants): x_hat = (y - beta) / gamma is
@@ -410,6 +444,45 @@ def flash_attention_encoder(q, k, v, key_bias=None, scale=1.0, dropout_p=0.0, tr
     seed = _draw_seed(generator) if p > 0.0 else 0
     return _FlashAttnExFn.apply(q, k, v, key_bias, float(scale), p, int(seed) & ((1 << 63) - 1),
                                 out_layout == "bshd")
+
+
+class _FlashAttnQkvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv5, kbias, scale, p, seed):
+        B, S, _, H, D = qkv5.shape
+        _macs(2 * B * H * S * S * D)
+        o, lse = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed)
+        ctx.save_for_backward(qkv5, o, lse, kbias)
+        ctx.scale, ctx.p, ctx.seed = scale, p, seed
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv5, o, lse, kbias = ctx.saved_tensors
+        dqkv = hip_ops().flash_attn_qkv_bwd(do.contiguous(), qkv5, o, lse, kbias, ctx.scale, ctx.p, ctx.seed)
+        return dqkv, None, None, None, None
+
+
+def flash_attention_qkv(qkv, num_heads, key_bias=None, scale=1.0, dropout_p=0.0, training=True, generator=None):
+    """Encoder attention straight from the fused QKV projection: qkv [B, S, 3*H*D] (q | k | v,
+    heads contiguous inside each) -> context [B, S, H*D], same math as flash_attention_encoder
+    (same keep mask for the same seed) without the head split / merge copies; the backward
+    returns dqkv in the qkv layout."""
+    B, S, C = qkv.shape
+    D = C // (3 * num_heads)
+    p = float(dropout_p) if training else 0.0
+    if key_bias is not None:
+        key_bias = key_bias.reshape(B, S).float().contiguous()
+    seed = (_draw_seed(generator) if p > 0.0 else 0) & ((1 << 63) - 1)
+    o = _FlashAttnQkvFn.apply(qkv.contiguous().view(B, S, 3, num_heads, D), key_bias, float(scale), p, int(seed))
+    return o.view(B, S, num_heads * D)
+
+
+def qkv_flash_supported(qkv: torch.Tensor, num_heads: int) -> bool:
+    if not (qkv.is_cuda and qkv.dtype in (torch.bfloat16, torch.float16) and qkv.dim() == 3):
+        return False
+    B, S, C = qkv.shape
+    return C % (3 * num_heads) == 0 and C // (3 * num_heads) in (64, 128) and S % 8 == 0
 
 
 def flash_dropout_keep_mask(B, H, S, p, seed, device=None):

@@ -137,27 +137,35 @@ class DeepSpeedTransformerFunction:
         gen = layer._generator if layer is not None else None
         eps = cfg.layer_norm_eps
         x = input
-        ln = native.layer_norm_invertible if getattr(cfg, "normalize_invertible", False) else native.layer_norm
-        inp = ln(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
+        invertible = getattr(cfg, "normalize_invertible", False)
+        ln = native.layer_norm_invertible if invertible else native.layer_norm
+        # pre-LN: the block input feeds both the LayerNorm and the residual add; the fused form
+        # returns it as a second output so the LN backward adds the residual gradient in-kernel
+        fuse_res = cfg.pre_layer_norm and not invertible
+        if fuse_res:
+            inp, x = native.layer_norm_residual(x, norm_w, norm_b, eps)
+        else:
+            inp = ln(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
         qkv = _linear(inp, attn_qkvw, attn_qkvb)
         fast = _use_head_kernels(qkv, hd)
-        if fast:
-            q, k, v = _SplitHeads.apply(qkv, nh)  # contiguous [B, nh, S, hd]: batched GEMMs without copies
-        else:
-            q, k, v = qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, hd]
         mask = None
         if input_mask is not None:
             mask = input_mask
             if mask.dim() == 2:
                 mask = mask[:, None, None, :]
             mask = mask.reshape(B, 1, -1, S)
-        if fast and _ENCODER_FLASH and native.encoder_flash_supported(q, mask is None or mask.shape[2] == 1):
-            # one fused kernel per direction: scores, key-padding bias, softmax, dropout and P V
-            # stay on chip; the output is written token-major [B, S, nh, hd] for the projection
-            ctx = native.flash_attention_encoder(q, k, v, None if mask is None else mask.reshape(B, S),
-                                                 1.0 / math.sqrt(hd), cfg.attn_dropout_ratio, training, gen,
-                                                 out_layout="bshd").view(B, S, Hd)
+        if (fast and _ENCODER_FLASH and native.qkv_flash_supported(qkv, nh)
+                and (mask is None or mask.shape[2] == 1)):
+            # one fused kernel per direction reading q, k, v straight out of the QKV projection:
+            # scores, key-padding bias, softmax, dropout and P V stay on chip, the context is
+            # written token-major [B, S, nh * hd] for the output projection, dqkv in qkv's layout
+            ctx = native.flash_attention_qkv(qkv, nh, None if mask is None else mask.reshape(B, S),
+                                             1.0 / math.sqrt(hd), cfg.attn_dropout_ratio, training, gen)
         else:
+            if fast:
+                q, k, v = _SplitHeads.apply(qkv, nh)  # contiguous [B, nh, S, hd]: batched GEMMs without copies
+            else:
+                q, k, v = qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, hd]
             scores = torch.matmul(q, k.transpose(-1, -2))
             if mask is not None:
                 mask = mask.to(scores.dtype).contiguous()
@@ -170,7 +178,10 @@ class DeepSpeedTransformerFunction:
             ctx = _MergeHeads.apply(ctx) if fast else ctx.transpose(1, 2).reshape(B, S, Hd)
         attn_out = _linear(ctx, attn_ow)
         add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen)
-        ff1_inp = ln(add_res, attn_nw, attn_nb, eps)
+        if fuse_res:
+            ff1_inp, add_res = native.layer_norm_residual(add_res, attn_nw, attn_nb, eps)
+        else:
+            ff1_inp = ln(add_res, attn_nw, attn_nb, eps)
         inter = _gelu_tanh(_linear(ff1_inp, inter_w), inter_b)
         out = _linear(inter, output_w)
         if cfg.pre_layer_norm:

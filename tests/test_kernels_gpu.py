@@ -657,3 +657,31 @@ def test_sum_slices_and_colsum_accumulate(out_f32, accumulate):
     got = native.colsum(x, acc, accumulate=accumulate)
     assert got.data_ptr() == acc.data_ptr()
     assert (got.float() - want).abs().max().item() <= 2e-2 * want.abs().max().item()
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_qkv_layout_flash_matches_head_major(p):
+    """Encoder flash attention reading q, k, v straight from the fused QKV output (and writing
+    dqkv in that layout) equals the head-major path bit for bit (same kernels, same keep mask)."""
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(2)
+    dev = _dev()
+    B, S, H, D = 3, 256, 4, 64
+    qkv = torch.randn(B, S, 3 * H * D, device=dev, dtype=torch.bfloat16)
+    bias = torch.zeros(B, S, device=dev)
+    bias[1, -40:] = -10000.0
+    g = torch.randn(B, S, H * D, device=dev, dtype=torch.bfloat16)
+    seed_fn = native._draw_seed
+    try:
+        native._draw_seed = lambda generator=None: 987654321
+        a = qkv.clone().requires_grad_(True)
+        oa = native.flash_attention_qkv(a, H, bias, D ** -0.5, p, True)
+        (oa.float() * g.float()).sum().backward()
+        b = qkv.clone().requires_grad_(True)
+        q, k, v = b.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
+        ob = native.flash_attention_encoder(q, k, v, bias, D ** -0.5, p, True, out_layout="bshd").reshape(B, S, H * D)
+        (ob.float() * g.float()).sum().backward()
+    finally:
+        native._draw_seed = seed_fn
+    assert torch.equal(oa, ob)
+    assert torch.equal(a.grad, b.grad)
