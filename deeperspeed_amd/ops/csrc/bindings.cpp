@@ -566,6 +566,27 @@ std::vector<Tensor> bias_dropout_residual(Tensor x, Tensor bias, Tensor res, dou
   return {y, mask};
 }
 
+// (dx, db) for a bias + dropout + residual block: dx = dy * mask / (1 - p), db = column sums of dx
+std::vector<Tensor> dropout_bwd_db(Tensor dy, Tensor mask, double p) {
+  check_dev(dy, "dropout_bwd_db"); check_dev(mask, "dropout_bwd_db");
+  TORCH_CHECK(dy.is_contiguous() && mask.is_contiguous() && mask.numel() == dy.numel() &&
+                  mask.scalar_type() == at::kByte, "dropout_bwd_db: contiguous dy and uint8 mask of its size");
+  const int64_t C = dy.size(-1), rows = dy.numel() / C;
+  const int dt = dcode(dy);
+  const int vn = dt == dsa::kCodeF32 ? 4 : 8;
+  TORCH_CHECK(C % vn == 0 && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(mask.data_ptr()) % 8 == 0, "dropout_bwd_db: 16-byte rows");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  int cb, rc, pr;
+  dsa::dropout_bwd_colsum_dims(rows, (int)C, dt, &cb, &rc, &pr);
+  Tensor dx = at::empty_like(dy);
+  Tensor db = at::empty({C}, dy.options());
+  Tensor partial = at::empty({(int64_t)pr * C}, dy.options().dtype(at::kFloat));
+  dsa::launch_dropout_bwd_colsum(dy.data_ptr(), mask.data_ptr<uint8_t>(), dx.data_ptr(), db.data_ptr(),
+                                 partial.data_ptr<float>(), rows, (int)C, (float)p, dt, cur_stream());
+  return {dx, db};
+}
+
 Tensor dropout_bwd(Tensor dy, Tensor mask, double p) {
   check_dev(dy, "dy"); check_dev(mask, "mask");
   TORCH_CHECK(mask.numel() == dy.numel() && mask.scalar_type() == at::kByte, "dropout_bwd: mask");
@@ -859,6 +880,7 @@ void register_gemm_lt(pybind11::module& m);  // gemm_lt.cpp
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_gemm_lt(m);
   m.def("sum_slices", &sum_slices);
+  m.def("dropout_bwd_db", &dropout_bwd_db);
   m.def("add3", &add3, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c") = pybind11::none());
   m.def("sparse_flash_fwd", &sparse_flash_fwd);
   m.def("flash_attn_fwd_ex", &flash_attn_fwd_ex);

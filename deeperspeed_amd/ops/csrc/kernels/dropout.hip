@@ -191,6 +191,67 @@ __global__ void __launch_bounds__(256) dropout_bwd_vec_kernel(const T* __restric
   }
 }
 
+// dropout backward of a bias + dropout + residual block that also yields the bias gradient:
+// dx = dy * mask / (1 - p) and per-(block, row-lane) column partials of dx, folded afterwards by
+// colsum_kernel, so dx is not read a second time for its column sums.  A block covers tpr
+// threads x VN columns and 256 / tpr rows at a time (narrow rows keep every thread busy).
+template <typename T>
+__global__ void __launch_bounds__(256) dropout_bwd_colsum_kernel(const T* __restrict__ dy,
+                                                                 const uint8_t* __restrict__ mask,
+                                                                 T* __restrict__ dx, float* __restrict__ partial,
+                                                                 int64_t rows, int C, float scale) {
+  constexpr int VN = Vec16<T>::N;
+  const int cv = C / VN;
+  const int tpr = cv < 256 ? cv : 256, rpb = 256 / tpr;
+  const int t = threadIdx.x % tpr, rs = threadIdx.x / tpr;
+  const int c0 = (blockIdx.x * tpr + t) * VN;
+  if (rs >= rpb || c0 >= C) return;
+  const int64_t chunk = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = blockIdx.y * chunk;
+  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float acc[VN];
+#pragma unroll
+  for (int j = 0; j < VN; ++j) acc[j] = 0.f;
+  for (int64_t r = r0 + rs; r < r1; r += rpb) {
+    float g[VN];
+    bool keep[VN];
+    Vec16<T>::load(dy + r * C + c0, g);
+    load_mask<VN>(mask + r * C + c0, keep);
+#pragma unroll
+    for (int k = 0; k < VN; ++k) {
+      g[k] = keep[k] ? g[k] * scale : 0.f;
+      acc[k] += g[k];
+    }
+    Vec16<T>::store(dx + r * C + c0, g);
+  }
+  float* pp = partial + ((int64_t)blockIdx.y * rpb + rs) * C + c0;
+#pragma unroll
+  for (int j = 0; j < VN; j += 4) *reinterpret_cast<float4*>(pp + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+}
+
+// partial rows for dropout_bwd_colsum: row chunks x rows-per-block
+void dropout_bwd_colsum_dims(int64_t rows, int C, int dt, int* cblocks, int* rchunks, int* prows) {
+  const int vn = dt == kF32 ? 4 : 8;
+  const int cv = C / vn, tpr = cv < 256 ? cv : 256, rpb = 256 / tpr;
+  *cblocks = (cv + tpr - 1) / tpr;
+  int64_t rc = 1024 / *cblocks;  // ~1024 blocks, each walking >= 16 rows
+  if (rc > rows / (16 * rpb)) rc = rows / (16 * rpb);
+  if (rc < 1) rc = 1;
+  *rchunks = (int)rc;
+  *prows = (int)rc * rpb;
+}
+
+void launch_dropout_bwd_colsum(const void* dy, const uint8_t* mask, void* dx, void* db, float* partial, int64_t rows,
+                               int C, float p, int dt, hipStream_t s) {
+  if (rows <= 0) return;
+  int cb, rc, pr;
+  dropout_bwd_colsum_dims(rows, C, dt, &cb, &rc, &pr);
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((dropout_bwd_colsum_kernel<T>), dim3(cb, rc), dim3(256), 0, s, (const T*)dy, mask, (T*)dx,
+                       partial, rows, C, 1.f / (1.f - p)));
+  launch_colsum_partials(partial, pr, C, db, 0, dt, s);
+}
+
 static inline bool vec_ok(int64_t n, int vn, std::initializer_list<const void*> ptrs) {
   if (n % vn) return false;
   for (const void* q : ptrs)

@@ -736,8 +736,12 @@ class _BiasDropoutResidualFn(torch.autograd.Function):
     def backward(ctx, dy):
         (mask,) = ctx.saved_tensors
         if dy.is_cuda:
-            dx = hip_ops().dropout_bwd(dy.contiguous(), mask, ctx.p)
-            db = colsum(dx.reshape(-1, dx.shape[-1]))
+            dy = dy.contiguous()
+            if dy.shape[-1] % (4 if dy.dtype == torch.float32 else 8) == 0 and dy.data_ptr() % 16 == 0:
+                dx, db = hip_ops().dropout_bwd_db(dy, mask, ctx.p)  # bias gradient in the same pass
+            else:
+                dx = hip_ops().dropout_bwd(dy, mask, ctx.p)
+                db = colsum(dx.reshape(-1, dx.shape[-1]))
         else:
             dx = (dy.float() * mask / (1 - ctx.p)).to(dy.dtype)
             db = dx.reshape(-1, dx.shape[-1]).float().sum(0).to(dy.dtype)

@@ -685,3 +685,19 @@ def test_qkv_layout_flash_matches_head_major(p):
         native._draw_seed = seed_fn
     assert torch.equal(oa, ob)
     assert torch.equal(a.grad, b.grad)
+
+
+@pytest.mark.parametrize("C", [1024, 4096, 264])
+def test_dropout_bwd_with_bias_grad(C):
+    """Dropout backward fused with the bias-gradient column sums equals mask * dy / (1-p) and
+    its column sums."""
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(1)
+    dev = _dev()
+    dy = torch.randn(2000, C, device=dev, dtype=torch.bfloat16)
+    mask = (torch.rand(2000, C, device=dev) >= 0.1).to(torch.uint8)
+    dx, db = native.hip_ops().dropout_bwd_db(dy, mask, 0.1)
+    ref = dy.float() * mask.float() / 0.9
+    assert (dx.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    want = ref.sum(0)
+    assert (db.float() - want).abs().max().item() < 2e-2 * want.abs().max().item()
