@@ -717,15 +717,13 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
 // index per value from the C layout, LSE/Delta broadcast from LDS), then
 //   dV^T += dO^T P   (A = dO^T via tr reads, B = P from registers)
 //   dK^T += Q^T dS   (A = Q^T via tr reads,  B = dS from registers)
-template <typename T, int D, bool CAUSAL, int EX = 0>
-__global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(const uint16_t* __restrict__ Q,
-                                                             const uint16_t* __restrict__ K,
-                                                             const uint16_t* __restrict__ V,
-                                                             const uint16_t* __restrict__ dO,
-                                                             const float* __restrict__ LSE,
-                                                             const float* __restrict__ DELTA,
-                                                             uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
-                                                             int S, float scale, int onh, Extra ex = Extra()) {
+template <typename T, int D, bool CAUSAL, int EX = 0, bool FQ = false>
+__device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint16_t* __restrict__ Q,
+                                             const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                                             const uint16_t* __restrict__ dO, const float* __restrict__ LSE,
+                                             const float* __restrict__ DELTA, uint16_t* __restrict__ dK,
+                                             uint16_t* __restrict__ dV, int S, float scale, int onh, const Extra& ex,
+                                             uint16_t* __restrict__ dQ = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   float* stats = reinterpret_cast<float*>(smem + 4 * TS);  // [2 stages][LSE 64 | DELTA 64]
@@ -733,7 +731,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
   const int nkb = (S + BM2 - 1) / BM2;
-  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int task = xcd_task(vblock, nblock);
   const int64_t bh = task / nkb;
   const int kb = (task - (int)bh * nkb) * BM2;
   const int mykey = kb + 32 * w + c32;
@@ -745,6 +743,17 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
   const float kb2 = (BIAS && mykey < S) ? ex.kbias[(bh / ex.hdiv) * (int64_t)S + mykey] * LOG2E : 0.f;
   const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
   const int dshift = (mykey & 1) * 16;
+  // FQ (S <= BM2: this workgroup owns every key of the head): K [BM2][D+8] and the tile's dS
+  // [BN2 queries][BM2 + 8 keys] also live in LDS, and dQ = dS K is formed per query tile here
+  uint16_t* const Ks = smem + 4 * TS + 4 * BN2 * 2;
+  uint16_t* const dSs = Ks + BM2 * (D + 8);
+  if constexpr (FQ) {
+    uint4 kr2[D / 32];
+    tile_load<D>(kr2, K + base, 0, S, ldi);
+    tile_store<D>(Ks, kr2);
+    tile_load<D>(kr2, K + base, BN2, S, ldi);
+    tile_store<D>(Ks + BN2 * (D + 8), kr2);
+  }
 
   s16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
@@ -844,6 +853,11 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
           dsv[r] = pv[r] * (pacc[r] - del_s[qi]);
         }
       }
+      if constexpr (FQ) {  // dS[q][key] for the tile's dQ (all 4 waves' keys)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          dSs[(32 * t + 8 * (r >> 2) + 4 * h + (r & 3)) * (BM2 + 8) + 32 * w + c32] = to16<T>(dsv[r]);
+      }
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ks = 2 * t + kk;
@@ -859,6 +873,43 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
           const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + row1 * (D + 8) + col));
           const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * (D + 8) + col));
           dk[dt] = Mfma32<T>::run(s16x8{qx[0], qx[1], qx[2], qx[3], qy[0], qy[1], qy[2], qy[3]}, sf, dk[dt]);
+        }
+      }
+    }
+    if constexpr (FQ) {
+      // dQ^T[d, q] = sum_k K^T[d, k] dS^T[k, q] for this 64-query tile: wave w owns query block
+      // w >> 1 and d blocks (w & 1) + 2j; K^T fragments by transposed LDS reads, dS^T fragments
+      // are 4+4 keys of one query row (the C-layout key order the dQ kernel uses)
+      __syncthreads();
+      const int qb2 = w >> 1;
+#pragma unroll
+      for (int dj = 0; dj < D / 64; ++dj) {
+        const int dt = (w & 1) + 2 * dj;
+        f32x16 dq;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < BM2 / 16; ++ks) {
+          const uint16_t* srow = dSs + (32 * qb2 + c32) * (BM2 + 8) + 16 * ks + 4 * h;
+          const s16x4 lo = *reinterpret_cast<const s16x4*>(srow);
+          const s16x4 hi = *reinterpret_cast<const s16x4*>(srow + 8);
+          const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
+          const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
+          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * (D + 8) + col));
+          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * (D + 8) + col));
+          dq = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]},
+                              s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}, dq);
+        }
+        const int myq = i0 + 32 * qb2 + c32;
+        if (myq < S) {
+          uint16_t* dqr = dQ + base + (int64_t)myq * ldi;
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            ushort4 v4;
+            v4.x = to16<T>(dq[4 * rb + 0] * scale); v4.y = to16<T>(dq[4 * rb + 1] * scale);
+            v4.z = to16<T>(dq[4 * rb + 2] * scale); v4.w = to16<T>(dq[4 * rb + 3] * scale);
+            *reinterpret_cast<ushort4*>(dqr + 32 * dt + 8 * rb + 4 * h) = v4;
+          }
         }
       }
     }
@@ -887,20 +938,18 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(co
 // registers; per 64-key tile: S^T, dP^T (A = K / V rows from LDS), dS^T in registers, then
 //   dQ^T += K^T dS^T   (A = K^T via tr reads, B = dS^T from registers)
 template <typename T, int D, bool CAUSAL, int EX = 0>
-__global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __restrict__ Q,
-                                                           const uint16_t* __restrict__ K,
-                                                           const uint16_t* __restrict__ V,
-                                                           const uint16_t* __restrict__ dO,
-                                                           const float* __restrict__ LSE,
-                                                           const float* __restrict__ DELTA, uint16_t* __restrict__ dQ,
-                                                           int S, float scale, int onh, Extra ex = Extra()) {
+__device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_t* __restrict__ Q,
+                                           const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+                                           const uint16_t* __restrict__ dO, const float* __restrict__ LSE,
+                                           const float* __restrict__ DELTA, uint16_t* __restrict__ dQ, int S,
+                                           float scale, int onh, const Extra& ex) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
   const int nqb = (S + BM2 - 1) / BM2;
-  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int task = xcd_task(vblock, nblock);
   const int64_t bh = task / nqb;
   const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
   const int myq = qb + 32 * w + c32;
@@ -1024,7 +1073,54 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(const uint16_t* __res
   }
 }
 
+
+// kernel entry points: the two backward halves on their own, or both in one launch (dK/dV
+// workgroups first, then dQ): at short sequences each half alone is latency-bound and leaves
+// the chip idle in its tail, one grid lets the hardware overlap them
+template <typename T, int D, bool CAUSAL, int EX = 0>
+__global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh, Extra ex = Extra()) {
+  dkdv_v2_body<T, D, CAUSAL, EX>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh, ex);
+}
+
+template <typename T, int D, bool CAUSAL, int EX = 0>
+__global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    uint16_t* __restrict__ dQ, int S, float scale, int onh, Extra ex = Extra()) {
+  dq_v2_body<T, D, CAUSAL, EX>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh, ex);
+}
+
+template <typename T, int D, bool CAUSAL, int EX = 0>
+__global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_both_v2_kernel(
+    int ndkdv, const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    uint16_t* __restrict__ dQ, uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh,
+    Extra ex = Extra()) {
+  if ((int)blockIdx.x < ndkdv)
+    dkdv_v2_body<T, D, CAUSAL, EX>(blockIdx.x, ndkdv, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh, ex);
+  else
+    dq_v2_body<T, D, CAUSAL, EX>(blockIdx.x - ndkdv, gridDim.x - ndkdv, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh,
+                                 ex);
+}
+
 template <int D> constexpr int dkdv_v2_lds() { return 2 * 2 * BN2 * (D + 8) * 2 + 2 * 2 * BN2 * 4; }
+// + K [BM2][D+8] and one tile's dS [BN2][BM2+8] for the fused short-sequence backward
+template <int D> constexpr int bwd_short_lds() { return dkdv_v2_lds<D>() + BM2 * (D + 8) * 2 + BN2 * (BM2 + 8) * 2; }
+
+// Whole backward of one head in one workgroup for S <= BM2 (= 128, BERT's sequence): dK / dV
+// as in the dK/dV kernel, and dQ from the same dS tiles through LDS -- Q, K, V and dO are read
+// once instead of twice, and the separate dQ launch disappears.
+template <typename T, int D, int EX = 0>
+__global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_short_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    uint16_t* __restrict__ dQ, uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh,
+    Extra ex = Extra()) {
+  dkdv_v2_body<T, D, false, EX, true>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh, ex, dQ);
+}
 
 template <int D> constexpr int fwd_v2_lds() { return 2 * 2 * BN2 * (D + 8) * 2; }
 
@@ -1607,11 +1703,18 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
                       int dt, hipStream_t s, int onh) {
   const int64_t rows = (int64_t)BH * S;
   static const bool v1_env = getenv("DSA_FLASH_BWD_V1") != nullptr;
+  // DSA_FLASH_BWD_MERGE=1: dK/dV and dQ workgroups in one launch (measured neutral, r2v)
+  static const bool merge = getenv("DSA_FLASH_BWD_MERGE") && getenv("DSA_FLASH_BWD_MERGE")[0] == '1';
   const bool v1 = v1_env && onh == 0;  // the v1 kernels read dO head-major only
   FA_DISPATCH(dt, D, causal,
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
-    if (!v1) {
+    if (!v1 && merge) {
+      const int g = (S + fa::BM2 - 1) / fa::BM2 * BH;
+      hipLaunchKernelGGL((fa::bwd_both_v2_kernel<T, DD, CC>), dim3(2 * g), dim3(256), fa::dkdv_v2_lds<DD>(), s, g,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
+                         delta, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, fa::Extra());
+    } else if (!v1) {
       hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
                          fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                          (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh);
@@ -1683,15 +1786,31 @@ void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const v
   const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild);
   const int64_t rows = (int64_t)BH * S;
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
+  // DSA_FLASH_BWD_MERGE=1: dK/dV and dQ workgroups in one launch (measured neutral, r2v)
+  static const bool merge = getenv("DSA_FLASH_BWD_MERGE") && getenv("DSA_FLASH_BWD_MERGE")[0] == '1';
+  // S <= 128: one workgroup per head does dK, dV and dQ (DSA_FLASH_BWD_SHORT=0: two kernels)
+  static const bool short_ok = !(getenv("DSA_FLASH_BWD_SHORT") && getenv("DSA_FLASH_BWD_SHORT")[0] == '0');
+  const bool use_short = short_ok && S <= fa::BM2;
   FA_EX_DISPATCH(dt, D, kbias, pdrop,
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
-    hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::dkdv_v2_lds<DD>(), s,
-                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                       (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex);
-    hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
-                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                       (uint16_t*)dq, S, scale, onh, ex));
+    if (use_short)
+      hipLaunchKernelGGL((fa::bwd_short_kernel<T, DD, EE>), dim3(grid), dim3(256), fa::bwd_short_lds<DD>(), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex);
+    else if (merge)
+      hipLaunchKernelGGL((fa::bwd_both_v2_kernel<T, DD, false, EE>), dim3(2 * grid), dim3(256),
+                         fa::dkdv_v2_lds<DD>(), s, (int)grid, (const uint16_t*)q, (const uint16_t*)k,
+                         (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq, (uint16_t*)dk,
+                         (uint16_t*)dv, S, scale, onh, ex);
+    else {
+      hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::dkdv_v2_lds<DD>(), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex);
+      hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dq, S, scale, onh, ex);
+    });
 }
 
 // default: register prefetch + double-buffered LDS (2 workgroups / CU, measured faster);
