@@ -505,7 +505,7 @@ constexpr float LAZY_TH = 8.0f;
 //            kernels regenerate it in their own register layouts and nothing S x S is stored:
 //            one 32-bit hash yields the 16-bit draws of keys 2j and 2j+1 of a query row.
 //            The normaliser l / LSE stays the undropped one; O = (P * Z) V / (1 - p).
-constexpr int EX_BIAS = 1, EX_DROP = 2;
+constexpr int EX_BIAS = 1, EX_DROP = 2, EX_QKV = 4;  // EX_QKV: token-major q/k/v (Extra::inh/ild)
 struct Extra {
   const float* kbias = nullptr;
   int hdiv = 1;
@@ -518,12 +518,18 @@ struct Extra {
   int inh = 0;
   int64_t ild = 0;
 };
-template <int D>
+// compile-time layout switch: the head-major kernels keep constant row strides (immediate load
+// offsets); only EX_QKV instantiations pay for the runtime stride
+template <int D, int EX>
 __device__ __forceinline__ int64_t in_base(const Extra& ex, int64_t bh, int S) {
-  return ex.inh ? (bh / ex.inh) * (int64_t)S * ex.ild + (bh % ex.inh) * D : bh * (int64_t)S * D;
+  if constexpr ((EX & EX_QKV) != 0) return (bh / ex.inh) * (int64_t)S * ex.ild + (bh % ex.inh) * D;
+  return bh * (int64_t)S * D;
 }
-template <int D>
-__device__ __forceinline__ int64_t in_ld(const Extra& ex) { return ex.inh ? ex.ild : D; }
+template <int D, int EX>
+__device__ __forceinline__ int64_t in_ld(const Extra& ex) {
+  if constexpr ((EX & EX_QKV) != 0) return ex.ild;
+  return D;
+}
 constexpr float LOG2E = 1.4426950408889634f;
 __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
   x ^= x >> 16;
@@ -557,7 +563,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   const int64_t bh = task / nqb;
   const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
   const int myq = qb + 32 * w + c32;
-  const int64_t ib = in_base<D>(ex, bh, S), ldi = in_ld<D>(ex);
+  const int64_t ib = in_base<D, EX>(ex, bh, S), ldi = in_ld<D, EX>(ex);
   const uint16_t* Qb = Q + ib;
   const uint16_t* Kb = K + ib;
   const uint16_t* Vb = V + ib;
@@ -735,7 +741,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   const int64_t bh = task / nkb;
   const int kb = (task - (int)bh * nkb) * BM2;
   const int mykey = kb + 32 * w + c32;
-  const int64_t base = in_base<D>(ex, bh, S), ldi = in_ld<D>(ex);
+  const int64_t base = in_base<D, EX>(ex, bh, S), ldi = in_ld<D, EX>(ex);
   const int64_t obase = o_base<D>(bh, S, onh);
   const float sl2 = scale * 1.4426950408889634f;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
@@ -953,7 +959,7 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
   const int64_t bh = task / nqb;
   const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
   const int myq = qb + 32 * w + c32;
-  const int64_t base = in_base<D>(ex, bh, S), ldi = in_ld<D>(ex);
+  const int64_t base = in_base<D, EX>(ex, bh, S), ldi = in_ld<D, EX>(ex);
   const float sl2 = scale * 1.4426950408889634f;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
   const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
@@ -1742,11 +1748,16 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
       constexpr int EE = decltype(ee)::value;                                                        \
       __VA_ARGS__;                                                                                   \
     };                                                                                               \
+    auto _q = [&](auto tt, auto dd, auto ee) {                                                       \
+      constexpr int E0 = decltype(ee)::value;                                                        \
+      if (inh > 0) _go(tt, dd, std::integral_constant<int, E0 | fa::EX_QKV>{});                      \
+      else _go(tt, dd, ee);                                                                          \
+    };                                                                                               \
     auto _e = [&](auto tt, auto dd) {                                                                \
-      if (kbias && pdrop > 0.f) _go(tt, dd, std::integral_constant<int, fa::EX_BIAS | fa::EX_DROP>{}); \
-      else if (kbias) _go(tt, dd, std::integral_constant<int, fa::EX_BIAS>{});                      \
-      else if (pdrop > 0.f) _go(tt, dd, std::integral_constant<int, fa::EX_DROP>{});                \
-      else _go(tt, dd, std::integral_constant<int, 0>{});                                           \
+      if (kbias && pdrop > 0.f) _q(tt, dd, std::integral_constant<int, fa::EX_BIAS | fa::EX_DROP>{}); \
+      else if (kbias) _q(tt, dd, std::integral_constant<int, fa::EX_BIAS>{});                       \
+      else if (pdrop > 0.f) _q(tt, dd, std::integral_constant<int, fa::EX_DROP>{});                 \
+      else _q(tt, dd, std::integral_constant<int, 0>{});                                            \
     };                                                                                               \
     auto _d = [&](auto tt) {                                                                         \
       if (D == 64) _e(tt, std::integral_constant<int, 64>{});                                       \
