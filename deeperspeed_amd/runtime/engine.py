@@ -576,6 +576,7 @@ class DeepSpeedEngine(Module):
 
     def _configure_fp16_optimizer(self, optimizer):
         from .zero.stage_1_and_2 import DeepSpeedZeroOptimizer
+        self._resolve_bucket_sizes(self._config.zero_config)
         dynamic = self.dynamic_loss_scale() and not self.bfloat16_enabled()
         if getattr(optimizer, "requires_per_param_masters", False):
             # per-tensor optimizer math (LAMB trust ratio): reference engine.py picks
@@ -604,9 +605,23 @@ class DeepSpeedEngine(Module):
             off["aio"] = dict(aio)
         return off
 
+    def _resolve_bucket_sizes(self, zc):
+        """'auto' ZeRO bucket sizes from the data-parallel world (runtime/comm/bucket_sizing.py)."""
+        from .comm import bucket_sizing
+        world = dist.get_world_size(self.data_parallel_group) if dist.is_initialized() else 1
+        esize = 2 if (self.fp16_enabled() or self.bfloat16_enabled()) else 4
+        for key, scale in (("reduce_bucket_size", 1.0), ("allgather_bucket_size", 1.0),
+                           ("stage3_prefetch_bucket_size", 1.0)):
+            v = getattr(zc, key)
+            if isinstance(v, str):
+                setattr(zc, key, bucket_sizing.resolve(v, world, esize, scale))
+                if self.global_rank == 0:
+                    logger.info(f"ZeRO {key}=auto -> {getattr(zc, key):,} elements for {world} data-parallel ranks")
+
     def _configure_zero_optimizer(self, optimizer):
         stage = self.zero_optimization_stage()
         zc = self._config.zero_config
+        self._resolve_bucket_sizes(zc)
         dynamic = self.dynamic_loss_scale() and not self.bfloat16_enabled()
         common = dict(dp_process_group=self.data_parallel_group, mpu=self.mpu, clip_grad=self.gradient_clipping(),
                       static_loss_scale=self.loss_scale() or 1.0, dynamic_loss_scale=dynamic,

@@ -106,8 +106,12 @@ class DeepSpeedZeroConfig(DeepSpeedConfigObject):
         if self.overlap_comm is None:
             self.overlap_comm = self.stage == ZERO_OPTIMIZATION_WEIGHTS
         self.stage = int(self.stage)
-        self.reduce_bucket_size = int(self.reduce_bucket_size)
-        self.allgather_bucket_size = int(self.allgather_bucket_size)
+        # "auto" bucket sizes stay strings here and are sized for the data-parallel world by the
+        # engine (runtime/comm/bucket_sizing.py: ring latency vs xGMI bandwidth)
+        for key in ("reduce_bucket_size", "allgather_bucket_size", "stage3_prefetch_bucket_size"):
+            v = getattr(self, key)
+            if not (isinstance(v, str) and v.strip().lower() == "auto"):
+                setattr(self, key, int(float(v)))
         self.offload_param = _parse_offload(zd.get("offload_param"), _OFFLOAD_PARAM_DEFAULTS)
         self.offload_optimizer = _parse_offload(zd.get("offload_optimizer"), _OFFLOAD_OPT_DEFAULTS)
         # deprecated booleans map onto the new sections
