@@ -300,12 +300,16 @@ class NeoXTransformerLayer(nn.Module):
         self.mlp = NeoXMLP(cfg, device, dtype)
 
     def _block(self, x):
-        a = self.attention(self.input_layernorm(x))
+        # each LayerNorm hands its input on as a second output, so the gradients of the residual
+        # stream are summed inside the LN-backward kernels instead of by separate adds
+        h1, x = self.input_layernorm(x, residual_out=True)
+        a = self.attention(h1)
         if self.cfg.use_parallel_residual:
-            m = self.mlp(self.post_attention_layernorm(x))
-            return residual_sum(x, a, m)
+            h2, x = self.post_attention_layernorm(x, residual_out=True)
+            return residual_sum(x, a, self.mlp(h2))
         x = x + a
-        return residual_sum(x, self.mlp(self.post_attention_layernorm(x)))
+        h2, x = self.post_attention_layernorm(x, residual_out=True)
+        return residual_sum(x, self.mlp(h2))
 
     def _block_ckpt(self, x):
         self.attention._stash_key = (x.untyped_storage().data_ptr(), x.storage_offset(), tuple(x.shape))

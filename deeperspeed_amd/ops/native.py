@@ -172,7 +172,11 @@ class FusedLayerNorm(torch.nn.Module):
         self.weight = torch.nn.Parameter(torch.ones(hidden, dtype=dtype, device=device))
         self.bias = torch.nn.Parameter(torch.zeros(hidden, dtype=dtype, device=device))
 
-    def forward(self, x):
+    def forward(self, x, residual_out: bool = False):
+        """LayerNorm(x); with residual_out, (LayerNorm(x), x) where the second output carries the
+        residual branch's gradient into the LN-backward kernel (layer_norm_residual)."""
+        if residual_out:
+            return layer_norm_residual(x, self.weight, self.bias, self.eps)
         return layer_norm(x, self.weight, self.bias, self.eps)
 
     def extra_repr(self):
