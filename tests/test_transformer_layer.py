@@ -208,3 +208,25 @@ def test_encoder_flash_keep_mask_statistics():
     both = (d[..., 0::2] * d[..., 1::2]).mean().item()  # the two halves of one hash
     assert abs(both - 0.01) < 0.003
     assert native.flash_dropout_keep_mask(1, 1, 64, 0.0, 5).all()
+
+
+def test_layer_norm_residual_passthrough_gradients():
+    """(LN(x), x) with the residual gradient summed in the LN backward equals LN(x) + separate
+    residual use of x (CPU reference path of native.layer_norm_residual)."""
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(0)
+    x = torch.randn(6, 10, 32, dtype=torch.float32)
+    w = torch.randn(32, dtype=torch.float32) * 0.1 + 1
+    b = torch.randn(32, dtype=torch.float32) * 0.1
+    gy, gr = torch.randn(6, 10, 32, dtype=torch.float32), torch.randn(6, 10, 32, dtype=torch.float32)
+    res = []
+    for fused in (True, False):
+        xi, wi, bi = (t.clone().requires_grad_(True) for t in (x, w, b))
+        if fused:
+            y, xr = native.layer_norm_residual(xi, wi, bi, 1e-5)
+        else:
+            y, xr = torch.nn.functional.layer_norm(xi, (32,), wi, bi, 1e-5), xi
+        ((y * gy).sum() + (xr * gr).sum()).backward()
+        res.append((y.detach(), xi.grad, wi.grad, bi.grad))
+    for a, c in zip(*res):
+        assert torch.allclose(a, c, atol=1e-4, rtol=1e-4)
