@@ -29,8 +29,19 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+# stdout carries exactly one line, the result JSON: everything else printed to fd 1 (framework
+# logs, the RCCL banner written by the C library) goes to stderr; emit_result() writes to the
+# original stdout
+_RESULT_FD = os.dup(1)
+sys.stdout.flush()
+os.dup2(2, 1)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def emit_result(out):
+    os.write(_RESULT_FD, (json.dumps(out) + "\n").encode())
 
 REF_TOKENS_PER_GPU = 410.0  # BASELINE.md "North-star planning targets (derived)"
 
@@ -395,7 +406,7 @@ def main():
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N), BASELINE.md derived target"},
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit_result(out)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -472,7 +483,7 @@ def run_pipeline(args, cfg, mb, ga, world, rank, dev):
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1)},
     }
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit_result(out)
     dist.barrier()
     dist.destroy_process_group()
 
