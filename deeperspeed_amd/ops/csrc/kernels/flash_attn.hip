@@ -444,6 +444,19 @@ template <> struct Mfma32<f16_t> {
 constexpr int BM2 = 128;
 constexpr int BN2 = 64;
 
+// reductions across the two 32-lane halves of a wave (the two halves of a query row's keys):
+// v_permlane32_swap of x with itself leaves {lower half, upper half} values of the lane pair in
+// the two results on EVERY lane, so max / sum need no ds_bpermute round trip through the LDS
+// crossbar and no select; both halves add in the same order (bit-identical row statistics)
+__device__ __forceinline__ float xhalf_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // raw v_exp_f32 (no denormal range fix-up: softmax weights below 2^-126 are zero anyway)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -643,7 +656,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 32; ++i) mx = fmaxf(mx, sv[i]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xhalf_max(mx);
     const float mt = mx * a2;
     if (!LAZY || __any(mt > m + LAZY_TH)) {  // wave-uniform
       const float mn = fmaxf(m, mt);
@@ -666,7 +679,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
       ps1 += sv[i + 1];
     }
     ps += ps1;
-    ps += __shfl_xor(ps, 32, 64);
+    ps = xhalf_sum(ps);
     l += ps;
     if constexpr (DROP) {  // values 2i, 2i+1 of a lane are keys 2j, 2j+1 of its query row
 #pragma unroll
@@ -1267,7 +1280,7 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sfwd_kernel(const uint16_t* _
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 32; ++i) mx = fmaxf(mx, sv[i]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xhalf_max(mx);
     const float mt = mx * sl2;
     if (__any(mt > m + LAZY_TH)) {
       const float mn = fmaxf(m, mt);
@@ -1289,7 +1302,7 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sfwd_kernel(const uint16_t* _
       ps1 += sv[i + 1];
     }
     ps += ps1;
-    ps += __shfl_xor(ps, 32, 64);
+    ps = xhalf_sum(ps);
     l += ps;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
