@@ -208,6 +208,11 @@ def main():
         zcfg.update(stage3_force_sharded=True, grad_accum_dtype="param")
     if resident:
         zcfg["resident_grads"] = True
+    # bound single-rank ZeRO-3: the fused Adam step overlaps the next forward (side stream,
+    # per-bucket events); DSA_OVERLAP_STEP=0 keeps the serial step
+    if (world == 1 and not args.force_sharded and offload in ("compact", "none")
+            and os.environ.get("DSA_OVERLAP_STEP", "1") != "0"):
+        zcfg["overlap_step"] = True
     if offload == "compact":
         zcfg["compact_master"] = True
     elif offload == "moments":
@@ -402,6 +407,7 @@ def main():
                    "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) / 2**30, 1),
                    "max_live_parameters": live, "stashed_attention_layers": stashed,
                    "zero3_path": "sharded" if (world > 1 or args.force_sharded) else "bound-single-rank",
+                   "overlap_step": bool(zcfg.get("overlap_step", False)),
                    "resident_grads": resident,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N), BASELINE.md derived target"},
     }

@@ -652,7 +652,7 @@ class DeepSpeedEngine(Module):
                                                  param_persistence_threshold=zc.stage3_param_persistence_threshold,
                                                  unit_max_numel=unit, offload_param=zc.offload_param,
                                                  overlap_comm=zc.overlap_comm, sub_group_size=zc.sub_group_size,
-                                                 **common)
+                                                 overlap_step=bool(getattr(zc, "overlap_step", False)), **common)
         raise NotImplementedError("ZeRO stage {} not implemented".format(stage))
 
     def _configure_progressive_layer_drop(self):
@@ -999,13 +999,21 @@ class DeepSpeedEngine(Module):
         elif not valid:
             logger.warning(msg)
 
+    def synchronize(self):
+        """Order the current stream after an overlapped optimizer step (zero_optimization.overlap_step)."""
+        sync = getattr(self.optimizer, "synchronize_step", None)
+        if sync is not None:
+            sync()
+
     def module_state_dict(self, destination=None, prefix="", keep_vars=False):
+        self.synchronize()
         return self.module.state_dict(destination=destination, prefix=prefix, keep_vars=keep_vars)
 
     def load_module_state_dict(self, state_dict, strict=True):
         self.module.load_state_dict(state_dict, strict=strict)
 
     def save_checkpoint(self, save_dir, tag=None, client_state=None, save_latest=True):
+        self.synchronize()
         client_state = client_state or {}
         if self.zero_optimization_partition_weights():
             pass  # shards are always in partitioned form
@@ -1112,6 +1120,7 @@ class DeepSpeedEngine(Module):
 
     def load_checkpoint(self, load_dir, tag=None, load_module_strict=True, load_optimizer_states=True,
                         load_lr_scheduler_states=True):
+        self.synchronize()
         if tag is None:
             latest_path = os.path.join(load_dir, "latest")
             if os.path.isfile(latest_path):

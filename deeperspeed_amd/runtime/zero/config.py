@@ -49,6 +49,9 @@ _SCALARS = {
     # over dp>1, else the parameter dtype; "fp32"; "param").  `stage3_unit_max_numel` bounds
     # the module subtree that forms one gather/reduce unit.
     "stage3_force_sharded": False,
+    # MI355X extension: the bound single-rank ZeRO-3 optimizer step runs on a side stream,
+    # overlapped with the next forward (stage3.py, overlapped step)
+    "overlap_step": False,
     "resident_grads": False,
     "grad_accum_dtype": "auto",
     "stage3_unit_max_numel": int(2e8),

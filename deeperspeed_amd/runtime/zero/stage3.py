@@ -142,7 +142,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                  gradient_predivide_factor=1.0, gradient_accumulation_steps=1, offload_optimizer=None,
                  offload_param=None, timers=None, overlap_comm=True, sub_group_size=int(1e12), verbose=False,
                  compact_master=False, force_sharded=False, resident_grads=False, grad_accum_dtype="auto",
-                 reduce_scatter=True, reduce_bucket_size=0):
+                 reduce_scatter=True, reduce_bucket_size=0, overlap_step=False):
         super().__init__(init_optimizer, dp_process_group=dp_process_group, mpu=mpu, clip_grad=clip_grad,
                          static_loss_scale=static_loss_scale, dynamic_loss_scale=dynamic_loss_scale,
                          dynamic_loss_args=dynamic_loss_args, fp32_reduce=fp32_reduce,
@@ -223,6 +223,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             for g in self.groups:
                 g.shard_param = None  # the NVMe files are the only copy from here on
         self._register_hooks()
+        self._setup_overlap_step(bool(overlap_step))
         for m in module.modules():
             for p in m.__dict__.get("_external_params", []):
                 self.register_external_parameter(m, p)
@@ -492,6 +493,76 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def unit_of(self, p) -> Optional[ZeroUnit]:
         return self._unit_of_param.get(id(p))
 
+    # ------------------------------------------------------------------ overlapped step
+    # MI355X extension (`zero_optimization.overlap_step`, bound single-rank path): the fused
+    # Adam of one optimizer step runs on a side stream, bucket by bucket, while the next
+    # forward starts on the compute stream; each module's forward pre-hook waits only for the
+    # event of the bucket(s) holding its own parameters, so layer 0 resumes after the first
+    # bucket's update instead of after the whole step (HBM-bound Adam next to compute-bound
+    # GEMMs).  Gradients are zeroed on the side stream after their update, and the next
+    # backward (and every state access: checkpoints, zero_grad, ...) first waits for the whole
+    # step.  Parameters read outside a module forward right after step() need
+    # `synchronize_step()` (the engine calls it before checkpointing).
+    def _setup_overlap_step(self, enabled: bool):
+        self._overlap_step = (enabled and self.single and self.offload is None and self.fused
+                              and torch.cuda.is_available() and str(self.device).startswith("cuda"))
+        self._step_stream = None
+        self._step_done = None
+        self._bucket_events: Dict[tuple, torch.cuda.Event] = {}
+        if not self._overlap_step:
+            return
+        self._step_stream = torch.cuda.Stream(device=self.device)
+        self._bucket_key = {}
+        owner = {}
+        for gi, g in enumerate(self.groups):
+            for bi, b in enumerate(g.buckets):
+                self._bucket_key[id(b)] = (gi, bi)
+                for p in b.params:
+                    owner[id(p)] = (gi, bi)
+        self._module_buckets = {}
+        for m in self.module.modules():
+            keys = sorted({owner[id(p)] for p in m.parameters(recurse=False) if id(p) in owner})
+            if keys:
+                self._module_buckets[m] = keys
+                self._handles.append(m.register_forward_pre_hook(self._wait_bucket_updates))
+
+    def _wait_bucket_updates(self, module, inputs):
+        if not self._bucket_events:
+            return
+        cur = torch.cuda.current_stream()
+        for key in self._module_buckets.get(module, ()):
+            ev = self._bucket_events.get(key)
+            if ev is not None:
+                cur.wait_event(ev)
+
+    def synchronize_step(self):
+        """Order the compute stream after an overlapped optimizer step (no host wait)."""
+        if self._step_done is not None:
+            torch.cuda.current_stream().wait_event(self._step_done)
+            self._step_done = None
+            self._bucket_events = {}
+
+    def step(self, closure=None):
+        if not self._overlap_step:
+            return super().step(closure)
+        self.synchronize_step()
+        overflow, total = self._check_overflow_and_scale()  # host sync: the gradients are final
+        if overflow:
+            self.zero_grad()
+            return
+        grad_scale, _ = self._unscale_and_clip_coef(total)
+        side, cur = self._step_stream, torch.cuda.current_stream()
+        side.wait_stream(cur)
+        self._bucket_events = {}
+        with torch.cuda.stream(side):
+            self._inner_step(grad_scale)
+            self._post_step()
+            for g in self.groups:  # each bucket's gradients after its update, on the same stream
+                g.shard_grad.zero_()
+            self._grads_nonzero = False
+        self._step_done = torch.cuda.Event()
+        self._step_done.record(side)
+
     # ------------------------------------------------------------------ hooks
     def _register_hooks(self):
         self._handles = []
@@ -691,6 +762,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
 
     # ------------------------------------------------------------------ step
     def backward(self, loss, retain_graph=False):
+        self.synchronize_step()
         self._bwd_pos = 0
         self.loss_scaler.backward(loss.float(), retain_graph=retain_graph)
 
@@ -705,6 +777,18 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def _after_bucket_update(self, g, b):
         if self.param_nvme and g.shard_param is None:
             self._pswap.swap_out(self._pkey[id(b)])
+        if self._overlap_step and torch.cuda.current_stream() == self._step_stream:
+            ev = torch.cuda.Event()
+            ev.record(self._step_stream)
+            self._bucket_events[self._bucket_key[id(b)]] = ev
+
+    def state_dict(self):
+        self.synchronize_step()
+        return super().state_dict()
+
+    def load_state_dict(self, *args, **kwargs):
+        self.synchronize_step()
+        return super().load_state_dict(*args, **kwargs)
 
     def param_shard_host(self, g) -> torch.Tensor:
         """This rank's low-precision shard of group g as a host tensor (checkpoints)."""
@@ -745,6 +829,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                 self._wait(u)
 
     def zero_grad(self, set_to_none=True):
+        self.synchronize_step()
         for g in self.groups:
             g.shard_grad.zero_()
         self._grads_nonzero = False

@@ -16,7 +16,7 @@ def _env():
     os.environ.setdefault("WORLD_SIZE", "1")
 
 
-def _run(stage, offload=None, steps=4, ga=2, offload_param=None, compact=False):
+def _run(stage, offload=None, steps=4, ga=2, offload_param=None, compact=False, overlap_step=False, weights=False):
     _env()
     import deeperspeed_amd as ds
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
@@ -31,6 +31,8 @@ def _run(stage, offload=None, steps=4, ga=2, offload_param=None, compact=False):
         z["offload_param"] = {"device": offload_param, "pin_memory": True, "nvme_path": "/tmp/dsa_pnvme"}
     if compact:
         z["compact_master"] = True
+    if overlap_step:
+        z["overlap_step"] = True
     conf = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": ga,
             "optimizer": {"type": "Adam", "params": {"lr": 3e-4}}, "fp16": {"enabled": True, "type": "bfloat16"},
             "fp32_allreduce": False, "gradient_clipping": 1.0, "zero_optimization": z}
@@ -45,7 +47,20 @@ def _run(stage, offload=None, steps=4, ga=2, offload_param=None, compact=False):
             engine.backward(loss)
             engine.step()
         losses.append(float(loss))
+    if weights:
+        engine.synchronize()
+        return losses, [p.detach().float().cpu() for p in engine.module.parameters()]
     return losses
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_overlapped_step_is_exact(compact):
+    """zero_optimization.overlap_step: the bound ZeRO-3 Adam runs on a side stream next to the
+    next forward (per-bucket events); losses and weights equal the serial step bit for bit."""
+    base, wb = _run(3, None, steps=3, ga=2, compact=compact, weights=True)
+    over, wo = _run(3, None, steps=3, ga=2, compact=compact, overlap_step=True, weights=True)
+    assert base == over
+    assert all(torch.equal(a, b) for a, b in zip(wb, wo))
 
 
 @pytest.mark.parametrize("stage", [0, 1, 2, 3])
