@@ -314,6 +314,17 @@ def main():
             m.attention.stash_outputs = True
         log(f"selective recompute: {n}/{len(layers)} layers keep attention outputs "
             f"({n * per_layer / 2**30:.1f} GiB; reserved peak {torch.cuda.max_memory_reserved() / 2**30:.1f} GiB)")
+        # the remaining layers park their stash in pinned host memory (copy engines over PCIe,
+        # prefetched back by the recompute of the layers above): opt-in, DSA_STASH_OFFLOAD=1 -- on the
+        # measured box the PCIe copies throttled the forward (profiles/aux/host_stash_ab.log)
+        if os.environ.get("DSA_STASH_OFFLOAD", "0") == "1" and n < len(layers):
+            from deeperspeed_amd.runtime.activation_checkpointing import host_stash as hs
+            hs.host_stash().max_backlog = int(os.environ.get("DSA_STASH_OFFLOAD_BACKLOG", "6"))
+            for m in layers[: len(layers) - n]:
+                m.attention.stash_outputs = True
+                m.attention.stash_offload = True
+            log(f"selective recompute: {len(layers) - n} more layers park theirs in pinned host memory "
+                f"({(len(layers) - n) * per_layer / 2**30:.1f} GiB)")
         torch.cuda.reset_peak_memory_stats()
         return n
 
@@ -331,9 +342,13 @@ def main():
         if over <= 0:
             return n
         drop = min(n, int(-(-over // per_layer)))
+        offload = any(l.attention.stash_offload for l in layers)
         for m in layers[len(layers) - n: len(layers) - n + drop]:
-            m.attention.stash_outputs = False
             m.attention._stash.clear()
+            if offload:
+                m.attention.stash_offload = True  # parked in host memory instead of HBM
+            else:
+                m.attention.stash_outputs = False
         torch.cuda.empty_cache()
         log(f"stash safety: reserved peak {torch.cuda.max_memory_reserved() / 2**30:.1f} GiB is within "
             f"{floor / 2**30:.1f} GiB of the budget; {drop} layer(s) back to full recompute ({n - drop} stashed)")
@@ -406,6 +421,8 @@ def main():
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
                    "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) / 2**30, 1),
                    "max_live_parameters": live, "stashed_attention_layers": stashed,
+                   "host_stashed_attention_layers": sum(1 for m in engine.module.modules()
+                                                        if getattr(m, "stash_offload", False)),
                    "zero3_path": "sharded" if (world > 1 or args.force_sharded) else "bound-single-rank",
                    "overlap_step": bool(zcfg.get("overlap_step", False)),
                    "resident_grads": resident,

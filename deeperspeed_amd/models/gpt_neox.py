@@ -202,8 +202,13 @@ class NeoXAttention(nn.Module):
         # same storage), so several forwards in flight before their backwards (pipeline 1F1B,
         # forward-forward-backward loops) each recompute with their own tensors.
         self.stash_outputs = False
+        # stash_offload: the stash is parked in pinned host memory between the forward and the
+        # recompute (runtime/activation_checkpointing/host_stash.py) -- for layers beyond the
+        # HBM budget; the recompute of the layer above prefetches it back
+        self.stash_offload = False
         self._stash = {}
         self._stash_key = None  # set by the enclosing layer around each block call
+        self.__dict__["_below"] = []  # attention modules of the next layers in backward order
 
     _STASH_LIMIT = 16  # in-flight checkpointed forwards per layer (pipeline depth bound)
 
@@ -215,6 +220,13 @@ class NeoXAttention(nn.Module):
         stash = self._stash.pop(key, None) if (key is not None and self._stash and torch.is_grad_enabled()
                                                and ds_ckpt.is_recomputing()) else None
         if stash is not None:
+            from ..runtime.activation_checkpointing.host_stash import StashEntry, host_stash
+            if isinstance(stash, StashEntry):
+                stash = host_stash().fetch(stash)
+            for below in self.__dict__["_below"]:  # start bringing the next layers' stashes back
+                for e in below._stash.values():
+                    if isinstance(e, StashEntry):
+                        host_stash().prefetch(e)
             self.query_key_value.grad_only_next = True  # gradient handle only: q, k, v are kept
             qkv = self.query_key_value(x)
             q, k, v = rotary_split(qkv, cfg.num_heads, cfg.head_dim, cfg.rotary_dim, cfg.rotary_base, qscale=qs,
@@ -235,7 +247,11 @@ class NeoXAttention(nn.Module):
                     if key in self._stash or len(self._stash) >= self._STASH_LIMIT:
                         raise RuntimeError(f"layer {self.layer_number}: selective-recompute stash for this input "
                                            f"was never consumed (forward without backward?)")
-                    self._stash[key] = (q, k, v, ctx, lse)
+                    if self.stash_offload:
+                        from ..runtime.activation_checkpointing.host_stash import host_stash
+                        self._stash[key] = host_stash().park(id(self), (q, k, v, ctx, lse))
+                    else:
+                        self._stash[key] = (q, k, v, ctx, lse)
             else:
                 ctx = attention(q, k, v, causal=True, softmax_scale=1.0, dropout_p=cfg.attention_dropout,
                                 training=self.training, out_layout="bshd")
@@ -284,6 +300,16 @@ class NeoXMLP(nn.Module):
 
     def forward(self, x):
         return self.dense_4h_to_h(self.dense_h_to_4h(x))
+
+
+STASH_PREFETCH_DEPTH = 2  # layers whose host-parked stash a recompute starts bringing back
+
+
+def link_stash_prefetch(attentions):
+    """Each attention module learns the modules recomputed right after it in backward (the
+    layers below), whose host-parked stashes its own recompute prefetches."""
+    for i, a in enumerate(attentions):
+        a.__dict__["_below"] = [attentions[j] for j in range(i - 1, max(-1, i - 1 - STASH_PREFETCH_DEPTH), -1)]
 
 
 class NeoXTransformerLayer(nn.Module):
@@ -335,6 +361,7 @@ class GPTNeoX(nn.Module):
         self.cfg = cfg
         self.embed_in = nn.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
         self.layers = nn.ModuleList([NeoXTransformerLayer(cfg, i, device, dtype) for i in range(cfg.num_layers)])
+        link_stash_prefetch([l.attention for l in self.layers])
         self.final_layer_norm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
         self.embed_out = Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
         self.reset_parameters()

@@ -8,7 +8,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _grads(stash_layers):
+def _grads(stash_layers, offload=False):
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
     torch.manual_seed(0)
     cfg = get_config("tiny", hidden_size=384, num_heads=4, num_layers=3, max_seq_len=128,
@@ -17,6 +17,7 @@ def _grads(stash_layers):
     layers = [m for m in model.modules() if type(m).__name__ == "NeoXTransformerLayer"]
     for m in layers[:stash_layers]:
         m.attention.stash_outputs = True
+        m.attention.stash_offload = offload
     g = torch.Generator(device="cuda").manual_seed(1)
     ids = torch.randint(0, cfg.vocab_size, (2, 128), device="cuda", generator=g)
     for _ in range(2):  # second pass reuses nothing stale from the first
@@ -27,16 +28,20 @@ def _grads(stash_layers):
     return float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
 
 
-def test_stash_matches_full_recompute():
+@pytest.mark.parametrize("offload", [False, True])
+def test_stash_matches_full_recompute(offload):
+    """HBM stash, and the stash parked in pinned host memory (D2H on a copy stream, prefetched
+    back by the recompute of the layer above) give the full-recompute gradients."""
     l0, g0 = _grads(0)
-    l1, g1 = _grads(2)
+    l1, g1 = _grads(3 if offload else 2, offload)
     assert l0 == l1
     assert g0.keys() == g1.keys()
     for n in g0:
         torch.testing.assert_close(g1[n], g0[n], atol=1e-3, rtol=1e-3, msg=n)
 
 
-def test_stash_two_forwards_before_backward():
+@pytest.mark.parametrize("offload", [False, True])
+def test_stash_two_forwards_before_backward(offload):
     """Two checkpointed forwards in flight (pipeline 1F1B pattern): each backward must
     recompute with its own micro-batch's stash."""
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
@@ -49,6 +54,7 @@ def test_stash_two_forwards_before_backward():
         for m in model.modules():
             if type(m).__name__ == "NeoXAttention":
                 m.stash_outputs = stash
+                m.stash_offload = stash and offload
         g = torch.Generator(device="cuda").manual_seed(3)
         a = torch.randint(0, cfg.vocab_size, (2, 128), device="cuda", generator=g)
         b = torch.randint(0, cfg.vocab_size, (2, 128), device="cuda", generator=g)
