@@ -15,6 +15,7 @@ pipeline engine (`to_pipeline()` builds a PipelineModule of LayerSpecs).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field, asdict
 from typing import Optional
 
@@ -100,9 +101,22 @@ class LinearBiasGeLU(nn.Linear):
     def __init__(self, in_features, out_features, approximate=False, device=None, dtype=None):
         super().__init__(in_features, out_features, device=device, dtype=dtype)
         self.approximate = approximate
+        # set by NeoXMLP when the consumer is a gradient-only linear during recompute: the
+        # activation is then produced transposed (its only reader is that linear's weight
+        # gradient, which wants it reduction-contiguous)
+        self.colmajor_in_recompute = False
 
     def forward(self, x):
-        return native.bias_gelu(linear(x, self.weight), self.bias, self.approximate)
+        u = linear(x, self.weight)
+        if (self.colmajor_in_recompute and _SKIP_OUTPUTS and torch.is_grad_enabled() and COLMAJOR_GELU
+                and native.bias_gelu_t_supported(u)):
+            return native.bias_gelu_colmajor(u, self.bias, self.approximate)
+        # the backward also writes du^T for this layer's own weight gradient
+        return native.bias_gelu(u, self.bias, self.approximate, offer_t=u.is_cuda)
+
+
+# DSA_COLMAJOR_GELU=0: the recompute writes the GeLU output row-major (fc2's wgrad transposes it)
+COLMAJOR_GELU = os.environ.get("DSA_COLMAJOR_GELU", "1") != "0"
 
 
 _SKIP_OUTPUTS = 0
@@ -297,6 +311,7 @@ class NeoXMLP(nn.Module):
         self.dense_h_to_4h = LinearBiasGeLU(cfg.hidden_size, cfg.intermediate_size, cfg.gelu_approximate,
                                             device=device, dtype=dtype)
         self.dense_4h_to_h = OutputLinear(cfg.intermediate_size, cfg.hidden_size, device=device, dtype=dtype)
+        self.dense_h_to_4h.colmajor_in_recompute = self.dense_4h_to_h.skip_in_recompute
 
     def forward(self, x):
         return self.dense_4h_to_h(self.dense_h_to_4h(x))

@@ -321,6 +321,47 @@ Tensor transpose2d(Tensor x, OptT colsum_out, bool accum) {
   return y;
 }
 
+// gelu(x + b)^T for x [R, C] contiguous 16-bit (R % 128 == 0, C % 64 == 0): the activation
+// recompute's fc1 output handed straight to fc2's weight gradient in the layout it wants.
+Tensor bias_gelu_fwd_t(Tensor x, OptT b, bool approx) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && aligned16(x.data_ptr()), "bias_gelu_fwd_t: x must be contiguous 2-D");
+  const int dt = dcode(x);
+  TORCH_CHECK(dt != dsa::kCodeF32, "bias_gelu_fwd_t: 16-bit dtypes only");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(dsa::transpose_supported(R, C), "bias_gelu_fwd_t: rows must be a multiple of 128 and cols of 64");
+  if (b.has_value()) TORCH_CHECK(b->numel() == C && b->scalar_type() == x.scalar_type() && b->is_contiguous(),
+                                 "bias_gelu_fwd_t: bias");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor yt = at::empty({C, R}, x.options());
+  dsa::launch_bias_gelu_fwd_t(x.data_ptr(), b.has_value() ? b->data_ptr() : nullptr, yt.data_ptr(), R, (int)C,
+                              approx ? 1 : 0, dt, cur_stream());
+  return yt;
+}
+
+// Returns (dx, dx^T, dbias): dx = dy * gelu'(x + b) for contiguous 2-D dy, x [R, C].
+std::vector<Tensor> bias_gelu_bwd_t(Tensor dy, Tensor x, OptT b, bool approx) {
+  check_dev(dy, "dy"); check_dev(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type() && x.dim() == 2 && x.is_contiguous() &&
+              dy.is_contiguous() && aligned16(x.data_ptr()) && aligned16(dy.data_ptr()), "bias_gelu_bwd_t: operands");
+  const int dt = dcode(x);
+  TORCH_CHECK(dt != dsa::kCodeF32, "bias_gelu_bwd_t: 16-bit dtypes only");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(dsa::transpose_supported(R, C), "bias_gelu_bwd_t: rows must be a multiple of 128 and cols of 64");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor dx = at::empty_like(x), dxt = at::empty({C, R}, x.options());
+  Tensor db, partial;
+  if (b.has_value()) {
+    TORCH_CHECK(b->numel() == C && b->scalar_type() == x.scalar_type() && b->is_contiguous(), "bias_gelu_bwd_t: bias");
+    db = at::empty_like(*b);
+    partial = at::empty({dsa::transpose_partial_rows(R) * C}, x.options().dtype(at::kFloat));
+  }
+  dsa::launch_bias_gelu_bwd_t(dy.data_ptr(), x.data_ptr(), b.has_value() ? b->data_ptr() : nullptr, dx.data_ptr(),
+                              dxt.data_ptr(), partial.defined() ? partial.data_ptr<float>() : nullptr,
+                              b.has_value() ? db.data_ptr() : nullptr, R, (int)C, approx ? 1 : 0, dt, cur_stream());
+  return {dx, dxt, db};
+}
+
 // BERT head layout moves (16-bit, head dim % 8 == 0)
 std::vector<Tensor> heads_split(Tensor qkv, int64_t NH) {
   check_dev(qkv, "qkv");
@@ -918,6 +959,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("bias_gelu_fwd_t", &bias_gelu_fwd_t);
+  m.def("bias_gelu_bwd_t", &bias_gelu_bwd_t);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);
   m.def("heads_split", &heads_split);
   m.def("heads_merge", &heads_merge);

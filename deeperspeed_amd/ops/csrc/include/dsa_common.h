@@ -40,6 +40,26 @@ __device__ __forceinline__ uint16_t f32_to_f16(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// GeLU (exact erf, or the tanh approximation) and its derivative, fp32
+__device__ __forceinline__ float gelu_f(float x, bool approx) {
+  if (approx) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  }
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+__device__ __forceinline__ float dgelu_f(float x, bool approx) {
+  if (approx) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    const float u = k0 * (x + k1 * x * x * x);
+    const float t = tanhf(u);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+  }
+  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
 template <typename T> struct Conv;
 template <> struct Conv<float> {
   __device__ __forceinline__ static float load(const float* p, int64_t i) { return p[i]; }

@@ -69,6 +69,12 @@ bool transpose_supported(int64_t R, int64_t C);
 int64_t transpose_partial_rows(int64_t R);
 void launch_transpose(const void* x, void* y, float* partial, void* colsum_out, int colsum_accum, int64_t R, int C,
                       int64_t ldx, int dt, hipStream_t s);
+// yt[C][R] = gelu(x[R][C] + b)^T (same shape rules, x contiguous)
+void launch_bias_gelu_fwd_t(const void* x, const void* b, void* yt, int64_t R, int C, int approx, int dt,
+                            hipStream_t s);
+// dx = dy * gelu'(x + b) row-major and dxt = dx^T; db = column sums of dx (when partial != null)
+void launch_bias_gelu_bwd_t(const void* dy, const void* x, const void* b, void* dx, void* dxt, float* partial,
+                            void* db, int64_t R, int C, int approx, int dt, hipStream_t s);
 
 // attn_elem.hip
 void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const float* cs, int B, int S, int NH,

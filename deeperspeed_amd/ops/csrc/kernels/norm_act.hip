@@ -375,24 +375,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
 // ---------------------------------------------------------------------------
 // bias + GeLU (exact erf or tanh approximation)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float gelu_f(float x, bool approx) {
-  if (approx) {
-    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-    return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
-  }
-  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
-}
-__device__ __forceinline__ float dgelu_f(float x, bool approx) {
-  if (approx) {
-    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-    const float u = k0 * (x + k1 * x * x * x);
-    const float t = tanhf(u);
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
-  }
-  const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
+// gelu_f / dgelu_f live in dsa_common.h (shared with the transposing GeLU kernels)
 
 template <typename T>
 __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict__ x, const T* __restrict__ b,

@@ -7,6 +7,12 @@
 // so the transpose of dY also produces it (fp32 partial per 128-row tile, reduced by
 // colsum_kernel), replacing a separate full read of dY.
 //
+// The same tile walk also runs the MLP's bias + GeLU with a transposed output: forward (the
+// activation recompute, where fc2's forward value is never read and its weight gradient wants
+// gelu(u + b)^T) and backward (du = dy * gelu'(u + b) row-major for fc1's input gradient, du^T
+// + its column sum for fc1's weight / bias gradients), each replacing an elementwise pass plus a
+// separate transpose of a [tokens, 4h] tensor.
+//
 // Reference counterpart: `Transpose_Kernel` / `transform_0213` (csrc/transformer/
 // transform_kernels.cu:7,56) and `column_sum_reduce` (csrc/transformer/general_kernels.cu:6).
 //
@@ -35,10 +41,45 @@ __device__ __forceinline__ int swz(int row, int cc) {
 template <typename T> __device__ __forceinline__ float h2f(short v);
 template <> __device__ __forceinline__ float h2f<bf16_t>(short v) { return bf16_to_f32((uint16_t)v); }
 template <> __device__ __forceinline__ float h2f<f16_t>(short v) { return f16_to_f32((uint16_t)v); }
+template <typename T> __device__ __forceinline__ uint16_t f2h(float v);
+template <> __device__ __forceinline__ uint16_t f2h<bf16_t>(float v) { return f32_to_bf16(v); }
+template <> __device__ __forceinline__ uint16_t f2h<f16_t>(float v) { return f32_to_f16(v); }
 
-template <typename T, bool SUM>
+// Elementwise op applied to each loaded 8-element chunk before it is staged for the transpose.
+enum TrOp : int {
+  kCopy = 0,     // y^T = x^T
+  kGeluFwd = 1,  // y^T = gelu(x + b)^T  (only the transposed output is written)
+  kGeluBwd = 2,  // g = x * gelu'(x2 + b): g written row-major to yr AND transposed to y
+};
+
+template <typename T>
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = h2f<T>((short)(w[j] & 0xffff));
+    f[2 * j + 1] = h2f<T>((short)(w[j] >> 16));
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 o;
+  o.x = (uint32_t)f2h<T>(f[0]) | ((uint32_t)f2h<T>(f[1]) << 16);
+  o.y = (uint32_t)f2h<T>(f[2]) | ((uint32_t)f2h<T>(f[3]) << 16);
+  o.z = (uint32_t)f2h<T>(f[4]) | ((uint32_t)f2h<T>(f[5]) << 16);
+  o.w = (uint32_t)f2h<T>(f[6]) | ((uint32_t)f2h<T>(f[7]) << 16);
+  return o;
+}
+
+// x2 / bias / yr / approx are used by the GeLU ops only (x2: the GeLU input of kGeluBwd, same
+// layout as x; yr: row-major output [R][C], row stride C).
+template <typename T, bool SUM, int OP>
 __global__ void __launch_bounds__(256) transpose_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
-                                                        float* __restrict__ partial, int64_t R, int C, int64_t ldx) {
+                                                        float* __restrict__ partial, int64_t R, int C, int64_t ldx,
+                                                        const uint16_t* __restrict__ x2,
+                                                        const uint16_t* __restrict__ bias,
+                                                        uint16_t* __restrict__ yr, int approx) {
   __shared__ __attribute__((aligned(16))) uint16_t tile[TR * TC];
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.y * TR;
@@ -48,6 +89,40 @@ __global__ void __launch_bounds__(256) transpose_kernel(const uint16_t* __restri
   for (int i = 0; i < 4; ++i) {
     const int c = t + 256 * i, row = c >> 3, cc = c & 7;
     v[i] = *reinterpret_cast<const uint4*>(x + (r0 + row) * ldx + c0 + cc * 8);
+  }
+  if constexpr (OP != kCopy) {
+    uint4 u[4];
+    if constexpr (OP == kGeluBwd) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = t + 256 * i, row = c >> 3, cc = c & 7;
+        u[i] = *reinterpret_cast<const uint4*>(x2 + (r0 + row) * ldx + c0 + cc * 8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = t + 256 * i, row = c >> 3, cc = c & 7;
+      float f[8], b[8];
+      unpack8<T>(v[i], f);
+      if (bias) {
+        unpack8<T>(*reinterpret_cast<const uint4*>(bias + c0 + cc * 8), b);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = 0.f;
+      }
+      if constexpr (OP == kGeluFwd) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j] + b[j], approx);
+      } else {
+        float xi[8];
+        unpack8<T>(u[i], xi);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= dgelu_f(xi[j] + b[j], approx);
+      }
+      v[i] = pack8<T>(f);
+      if constexpr (OP == kGeluBwd)
+        *reinterpret_cast<uint4*>(yr + (r0 + row) * (int64_t)C + c0 + cc * 8) = v[i];
+    }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -96,12 +171,36 @@ void launch_transpose(const void* x, void* y, float* partial, void* colsum_out, 
   const dim3 grid(C / TC, (unsigned)(R / TR));
   DSA_DISPATCH_16(dt, T,
     if (partial) {
-      hipLaunchKernelGGL((transpose_kernel<T, true>), grid, dim3(256), 0, s, (const uint16_t*)x, (uint16_t*)y,
-                         partial, R, C, ldx);
+      hipLaunchKernelGGL((transpose_kernel<T, true, kCopy>), grid, dim3(256), 0, s, (const uint16_t*)x, (uint16_t*)y,
+                         partial, R, C, ldx, nullptr, nullptr, nullptr, 0);
       launch_colsum_partials(partial, (int)(R / TR), C, colsum_out, colsum_accum, dt, s);
     } else {
-      hipLaunchKernelGGL((transpose_kernel<T, false>), grid, dim3(256), 0, s, (const uint16_t*)x, (uint16_t*)y,
-                         nullptr, R, C, ldx);
+      hipLaunchKernelGGL((transpose_kernel<T, false, kCopy>), grid, dim3(256), 0, s, (const uint16_t*)x, (uint16_t*)y,
+                         nullptr, R, C, ldx, nullptr, nullptr, nullptr, 0);
+    });
+}
+
+void launch_bias_gelu_fwd_t(const void* x, const void* b, void* yt, int64_t R, int C, int approx, int dt,
+                            hipStream_t s) {
+  const dim3 grid(C / TC, (unsigned)(R / TR));
+  DSA_DISPATCH_16(dt, T,
+    hipLaunchKernelGGL((transpose_kernel<T, false, kGeluFwd>), grid, dim3(256), 0, s, (const uint16_t*)x,
+                       (uint16_t*)yt, nullptr, R, C, (int64_t)C, nullptr, (const uint16_t*)b, nullptr, approx));
+}
+
+void launch_bias_gelu_bwd_t(const void* dy, const void* x, const void* b, void* dx, void* dxt, float* partial,
+                            void* db, int64_t R, int C, int approx, int dt, hipStream_t s) {
+  const dim3 grid(C / TC, (unsigned)(R / TR));
+  DSA_DISPATCH_16(dt, T,
+    if (partial) {
+      hipLaunchKernelGGL((transpose_kernel<T, true, kGeluBwd>), grid, dim3(256), 0, s, (const uint16_t*)dy,
+                         (uint16_t*)dxt, partial, R, C, (int64_t)C, (const uint16_t*)x, (const uint16_t*)b,
+                         (uint16_t*)dx, approx);
+      launch_colsum_partials(partial, (int)(R / TR), C, db, 0, dt, s);
+    } else {
+      hipLaunchKernelGGL((transpose_kernel<T, false, kGeluBwd>), grid, dim3(256), 0, s, (const uint16_t*)dy,
+                         (uint16_t*)dxt, nullptr, R, C, (int64_t)C, (const uint16_t*)x, (const uint16_t*)b,
+                         (uint16_t*)dx, approx);
     });
 }
 

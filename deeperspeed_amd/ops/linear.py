@@ -82,20 +82,66 @@ def _bound_grad(p: torch.Tensor):
     return g
 
 
+# One slot: a tensor produced together with its transpose by the kernel that wrote it (the
+# bias+GeLU backward writes du and du^T), consumed by the next weight gradient whose output
+# gradient is that same tensor.  The slot holds the tensor itself, so its storage cannot be
+# recycled for another tensor while the entry exists (no false address matches).
+_pre_t = [None]
+
+
+def offer_transposed(t: torch.Tensor, t_t: torch.Tensor):
+    """Record t_t = t^T (contiguous) for the weight gradient that will read t."""
+    _pre_t[0] = (t, t_t)
+
+
+def _take_transposed(x2: torch.Tensor):
+    e = _pre_t[0]
+    if e is None:
+        return None
+    t, t_t = e
+    if (t.data_ptr() == x2.data_ptr() and t.numel() == x2.numel() and x2.dim() == 2
+            and tuple(t_t.shape) == (x2.size(1), x2.size(0)) and x2.is_contiguous()):
+        _pre_t[0] = None
+        return t_t
+    return None
+
+
+def _t_operand(x2, colsum_out=None):
+    """x2^T contiguous (x2 [M, K]): free when x2 is a column-major view or its transpose was
+    offered by the kernel that wrote it, else one HIP transpose (which also folds
+    colsum_out += sum(x2) into the same read)."""
+    from . import native
+    pre = x2.t() if (x2.t().is_contiguous() and x2.stride(1) != 1) else _take_transposed(x2)
+    if pre is not None:
+        if colsum_out is not None:
+            native.colsum(x2, colsum_out, accumulate=True)
+        return pre
+    if native.transpose_supported(x2):
+        return native.transpose2d(x2, colsum_out, accum=colsum_out is not None)
+    return None
+
+
 def _nt_operands(g2, x2, bias_grad):
-    """(dy^T, x^T) contiguous along the tokens via the HIP transpose, with bias_grad (+)= sum(dy)
-    folded into the transpose of dy; None when the path does not apply."""
+    """(dy^T, x^T) contiguous along the tokens, with bias_grad (+)= sum(dy) folded into the
+    transpose of dy; None when the path does not apply."""
     if not (WGRAD_NT and g2.is_cuda and g2.dtype == x2.dtype
             and g2.size(1) * x2.size(1) >= WGRAD_NT_MIN_NUMEL
             and (g2.numel() + x2.numel()) * g2.element_size() <= WGRAD_NT_MAX_BYTES):
         return None
-    from . import native
-    if not (native.transpose_supported(g2) and native.transpose_supported(x2)):
-        return None
     if bias_grad is not None and (bias_grad.dtype != g2.dtype or not bias_grad.is_contiguous()):
         return None
+    from . import native
+    if not ((native.transpose_supported(g2) or _pre_t[0] is not None)
+            and (native.transpose_supported(x2) or (x2.t().is_contiguous() and x2.stride(1) != 1))):
+        return None
+    xt = _t_operand(x2)
+    if xt is None:
+        return None
+    gt = _t_operand(g2, bias_grad)
+    if gt is None:
+        return None
     _nt_count[0] += 1
-    return native.transpose2d(g2, bias_grad, accum=True), native.transpose2d(x2)
+    return gt, xt
 
 
 def _split_k(g2, x2):

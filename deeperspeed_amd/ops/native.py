@@ -9,6 +9,7 @@ implementation of the same math; that path is never taken for tensors on the MI3
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -188,9 +189,33 @@ def _gelu_ref(x, approx):
     return torch.nn.functional.gelu(x, approximate="tanh" if approx else "none")
 
 
+def _gelu_t_ok(x2: torch.Tensor) -> bool:
+    """Shapes the transposing bias+GeLU kernels take (transpose.hip tile rules)."""
+    return (x2.is_cuda and x2.dim() == 2 and x2.dtype in (torch.bfloat16, torch.float16) and x2.is_contiguous()
+            and x2.size(0) % 128 == 0 and x2.size(1) % 64 == 0 and x2.size(0) > 0 and x2.data_ptr() % 16 == 0)
+
+
+def _gelu_bwd(dy, x, bias, approx, offer_t):
+    """(dx, db) of y = gelu(x + bias).  With offer_t, on the GPU one pass also writes dx^T and
+    hands it to ops.linear as the pre-transposed output gradient of the linear that produced x
+    (its weight gradient then skips the transpose of dx)."""
+    C = x.shape[-1]
+    if offer_t and DUAL_GELU_BWD and _gelu_t_ok(x.view(-1, C)) and dy.is_contiguous() \
+            and (bias is None or bias.is_contiguous()):
+        dx, dxt, db = hip_ops().bias_gelu_bwd_t(dy.view(-1, C), x.view(-1, C), bias, approx)
+        from . import linear as _linear
+        _linear.offer_transposed(dx, dxt)
+        return dx.view(x.shape), db
+    return hip_ops().bias_gelu_bwd(dy, x, bias, approx)
+
+
+# DSA_DUAL_GELU_BWD=0: the bias+GeLU backward writes only dx (the linear transposes it itself)
+DUAL_GELU_BWD = os.environ.get("DSA_DUAL_GELU_BWD", "1") != "0"
+
+
 class _BiasGeluFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, approx):
+    def forward(ctx, x, bias, approx, offer_t=False):
         x = x.contiguous()
         _macs(2 * x.numel())
         if x.is_cuda:
@@ -199,6 +224,7 @@ class _BiasGeluFn(torch.autograd.Function):
             y = _gelu_ref((x.float() + (bias.float() if bias is not None else 0)), approx).to(x.dtype)
         ctx.save_for_backward(x, bias)
         ctx.approx = approx
+        ctx.offer_t = offer_t
         ctx.has_bias = bias is not None
         return y
 
@@ -207,7 +233,7 @@ class _BiasGeluFn(torch.autograd.Function):
         x, bias = ctx.saved_tensors
         dy = dy.contiguous()
         if x.is_cuda:
-            dx, db = hip_ops().bias_gelu_bwd(dy, x, bias, ctx.approx)
+            dx, db = _gelu_bwd(dy, x, bias, ctx.approx, ctx.offer_t)
         else:
             with torch.enable_grad():
                 xi = (x.float() + (bias.float() if bias is not None else 0)).detach().requires_grad_(True)
@@ -215,11 +241,46 @@ class _BiasGeluFn(torch.autograd.Function):
                 (g,) = torch.autograd.grad(y, xi, dy.float())
             dx = g.to(x.dtype)
             db = g.reshape(-1, g.shape[-1]).sum(0).to(bias.dtype) if bias is not None else None
+        return dx, (db if ctx.has_bias else None), None, None
+
+
+def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False, offer_t: bool = False):
+    """gelu(x + bias).  offer_t: x is the output of an ops.linear whose weight gradient takes
+    the reduction-contiguous path -- the backward then also forms dx^T for it in the same pass."""
+    return _BiasGeluFn.apply(x, bias, approximate, offer_t)
+
+
+class _BiasGeluTFn(torch.autograd.Function):
+    """gelu(x + bias) returned TRANSPOSED, [C, M] for x [M, C] (one tiled HIP pass)."""
+
+    @staticmethod
+    def forward(ctx, x2, bias, approx):
+        _macs(2 * x2.numel())
+        yt = hip_ops().bias_gelu_fwd_t(x2, bias, approx)
+        ctx.save_for_backward(x2, bias)
+        ctx.approx = approx
+        ctx.has_bias = bias is not None
+        return yt
+
+    @staticmethod
+    def backward(ctx, dyt):
+        x2, bias = ctx.saved_tensors
+        dx, db = _gelu_bwd(dyt.t().contiguous(), x2, bias, ctx.approx, True)
         return dx, (db if ctx.has_bias else None), None
 
 
-def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False):
-    return _BiasGeluFn.apply(x, bias, approximate)
+def bias_gelu_t_supported(x: torch.Tensor) -> bool:
+    return _gelu_t_ok(x.reshape(-1, x.shape[-1])) if x.is_cuda and x.is_contiguous() else False
+
+
+def bias_gelu_colmajor(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False) -> torch.Tensor:
+    """gelu(x + bias) with the value of bias_gelu but stored column-major: a [..., C] view of a
+    contiguous [C, M] tensor.  For a consumer that only needs y^T -- the gradient-only fc2 of an
+    activation recompute, whose weight gradient reads its input transposed -- this saves the
+    separate transpose.  (Any reader of y gets the right values, only slower.)"""
+    C = x.shape[-1]
+    yt = _BiasGeluTFn.apply(x.reshape(-1, C), bias, approximate)
+    return yt.t().view(*x.shape[:-1], C)
 
 
 class _Add3Fn(torch.autograd.Function):
