@@ -382,7 +382,7 @@ def main():
 
     if args.profile_steps > 0:
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
             for _ in range(args.profile_steps):
                 train_step()
             torch.cuda.synchronize()
@@ -390,6 +390,10 @@ def main():
             os.makedirs("gpurun_out", exist_ok=True)
             with open("gpurun_out/torch_profile.txt", "w") as f:
                 f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+                f.write("\n\nby input shape\n")
+                f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=120,
+                                                                           max_name_column_width=60,
+                                                                           max_shapes_column_width=120))
 
     global_batch = mb * ga * world
     tokens = global_batch * args.seq * args.steps
