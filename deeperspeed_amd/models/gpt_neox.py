@@ -174,11 +174,14 @@ class OutputLinear(nn.Linear):
     block."""
 
     skip_in_recompute = True
+    # parallel residual: attention `dense` and MLP `dense_4h_to_h` receive the same output
+    # gradient; the first weight gradient's transpose of it is reused by the second
+    share_grad_t = False
 
     def forward(self, x):
         if _SKIP_OUTPUTS and self.skip_in_recompute and torch.is_grad_enabled():
-            return grad_only_linear(x, self.weight, self.bias)
-        return linear(x, self.weight, self.bias)
+            return grad_only_linear(x, self.weight, self.bias, self.share_grad_t)
+        return linear(x, self.weight, self.bias, self.share_grad_t)
 
 
 def make_sparsity_config(cfg: GPTNeoXConfig):
@@ -339,6 +342,8 @@ class NeoXTransformerLayer(nn.Module):
                                                               dtype=dtype)
         self.attention = NeoXAttention(cfg, device, dtype, layer_number)
         self.mlp = NeoXMLP(cfg, device, dtype)
+        if cfg.use_parallel_residual:
+            self.attention.dense.share_grad_t = self.mlp.dense_4h_to_h.share_grad_t = True
 
     def _block(self, x):
         # each LayerNorm hands its input on as a second output, so the gradients of the residual

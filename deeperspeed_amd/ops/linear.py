@@ -82,34 +82,41 @@ def _bound_grad(p: torch.Tensor):
     return g
 
 
-# One slot: a tensor produced together with its transpose by the kernel that wrote it (the
-# bias+GeLU backward writes du and du^T), consumed by the next weight gradient whose output
-# gradient is that same tensor.  The slot holds the tensor itself, so its storage cannot be
-# recycled for another tensor while the entry exists (no false address matches).
-_pre_t = [None]
+# Pre-transposed operands: a tensor recorded together with its contiguous transpose, consumed
+# by the next weight gradient that reads that same tensor -- du and du^T written in one pass by
+# the bias+GeLU backward (fc1's wgrad), and the block-output gradient that the parallel-residual
+# branches share (fc2's wgrad transposes it, the attention output projection reuses it).  Each
+# entry holds the tensor itself, so its storage cannot be recycled for another tensor while the
+# entry exists (no false address matches); at most _PRE_T_SLOTS entries are kept.
+_pre_t = []
+_PRE_T_SLOTS = 2
 
 
 def offer_transposed(t: torch.Tensor, t_t: torch.Tensor):
-    """Record t_t = t^T (contiguous) for the weight gradient that will read t."""
-    _pre_t[0] = (t, t_t)
+    """Record t_t = t^T (contiguous) for a later weight gradient that reads t."""
+    _pre_t.append((t, t_t))
+    if len(_pre_t) > _PRE_T_SLOTS:
+        del _pre_t[0]
+
+
+def clear_transposed():
+    _pre_t.clear()
 
 
 def _take_transposed(x2: torch.Tensor):
-    e = _pre_t[0]
-    if e is None:
-        return None
-    t, t_t = e
-    if (t.data_ptr() == x2.data_ptr() and t.numel() == x2.numel() and x2.dim() == 2
-            and tuple(t_t.shape) == (x2.size(1), x2.size(0)) and x2.is_contiguous()):
-        _pre_t[0] = None
-        return t_t
+    for i, (t, t_t) in enumerate(_pre_t):
+        if (t.data_ptr() == x2.data_ptr() and t.numel() == x2.numel() and x2.dim() == 2
+                and tuple(t_t.shape) == (x2.size(1), x2.size(0)) and x2.is_contiguous()):
+            del _pre_t[i]
+            return t_t
     return None
 
 
-def _t_operand(x2, colsum_out=None):
+def _t_operand(x2, colsum_out=None, offer=False):
     """x2^T contiguous (x2 [M, K]): free when x2 is a column-major view or its transpose was
     offered by the kernel that wrote it, else one HIP transpose (which also folds
-    colsum_out += sum(x2) into the same read)."""
+    colsum_out += sum(x2) into the same read; with `offer` the result is kept for the next
+    weight gradient of the same x2)."""
     from . import native
     pre = x2.t() if (x2.t().is_contiguous() and x2.stride(1) != 1) else _take_transposed(x2)
     if pre is not None:
@@ -117,11 +124,18 @@ def _t_operand(x2, colsum_out=None):
             native.colsum(x2, colsum_out, accumulate=True)
         return pre
     if native.transpose_supported(x2):
-        return native.transpose2d(x2, colsum_out, accum=colsum_out is not None)
+        xt = native.transpose2d(x2, colsum_out, accum=colsum_out is not None)
+        if offer and SHARE_GRAD_T:
+            offer_transposed(x2, xt)
+        return xt
     return None
 
 
-def _nt_operands(g2, x2, bias_grad):
+# DSA_SHARE_GRAD_T=0: every weight gradient transposes its own output gradient
+SHARE_GRAD_T = os.environ.get("DSA_SHARE_GRAD_T", "1") != "0"
+
+
+def _nt_operands(g2, x2, bias_grad, offer_gt=False):
     """(dy^T, x^T) contiguous along the tokens, with bias_grad (+)= sum(dy) folded into the
     transpose of dy; None when the path does not apply."""
     if not (WGRAD_NT and g2.is_cuda and g2.dtype == x2.dtype
@@ -131,13 +145,13 @@ def _nt_operands(g2, x2, bias_grad):
     if bias_grad is not None and (bias_grad.dtype != g2.dtype or not bias_grad.is_contiguous()):
         return None
     from . import native
-    if not ((native.transpose_supported(g2) or _pre_t[0] is not None)
+    if not ((native.transpose_supported(g2) or _pre_t)
             and (native.transpose_supported(x2) or (x2.t().is_contiguous() and x2.stride(1) != 1))):
         return None
     xt = _t_operand(x2)
     if xt is None:
         return None
-    gt = _t_operand(g2, bias_grad)
+    gt = _t_operand(g2, bias_grad, offer=offer_gt)
     if gt is None:
         return None
     _nt_count[0] += 1
@@ -177,8 +191,10 @@ def input_grad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 
 
 def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, bias, need_w: bool,
-                           need_b: bool):
+                           need_b: bool, offer_gt: bool = False):
     """Weight/bias gradients of y = x W^T (+ b) for flattened g2 = dy [M, out], x2 = x [M, in].
+    offer_gt: another linear's weight gradient reads the same dy (parallel-residual branch
+    outputs), so a transpose of dy made here is kept for it.
 
     Returns (dw, db) for autograd, or None entries for parameters whose gradient was
     accumulated in place."""
@@ -197,7 +213,7 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
             return None, None
         return _wgrad_split(g2, x2, split), (native.colsum(g2) if has_b else None)
     if gw is not None and gw.is_contiguous():
-        nt = _nt_operands(g2, x2, bias.grad if has_b else None)
+        nt = _nt_operands(g2, x2, bias.grad if has_b else None, offer_gt)
         if nt is not None:
             gw.addmm_(nt[0], nt[1].t())
         else:
@@ -210,7 +226,7 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
         return None, None
     if need_w:
         db = torch.zeros(g2.size(1), dtype=g2.dtype, device=g2.device) if has_b else None
-        nt = _nt_operands(g2, x2, db)
+        nt = _nt_operands(g2, x2, db, offer_gt)
         if nt is not None:
             return nt[0] @ nt[1].t(), db
         dw = g2.t() @ x2
@@ -232,9 +248,10 @@ def forward_gemm(x, weight, bias=None):
 
 class _AccumLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, share_gt=False):
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
+        ctx.share_gt = share_gt
         return forward_gemm(x, weight, bias)
 
     @staticmethod
@@ -246,8 +263,8 @@ class _AccumLinear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = input_grad(g2, weight).view(x.shape)
         dw, db = accumulate_param_grads(g2, x.reshape(-1, x.shape[-1]), weight, bias, ctx.needs_input_grad[1],
-                                        bias is not None and ctx.needs_input_grad[2])
-        return dx, dw, db
+                                        bias is not None and ctx.needs_input_grad[2], ctx.share_gt)
+        return dx, dw, db, None
 
 
 class _GradOnlyLinear(torch.autograd.Function):
@@ -255,9 +272,10 @@ class _GradOnlyLinear(torch.autograd.Function):
     costs nothing; backward produces the exact input / weight / bias gradients."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, share_gt=False):
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
+        ctx.share_gt = share_gt
         return x.new_zeros(1).expand(*x.shape[:-1], weight.shape[0])
 
     @staticmethod
@@ -269,19 +287,20 @@ class _GradOnlyLinear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = input_grad(g2, weight).view(x.shape)
         dw, db = accumulate_param_grads(g2, x.reshape(-1, x.shape[-1]), weight, bias, ctx.needs_input_grad[1],
-                                        bias is not None and ctx.needs_input_grad[2])
-        return dx, dw, db
+                                        bias is not None and ctx.needs_input_grad[2], ctx.share_gt)
+        return dx, dw, db, None
 
 
-def linear(x, weight, bias=None):
-    """F.linear whose weight gradient accumulates in place when a gradient is bound."""
+def linear(x, weight, bias=None, share_grad_t=False):
+    """F.linear whose weight gradient accumulates in place when a gradient is bound.
+    share_grad_t: the output gradient is also another linear's (see accumulate_param_grads)."""
     if torch.is_grad_enabled() and weight.requires_grad:
-        return _AccumLinear.apply(x, weight, bias)
+        return _AccumLinear.apply(x, weight, bias, share_grad_t)
     return forward_gemm(x, weight, bias)
 
 
-def grad_only_linear(x, weight, bias=None):
-    return _GradOnlyLinear.apply(x, weight, bias)
+def grad_only_linear(x, weight, bias=None, share_grad_t=False):
+    return _GradOnlyLinear.apply(x, weight, bias, share_grad_t)
 
 
 class Linear(nn.Linear):

@@ -71,10 +71,10 @@ def test_bias_gelu_colmajor_autograd():
     torch.testing.assert_close(y, y2, atol=0, rtol=0)
     torch.testing.assert_close(x.grad, x2.grad, atol=0, rtol=0)
     torch.testing.assert_close(b.grad.float(), b2.grad.float(), atol=0.1, rtol=1e-2)
-    lin._pre_t[0] = None
+    lin.clear_transposed()
 
 
-def _mlp_grads(colmajor, dual, monkeypatch):
+def _mlp_grads(colmajor, dual, monkeypatch, share=None):
     from deeperspeed_amd.models import gpt_neox
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
     from deeperspeed_amd.ops import linear as lin
@@ -82,6 +82,7 @@ def _mlp_grads(colmajor, dual, monkeypatch):
     monkeypatch.setattr(gpt_neox, "COLMAJOR_GELU", colmajor)
     monkeypatch.setattr(native, "DUAL_GELU_BWD", dual)
     monkeypatch.setattr(lin, "WGRAD_NT_MIN_NUMEL", 0)  # tiny weights take the transposed wgrad path
+    monkeypatch.setattr(lin, "SHARE_GRAD_T", dual if share is None else share)
     torch.manual_seed(0)
     cfg = get_config("tiny", hidden_size=384, num_heads=4, num_layers=2, max_seq_len=128, checkpoint_activations=True)
     model = GPTNeoX(cfg, device="cuda", dtype=torch.bfloat16).train()
@@ -91,13 +92,16 @@ def _mlp_grads(colmajor, dual, monkeypatch):
     loss = model(ids, labels=ids)
     loss.backward()
     assert lin.nt_wgrad_count() > nt0
-    assert lin._pre_t[0] is None, "offered du^T was not consumed by fc1's weight gradient"
+    # every offered transpose (du^T for fc1; the block-output gradient^T that fc2 and the
+    # attention output projection share) was consumed
+    assert not lin._pre_t, [tuple(t.shape) for t, _ in lin._pre_t]
     return float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
 
 
-def test_neox_recompute_colmajor_gelu_matches(monkeypatch):
+@pytest.mark.parametrize("share", [False, True])
+def test_neox_recompute_colmajor_gelu_matches(monkeypatch, share):
     l0, g0 = _mlp_grads(False, False, monkeypatch)
-    l1, g1 = _mlp_grads(True, True, monkeypatch)
+    l1, g1 = _mlp_grads(True, True, monkeypatch, share)
     assert l0 == l1
     assert g0.keys() == g1.keys()
     for n in g0:

@@ -96,11 +96,12 @@ def test_sumsq_and_colsum():
     assert torch.allclose(native.colsum(y).float(), y.float().sum(0), atol=0.2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("hd,rot", [(96, 24), (128, 32), (64, 64), (96, 96), (32, 8)])
-def test_rotary_split_matches_reference(hd, rot):
+@pytest.mark.parametrize("hd,rot", [(96, 24), (128, 32), (64, 64), (96, 96), (32, 8), (64, 16), (128, 128), (80, 20)])
+@pytest.mark.parametrize("S,NH", [(40, 4), (41, 5)])  # 41 x 5: the last chunk-kernel block is partial
+def test_rotary_split_matches_reference(hd, rot, S, NH):
     from deeperspeed_amd.ops import attention as A
     torch.manual_seed(3)
-    B, S, NH = 2, 40, 4
+    B = 2
     qkv = torch.randn(B, S, NH * 3 * hd, device=_dev(), dtype=torch.bfloat16, requires_grad=True)
     q, k, v = A.rotary_split(qkv, NH, hd, rot, qscale=0.5)
     g = [torch.randn_like(t) for t in (q, k, v)]
