@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import native
-from ..ops.linear import Linear, grad_only_linear, linear
+from ..ops.linear import Linear, grad_only_linear, linear, nt_wgrad_planned
 from ..ops.attention import attention, rotary_split
 from ..runtime.activation_checkpointing import checkpointing as ds_ckpt
 
@@ -111,8 +111,10 @@ class LinearBiasGeLU(nn.Linear):
         if (self.colmajor_in_recompute and _SKIP_OUTPUTS and torch.is_grad_enabled() and COLMAJOR_GELU
                 and native.bias_gelu_t_supported(u)):
             return native.bias_gelu_colmajor(u, self.bias, self.approximate)
-        # the backward also writes du^T for this layer's own weight gradient
-        return native.bias_gelu(u, self.bias, self.approximate, offer_t=u.is_cuda)
+        # the backward also writes du^T when this layer's own weight gradient will read it
+        offer = u.is_cuda and nt_wgrad_planned(u.numel() // self.out_features, self.out_features, self.in_features,
+                                               u.element_size(), g_ready=True)
+        return native.bias_gelu(u, self.bias, self.approximate, offer_t=offer)
 
 
 # DSA_COLMAJOR_GELU=0: the recompute writes the GeLU output row-major (fc2's wgrad transposes it)
@@ -175,13 +177,21 @@ class OutputLinear(nn.Linear):
 
     skip_in_recompute = True
     # parallel residual: attention `dense` and MLP `dense_4h_to_h` receive the same output
-    # gradient; the first weight gradient's transpose of it is reused by the second
-    share_grad_t = False
+    # gradient; the first weight gradient's transpose of it is reused by the second.
+    # share_partner = the other projection's (out, in), set by the layer.
+    share_partner = None
+
+    def _share(self, x):
+        if self.share_partner is None or not x.is_cuda:
+            return False
+        M = x.numel() // x.shape[-1]
+        return all(nt_wgrad_planned(M, o, i, x.element_size())
+                   for o, i in ((self.out_features, self.in_features), self.share_partner))
 
     def forward(self, x):
         if _SKIP_OUTPUTS and self.skip_in_recompute and torch.is_grad_enabled():
-            return grad_only_linear(x, self.weight, self.bias, self.share_grad_t)
-        return linear(x, self.weight, self.bias, self.share_grad_t)
+            return grad_only_linear(x, self.weight, self.bias, self._share(x))
+        return linear(x, self.weight, self.bias, self._share(x))
 
 
 def make_sparsity_config(cfg: GPTNeoXConfig):
@@ -343,7 +353,8 @@ class NeoXTransformerLayer(nn.Module):
         self.attention = NeoXAttention(cfg, device, dtype, layer_number)
         self.mlp = NeoXMLP(cfg, device, dtype)
         if cfg.use_parallel_residual:
-            self.attention.dense.share_grad_t = self.mlp.dense_4h_to_h.share_grad_t = True
+            d, f = self.attention.dense, self.mlp.dense_4h_to_h
+            d.share_partner, f.share_partner = (f.out_features, f.in_features), (d.out_features, d.in_features)
 
     def _block(self, x):
         # each LayerNorm hands its input on as a second output, so the gradients of the residual

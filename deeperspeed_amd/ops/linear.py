@@ -135,18 +135,33 @@ def _t_operand(x2, colsum_out=None, offer=False):
 SHARE_GRAD_T = os.environ.get("DSA_SHARE_GRAD_T", "1") != "0"
 
 
+def nt_wgrad_planned(M: int, out_features: int, in_features: int, elem_size: int = 2, g_ready: bool = False,
+                     x_ready: bool = False) -> bool:
+    """Whether the weight gradient of a [out, in] linear over M tokens takes the
+    reduction-contiguous (transposed-operand) path -- the predicate producers of pre-transposed
+    operands check before offering one.  g_ready / x_ready: that operand is already available
+    transposed, so it adds no transient copy."""
+    if not WGRAD_NT or out_features * in_features < WGRAD_NT_MIN_NUMEL:
+        return False
+    if (WGRAD_SPLIT > 1 and M >= WGRAD_SPLIT_MIN_TOKENS and M % WGRAD_SPLIT == 0
+            and -(-out_features // 256) * -(-in_features // 256) <= WGRAD_SPLIT_MAX_TILES):
+        return False  # split-K path (_split_k)
+    copies = (0 if g_ready else M * out_features) + (0 if x_ready else M * in_features)
+    return copies * elem_size <= WGRAD_NT_MAX_BYTES
+
+
 def _nt_operands(g2, x2, bias_grad, offer_gt=False):
     """(dy^T, x^T) contiguous along the tokens, with bias_grad (+)= sum(dy) folded into the
     transpose of dy; None when the path does not apply."""
-    if not (WGRAD_NT and g2.is_cuda and g2.dtype == x2.dtype
-            and g2.size(1) * x2.size(1) >= WGRAD_NT_MIN_NUMEL
-            and (g2.numel() + x2.numel()) * g2.element_size() <= WGRAD_NT_MAX_BYTES):
+    x_ready = x2.t().is_contiguous() and x2.stride(1) != 1
+    g_ready = any(t.data_ptr() == g2.data_ptr() for t, _ in _pre_t)
+    if not (g2.is_cuda and g2.dtype == x2.dtype
+            and nt_wgrad_planned(g2.size(0), g2.size(1), x2.size(1), g2.element_size(), g_ready, x_ready)):
         return None
     if bias_grad is not None and (bias_grad.dtype != g2.dtype or not bias_grad.is_contiguous()):
         return None
     from . import native
-    if not ((native.transpose_supported(g2) or _pre_t)
-            and (native.transpose_supported(x2) or (x2.t().is_contiguous() and x2.stride(1) != 1))):
+    if not ((g_ready or native.transpose_supported(g2)) and (x_ready or native.transpose_supported(x2))):
         return None
     xt = _t_operand(x2)
     if xt is None:

@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 from torch.nn.modules import Module
 
+from ..ops import linear as _linear_ops
 from ..ops.adam.fused_adam import FusedAdam
 from ..utils.distributed import init_distributed
 from ..utils import comm
@@ -767,6 +768,7 @@ class DeepSpeedEngine(Module):
             self.optimizer.backward(loss)
         else:
             loss.backward()
+        _linear_ops.clear_transposed()  # pre-transposed operands never outlive their backward
         if self.wall_clock_breakdown():
             self.timers("backward_inner").stop()
             self.timers("backward_inner_microstep").stop()
