@@ -19,6 +19,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ...ops import linear as _linear_ops
 from ...utils.logging import logger, log_dist
 from ...utils.timer import ThroughputTimer
 from ..engine import DeepSpeedEngine
@@ -411,6 +412,7 @@ class PipelineEngine(DeepSpeedEngine):
                 torch.autograd.backward(tensors=out_t, grad_tensors=grads)
             else:
                 torch.autograd.backward(tensors=(outputs,), grad_tensors=(grads[0],))
+        _linear_ops.clear_transposed()  # pre-transposed operands never outlive their backward
         self.pipe_buffers["output_tensors"][buffer_id] = None
         self.pipe_buffers["outputs"][buffer_id] = None
         if self.wall_clock_breakdown():
