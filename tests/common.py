@@ -6,6 +6,7 @@ RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set (127.0.0.1) and torch.distributed initia
 fails or hangs fails the test; stragglers are killed after a timeout.
 """
 
+import datetime
 import functools
 import os
 import socket
@@ -40,7 +41,10 @@ def _worker(rank, world_size, port, fn, args, kwargs, errq, backend="gloo"):
         import torch.distributed as dist
         if backend == "nccl":  # RCCL: one rank per visible GPU
             torch.cuda.set_device(rank % torch.cuda.device_count())
-        dist.init_process_group(backend, rank=rank, world_size=world_size)
+        # the parent owns the rendezvous store (bound to a kernel-chosen port before any worker
+        # starts), so no two runs can race for a port picked by probing
+        store = dist.TCPStore("127.0.0.1", port, is_master=False, timeout=datetime.timedelta(seconds=120))
+        dist.init_process_group(backend, store=store, rank=rank, world_size=world_size)
         fn(*args, **kwargs)
         dist.barrier()
         dist.destroy_process_group()
@@ -52,7 +56,9 @@ def _worker(rank, world_size, port, fn, args, kwargs, errq, backend="gloo"):
 def run_distributed(fn, world_size, *args, timeout=DEFAULT_TIMEOUT, backend="gloo", **kwargs):
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
-    port = _free_port()
+    import torch.distributed as dist
+    server = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False)
+    port = server.port
     procs = [ctx.Process(target=_worker, args=(r, world_size, port, fn, args, kwargs, errq, backend))
              for r in range(world_size)]
     for p in procs:
@@ -79,6 +85,7 @@ def run_distributed(fn, world_size, *args, timeout=DEFAULT_TIMEOUT, backend="glo
         bad = [p.exitcode for p in procs if p.exitcode != 0]
         if bad:
             failed = (-1, f"worker exit codes {bad}")
+    del server
     if failed is not None:
         pytest.fail(f"rank {failed[0]} failed:\n{failed[1]}")
 
