@@ -307,7 +307,7 @@ def main():
             return 0
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
-        margin = float(os.environ.get("DSA_STASH_MARGIN_GIB", "3")) * 2**30
+        margin = float(os.environ.get("DSA_STASH_MARGIN_GIB", "2")) * 2**30
         free = hbm / share - torch.cuda.max_memory_reserved() - margin
         n = int(max(0, min(len(layers), free // per_layer)))
         for m in layers[-n:] if n else []:
