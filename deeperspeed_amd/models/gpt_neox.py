@@ -417,12 +417,13 @@ class GPTNeoX(nn.Module):
         logits = self.embed_out(x)
         if labels is None:
             return logits
-        return lm_loss(logits, labels)
+        return lm_loss(logits, labels, internal=True)
 
 
-def lm_loss(logits, labels):
-    """Mean next-token loss (labels already aligned with logits); fused HIP kernel on GPU."""
-    return native.cross_entropy(logits, labels)
+def lm_loss(logits, labels, internal=False):
+    """Mean next-token loss (labels already aligned with logits); fused HIP kernel on GPU.
+    internal: the logits never leave the model, so the backward writes dlogits over them."""
+    return native.cross_entropy(logits, labels, inplace_grad=internal)
 
 
 # -------------------------------------------------------------------------- pipeline form

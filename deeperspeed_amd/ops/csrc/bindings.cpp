@@ -655,12 +655,14 @@ std::vector<Tensor> xent_fwd(Tensor logits, Tensor labels) {
 }
 
 // dloss: fp32 [R] per-row upstream grads, or a single element broadcast to every row
-Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dloss) {
+// inplace: dlogits overwrite the logits (each element is read once, by the thread that writes it)
+Tensor xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor dloss, bool inplace) {
   check_dev(logits, "logits"); check_dev(dloss, "dloss");
   TORCH_CHECK(dloss.scalar_type() == at::kFloat && (dloss.numel() == 1 || dloss.numel() == logits.size(0)),
               "xent_bwd: dloss");
+  TORCH_CHECK(!inplace || logits.is_contiguous(), "xent_bwd: in-place needs contiguous logits");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
-  Tensor dx = at::empty_like(logits);
+  Tensor dx = inplace ? logits : at::empty_like(logits);
   dsa::launch_xent_bwd(logits.data_ptr(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(), dloss.data_ptr<float>(),
                        dloss.numel() == 1 ? 0 : 1, dx.data_ptr(), logits.size(0), (int)logits.size(1), dcode(logits),
                        cur_stream());
@@ -940,7 +942,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_dropout_residual", &bias_dropout_residual);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("xent_fwd", &xent_fwd);
-  m.def("xent_bwd", &xent_bwd);
+  m.def("xent_bwd", &xent_bwd, py::arg("logits"), py::arg("labels"), py::arg("lse"), py::arg("dloss"),
+        py::arg("inplace") = false);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("rotary_split_fwd", &rotary_split_fwd);

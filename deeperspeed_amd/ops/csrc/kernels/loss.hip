@@ -56,10 +56,11 @@ __global__ void __launch_bounds__(256) xent_fwd_kernel(const T* __restrict__ x, 
   }
 }
 
+// x and dx may alias (in-place backward): every element is loaded and stored by the same thread
 template <typename T>
-__global__ void __launch_bounds__(256) xent_bwd_kernel(const T* __restrict__ x, const int64_t* __restrict__ labels,
+__global__ void __launch_bounds__(256) xent_bwd_kernel(const T* x, const int64_t* __restrict__ labels,
                                                        const float* __restrict__ lse, const float* __restrict__ dloss,
-                                                       int64_t dloss_stride, T* __restrict__ dx, int V) {
+                                                       int64_t dloss_stride, T* dx, int V) {
   const int64_t row = blockIdx.x;
   const T* xr = x + row * (int64_t)V;
   T* dr = dx + row * (int64_t)V;

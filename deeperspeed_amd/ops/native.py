@@ -597,7 +597,8 @@ def _cpu_flatten():
 # --------------------------------------------------------------------------- fused LM loss
 class _CrossEntropyFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, labels):
+    def forward(ctx, logits, labels, inplace_grad=False):
+        ctx.inplace = inplace_grad and logits.is_contiguous()
         x = logits.reshape(-1, logits.shape[-1]).contiguous()
         lab = labels.reshape(-1).contiguous()
         _macs(3 * x.numel())
@@ -610,15 +611,28 @@ class _CrossEntropyFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, lab, lse, nvalid = ctx.saved_tensors
-        dx = hip_ops().xent_bwd(x, lab, lse, (g.float() / nvalid).reshape(1).contiguous())
-        return dx.view(ctx.shape), None
+        # caller-owned logits (inplace_grad: nothing else reads them) are dead once their gradient
+        # exists, so it is written over them (one [tokens, vocab] buffer instead of two at the
+        # head of backward); the version bump makes a second backward through this graph fail
+        # loudly instead of reading gradients as logits
+        inplace = XENT_INPLACE and ctx.inplace
+        dx = hip_ops().xent_bwd(x, lab, lse, (g.float() / nvalid).reshape(1).contiguous(), inplace)
+        if inplace:
+            torch.autograd.graph.increment_version(x)
+        return dx.view(ctx.shape), None, None
 
 
-def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+# DSA_XENT_INPLACE=0: the cross-entropy backward writes dlogits into a fresh buffer
+XENT_INPLACE = os.environ.get("DSA_XENT_INPLACE", "1") != "0"
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, inplace_grad: bool = False) -> torch.Tensor:
     """Mean token cross-entropy (labels < 0 ignored) on 16-bit logits without fp32 copies
-    of the [tokens, vocab] tensor; fp32 PyTorch path on CPU / fp32 logits."""
+    of the [tokens, vocab] tensor; fp32 PyTorch path on CPU / fp32 logits.  inplace_grad: the
+    caller guarantees nothing reads `logits` after the backward (an LM head's internal output),
+    so their gradient may overwrite them."""
     if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float16) and logits.shape[-1] % 8 == 0:
-        return _CrossEntropyFn.apply(logits, labels)
+        return _CrossEntropyFn.apply(logits, labels, inplace_grad)
     return torch.nn.functional.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), labels.reshape(-1),
                                              ignore_index=-100)
 

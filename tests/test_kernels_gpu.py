@@ -703,3 +703,27 @@ def test_dropout_bwd_with_bias_grad(C):
     assert (dx.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
     want = ref.sum(0)
     assert (db.float() - want).abs().max().item() < 2e-2 * want.abs().max().item()
+
+
+def test_cross_entropy_inplace_grad():
+    """inplace_grad: dlogits written over the (internal) logits give the same input gradients,
+    and a second backward through the graph fails loudly instead of reading gradients."""
+    from deeperspeed_amd.ops import native
+    torch.manual_seed(5)
+    V = 50432
+    h = torch.randn(64, 256, device=_dev(), dtype=torch.bfloat16, requires_grad=True)
+    w = (0.05 * torch.randn(V, 256, device=_dev())).to(torch.bfloat16).requires_grad_(True)
+    lab = torch.randint(0, V, (64,), device=_dev())
+    grads = []
+    for inplace in (False, True):
+        h.grad = w.grad = None
+        loss = native.cross_entropy(h @ w.t(), lab, inplace_grad=inplace)
+        loss.backward()
+        grads.append((float(loss), h.grad.clone(), w.grad.clone()))
+    assert grads[0][0] == grads[1][0]
+    torch.testing.assert_close(grads[0][1], grads[1][1], atol=0, rtol=0)
+    torch.testing.assert_close(grads[0][2], grads[1][2], atol=0, rtol=0)
+    loss = native.cross_entropy(h @ w.t(), lab, inplace_grad=True)
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError):
+        loss.backward()
