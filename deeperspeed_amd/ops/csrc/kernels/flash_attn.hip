@@ -15,7 +15,9 @@
 // become A operands.  Workgroup = 4 waves = 64 rows (queries for fwd/dQ, keys for dK/dV).
 // Backward is FA2-style without atomics: one kernel owns dK/dV per key block, one owns dQ
 // per query block (both recompute P from the saved LSE).
+#include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "../include/dsa_common.h"
 #include "../include/launchers.h"
@@ -469,6 +471,28 @@ __device__ __forceinline__ int xcd_task(int lin, int n) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
+// Buffer-load form of tile_load for a loop that walks tiles of one head: the head's rows sit
+// behind one buffer resource (scalar registers) sized to its S rows, so a row past the end
+// reads 0 in hardware and each lane keeps only a 32-bit offset -- the pointer form holds a
+// 64-bit address per chunk plus a bounds branch, which spilled registers in the dK/dV kernel.
+typedef unsigned int fa_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const uint16_t* g, int S, int ld) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)g, (short)0, S * ld * 2, 0x00020000);
+}
+
+template <int D>
+__device__ __forceinline__ void tile_load_buf(uint4 (&r)[D / 32], __amdgpu_buffer_rsrc_t rs, int r0, int ld) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int k = 0; k < D / 32; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    const int row = c / CH, ch = c - row * CH;
+    const fa_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ((r0 + row) * ld + ch * 8) * 2, 0, 0);
+    r[k] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void tile_load(uint4 (&r)[D / 32], const uint16_t* __restrict__ g, int r0, int S,
                                           int ld = D) {
@@ -736,7 +760,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
 // index per value from the C layout, LSE/Delta broadcast from LDS), then
 //   dV^T += dO^T P   (A = dO^T via tr reads, B = P from registers)
 //   dK^T += Q^T dS   (A = Q^T via tr reads,  B = dS from registers)
-template <typename T, int D, bool CAUSAL, int EX = 0, bool FQ = false>
+template <typename T, int D, bool CAUSAL, int EX = 0, bool FQ = false, bool BUF = true>
 __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint16_t* __restrict__ Q,
                                              const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                                              const uint16_t* __restrict__ dO, const float* __restrict__ LSE,
@@ -790,9 +814,16 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   const int ntiles = qstart < S ? (S - qstart + BN2 - 1) / BN2 : 0;
   uint4 qr[D / 32], orr[D / 32];
   float st_l = 0.f, st_d = 0.f;
+  const __amdgpu_buffer_rsrc_t q_rs = head_rsrc(Q + base, S, (int)ldi);
+  const __amdgpu_buffer_rsrc_t o_rs = head_rsrc(dO + obase, S, o_ld<D>(onh));
   auto load_tile = [&](int i0) {
-    tile_load<D>(qr, Q + base, i0, S, ldi);
-    tile_load<D>(orr, dO + obase, i0, S, o_ld<D>(onh));
+    if constexpr (BUF) {
+      tile_load_buf<D>(qr, q_rs, i0, (int)ldi);
+      tile_load_buf<D>(orr, o_rs, i0, o_ld<D>(onh));
+    } else {
+      tile_load<D>(qr, Q + base, i0, S, ldi);
+      tile_load<D>(orr, dO + obase, i0, S, o_ld<D>(onh));
+    }
     if (threadIdx.x < BN2) {
       const int q = i0 + threadIdx.x;
       st_l = q < S ? LSE[bh * (int64_t)S + q] * 1.4426950408889634f : 0.f;
@@ -1096,12 +1127,13 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
 // kernel entry points: the two backward halves on their own, or both in one launch (dK/dV
 // workgroups first, then dQ): at short sequences each half alone is latency-bound and leaves
 // the chip idle in its tail, one grid lets the hardware overlap them
-template <typename T, int D, bool CAUSAL, int EX = 0>
+template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true>
 __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh, Extra ex = Extra()) {
-  dkdv_v2_body<T, D, CAUSAL, EX>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh, ex);
+  dkdv_v2_body<T, D, CAUSAL, EX, false, BUF>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh,
+                                             ex);
 }
 
 template <typename T, int D, bool CAUSAL, int EX = 0>
@@ -1725,6 +1757,10 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
   // DSA_FLASH_BWD_MERGE=1: dK/dV and dQ workgroups in one launch (measured neutral, r2v)
   static const bool merge = getenv("DSA_FLASH_BWD_MERGE") && getenv("DSA_FLASH_BWD_MERGE")[0] == '1';
   const bool v1 = v1_env && onh == 0;  // the v1 kernels read dO head-major only
+  static const bool bufload = !(getenv("DSA_FA_BUFLOAD") && getenv("DSA_FA_BUFLOAD")[0] == '0');
+  // the buffer resources of the dK/dV tile loads address one head's rows with 32-bit offsets
+  if ((int64_t)S * (onh ? onh * D : D) * 2 >= (1LL << 31))
+    throw std::runtime_error("flash bwd: S * row stride too large for 32-bit buffer offsets");
   FA_DISPATCH(dt, D, causal,
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
@@ -1734,9 +1770,17 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
                          delta, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, fa::Extra());
     } else if (!v1) {
-      hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
-                         fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh);
+      // DSA_FA_BUFLOAD=0: the dK/dV kernel stages its Q / dO tiles with pointer loads (A/B only)
+      if (bufload)
+        hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC, 0, true>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
+                           dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
+                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
+                           scale, onh);
+      else
+        hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC, 0, false>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
+                           dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
+                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
+                           scale, onh);
       hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
                          fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                          (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale, onh);
@@ -1815,6 +1859,9 @@ void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const v
   // S <= 128: one workgroup per head does dK, dV and dQ (DSA_FLASH_BWD_SHORT=0: two kernels)
   static const bool short_ok = !(getenv("DSA_FLASH_BWD_SHORT") && getenv("DSA_FLASH_BWD_SHORT")[0] == '0');
   const bool use_short = short_ok && S <= fa::BM2;
+  // the buffer resources of the dK/dV tile loads address one head's rows with 32-bit offsets
+  if ((int64_t)S * std::max<int64_t>(ild > 0 ? ild : D, onh ? (int64_t)onh * D : D) * 2 >= (1LL << 31))
+    throw std::runtime_error("flash bwd: S * row stride too large for 32-bit buffer offsets");
   FA_EX_DISPATCH(dt, D, kbias, pdrop,
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
