@@ -584,7 +584,7 @@ __device__ __forceinline__ uint32_t drop_pair(uint32_t hb, int q, int half_s, in
   return drop_mix(((uint32_t)q * (uint32_t)half_s + (uint32_t)j) * 0x85ebca6bu ^ hb);
 }
 
-template <typename T, int D, bool CAUSAL, bool LAZY = true, int EX = 0>
+template <typename T, int D, bool CAUSAL, bool LAZY = true, int EX = 0, bool BUF = true>
 __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                         float* __restrict__ LSE, int S, float scale, int onh,
@@ -623,8 +623,14 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   const int kend = CAUSAL ? min(S, qb + BM2) : S;
   const int ntiles = (kend + BN2 - 1) / BN2;
   uint4 kr[D / 32], vr[D / 32];
-  tile_load<D>(kr, Kb, 0, S, ldi);
-  tile_load<D>(vr, Vb, 0, S, ldi);
+  const __amdgpu_buffer_rsrc_t k_rs = head_rsrc(Kb, S, (int)ldi), v_rs = head_rsrc(Vb, S, (int)ldi);
+  if constexpr (BUF) {
+    tile_load_buf<D>(kr, k_rs, 0, (int)ldi);
+    tile_load_buf<D>(vr, v_rs, 0, (int)ldi);
+  } else {
+    tile_load<D>(kr, Kb, 0, S, ldi);
+    tile_load<D>(vr, Vb, 0, S, ldi);
+  }
   tile_store<D>(smem, kr);
   tile_store<D>(smem + TS, vr);
   __syncthreads();
@@ -632,8 +638,13 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     const int j0 = it * BN2;
     const bool has_next = it + 1 < ntiles;
     if (has_next) {
-      tile_load<D>(kr, Kb, j0 + BN2, S, ldi);
-      tile_load<D>(vr, Vb, j0 + BN2, S, ldi);
+      if constexpr (BUF) {
+        tile_load_buf<D>(kr, k_rs, j0 + BN2, (int)ldi);
+        tile_load_buf<D>(vr, v_rs, j0 + BN2, (int)ldi);
+      } else {
+        tile_load<D>(kr, Kb, j0 + BN2, S, ldi);
+        tile_load<D>(vr, Vb, j0 + BN2, S, ldi);
+      }
     }
     const uint16_t* Ks = smem + (it & 1) * 2 * TS;
     const uint16_t* Vs = Ks + TS;
@@ -987,7 +998,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
 // dQ: one wave = 32 queries (lane = query column of S^T = K Q^T); Q and dO are B operands in
 // registers; per 64-key tile: S^T, dP^T (A = K / V rows from LDS), dS^T in registers, then
 //   dQ^T += K^T dS^T   (A = K^T via tr reads, B = dS^T from registers)
-template <typename T, int D, bool CAUSAL, int EX = 0>
+template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true>
 __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_t* __restrict__ Q,
                                            const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                                            const uint16_t* __restrict__ dO, const float* __restrict__ LSE,
@@ -1028,8 +1039,14 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
   const int kend = CAUSAL ? min(S, qb + BM2) : S;
   const int ntiles = (kend + BN2 - 1) / BN2;
   uint4 kr[D / 32], vr[D / 32];
-  tile_load<D>(kr, K + base, 0, S, ldi);
-  tile_load<D>(vr, V + base, 0, S, ldi);
+  const __amdgpu_buffer_rsrc_t k_rs = head_rsrc(K + base, S, (int)ldi), v_rs = head_rsrc(V + base, S, (int)ldi);
+  if constexpr (BUF) {
+    tile_load_buf<D>(kr, k_rs, 0, (int)ldi);
+    tile_load_buf<D>(vr, v_rs, 0, (int)ldi);
+  } else {
+    tile_load<D>(kr, K + base, 0, S, ldi);
+    tile_load<D>(vr, V + base, 0, S, ldi);
+  }
   tile_store<D>(smem, kr);
   tile_store<D>(smem + TS, vr);
   __syncthreads();
@@ -1037,8 +1054,13 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
     const int j0 = it * BN2;
     const bool has_next = it + 1 < ntiles;
     if (has_next) {
-      tile_load<D>(kr, K + base, j0 + BN2, S, ldi);
-      tile_load<D>(vr, V + base, j0 + BN2, S, ldi);
+      if constexpr (BUF) {
+        tile_load_buf<D>(kr, k_rs, j0 + BN2, (int)ldi);
+        tile_load_buf<D>(vr, v_rs, j0 + BN2, (int)ldi);
+      } else {
+        tile_load<D>(kr, K + base, j0 + BN2, S, ldi);
+        tile_load<D>(vr, V + base, j0 + BN2, S, ldi);
+      }
     }
     const uint16_t* Ks = smem + (it & 1) * 2 * TS;
     const uint16_t* Vs = Ks + TS;
@@ -1136,12 +1158,12 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(
                                              ex);
 }
 
-template <typename T, int D, bool CAUSAL, int EX = 0>
+template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true>
 __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     uint16_t* __restrict__ dQ, int S, float scale, int onh, Extra ex = Extra()) {
-  dq_v2_body<T, D, CAUSAL, EX>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh, ex);
+  dq_v2_body<T, D, CAUSAL, EX, BUF>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh, ex);
 }
 
 template <typename T, int D, bool CAUSAL, int EX = 0>
@@ -1730,6 +1752,10 @@ void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, floa
                       bool causal, float scale, int dt, hipStream_t s, int onh) {
   static const bool v1 = getenv("DSA_FLASH_FWD_V1") != nullptr;
   static const bool eager = getenv("DSA_FLASH_EAGER_RESCALE") != nullptr;
+  static const bool bufload = !(getenv("DSA_FA_BUFLOAD") && getenv("DSA_FA_BUFLOAD")[0] == '0');
+  // K / V tiles are addressed per head with 32-bit buffer offsets
+  if ((int64_t)S * D * 2 >= (1LL << 31))
+    throw std::runtime_error("flash fwd: S * head dim too large for 32-bit buffer offsets");
   if (!v1 || onh) {
     dim3 grid2((S + fa::BM2 - 1) / fa::BM2, BH);
     FA_DISPATCH(dt, D, causal,
@@ -1737,8 +1763,12 @@ void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, floa
         hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, false>), dim3(grid2.x * grid2.y), dim3(256),
                            fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                            (uint16_t*)o, lse, S, scale, onh);
-      else
+      else if (bufload)
         hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true>), dim3(grid2.x * grid2.y), dim3(256),
+                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                           (uint16_t*)o, lse, S, scale, onh);
+      else  // DSA_FA_BUFLOAD=0: pointer-form K / V tile loads (A/B only)
+        hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true, 0, false>), dim3(grid2.x * grid2.y), dim3(256),
                            fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                            (uint16_t*)o, lse, S, scale, onh));
     return;
@@ -1781,9 +1811,14 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
                            dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
                            (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
                            scale, onh);
-      hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
-                         fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale, onh);
+      if (bufload)
+        hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
+                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                           (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale, onh);
+      else
+        hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC, 0, false>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
+                           dim3(256), fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
+                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale, onh);
     } else {
       hipLaunchKernelGGL((fa::bwd_dkdv_kernel<T, DD, CC>), dim3((S + fa::BM - 1) / fa::BM, BH), dim3(256),
                          fa::dkdv_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
@@ -1841,6 +1876,8 @@ void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, f
                          int onh, int inh, int64_t ild) {
   const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild);
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
+  if ((int64_t)S * (ild > 0 ? ild : D) * 2 >= (1LL << 31))
+    throw std::runtime_error("flash fwd: S * row stride too large for 32-bit buffer offsets");
   FA_EX_DISPATCH(dt, D, kbias, pdrop,
     hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, false, true, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
                        (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale, onh,
