@@ -1214,16 +1214,19 @@ template <int D> constexpr int dq_lds() { return (2 * BN * (D + 8) + 4 * 16 * (B
 // 6.  S must be a multiple of 64.  Causal masking (GPT) is applied on top of the layout.
 constexpr int STILE = 64;
 
+// g is one head's base (wave-uniform): the tile loads go through a buffer resource sized to the
+// head's S rows (32-bit lane offsets, rows past S read 0 in hardware; see tile_load_buf)
 template <int D, int NT>
 __device__ __forceinline__ void stile_load(uint4 (&r)[8 * D / NT], const uint16_t* __restrict__ g, int r0, int S,
                                            int ld = D) {
   constexpr int CH = D / 8;
+  const __amdgpu_buffer_rsrc_t rs = head_rsrc(g, S, ld);
 #pragma unroll
   for (int k = 0; k < 8 * D / NT; ++k) {
     const int c = threadIdx.x + NT * k;
     const int row = c / CH, ch = c - row * CH;
-    r[k] = (r0 + row < S) ? *reinterpret_cast<const uint4*>(g + (int64_t)(r0 + row) * ld + ch * 8)
-                          : make_uint4(0, 0, 0, 0);
+    const fa_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ((r0 + row) * ld + ch * 8) * 2, 0, 0);
+    r[k] = make_uint4(v.x, v.y, v.z, v.w);
   }
 }
 
