@@ -624,7 +624,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   const int ntiles = (kend + BN2 - 1) / BN2;
   uint4 kr[D / 32], vr[D / 32];
   const __amdgpu_buffer_rsrc_t k_rs = head_rsrc(Kb, S, (int)ldi), v_rs = head_rsrc(Vb, S, (int)ldi);
-  if constexpr (BUF) {
+  if constexpr (BUF && EX == 0) {
     tile_load_buf<D>(kr, k_rs, 0, (int)ldi);
     tile_load_buf<D>(vr, v_rs, 0, (int)ldi);
   } else {
@@ -638,7 +638,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     const int j0 = it * BN2;
     const bool has_next = it + 1 < ntiles;
     if (has_next) {
-      if constexpr (BUF) {
+      if constexpr (BUF && EX == 0) {
         tile_load_buf<D>(kr, k_rs, j0 + BN2, (int)ldi);
         tile_load_buf<D>(vr, v_rs, j0 + BN2, (int)ldi);
       } else {
@@ -828,7 +828,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   const __amdgpu_buffer_rsrc_t q_rs = head_rsrc(Q + base, S, (int)ldi);
   const __amdgpu_buffer_rsrc_t o_rs = head_rsrc(dO + obase, S, o_ld<D>(onh));
   auto load_tile = [&](int i0) {
-    if constexpr (BUF) {
+    if constexpr (BUF && EX == 0) {
       tile_load_buf<D>(qr, q_rs, i0, (int)ldi);
       tile_load_buf<D>(orr, o_rs, i0, o_ld<D>(onh));
     } else {
@@ -1040,7 +1040,7 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
   const int ntiles = (kend + BN2 - 1) / BN2;
   uint4 kr[D / 32], vr[D / 32];
   const __amdgpu_buffer_rsrc_t k_rs = head_rsrc(K + base, S, (int)ldi), v_rs = head_rsrc(V + base, S, (int)ldi);
-  if constexpr (BUF) {
+  if constexpr (BUF && EX == 0) {
     tile_load_buf<D>(kr, k_rs, 0, (int)ldi);
     tile_load_buf<D>(vr, v_rs, 0, (int)ldi);
   } else {
@@ -1054,7 +1054,7 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
     const int j0 = it * BN2;
     const bool has_next = it + 1 < ntiles;
     if (has_next) {
-      if constexpr (BUF) {
+      if constexpr (BUF && EX == 0) {
         tile_load_buf<D>(kr, k_rs, j0 + BN2, (int)ldi);
         tile_load_buf<D>(vr, v_rs, j0 + BN2, (int)ldi);
       } else {
