@@ -82,7 +82,10 @@ def parse():
                    help="keep gradients resident across micro-batches, one reduce-scatter per step "
                         "(auto: when the spare HBM holds a bf16 copy of the gradients)")
     p.add_argument("--dist-backend", type=str, default="nccl",
-                   help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU")
+                   help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU (forced on CPU)")
+    p.add_argument("--fp32-reduce", type=str, default="off", choices=["on", "off"],
+                   help="reduce bf16 gradients in fp32 (DeeperSpeed's bf16 default fp32_allreduce; "
+                        "tests/test_zero_reduce_precision.py measures what bf16 reduction costs)")
     return p.parse_args()
 
 
@@ -115,13 +118,86 @@ def log(msg):
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without an external launcher: start N rank processes of this script,
+    one per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment), relay rank 0's
+    result line, and stop every rank as soon as one fails (the contract of the framework's own
+    launcher, launcher/launch.py; reference deepspeed/launcher/launch.py:121-175).  The parent
+    never initialises HIP: only the rank processes touch the GPU."""
+    import signal
+    import subprocess
+    import threading
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=addr, MASTER_PORT=port)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else 2,
+                                      start_new_session=True))
+    lines = []
+    reader = threading.Thread(target=lambda: lines.extend(procs[0].stdout.readlines()), daemon=True)
+    reader.start()
+
+    def signal_all(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except (ProcessLookupError, PermissionError):
+                    pass
+
+    def stop_all(grace=30.0):
+        signal_all(signal.SIGTERM)
+        deadline = time.time() + grace
+        while any(p.poll() is None for p in procs) and time.time() < deadline:
+            time.sleep(0.2)
+        signal_all(signal.SIGKILL)
+
+    def on_signal(signum, frame):
+        stop_all(10.0)
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGINT, on_signal)
+    signal.signal(signal.SIGTERM, on_signal)
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = next(((r, c) for r, c in enumerate(codes) if c not in (None, 0)), None)
+        if bad is not None:
+            r, c = bad
+            rc = c if c > 0 else 128 - c
+            print(f"[bench] rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr, flush=True)
+            stop_all()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    reader.join(timeout=10)
+    if rc == 0:
+        for ln in lines:
+            os.write(_RESULT_FD, ln)
+    return rc
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if launched == 0 and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = launched or 1
     if world != args.gpus:
-        # single-process launch with --gpus 1 (or a mismatch): trust the launcher's world
-        if world == 1 and args.gpus != 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+        log(f"--gpus {args.gpus} differs from the launcher's WORLD_SIZE={world}; using {world}")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
     os.environ.setdefault("RANK", "0")
@@ -132,17 +208,43 @@ def main():
     import deeperspeed_amd as ds
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
     from deeperspeed_amd.ops import native
+    from deeperspeed_amd.runtime import memory_fit
 
-    ds.init_distributed(dist_backend=args.dist_backend)
+    on_gpu = torch.cuda.is_available()
+    ds.init_distributed(dist_backend=args.dist_backend if on_gpu else "gloo")
     rank = dist.get_rank()
-    # one rank per GPU; more ranks than GPUs (a rehearsal of the N-GPU path on one card)
-    # share the device and split its memory budget
-    ndev = torch.cuda.device_count()
-    local = int(os.environ["LOCAL_RANK"]) % ndev
-    share = -(-int(os.environ.get("LOCAL_WORLD_SIZE", "1")) // ndev)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    native.hip_ops()  # fail loudly if the HIP extension is missing
+    if os.environ.get("DSA_BENCH_FAIL_RANK") == str(rank):  # teardown test hook (tests/test_bench_contract.py)
+        raise SystemExit(7)
+    if on_gpu:
+        # one rank per GPU; more ranks than GPUs (a rehearsal of the N-GPU path on one card)
+        # share the device and split its memory budget
+        ndev = torch.cuda.device_count()
+        local = int(os.environ["LOCAL_RANK"]) % ndev
+        share = -(-int(os.environ.get("LOCAL_WORLD_SIZE", "1")) // ndev)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        native.hip_ops()  # fail loudly if the HIP extension is missing
+        hbm = torch.cuda.get_device_properties(local).total_memory
+    else:  # CPU / gloo: the plumbing of the contract (tests), no memory planning
+        local, share, dev, hbm = 0, 1, torch.device("cpu"), float(1 << 60)
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    def reserved_peak():
+        return torch.cuda.max_memory_reserved(local) if on_gpu else 0
+
+    def device_peak():
+        """Peak HBM of this rank: the allocator's reserved peak plus what lives outside it
+        (RCCL buffers, runtime); the outside part is only attributable with one rank per GPU."""
+        if not on_gpu:
+            return 0
+        outside = 0
+        if share == 1:
+            free, total = torch.cuda.mem_get_info(local)
+            outside = max(0, (total - free) - torch.cuda.memory_reserved(local))
+        return reserved_peak() + outside
 
     over = {"num_layers": args.layers} if args.layers else {}
     if args.hidden:
@@ -151,9 +253,9 @@ def main():
         over["sparse_attention"] = {"mode": args.sparse, "block": args.block}
     cfg = get_config(args.model, max_seq_len=args.seq, checkpoint_activations=True, **over)
     big = get_config(args.model).num_params() > 5e9  # batch shape of the full model, also under --layers
-    hbm = torch.cuda.get_device_properties(local).total_memory
     budget = 0.97 * hbm / share
     reserve = 0.03 * hbm / share  # allocator fragmentation, RCCL / runtime buffers
+    P = cfg.num_params()
 
     def layout(mb, ga):
         """Model-state layout for one (micro-batch, grad-accum): compact fp32 master (bf16
@@ -161,8 +263,9 @@ def main():
         less) > everything in HBM > fp32 master on the host; then recompute only if needed."""
         offload = args.offload
         if offload == "auto":
-            offload = next((o for o in ("compact", "none", "master")
-                            if plan_memory(cfg, mb, args.seq, world, o, True, ga) < budget), "master")
+            offload = "none" if not on_gpu else next(
+                (o for o in ("compact", "none", "master")
+                 if plan_memory(cfg, mb, args.seq, world, o, True, ga) < budget), "master")
         ckpt = args.ckpt
         if ckpt == "auto":
             ckpt = "off" if plan_memory(cfg, mb, args.seq, world, offload, False, ga) < budget else "on"
@@ -170,9 +273,9 @@ def main():
 
     # Per-GPU work is fixed at 16 sequences per optimizer step for the big models (weak
     # scaling).  When the shards are small enough (N >= 4 for 20B), micro-batch 8 x 2 runs
-    # without recompute AND keeps every gathered unit resident: hipBLASLt is ~4 % faster at
-    # M = 16384 tokens than at 8192 (profiles/aux/gemm_m16k.log) and the per-micro-batch
-    # ZeRO-3 gradient reduce-scatters halve.  Otherwise micro-batch 4 x 4.
+    # without recompute and leaves room to keep every gathered unit resident: hipBLASLt is ~4 %
+    # faster at M = 16384 tokens than at 8192 (profiles/aux/gemm_m16k.log) and the
+    # per-micro-batch ZeRO-3 gradient reduce-scatters halve.  Otherwise micro-batch 4 x 4.
     if args.micro_batch or args.grad_accum or not big:
         mb = args.micro_batch or (4 if big else 8)
         ga = args.grad_accum or (4 if big else 2)
@@ -180,28 +283,29 @@ def main():
     else:
         for mb, ga in ((8, 2), (4, 4)):
             offload, ckpt, planned = layout(mb, ga)
-            if ckpt == "off" and planned + 2 * cfg.num_params() + reserve < budget:
+            if ckpt == "off" and planned + 2 * P + reserve < budget:
                 break
     cfg.checkpoint_activations = ckpt == "on"
-    # ZeRO-3 parameter retention (stage3_max_live_parameters): HBM left after states and
-    # activations keeps gathered bf16 units resident between their forward and backward use
-    # and across the micro-batches of one optimizer step, so a unit is all-gathered once per
-    # step instead of twice per micro-batch when the whole model fits (it does at N>=2 on
-    # 288 GB parts: 41 GB of bf16 weights for 20B)
-    spare = budget - planned - reserve
-    live = int(max(0.0, min(spare / 2, cfg.num_params() * 1.0)))  # bf16 elements
-    if args.max_live is not None:
-        live = int(args.max_live)
-    # resident gradients (one reduce-scatter per optimizer step instead of one per
-    # micro-batch): a bf16 copy of the full gradients, planned after parameter retention
+    # ZeRO-3 retention (stage3_max_live_parameters) and resident gradients only buy speed.
+    # They are sized from MEASUREMENT (runtime/memory_fit.py): the first warmup step runs lean
+    # (none of either), its measured peak decides what the rest of HBM is granted to, and every
+    # later warmup step gives back retention, then resident gradients, then halves the
+    # micro-batch if the peak comes within DSA_MEM_FLOOR_GIB of the device.
     sharded = world > 1 or args.force_sharded
-    resident = args.resident_grads == "on" or (
-        args.resident_grads == "auto" and sharded and ga > 1 and world > 1 and
-        spare - 2 * live >= 2 * cfg.num_params() + reserve)
+    fit = None
+    if args.zero == 3 and sharded and ckpt == "off" and on_gpu and args.pipe == 1:
+        fit = memory_fit.FitState(params=P, world=world, micro_batch=mb, grad_accum=ga,
+                                  auto_live=args.max_live is None, auto_resident=args.resident_grads == "auto")
+    live = int(args.max_live) if args.max_live is not None else (0 if fit else int(min(P, 1e9)))
+    resident = args.resident_grads == "on"
+    if fit is not None:
+        fit.live, fit.resident = live, resident
+    floor = float(os.environ.get("DSA_MEM_FLOOR_GIB", "3")) * 2**30
+    limit = hbm / share - floor
     zcfg = {"stage": args.zero, "overlap_comm": True, "reduce_scatter": True, "reduce_bucket_size": int(2e8),
             "stage3_prefetch_bucket_size": int(5e8), "stage3_param_persistence_threshold": int(1e6),
             "stage3_unit_max_numel": int(2e8), "stage3_max_live_parameters": live,
-            "stage3_max_reuse_distance": int(2 * cfg.num_params())}
+            "stage3_max_reuse_distance": int(2 * P)}
     if args.force_sharded:
         # the bypass accumulates micro-batch gradients in bf16 in the bound shard; the forced
         # sharded path does the same (an fp32 shard would not fit next to 20B's states)
@@ -210,7 +314,7 @@ def main():
         zcfg["resident_grads"] = True
     # bound single-rank ZeRO-3: the fused Adam step overlaps the next forward (side stream,
     # per-bucket events); DSA_OVERLAP_STEP=0 keeps the serial step
-    if (world == 1 and not args.force_sharded and offload in ("compact", "none")
+    if (world == 1 and not args.force_sharded and offload in ("compact", "none") and on_gpu
             and os.environ.get("DSA_OVERLAP_STEP", "1") != "0"):
         zcfg["overlap_step"] = True
     if offload == "compact":
@@ -229,29 +333,35 @@ def main():
         "optimizer": {"type": "Adam", "params": {"lr": 1e-4, "betas": [0.9, 0.95], "eps": 1e-8,
                                                   "weight_decay": 0.01}},
         "fp16": {"enabled": True, "type": "bfloat16"},
-        "fp32_allreduce": False,
+        "fp32_allreduce": args.fp32_reduce == "on",
         "gradient_clipping": 1.0,
         "zero_optimization": zcfg,
         "steps_per_print": 1000000,
         "wall_clock_breakdown": False,
     }
-    log(f"model={args.model} params={cfg.num_params() / 1e9:.2f}B world={world} mb={mb} ga={ga} seq={args.seq} "
+    log(f"model={args.model} params={P / 1e9:.2f}B world={world} mb={mb} ga={ga} seq={args.seq} "
         f"zero={args.zero} offload={offload} ckpt={ckpt} live={live / 1e9:.1f}B resident_grads={resident} "
-        f"force_sharded={args.force_sharded} hbm={hbm / 2**30:.0f} GiB "
-        f"planned={plan_memory(cfg, mb, args.seq, world, offload, ckpt == 'on', ga) / 2**30:.0f} GiB")
+        f"measured_fit={fit is not None} force_sharded={args.force_sharded} hbm={hbm / 2**30:.0f} GiB "
+        f"planned={planned / 2**30:.0f} GiB")
     if args.pipe > 1:
         return run_pipeline(args, cfg, mb, ga, world, rank, dev)
     t0 = time.time()
     torch.manual_seed(1234)
     model = GPTNeoX(cfg, device=dev, dtype=torch.bfloat16)
-    log(f"model built in {time.time() - t0:.1f}s, mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+    log(f"model built in {time.time() - t0:.1f}s")
     engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
     del model
-    log(f"engine ready in {time.time() - t0:.1f}s, mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+    log(f"engine ready in {time.time() - t0:.1f}s" +
+        (f", mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB" if on_gpu else ""))
 
     g = torch.Generator(device=dev)
     g.manual_seed(4321 + rank)
-    batches = [torch.randint(0, cfg.vocab_size, (mb, args.seq), device=dev, generator=g) for _ in range(ga)]
+    batches = []
+
+    def make_batches():
+        batches[:] = [torch.randint(0, cfg.vocab_size, (mb, args.seq), device=dev, generator=g) for _ in range(ga)]
+
+    make_batches()
 
     def train_step():
         loss = None
@@ -268,10 +378,10 @@ def main():
         for i in range(ga):
             for name, fn in (("fwd", lambda: engine(batches[i], labels=batches[i])),
                              ("bwd", lambda: engine.backward(loss)), ("step", engine.step)):
-                torch.cuda.synchronize()
+                sync()
                 t = time.time()
                 r = fn()
-                torch.cuda.synchronize()
+                sync()
                 ph[name] += time.time() - t
                 if name == "fwd":
                     loss = r
@@ -280,7 +390,7 @@ def main():
                         f"(peak {torch.cuda.max_memory_allocated() / 2**30:.2f})")
         return loss, ph
 
-    memtrace = os.environ.get("DSA_MEMTRACE", "0") == "1"
+    memtrace = os.environ.get("DSA_MEMTRACE", "0") == "1" and on_gpu
     if memtrace:  # per-layer activation footprint of the first forward (planner calibration)
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         marks = []
@@ -303,17 +413,17 @@ def main():
         HBM left above the allocator's reserved peak (minus a margin) keeps the attention
         q, k, v, output and LSE of as many layers as fit (NeoXAttention.stash_outputs), so their
         recompute skips the QKV GEMM, rotary split and flash forward."""
-        if not cfg.checkpoint_activations or args.sparse or os.environ.get("DSA_STASH", "1") == "0":
+        if not cfg.checkpoint_activations or args.sparse or not on_gpu or os.environ.get("DSA_STASH", "1") == "0":
             return 0
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
         margin = float(os.environ.get("DSA_STASH_MARGIN_GIB", "2")) * 2**30
-        free = hbm / share - torch.cuda.max_memory_reserved() - margin
+        free = hbm / share - reserved_peak() - margin
         n = int(max(0, min(len(layers), free // per_layer)))
         for m in layers[-n:] if n else []:
             m.attention.stash_outputs = True
         log(f"selective recompute: {n}/{len(layers)} layers keep attention outputs "
-            f"({n * per_layer / 2**30:.1f} GiB; reserved peak {torch.cuda.max_memory_reserved() / 2**30:.1f} GiB)")
+            f"({n * per_layer / 2**30:.1f} GiB; reserved peak {reserved_peak() / 2**30:.1f} GiB)")
         # the remaining layers park their stash in pinned host memory (copy engines over PCIe,
         # prefetched back by the recompute of the layers above): opt-in, DSA_STASH_OFFLOAD=1 -- on the
         # measured box the PCIe copies throttled the forward (profiles/aux/host_stash_ab.log)
@@ -337,8 +447,8 @@ def main():
             return n
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
-        floor = float(os.environ.get("DSA_STASH_FLOOR_GIB", "1.5")) * 2**30
-        over = torch.cuda.max_memory_reserved() - (hbm / share - floor)
+        sfloor = float(os.environ.get("DSA_STASH_FLOOR_GIB", "1.5")) * 2**30
+        over = reserved_peak() - (hbm / share - sfloor)
         if over <= 0:
             return n
         drop = min(n, int(-(-over // per_layer)))
@@ -350,30 +460,62 @@ def main():
             else:
                 m.attention.stash_outputs = False
         torch.cuda.empty_cache()
-        log(f"stash safety: reserved peak {torch.cuda.max_memory_reserved() / 2**30:.1f} GiB is within "
-            f"{floor / 2**30:.1f} GiB of the budget; {drop} layer(s) back to full recompute ({n - drop} stashed)")
+        log(f"stash safety: reserved peak {reserved_peak() / 2**30:.1f} GiB is within "
+            f"{sfloor / 2**30:.1f} GiB of the budget; {drop} layer(s) back to full recompute ({n - drop} stashed)")
         return n - drop
 
-    for i in range(args.warmup):
+    def refit(i):
+        """Measured memory fit after warmup step i (see `fit` above).  Returns True when the
+        configuration changed (one more untimed step must run with it before timing)."""
+        nonlocal mb, ga
+        # every rank must take the same decision (collective order): act on the most
+        # constrained rank's measurement
+        h = torch.tensor([limit - device_peak()], device=dev, dtype=torch.float64)
+        dist.all_reduce(h, op=dist.ReduceOp.MIN)
+        head = float(h.item())
+        if i == 0:
+            grow_margin = float(os.environ.get("DSA_FIT_MARGIN_GIB", "1")) * 2**30
+            acts = memory_fit.grow(fit, head - grow_margin)
+        else:
+            acts = memory_fit.shrink(fit, -head) if head < 0 else []
+        if not acts:
+            return False
+        if memory_fit.apply(engine, acts):
+            mb, ga = fit.micro_batch, fit.grad_accum
+            make_batches()
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+        log(f"memory fit after warmup {i}: peak {device_peak() / 2**30:.1f} GiB measured, headroom "
+            f"{head / 2**30:.1f} GiB -> {acts} (live={fit.live / 1e9:.2f}B resident={fit.resident} mb={mb} ga={ga})")
+        return True
+
+    i, extra = 0, 0
+    while i < args.warmup + extra:
         ts = time.time()
         loss, ph = timed_step()
         log(f"warmup {i} loss={float(loss.detach()):.4f} {time.time() - ts:.2f}s "
             + " ".join(f"{k}={v:.2f}s" for k, v in ph.items())
-            + f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB"
-            + f" reserved={torch.cuda.max_memory_reserved() / 2**30:.1f} GiB"
+            + (f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB"
+               f" reserved={reserved_peak() / 2**30:.1f} GiB device={device_peak() / 2**30:.1f} GiB" if on_gpu else "")
             + (f" zero3_pool={engine.optimizer._pool.held * 2 / 2**30:.1f} GiB"
                if hasattr(engine.optimizer, "_pool") else ""))
-        if i == 0 and args.warmup >= 2:
+        changed = False
+        if fit is not None:
+            changed = refit(i)
+        elif i == 0 and args.warmup >= 2:
             stashed = plan_stash()
         elif i == 1 and stashed:
             stashed = check_stash(stashed)
+        if changed and i == args.warmup + extra - 1 and extra < 3:
+            extra += 1  # the timed steps never run a configuration no warmup step has run
+        i += 1
 
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.time()
     for i in range(args.steps):
         loss = train_step()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     elapsed = time.time() - t_start
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -385,7 +527,7 @@ def main():
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
             for _ in range(args.profile_steps):
                 train_step()
-            torch.cuda.synchronize()
+            sync()
         if rank == 0:
             os.makedirs("gpurun_out", exist_ok=True)
             with open("gpurun_out/torch_profile.txt", "w") as f:
@@ -400,10 +542,16 @@ def main():
     tps = tokens / elapsed
     flops_tok = cfg.flops_per_token(args.seq, recompute=False)
     ms_step = elapsed / args.steps * 1000.0
+    opt = engine.optimizer
+    full_model = args.model == "gpt-neox-20b" and not (args.hidden or args.layers)
+    zpath = None
+    if args.zero == 3:
+        zpath = "sharded" if (world > 1 or args.force_sharded) else "bound-single-rank"
     out = {
-        "metric": ("tokens/sec (node) GPT-NeoX-20B ZeRO-3" if args.model == "gpt-neox-20b" and not (args.hidden or args.layers)
-                   else f"tokens/sec {args.model}" + (f" reshaped to {cfg.num_params() / 1e9:.1f}B (hidden {cfg.hidden_size},"
-                                                      f" {cfg.num_layers} layers)" if (args.hidden or args.layers) else ""))
+        "metric": ("tokens/sec (node) GPT-NeoX-20B ZeRO-3" if full_model and args.zero == 3
+                   else f"tokens/sec {args.model} ZeRO-{args.zero}" + (
+                       f" reshaped to {P / 1e9:.1f}B (hidden {cfg.hidden_size}, {cfg.num_layers} layers)"
+                       if (args.hidden or args.layers) else ""))
                   + (f" block-sparse {args.sparse} seq{args.seq}" if args.sparse else ""),
         "value": round(tps, 2),
         "unit": "tokens/s",
@@ -413,24 +561,31 @@ def main():
         "ms_per_step": round(ms_step, 2),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(tps / (REF_TOKENS_PER_GPU * world), 3),
+        "vs_baseline": round(tps / (REF_TOKENS_PER_GPU * world), 3) if full_model and args.zero == 3 else None,
         "dtype": "bf16",
         "data": "synthetic random tokens, random-init weights",
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq,
                    "parallelism": f"zero{args.zero}-dp{world}", "micro_batch": mb, "grad_accum": ga,
                    "offload": offload, "activation_checkpointing": ckpt == "on", "sparse_attention": args.sparse,
-                   "params_per_gpu": round(cfg.num_params() / world / 1e9, 3),
+                   "attention_density": round(cfg.attention_density(args.seq), 4),
+                   "params_per_gpu": round(P / world / 1e9, 3),
                    "model_tflops_per_gpu": round(tps * flops_tok / world / 1e12, 1),
                    "final_loss": round(float(loss.detach()), 4),
-                   "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
-                   "planned_hbm_gib": round(plan_memory(cfg, mb, args.seq, world, offload, ckpt == "on", ga) / 2**30, 1),
-                   "max_live_parameters": live, "stashed_attention_layers": stashed,
+                   "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None,
+                   "planned_hbm_gib": round(planned / 2**30, 1),
+                   "stashed_attention_layers": stashed,
                    "host_stashed_attention_layers": sum(1 for m in engine.module.modules()
                                                         if getattr(m, "stash_offload", False)),
-                   "zero3_path": "sharded" if (world > 1 or args.force_sharded) else "bound-single-rank",
+                   "zero3_path": zpath,
+                   "max_live_parameters": getattr(opt, "max_live_parameters", None) if args.zero == 3 else None,
+                   "resident_grads": bool(getattr(opt, "resident_grads", False)) if args.zero == 3 else None,
+                   "memory_fit_actions": [list(a) for a in fit.actions] if fit is not None else None,
+                   "fp32_reduce": args.fp32_reduce == "on",
+                   "dist_backend": dist.get_backend(),
                    "overlap_step": bool(zcfg.get("overlap_step", False)),
-                   "resident_grads": resident,
-                   "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N), BASELINE.md derived target"},
+                   "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N): BASELINE.md's derived target "
+                                    "(reference's best published ZeRO-3 49 TFLOPS/GPU on V100 at 6N FLOPs/token); "
+                                    "BASELINE.json publishes no number for this metric"},
     }
     if rank == 0:
         emit_result(out)
@@ -471,7 +626,7 @@ def run_pipeline(args, cfg, mb, ga, world, rank, dev):
                                     config_params=conf)
     log(f"pipeline PP={args.pipe} DP={dp} stage={engine.stage_id} params/stage="
         f"{sum(p.numel() for p in engine.module.parameters()) / 1e9:.2f}B optimizer={args.optimizer} "
-        f"ready in {time.time() - t0:.1f}s mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB")
+        f"ready in {time.time() - t0:.1f}s")
     g = torch.Generator(device=dev)
     g.manual_seed(4321 + engine.grid.get_data_parallel_id())
     batches = [torch.randint(0, cfg.vocab_size, (mb, args.seq), device=dev, generator=g) for _ in range(ga)]
@@ -479,18 +634,24 @@ def run_pipeline(args, cfg, mb, ga, world, rank, dev):
     def train_step():
         return engine.train_batch(iter([(b, b) for b in batches]))
 
+    on_gpu = dev.type == "cuda"
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     for i in range(args.warmup):
         ts = time.time()
         loss = train_step()
-        torch.cuda.synchronize()
-        log(f"warmup {i} loss={float(loss):.4f} {time.time() - ts:.2f}s "
-            f"peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB")
+        sync()
+        log(f"warmup {i} loss={float(loss):.4f} {time.time() - ts:.2f}s"
+            + (f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB" if on_gpu else ""))
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.time()
     for _ in range(args.steps):
         loss = train_step()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     t = torch.tensor([time.time() - t_start], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -507,7 +668,8 @@ def run_pipeline(args, cfg, mb, ga, world, rank, dev):
                    "grad_accum": ga, "optimizer": args.optimizer,
                    "model_tflops_per_gpu": round(tps * cfg.flops_per_token(args.seq) / world / 1e12, 1),
                    "final_loss": round(float(loss.detach()), 4),
-                   "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1)},
+                   "dist_backend": dist.get_backend(),
+                   "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None},
     }
     if rank == 0:
         emit_result(out)

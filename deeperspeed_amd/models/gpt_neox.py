@@ -70,12 +70,28 @@ class GPTNeoXConfig:
         return n
 
     def flops_per_token(self, seq_len=None, recompute=True):
-        """Model FLOPs per trained token (fwd+bwd[+recompute]) incl. attention."""
+        """Model FLOPs per trained token (fwd+bwd[+recompute]) incl. attention.  With block-sparse
+        attention only the layout's active score elements are counted (attention_density)."""
         s = seq_len or self.max_seq_len
         n = self.num_params(include_embeddings=False) + self.vocab_size * self.hidden_size  # output proj GEMM
         attn = 2 * self.num_layers * s * self.hidden_size  # QK^T + PV per token (causal halves, x2 fwd terms)
+        attn *= self.attention_density(s)
         mult = 8 if recompute else 6
         return mult * n + (mult // 2) * attn
+
+    def attention_density(self, seq_len=None) -> float:
+        """Fraction of the causal score triangle (s^2/2 elements) the attention computes: 1.0
+        dense; for a block-sparse layout the active blocks, diagonal blocks counted half."""
+        if not self.sparse_attention:
+            return 1.0
+        s = seq_len or self.max_seq_len
+        sc = make_sparsity_config(self)
+        lay = sc.make_layout(s).bool()
+        nb = lay.shape[-1]
+        lower = torch.tril(torch.ones(nb, nb, dtype=torch.bool), diagonal=-1)
+        diag = torch.eye(nb, dtype=torch.bool)
+        active = (lay & lower).sum().item() + 0.5 * (lay & diag).sum().item()
+        return float(active / lay.shape[0] * sc.block ** 2 / (s * s / 2.0))
 
 
 PRESETS = {

@@ -786,6 +786,24 @@ class DeepSpeedEngine(Module):
     def is_gradient_accumulation_boundary(self):
         return (self.micro_steps + 1) % self.gradient_accumulation_steps() == 0
 
+    def set_batch_shape(self, micro_batch: int, grad_accum: int):
+        """Re-split the per-rank batch (micro_batch x grad_accum, same product) between two
+        optimizer steps -- a trainer trading micro-batch activations for HBM.  Only legal at a
+        step boundary; the train batch size is unchanged."""
+        if self.micro_steps % self.gradient_accumulation_steps() != 0:
+            raise RuntimeError("set_batch_shape() must be called at an optimizer-step boundary")
+        c = self._config
+        if micro_batch * grad_accum != c.train_micro_batch_size_per_gpu * c.gradient_accumulation_steps:
+            raise ValueError("set_batch_shape() keeps train_batch_size: micro_batch * grad_accum must not change")
+        c.train_micro_batch_size_per_gpu = int(micro_batch)
+        c.gradient_accumulation_steps = int(grad_accum)
+        self.micro_steps = 0
+        opt = self.optimizer
+        if hasattr(opt, "gradient_accumulation_steps"):
+            opt.gradient_accumulation_steps = int(grad_accum)
+            if hasattr(opt, "refresh_grad_dtype"):  # the reduced-gradient dtype depends on GA
+                opt.refresh_grad_dtype()
+
     def zero_grad(self):
         if hasattr(self.optimizer, "groups"):
             self.optimizer.zero_grad()

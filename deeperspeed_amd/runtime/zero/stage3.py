@@ -841,6 +841,48 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
     def _zero_stage(self):
         return 3
 
+    # ------------------------------------------------------------------ memory knobs
+    # Called between optimizer steps by a trainer that sizes HBM from measurement (bench.py:
+    # a first step runs lean, the headroom it leaves is granted to retention / resident
+    # gradients, and a later step that comes too close to the HBM limit gives them back).
+    def set_max_live_parameters(self, numel: int):
+        """stage3_max_live_parameters at run time; takes effect from the next gather (retained
+        units above the new cap are dropped at the next step boundary, `_post_step`)."""
+        self.max_live_parameters = max(0, int(numel))
+
+    def set_resident_grads(self, enabled: bool):
+        """Turn resident unit gradients on/off at an optimizer-step boundary.  The reduced
+        shard gradient changes dtype with the mode under grad_accum_dtype "auto" (fp32 when
+        GA > 1 micro-batch reductions land in it, param dtype with one reduction per step) and
+        is re-allocated (zeroed: it is empty at a boundary)."""
+        enabled = bool(enabled) and not self.single
+        if enabled == self.resident_grads:
+            return
+        if any(u.grad_fulls for u in self._units) or self._grads_nonzero:
+            raise RuntimeError("set_resident_grads() must be called between optimizer steps")
+        self.resident_grads = enabled
+        self.refresh_grad_dtype()
+
+    def refresh_grad_dtype(self):
+        """Re-allocate the (empty) reduced shard gradients when the accumulation mode (resident
+        grads, gradient_accumulation_steps) changes the dtype they accumulate in."""
+        if self.single:
+            return
+        for g in self.groups:
+            gdt = self._grad_dtype(g)
+            if g.shard_grad is not None and g.shard_grad.dtype != gdt:
+                dev = g.shard_grad.device
+                g.shard_grad = None
+                g.shard_grad = torch.zeros(g.shard_numel, dtype=gdt, device=dev)
+        self._pool.clear()
+
+    def release_retained(self):
+        """Drop every retained (non-persistent, idle) gathered unit and the pool's free buffers."""
+        for u in self._units:
+            if not u.persistent and u.active == 0:
+                self._release(u)
+        self._pool.clear()
+
     # ------------------------------------------------------------------ model state helpers
     def register_external_parameter(self, module, param):
         owner = self.unit_of(param)

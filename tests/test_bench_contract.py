@@ -1,0 +1,61 @@
+"""bench.py contract on CPU/gloo: `python bench.py --gpus N` is ONE command that starts N rank
+processes itself (no external launcher), prints exactly one JSON line (rank 0's) and
+propagates the first rank failure after stopping the others."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None, timeout=240):
+    env = dict(os.environ, OMP_NUM_THREADS="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    env.pop("MASTER_PORT", None)
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout)
+
+
+def test_bench_self_spawns_ranks():
+    r = _run(["--gpus", "2", "--model", "tiny", "--seq", "64", "--steps", "2", "--warmup", "1",
+              "--dist-backend", "gloo"])
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.strip()]
+    assert len(lines) == 1, lines
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["parallelism"] == "zero3-dp2"
+    assert out["config"]["zero3_path"] == "sharded"
+    assert out["config"]["global_batch"] == 2 * out["config"]["micro_batch"] * out["config"]["grad_accum"]
+    assert out["value"] > 0 and out["vs_baseline"] is None  # tiny model: no baseline ratio
+
+
+def test_bench_zero2_label():
+    r = _run(["--gpus", "1", "--model", "tiny", "--seq", "64", "--steps", "1", "--warmup", "1", "--zero", "2"],
+             extra_env={"WORLD_SIZE": "1"})
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    out = json.loads(r.stdout.decode().strip())
+    assert out["config"]["zero3_path"] is None and out["config"]["parallelism"] == "zero2-dp1"
+    assert out["metric"].startswith("tokens/sec tiny ZeRO-2")
+
+
+def test_bench_rank_failure_stops_all():
+    r = _run(["--gpus", "2", "--model", "tiny", "--seq", "64", "--steps", "2", "--warmup", "1"],
+             extra_env={"DSA_BENCH_FAIL_RANK": "1"}, timeout=120)
+    assert r.returncode == 7
+    assert r.stdout.decode().strip() == ""
+    assert "rank 1 exited with status 7" in r.stderr.decode()
+
+
+@pytest.mark.slow
+def test_bench_pipeline_onebit_self_spawn():
+    r = _run(["--gpus", "4", "--model", "tiny", "--seq", "64", "--steps", "1", "--warmup", "1", "--pipe", "2",
+              "--optimizer", "onebitadam"], timeout=400)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    out = json.loads(r.stdout.decode().strip())
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "pp2-dp2"
