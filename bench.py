@@ -480,12 +480,13 @@ def main():
             acts = memory_fit.shrink(fit, -head) if head < 0 else []
         if not acts:
             return False
+        measured = device_peak()
         if memory_fit.apply(engine, acts):
             mb, ga = fit.micro_batch, fit.grad_accum
             make_batches()
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats()
-        log(f"memory fit after warmup {i}: peak {device_peak() / 2**30:.1f} GiB measured, headroom "
+        log(f"memory fit after warmup {i}: peak {measured / 2**30:.1f} GiB measured, headroom "
             f"{head / 2**30:.1f} GiB -> {acts} (live={fit.live / 1e9:.2f}B resident={fit.resident} mb={mb} ga={ga})")
         return True
 
