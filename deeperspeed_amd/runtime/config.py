@@ -262,6 +262,13 @@ class DeepSpeedConfig:
                                        f"expecting one of {list(ValidationMode.__members__)}")
         self.checkpoint_tag_validation_enabled = ValidationMode[mode] != ValidationMode.IGNORE
         self.checkpoint_tag_validation_fail = ValidationMode[mode] == ValidationMode.FAIL
+        # MI355X extension: "reference" writes ZeRO optimizer files in the reference's contiguous
+        # per-group layout (zero_to_fp32.py of DeepSpeed 0.3.15 reads them); "native" (default)
+        # writes this framework's per-bucket interleaved shards
+        self.checkpoint_zero_format = str(ck.get("zero_format", "native")).lower()
+        if self.checkpoint_zero_format not in ("native", "reference"):
+            raise DeepSpeedConfigError(f"checkpoint.zero_format must be 'native' or 'reference', "
+                                       f"got {self.checkpoint_zero_format!r}")
 
         self.aio_config = get_aio_config(pd)
         self.vocabulary_size = pd.get("vocabulary_size", None)

@@ -1096,11 +1096,30 @@ class DeepSpeedEngine(Module):
 
     def _save_zero_checkpoint(self, save_path, tag):
         zero_checkpoint_name = self._get_zero_ckpt_name(save_path, tag)
-        zero_sd = dict(optimizer_state_dict=self.optimizer.state_dict(), param_shapes=self._get_zero_param_shapes(),
-                       ds_version=__version__)
+        if getattr(self._config, "checkpoint_zero_format", "native") == "reference":
+            zero_sd = self._reference_zero_state()
+        else:
+            zero_sd = dict(optimizer_state_dict=self.optimizer.state_dict(),
+                           param_shapes=self._get_zero_param_shapes(), ds_version=__version__)
         torch.save(zero_sd, zero_checkpoint_name)
         self._copy_recovery_script(os.path.dirname(zero_checkpoint_name))
         log_dist(f"zero checkpoint saved {zero_checkpoint_name}", ranks=[0])
+
+    def _reference_zero_state(self):
+        """ZeRO optimizer file in the reference layout (checkpoint.zero_format = "reference"):
+        contiguous per-group fp32 partitions under the reference's keys, `param_shapes` as the
+        reference writes it (every module parameter in order, reference engine.py:1792-1798),
+        plus each optimizer group's parameter names so multi-group files consolidate exactly."""
+        from .zero.ref_layout import export_reference_state_dict
+        opt = self.optimizer
+        self.synchronize()
+        osd = export_reference_state_dict(opt, max_elems_per_comm=int(self.zero_reduce_bucket_size()),
+                                          sub_group_size=int(self.zero_sub_group_size()))
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        shapes = OrderedDict((n, torch.Size(getattr(p, "ds_shape", p.shape))) for n, p in self.module.named_parameters())
+        groups = [[names.get(id(p), str(id(p))) for p in plist] for plist in opt._orig_group_params]
+        return dict(optimizer_state_dict=osd, param_shapes=shapes, dsa_group_param_names=groups,
+                    ds_version=__version__)
 
     def _get_zero_param_shapes(self):
         names = {id(p): n for n, p in self.module.named_parameters()}
@@ -1161,6 +1180,14 @@ class DeepSpeedEngine(Module):
     def _load_checkpoint(self, load_dir, tag, load_module_strict=True, load_optimizer_states=True,
                          load_lr_scheduler_states=True):
         load_path = self._get_ckpt_name(load_dir, tag)
+        if not os.path.exists(load_path) and self.zero_optimization_partition_weights():
+            # ZeRO-3 model states are written per data-parallel rank: a larger world than the
+            # saving one reads rank 0's (its parameter shards are re-partitioned from every
+            # saved rank's file, _load_zero3_module)
+            alt = os.path.join(os.path.dirname(load_path),
+                               "zero_pp_rank_0_mp_rank_" + os.path.basename(load_path).split("_mp_rank_")[1])
+            if os.path.exists(alt):
+                load_path = alt
         if not os.path.exists(load_path):
             logger.warning("Client provided checkpoint load path: {} does not exist ... skip checkpoint load"
                            .format(load_path))

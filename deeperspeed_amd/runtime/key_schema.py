@@ -36,7 +36,7 @@ TOP: List[Tuple[str, str, object]] = [
     ("TENSORBOARD_JOB_NAME", "job_name", "DeepSpeedJobName"),
     ("PROGRESSIVE_LAYER_DROP", "progressive_layer_drop", _NODEF), ("PLD_ENABLED", "enabled", False),
     ("PLD_THETA", "theta", 1.0), ("PLD_GAMMA", "gamma", 0.001), ("CHECKPOINT", "checkpoint", _NODEF),
-    ("CHECKPOINT_TAG_VALIDATION", "tag_validation", "Warn"),
+    ("CHECKPOINT_TAG_VALIDATION", "tag_validation", "Warn"), ("CHECKPOINT_ZERO_FORMAT", "zero_format", "native"),
     ("SPARSE_ATTENTION", "sparse_attention", _NODEF), ("SPARSE_MODE", "mode", "fixed"),
     ("SPARSE_BLOCK", "block", 16), ("SPARSE_DIFFERENT_LAYOUT_PER_HEAD", "different_layout_per_head", False),
     ("SPARSE_NUM_LOCAL_BLOCKS", "num_local_blocks", 4), ("SPARSE_NUM_GLOBAL_BLOCKS", "num_global_blocks", 1),

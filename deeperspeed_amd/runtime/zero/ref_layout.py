@@ -126,6 +126,164 @@ def _merge_stage3(sds, group_numels):
     return masters, moments
 
 
+# ---------------------------------------------------------------------------- export
+def _ceil_div(a, b):
+    return -(-a // b)
+
+
+def _stage1_geometry(total: int, world: int, max_elems_per_comm: int):
+    """(sub_partition_size, num_comm_intervals) exactly as the reference computes them
+    (stage1.py:314-343 best_max_elems_per_comm, :580-610 sub-partition alignment)."""
+    mepc = int(max_elems_per_comm)
+    max_iv = _ceil_div(total, mepc)
+    pad_max = mepc * max_iv - total
+    min_iv = total // mepc
+    if min_iv > 0:
+        pad_min = _ceil_div(total, world * min_iv)
+        if pad_max > pad_min:
+            mepc = pad_min + mepc
+    part = _ceil_div(total, world)
+    comm_part = int(mepc // world)
+    if part <= comm_part:
+        return part, 1
+    return comm_part, _ceil_div(part, comm_part)
+
+
+def _reference_ranges(stage: int, numels: Sequence[int], world: int, rank: int, max_elems_per_comm: int,
+                      sub_group_size: int):
+    """Where this rank's reference-layout pieces come from.  Returns a list of flat tensors
+    (stage 1: one per comm interval; stage 2: one; stage 3: one per sub-group), each a list of
+    (param j, start in param, length) runs -- plus, for stage 3, zero-padding lengths (None j)."""
+    offs, acc = [], 0
+    for n in numels:
+        offs.append(acc)
+        acc += n
+    total = acc
+
+    def runs(lo, hi):
+        out = []
+        for j, (o, n) in enumerate(zip(offs, numels)):
+            a, b = max(lo, o), min(hi, o + n)
+            if a < b:
+                out.append((j, a - o, b - a))
+        return out
+
+    if stage == 2:
+        part = _ceil_div(total, world)
+        return [runs(rank * part, min((rank + 1) * part, total))]
+    if stage == 1:
+        sps, intervals = _stage1_geometry(total, world, max_elems_per_comm)
+        return [runs((c * world + rank) * sps, min((c * world + rank + 1) * sps, total)) for c in range(intervals)]
+    # stage 3: per-parameter ceil(n / world) ranges, padded, grouped into sub-groups
+    subs, cur, cur_n = [], [], 0
+    for j, n in enumerate(numels):
+        ps = _ceil_div(n, world)
+        lo = min(rank * ps, n)
+        hi = min((rank + 1) * ps, n)
+        if hi > lo:
+            cur.append((j, lo, hi - lo))
+        if ps - (hi - lo) > 0:
+            cur.append((None, 0, ps - (hi - lo)))
+        cur_n += ps
+        if (sub_group_size is not None and cur_n >= sub_group_size) or j == len(numels) - 1:
+            subs.append(cur)
+            cur, cur_n = [], 0
+    if sum(_ceil_div(n, world) for n in numels) <= (sub_group_size or 0) or sub_group_size is None:
+        # the reference keeps one sub-group when the whole group fits (stage3.py:1337-1338)
+        subs = [[r for s in subs for r in s]]
+    return subs
+
+
+def _assemble(runs, full: Dict[int, torch.Tensor]) -> torch.Tensor:
+    parts = [torch.zeros(ln) if j is None else full[j][st: st + ln] for j, st, ln in runs]
+    return torch.cat(parts) if parts else torch.zeros(0)
+
+
+def export_reference_state_dict(opt, max_elems_per_comm: int = int(5e8), sub_group_size: int = int(1e12),
+                                comm_device=None) -> dict:
+    """This rank's optimizer state in the reference (DeepSpeed 0.3.15) ZeRO-1/2/3 layout.
+
+    Collective over the data-parallel group: every bucket's fp32 master and Adam moments are
+    all-gathered one bucket at a time (the flat-arena shards interleave every bucket over the
+    ranks, the reference gives each rank one contiguous range), and each rank keeps only the
+    parameters its reference range touches.  Written keys mirror the reference exactly:
+    `single_partition_of_fp32_groups` + lean `base_optimizer_state` (stage 2, stage2.py:
+    1720-1751), `local_sub_partitions_of_fp32_groups` + per-interval lean states +
+    `num_comm_intervals_per_group` (stage 1, stage1.py:924-943), `fp32_flat_groups` + a torch
+    `optimizer_state_dict` over the sub-group flats (stage 3, stage3.py:3046-3059)."""
+    import torch.distributed as dist
+    stage = opt._zero_stage()
+    if stage not in (1, 2, 3):
+        raise ValueError(f"reference-layout export needs ZeRO stage 1-3 (got {stage})")
+    world, rank = opt._layout_world_rank()
+    group = opt.dp_group
+    dev = comm_device
+    if dev is None:
+        dev = opt.device if (dist.is_initialized() and dist.get_backend(group) == "nccl") else torch.device("cpu")
+    orig = opt._orig_group_params
+    where = {}  # id(p) -> (group index, position j)
+    for G, plist in enumerate(orig):
+        for j, p in enumerate(plist):
+            where[id(p)] = (G, j)
+    numels = [[p.ds_numel if hasattr(p, "ds_numel") else p.numel() for p in plist] for plist in orig]
+    plans = [_reference_ranges(stage, numels[G], world, rank, max_elems_per_comm, sub_group_size)
+             for G in range(len(orig))]
+    needed = [{j for flat in plans[G] for j, _, _ in flat if j is not None} for G in range(len(orig))]
+    names = ("master", "exp_avg", "exp_avg_sq")
+    full = {n: [dict() for _ in orig] for n in names}
+    steps = [0] * len(orig)
+    for gi, g in enumerate(opt.groups):
+        shards = {"master": opt.master_fp32(g).float()}
+        st = opt.optimizer.state.get(g.master, {}) if g.master is not None else {}
+        for n in ("exp_avg", "exp_avg_sq"):
+            t = opt._nvme_read_group(gi, n) if opt.nvme else st.get(n)
+            shards[n] = t.detach().float().cpu() if torch.is_tensor(t) else torch.zeros(g.shard_numel)
+        steps[g.group_index] = int(st.get("step", steps[g.group_index]) or 0) if st else steps[g.group_index]
+        for b in g.buckets:
+            keep = [i for i, p in enumerate(b.params) if where[id(p)][1] in needed[where[id(p)][0]]]
+            for n in names:
+                chunk = shards[n][b.shard_offset: b.shard_offset + b.chunk].to(dev)
+                out = torch.empty(b.numel, dtype=torch.float32, device=dev)
+                if world > 1:
+                    dist.all_gather_into_tensor(out, chunk, group=group)
+                else:
+                    out.copy_(chunk)
+                out = out.cpu()
+                for i in keep:
+                    G, j = where[id(b.params[i])]
+                    full[n][G][j] = out[b.offsets[i]: b.offsets[i] + b.numels[i]].clone()
+    sd = {"loss_scaler": opt.loss_scaler.state_dict(), "dynamic_loss_scale": opt.dynamic_loss_scale,
+          "overflow": opt.overflow, "zero_stage": stage, "partition_count": world}
+    hyper = [{k: v for k, v in pg.items() if k != "params"} for pg in opt.optimizer.param_groups]
+    if stage == 2:
+        sd["single_partition_of_fp32_groups"] = [_assemble(plans[G][0], full["master"][G]) for G in range(len(orig))]
+        sd["base_optimizer_state"] = [{"step": steps[G],
+                                       "exp_avg": _assemble(plans[G][0], full["exp_avg"][G]),
+                                       "exp_avg_sq": _assemble(plans[G][0], full["exp_avg_sq"][G])}
+                                      for G in range(len(orig))]
+    elif stage == 1:
+        sd["local_sub_partitions_of_fp32_groups"] = [[_assemble(r, full["master"][G]) for r in plans[G]]
+                                                     for G in range(len(orig))]
+        sd["base_optimizer_state"] = [[{"step": steps[G], "exp_avg": _assemble(r, full["exp_avg"][G]),
+                                        "exp_avg_sq": _assemble(r, full["exp_avg_sq"][G])} for r in plans[G]]
+                                      for G in range(len(orig))]
+        sd["num_comm_intervals_per_group"] = [len(plans[G]) for G in range(len(orig))]
+    else:
+        flats, state, pgs, k = [], {}, [], 0
+        for G in range(len(orig)):
+            ids = []
+            for r in plans[G]:
+                flats.append(_assemble(r, full["master"][G]))
+                state[k] = {"step": steps[G], "exp_avg": _assemble(r, full["exp_avg"][G]),
+                            "exp_avg_sq": _assemble(r, full["exp_avg_sq"][G])}
+                ids.append(k)
+                k += 1
+            pgs.append(dict(hyper[G] if G < len(hyper) else {}, params=ids))
+        sd["fp32_flat_groups"] = flats
+        sd["optimizer_state_dict"] = {"state": state, "param_groups": pgs}
+    return sd
+
+
 def merge_reference_shards(sds: Sequence[dict], group_numels: Sequence[Sequence[int]]
                            ) -> Tuple[List[List[torch.Tensor]], List[Dict]]:
     """Full per-parameter fp32 tensors from the saved optimizer states of every reference rank.

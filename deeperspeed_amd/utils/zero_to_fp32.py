@@ -29,7 +29,8 @@ def get_optim_files(checkpoint_dir):
     return sorted(files, key=rank_of)
 
 
-REFERENCE_KEYS = {2: "single_partition_of_fp32_groups", 3: "fp32_flat_groups"}
+REFERENCE_KEYS = {1: "local_sub_partitions_of_fp32_groups", 2: "single_partition_of_fp32_groups",
+                  3: "fp32_flat_groups"}
 
 
 class _PickledScaler:
@@ -60,38 +61,76 @@ def parse_optim_states(files):
 
 
 def _parse_reference(sds, osds):
-    """Reference (DeepSpeed 0.3.15) checkpoint: contiguous per-group partitions, `param_shapes`
-    = every module parameter in order (reference zero_to_fp32.py:70-151; that script reads
-    only the first group / sub-group, this one all of them)."""
+    """Reference-layout (DeepSpeed 0.3.15) checkpoint -- written by the reference or by this
+    framework with checkpoint.zero_format = "reference".  Returns per-group lists of full fp32
+    parameters in optimizer-group order, and the names to give them.
+
+    The reference script (zero_to_fp32.py:70-151) reads only param group 0 and assumes it holds
+    every module parameter in module order.  Here every group is read; with several groups the
+    file must record which parameter is where (`dsa_group_param_names`), otherwise the groups
+    cannot be mapped onto `param_shapes` (module order) and this raises instead of guessing."""
     stage = osds[0].get("zero_stage", 0)
     if stage not in REFERENCE_KEYS:
-        raise ValueError(f"reference checkpoint of zero stage {stage}: only stage 2 and 3 can be consolidated")
+        raise ValueError(f"reference checkpoint of zero stage {stage} cannot be consolidated")
     world = osds[0].get("partition_count", len(osds))
     if world != len(osds):
         raise ValueError(f"Expected {world} optimizer shards, found {len(osds)}")
-    # every param group (stage 2) / sub-group (stage 3) of a rank, in order: consecutive
-    # parameters, so their concatenation is the rank's range of every parameter in turn
-    shards = [torch.cat([t.reshape(-1).float() for t in o[REFERENCE_KEYS[stage]]]) for o in osds]
     shapes = sds[0]["param_shapes"]
     shapes = shapes[0] if isinstance(shapes, list) else shapes
-    return stage, world, shards, None, shapes
-
-
-def _reference_state_dict(stage, world, shards, shapes):
-    out = OrderedDict()
-    flat = torch.cat(shards) if stage == 2 else None
-    off = 0
-    for name, shape in shapes.items():
-        n = 1
-        for d in shape:
-            n *= d
+    group_names = sds[0].get("dsa_group_param_names")
+    key = REFERENCE_KEYS[stage]
+    if stage == 3:
+        pgs = osds[0].get("optimizer_state_dict", {}).get("param_groups")
+        nflat = len(osds[0][key])
+        subs = [list(pg["params"]) for pg in pgs] if pgs and all("params" in pg for pg in pgs) else [list(range(nflat))]
+    else:
+        subs = [[g] for g in range(len(osds[0][key]))]
+    if group_names is None:
+        if len(subs) > 1:
+            raise ValueError(f"checkpoint has {len(subs)} optimizer param groups but does not record which "
+                             f"parameters each holds; param_shapes is in module order, so the groups cannot "
+                             f"be mapped back (save with checkpoint.zero_format=reference from this framework)")
+        group_names = [list(shapes.keys())]
+    out_groups = []
+    for G, names in enumerate(group_names):
+        numels = [_numel(shapes[n]) for n in names]
         if stage == 2:
-            out[name] = flat[off: off + n].view(*shape).clone()
-            off += n
+            flat = torch.cat([o[key][G].reshape(-1).float() for o in osds])
+        elif stage == 1:
+            intervals = len(osds[0][key][G])
+            flat = torch.cat([osds[r][key][G][c].reshape(-1).float() for c in range(intervals) for r in range(world)])
+        if stage in (1, 2):
+            params, off = [], 0
+            for n in numels:
+                params.append(flat[off: off + n])
+                off += n
+            if off > flat.numel():
+                raise ValueError(f"group {G}: shards hold {flat.numel()} elements, its parameters need {off}")
         else:
-            part, _ = zero3_partitioned_param_info(n, world)
-            out[name] = torch.cat([s[off: off + part] for s in shards])[:n].view(*shape).clone()
-            off += part
+            per_rank = [torch.cat([o[key][k].reshape(-1).float() for k in subs[G]]) for o in osds]
+            params, off = [], 0
+            for n in numels:
+                part, _ = zero3_partitioned_param_info(n, world)
+                params.append(torch.cat([t[off: off + part] for t in per_rank])[:n])
+                off += part
+        out_groups.append(list(zip(names, params)))
+    return stage, world, out_groups, None, shapes
+
+
+def _numel(shape):
+    n = 1
+    for d in shape:
+        n *= int(d)
+    return n
+
+
+def _reference_state_dict(groups, shapes):
+    found = {name: t for grp in groups for name, t in grp}
+    out = OrderedDict()
+    for name, shape in shapes.items():  # module order, like the reference's output
+        if name not in found:
+            raise ValueError(f"parameter {name} is in param_shapes but in no optimizer group")
+        out[name] = found[name].view(*shape).clone()
     return out
 
 
@@ -109,7 +148,7 @@ def convert_zero_chkpt_to_fp32_consolid_state_dict(checkpoint_dir, output_file):
     stage, world, shards, layout, param_shapes = parse_optim_states(get_optim_files(checkpoint_dir))
     print(f"Detected checkpoint of type zero stage {stage}, world_size: {world}")
     if layout is None:
-        state_dict = _reference_state_dict(stage, world, shards, param_shapes)
+        state_dict = _reference_state_dict(shards, param_shapes)
         print(f"Saving fp32 state dict to {output_file} ({len(state_dict)} tensors, reference layout)")
         torch.save(state_dict, output_file)
         return state_dict
@@ -131,6 +170,9 @@ def convert_zero_chkpt_to_fp32_consolid_state_dict(checkpoint_dir, output_file):
 
 
 def zero3_partitioned_param_info(unpartitioned_numel, world_size):
+    """(per-rank partition, padding) of one ZeRO-3 parameter.  The reference's version floors
+    the partition (zero_to_fp32.py:63-67) and mis-reads any parameter whose size is not a
+    multiple of the world size; the partition is ceil(numel / world) (partition_parameters.py)."""
     remainder = unpartitioned_numel % world_size
     padding_numel = (world_size - remainder) if remainder else 0
     partitioned_numel = (unpartitioned_numel + padding_numel) // world_size
