@@ -211,11 +211,16 @@ std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tenso
 Tensor sum_slices(Tensor part, Tensor out, bool accumulate) {
   check_dev(part, "sum_slices"); check_dev(out, "sum_slices");
   TORCH_CHECK(part.is_contiguous() && out.is_contiguous() && part.dim() >= 2, "sum_slices: contiguous part [S, ...]");
-  TORCH_CHECK(part.scalar_type() == at::kBFloat16 || part.scalar_type() == at::kHalf, "sum_slices: 16-bit partials");
-  TORCH_CHECK(out.scalar_type() == part.scalar_type() || out.scalar_type() == at::kFloat, "sum_slices: out dtype");
   const int64_t n = part.numel() / part.size(0);
   TORCH_CHECK(out.numel() == n && n % 8 == 0, "sum_slices: out must hold one slice (numel % 8 == 0)");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(part.device());
+  if (part.scalar_type() == at::kFloat) {  // fp32 partials, any out dtype
+    dsa::launch_sum_slices_f32(part.data_ptr<float>(), (int)part.size(0), n, out.data_ptr(), accumulate ? 1 : 0,
+                               dcode(out), cur_stream());
+    return out;
+  }
+  TORCH_CHECK(part.scalar_type() == at::kBFloat16 || part.scalar_type() == at::kHalf, "sum_slices: partial dtype");
+  TORCH_CHECK(out.scalar_type() == part.scalar_type() || out.scalar_type() == at::kFloat, "sum_slices: out dtype");
   dsa::launch_sum_slices(part.data_ptr(), (int)part.size(0), n, out.data_ptr(), out.scalar_type() == at::kFloat,
                          accumulate ? 1 : 0, dcode(part), cur_stream());
   return out;

@@ -31,6 +31,8 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -81,6 +83,7 @@ class Ring {
   }
 
   unsigned entries() const { return entries_; }
+  unsigned unsubmitted() const { return unsubmitted_; }
 
   // Queue one read/write SQE (not yet visible to the kernel until enter()).
   void prep(bool read, int fd, void* buf, unsigned len, int64_t off, uint64_t tag) {
@@ -204,6 +207,8 @@ class Worker {
   Worker(int64_t block, int64_t qd, bool single_submit, bool overlap)
       : block_(block), qd_(std::max<int64_t>(1, qd)), single_(single_submit), overlap_(overlap) {
     uring_ = io_uring_usable() && ring_.open_ring((unsigned)qd_);
+    // test hook: the N-th io_uring_enter of this worker fails as if the ring broke (EIO)
+    if (const char* e = std::getenv("DSA_AIO_INJECT_ENTER_FAIL")) inject_fail_ = std::atoi(e);
     thread_ = std::thread([this] { loop(); });
   }
   ~Worker() {
@@ -253,34 +258,41 @@ class Worker {
     return ok;
   }
 
-  // Pieces of `block_` bytes, up to qd_ in flight on this worker's ring.
+  // io_uring_enter, retrying transient failures: EINTR (inside Ring::enter), EAGAIN (no kernel
+  // request slots right now: back off) and EBUSY (completion queue full: return so the caller
+  // reaps, then enters again).  < 0 only for a ring that is really unusable.
+  int enter_retry(unsigned min_complete) {
+    if (inject_fail_ > 0 && --inject_fail_ == 0) {
+      errno = EIO;
+      return -1;
+    }
+    for (int attempt = 0;; ++attempt) {
+      const int r = ring_.enter(min_complete);
+      if (r >= 0) return r;
+      if (errno == EBUSY) return 0;
+      if (errno == EAGAIN && attempt < 2000) {
+        usleep(100);
+        continue;
+      }
+      return r;
+    }
+  }
+
+  // Pieces of `block_` bytes, up to qd_ in flight on this worker's ring.  Every SQE that was
+  // queued is completed (or provably never reached the kernel) before this returns: the SQEs
+  // point into the caller's pinned buffer, which Python may free or reuse right after.
   bool run_uring(int fd, const Slice& s) {
     const int64_t npieces = (s.len + block_ - 1) / block_;
     const int64_t depth = std::min<int64_t>(qd_, ring_.entries());
     int64_t next = 0, inflight = 0;
-    bool ok = true;
+    bool ok = true, ring_ok = true;
     auto submit_one = [&](int64_t k, int64_t done_bytes) {
       const int64_t lo = k * block_ + done_bytes;
       const int64_t len = std::min(block_, s.len - k * block_) - done_bytes;
       ring_.prep(s.req->read, fd, s.req->buf + s.off + lo, (unsigned)len, s.off + lo,
                  ((uint64_t)k << 32) | (uint64_t)done_bytes);
     };
-    std::vector<int64_t> progress(npieces, 0);
-    while ((next < npieces || inflight > 0) && ok) {
-      // fill free slots
-      int64_t to_fill = depth - inflight;
-      if (!overlap_ && inflight > 0) to_fill = 0;  // lock-step: drain the batch first
-      int64_t filled = 0;
-      while (filled < to_fill && next < npieces) {
-        submit_one(next++, 0);
-        ++filled;
-        ++inflight;
-        if (single_) {
-          if (ring_.enter(0) < 0) return false;
-        }
-      }
-      // submit the batch (block submit) and wait for at least one completion
-      if (ring_.enter(1) < 0) return false;
+    auto reap_all = [&] {
       uint64_t tag;
       int res;
       while (ring_.reap(&tag, &res)) {
@@ -292,26 +304,65 @@ class Worker {
           ok = false;
           continue;
         }
-        if (res < want) {  // short transfer: resubmit the remainder of this piece
+        if (res < want && ok && ring_ok) {  // short transfer: resubmit the remainder of this piece
           submit_one(k, done0 + res);
           ++inflight;
         }
       }
+    };
+    while ((next < npieces || inflight > 0) && ok && ring_ok) {
+      // fill free slots
+      int64_t to_fill = depth - inflight;
+      if (!overlap_ && inflight > 0) to_fill = 0;  // lock-step: drain the batch first
+      int64_t filled = 0;
+      while (filled < to_fill && next < npieces && ring_ok) {
+        submit_one(next++, 0);
+        ++filled;
+        ++inflight;
+        if (single_ && enter_retry(0) < 0) ring_ok = false;
+      }
+      // submit the batch (block submit) and wait for at least one completion
+      if (ring_ok && enter_retry(1) < 0) ring_ok = false;
+      reap_all();
     }
-    // never leave SQEs referencing the buffer behind on error
+    // drain: an error ends the transfer, never the wait for what is already in flight
+    const auto t0 = std::chrono::steady_clock::now();
+    bool warned = false;
     while (inflight > 0) {
-      if (ring_.enter(1) < 0) break;
-      uint64_t tag;
-      int res;
-      while (ring_.reap(&tag, &res)) --inflight;
+      if (ring_ok) {
+        if (enter_retry(1) < 0) ring_ok = false;
+      } else {
+        // SQEs the kernel never consumed can never complete: the ring is abandoned with them
+        inflight -= ring_.unsubmitted();
+        if (inflight <= 0) break;
+        usleep(1000);  // any syscall runs pending io_uring task work: completions still land
+      }
+      reap_all();
+      const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (!ring_ok && waited > 10.0 && !warned) {
+        std::fprintf(stderr, "[aio] io_uring failed with %lld request(s) in flight; waiting for them\n",
+                     (long long)inflight);
+        warned = true;
+      }
+      if (!ring_ok && waited > 300.0) {
+        // returning now would let the kernel write into a buffer its owner is about to free
+        std::fprintf(stderr, "[aio] %lld io_uring request(s) never completed; aborting\n", (long long)inflight);
+        std::abort();
+      }
     }
-    return ok;
+    if (!ring_ok) {
+      std::fprintf(stderr, "[aio] io_uring unusable on this worker (errno %d); falling back to pread/pwrite\n",
+                   errno);
+      uring_ = false;
+    }
+    return ok && ring_ok;
   }
 
   int64_t block_, qd_;
   bool single_, overlap_;
   Ring ring_;
-  bool uring_ = false;
+  std::atomic<bool> uring_{false};
+  int inject_fail_ = 0;
   std::thread thread_;
   std::mutex mu_;
   std::condition_variable cv_;

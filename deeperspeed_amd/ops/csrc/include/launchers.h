@@ -49,6 +49,7 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
 // y = a + b (+ c), n % (16 B / elem) == 0
 void launch_sum_slices(const void* part, int S, int64_t n, void* out, bool out_f32, int accum, int dt,
                        hipStream_t s);
+void launch_sum_slices_f32(const float* part, int S, int64_t n, void* out, int accum, int out_dt, hipStream_t s);
 void dropout_bwd_colsum_dims(int64_t rows, int C, int dt, int* cblocks, int* rchunks, int* prows);
 void launch_dropout_bwd_colsum(const void* dy, const uint8_t* mask, void* dx, void* db, float* partial, int64_t rows,
                                int C, float p, int dt, hipStream_t s);

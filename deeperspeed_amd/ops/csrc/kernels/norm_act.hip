@@ -646,6 +646,44 @@ void launch_sum_slices(const void* part, int S, int64_t n, void* out, bool out_f
                          accum));
 }
 
+// fp32 partials (the split-K GEMMs write fp32: no bf16 rounding before the sum): out[i] (+)=
+// sum_s part[s][i] with out in bf16 / f16 / fp32 (T).
+template <typename T>
+__global__ void __launch_bounds__(256) sum_slices_f32_kernel(const float* __restrict__ part, int S, int64_t n,
+                                                             T* __restrict__ out, int accum) {
+  constexpr int VN = Vec16<T>::N;
+  const int64_t nvec = n / VN;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    float acc[VN];
+    if (accum) {
+      Vec16<T>::load(out + i * VN, acc);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) acc[j] = 0.f;
+    }
+    for (int sl = 0; sl < S; ++sl) {
+      const float* src = part + sl * n + i * VN;
+#pragma unroll
+      for (int j = 0; j < VN; j += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src + j);
+        acc[j] += v.x; acc[j + 1] += v.y; acc[j + 2] += v.z; acc[j + 3] += v.w;
+      }
+    }
+    Vec16<T>::store(out + i * VN, acc);
+  }
+}
+
+void launch_sum_slices_f32(const float* part, int S, int64_t n, void* out, int accum, int out_dt, hipStream_t s) {
+  if (n <= 0) return;
+  const int vn = out_dt == kF32 ? 4 : 8;
+  int64_t g = (n / vn + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  DSA_DISPATCH_T(out_dt, T,
+    hipLaunchKernelGGL((sum_slices_f32_kernel<T>), dim3((unsigned)g), dim3(256), 0, s, part, S, n, (T*)out, accum));
+}
+
 void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s) {
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 15) / 16), dim3(256), 0, s, partial, R, C, (T*)out, accum));

@@ -184,14 +184,16 @@ def _split_k(g2, x2):
 
 
 def _wgrad_split(g2, x2, s, out=None):
-    """dy^T x as s strided-batched partial GEMMs over token slices, folded with fp32 accumulation
-    by one HIP pass into `out` (accumulated: the bound gradient) or into a fresh tensor."""
+    """dy^T x as s strided-batched partial GEMMs over token slices.  The partials are written
+    in fp32 (hipBLASLt accumulates in fp32 and stores it: no bf16 rounding per partial) and
+    folded by one HIP pass into `out` (accumulated: the bound gradient) or a fresh tensor."""
     M = g2.size(0)
-    part = torch.bmm(g2.view(s, M // s, g2.size(1)).transpose(1, 2), x2.view(s, M // s, x2.size(1)))
+    part = torch.bmm(g2.view(s, M // s, g2.size(1)).transpose(1, 2), x2.view(s, M // s, x2.size(1)),
+                     out_dtype=torch.float32)
     from . import native
     if out is not None:
         return native.hip_ops().sum_slices(part, out, True)
-    return native.hip_ops().sum_slices(part, torch.empty(part.shape[1:], dtype=part.dtype, device=part.device),
+    return native.hip_ops().sum_slices(part, torch.empty(part.shape[1:], dtype=g2.dtype, device=part.device),
                                        False)
 
 

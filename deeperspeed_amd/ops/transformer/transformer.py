@@ -198,12 +198,23 @@ class DeepSpeedTransformerFunction:
 
 class DeepSpeedTransformerLayer(nn.Module):
     layer_id = 0
+    _stochastic_warned = False
 
     def __init__(self, config, initial_weights=None, initial_biases=None):
         super().__init__()
         self.config = config
         self.config.layer_id = DeepSpeedTransformerLayer.layer_id
         DeepSpeedTransformerLayer.layer_id += 1
+        if getattr(config, "stochastic_mode", False) and not DeepSpeedTransformerLayer._stochastic_warned:
+            # reference: a separate -D__STOCHASTIC_MODE__ build that drops block barriers in the
+            # LayerNorm reductions and does dropout in half2 math (csrc/transformer/
+            # normalize_kernels.cu:64-191, dropout_kernels.cu:68-187).  Nothing here has a racy
+            # fast variant to switch to: the LayerNorms reduce within one wave (no barrier) and
+            # dropout is already 16-byte vectorised, so the deterministic kernels run.
+            import warnings
+            warnings.warn("DeepSpeedTransformerConfig.stochastic_mode=True: no separate stochastic kernels on "
+                          "MI355X; the deterministic kernels (already barrier-free per row) are used", stacklevel=2)
+            DeepSpeedTransformerLayer._stochastic_warned = True
         if self.config.local_rank >= 0 and torch.cuda.is_available():
             torch.cuda.set_device(self.config.local_rank)
         H, I = config.hidden_size, config.intermediate_size

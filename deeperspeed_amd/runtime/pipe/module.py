@@ -338,9 +338,13 @@ class PipelineModule(nn.Module):
         return os.path.join(ckpt_dir, name + "-model_states.pt")
 
     def _stateful(self):
+        """Positions that own a layer file: whatever forward calls, when it has a state dict
+        (reference pipe/module.py:546-567 walks forward_funcs the same way).  A TiedLayerSpec
+        position with a forward_fn calls a partial, so it writes no file: the tied module is
+        saved (and restored, then broadcast to its tie group) by the position that calls it
+        directly -- GPT-NeoX's tied embedding / LM head."""
         for local, slot in enumerate(self._slots):
-            obj = slot.module if slot.module is not None else (
-                self.tied_modules[slot.tie_key] if slot.tie_key is not None else slot.fn)
+            obj = slot.fn
             if hasattr(obj, "state_dict") and hasattr(obj, "load_state_dict"):
                 yield local, obj
 

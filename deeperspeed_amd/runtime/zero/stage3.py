@@ -521,12 +521,39 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                     owner[id(p)] = (gi, bi)
         self._module_buckets = {}
         for m in self.module.modules():
+            # a parameter registered in several modules (tied weights) is waited for by each
             keys = sorted({owner[id(p)] for p in m.parameters(recurse=False) if id(p) in owner})
             if keys:
                 self._module_buckets[m] = keys
                 self._handles.append(m.register_forward_pre_hook(self._wait_bucket_updates))
+        # Parameters whose owning module's forward never runs (read by a parent or a sibling:
+        # F.linear(x, self.embed.weight), parameter containers) have no hook of their own.  The
+        # first overlapped forward waits for the WHOLE step at the root and records which
+        # modules' pre-hooks fire; from then on the root waits for the buckets of every module
+        # that did not fire.  (A parameter read before its own module's forward in the same
+        # pass still needs synchronize_step(): waits are stream-ordered, so any read after the
+        # owner's forward is safe.)
+        self._fired = set()
+        self._uncovered = None  # bucket keys the root waits for; None = not calibrated yet
+        self._handles.append(self.module.register_forward_pre_hook(self._root_wait_uncovered))
+
+    def _root_wait_uncovered(self, module, inputs):
+        if not self._bucket_events or _in_backward():
+            return
+        cur = torch.cuda.current_stream()
+        if self._uncovered is None:
+            cur.wait_event(self._step_done_event)  # calibration pass: the whole step
+            self._calibrating = True
+            self._fired = set()
+            return
+        for key in self._uncovered:
+            ev = self._bucket_events.get(key)
+            if ev is not None:
+                cur.wait_event(ev)
 
     def _wait_bucket_updates(self, module, inputs):
+        if getattr(self, "_calibrating", False):
+            self._fired.add(module)
         if not self._bucket_events:
             return
         cur = torch.cuda.current_stream()
@@ -535,8 +562,16 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             if ev is not None:
                 cur.wait_event(ev)
 
+    def _finish_calibration(self):
+        if getattr(self, "_calibrating", False):
+            self._calibrating = False
+            self._uncovered = sorted({k for m, keys in self._module_buckets.items() if m not in self._fired
+                                      for k in keys})
+
     def synchronize_step(self):
         """Order the compute stream after an overlapped optimizer step (no host wait)."""
+        if self._overlap_step:
+            self._finish_calibration()
         if self._step_done is not None:
             torch.cuda.current_stream().wait_event(self._step_done)
             self._step_done = None
@@ -562,6 +597,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             self._grads_nonzero = False
         self._step_done = torch.cuda.Event()
         self._step_done.record(side)
+        self._step_done_event = self._step_done
 
     # ------------------------------------------------------------------ hooks
     def _register_hooks(self):

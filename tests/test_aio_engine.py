@@ -90,3 +90,23 @@ def test_aio_engine_reported_and_psync_fallback(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DSA_AIO_ENGINE="psync"),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
+def test_aio_uring_failure_drains_and_falls_back(tmp_path, monkeypatch):
+    """An io_uring_enter failure mid-transfer (injected: the 3rd enter of the worker returns
+    EIO) fails that request, waits for every SQE already in flight against the buffer, then
+    moves the worker to pread/pwrite: later requests still round-trip exactly."""
+    aio = _aio()
+    if aio.aio_engine() != "io_uring":
+        pytest.skip("io_uring not available in this container")
+    monkeypatch.setenv("DSA_AIO_INJECT_ENTER_FAIL", "3")
+    h = aio.aio_handle(block_size=1 << 12, queue_depth=8, single_submit=True, overlap_events=True, thread_count=1)
+    x = torch.randn(1 << 18)
+    assert h.sync_pwrite(x, str(tmp_path / "a.swp")) != 1  # the injected failure is reported
+    for i in range(3):
+        y = torch.randn(300001)
+        f = str(tmp_path / f"b{i}.swp")
+        assert h.sync_pwrite(y, f) == 1
+        z = torch.empty_like(y)
+        assert h.sync_pread(z, f) == 1
+        assert torch.equal(y, z)

@@ -119,3 +119,26 @@ def test_split_k_wgrad_matches_fp32(bound):
     assert (w.grad.float() - ref_w).abs().max().item() < 2e-2 * ref_w.abs().max().item()
     assert (x.grad.float() - ref_x).abs().max().item() < 2e-2 * ref_x.abs().max().item()
     assert (b.grad.float() - dy.float().sum(0)).abs().max().item() < 2e-2 * dy.float().sum(0).abs().max().item()
+
+
+@pytest.mark.gpu
+def test_split_k_wgrad_as_accurate_as_one_gemm():
+    """BERT-Large shape (8192 tokens, 1024x1024): the split-K weight gradient (fp32 partials,
+    fp32 fold) is as close to the fp32 reference as a single GEMM with fp32 accumulation --
+    both are one bf16 rounding of an fp32 sum."""
+    from deeperspeed_amd.ops import linear as L
+    torch.manual_seed(1)
+    dev = torch.device("cuda")
+    M, fin, fout = 8192, 1024, 1024
+    x = torch.randn(M, fin, device=dev, dtype=torch.bfloat16)
+    dy = torch.randn(M, fout, device=dev, dtype=torch.bfloat16)
+    s = L._split_k(dy, x)
+    assert s > 1
+    split = L._wgrad_split(dy, x, s)
+    single = dy.t() @ x
+    ref = dy.float().t() @ x.float()
+    e_split = ((split.float() - ref).norm() / ref.norm()).item()
+    e_single = ((single.float() - ref).norm() / ref.norm()).item()
+    assert e_split <= 1.05 * e_single + 1e-6, (e_split, e_single)
+    # the rounding floor of one bf16 cast of the exact result
+    assert e_split < 3e-3, e_split

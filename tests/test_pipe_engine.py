@@ -19,6 +19,11 @@ class _Act(nn.Module):
         return torch.relu(x)
 
 
+def _lm_head(module, x):
+    """GPT-NeoX-style tied output projection: the embedding module's weight, used differently."""
+    return torch.nn.functional.linear(x, module.weight)
+
+
 def _specs(tied=False):
     from deeperspeed_amd.runtime.pipe.module import LayerSpec, TiedLayerSpec
     specs = []
@@ -28,7 +33,9 @@ def _specs(tied=False):
         specs.append(LayerSpec(nn.Linear, HID, HID))
     for _ in range(4):
         specs += [LayerSpec(nn.Linear, HID, HID), LayerSpec(_Act)]
-    if tied:
+    if tied == "fn":
+        specs.append(TiedLayerSpec("emb", nn.Linear, HID, HID, forward_fn=_lm_head))
+    elif tied:
         specs.append(TiedLayerSpec("emb", nn.Linear, HID, HID))
     else:
         specs.append(LayerSpec(nn.Linear, HID, HID))
@@ -84,6 +91,9 @@ def _pipe_body(out_dir, num_stages, zero_stage, tied, steps=3, ga=4):
     if dist.get_rank() == 0:
         files = os.listdir(os.path.join(out_dir, "pipe"))
         assert any(f.startswith("layer_00") for f in files) and "mp_rank_00_model_states.pt" in files
+        last = len(_specs(tied)) - 1
+        # a tied position with a forward_fn owns no layer file (reference pipe/module.py:546-567)
+        assert any(f.startswith(f"layer_{last:02d}") for f in files) == (tied != "fn"), files
     engine2_model = PipelineModule(layers=_specs(tied), num_stages=num_stages, loss_fn=nn.CrossEntropyLoss(),
                                    partition_method="uniform", seed_layers=True, base_seed=99)
     e2, _, _, _ = ds.initialize(model=engine2_model, model_parameters=list(engine2_model.parameters()),
@@ -113,9 +123,10 @@ def test_pipeline_equivalence(tmp_path):
         assert torch.allclose(a["sd"][k], b["sd"][k], atol=3e-2, rtol=3e-2), k
 
 
-def test_pipeline_tied_layers(tmp_path):
-    run_distributed(_pipe_body, 2, str(tmp_path), 2, 0, True)
-    res = torch.load(os.path.join(tmp_path, "pp2_z0_tTrue.pt"), weights_only=True)
+@pytest.mark.parametrize("tied", [True, "fn"])
+def test_pipeline_tied_layers(tmp_path, tied):
+    run_distributed(_pipe_body, 2, str(tmp_path), 2, 0, tied)
+    res = torch.load(os.path.join(tmp_path, f"pp2_z0_t{tied}.pt"), weights_only=True)
     assert res["losses"][-1] < res["losses"][0]
 
 
