@@ -16,6 +16,8 @@ backward (overlapped), not by a separate pass after the schedule.
 
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -105,6 +107,15 @@ class PipelineEngine(DeepSpeedEngine):
         self.has_attention_mask = self.module.__class__.__name__ == "GPT2ModelPipe"
         self._recv_meta = None
         self._bw_count = 0
+        # asynchronous p2p (DSA_PIPE_ASYNC_P2P=0 restores blocking transfers): sends are left in
+        # flight across the following compute, receives are waited by their consumer, and a
+        # receive is posted ahead of the compute instruction before it when no other p2p op
+        # lies in between (the per-pair order both ranks issue stays identical: no deadlock)
+        self._async_p2p = os.environ.get("DSA_PIPE_ASYNC_P2P", "1") != "0"
+        self._pending_sends = []
+        self._recv_handles = {}
+        self._prefetched = {}
+        self.p2p_trace = None  # set to a list to record (instruction, sends in flight, receives in flight)
         # warm-up handshake between neighbours (establishes the RCCL p2p channels)
         if self.is_pipe_parallel:
             if is_even(self.stage_id):
@@ -338,6 +349,7 @@ class PipelineEngine(DeepSpeedEngine):
     def _exec_forward_pass(self, buffer_id):
         self.tput_timer.start()
         self.mem_status("BEFORE FWD", reset_max=True)
+        self._wait_recv(("act", buffer_id))
         inputs = self.pipe_buffers["inputs"][buffer_id]
         if isinstance(inputs, tuple):
             inputs = tuple(t.clone() if torch.is_tensor(t) else t for t in inputs)
@@ -405,6 +417,7 @@ class PipelineEngine(DeepSpeedEngine):
             if self.is_pipe_partitioned:
                 outputs = (self.pipe_buffers["output_tensors"][buffer_id],) + tuple(
                     outputs[2:] if isinstance(outputs, tuple) else ())
+            self._wait_recv(("grad", buffer_id))
             grads = self.grad_layer
             if isinstance(outputs, tuple):
                 out_t = [t for t in outputs if torch.is_tensor(t) and t.is_floating_point() and t.requires_grad]
@@ -492,7 +505,8 @@ class PipelineEngine(DeepSpeedEngine):
             self.first_output_send = False
             self._send_tensor_meta(outputs, self.next_stage)
         items = [t.detach() for t in self._as_list(outputs)]
-        p2p.send_many(items, self.next_stage, fp32_comm=self._fp32_comm())
+        self._track_send(p2p.send_many(items, self.next_stage, fp32_comm=self._fp32_comm(),
+                                       async_op=self._async_p2p))
         if self.wall_clock_breakdown():
             self.timers("pipe_send_output").stop()
 
@@ -506,7 +520,8 @@ class PipelineEngine(DeepSpeedEngine):
         for t in self._as_list(inputs):
             if torch.is_tensor(t) and t.is_floating_point() and t.requires_grad:
                 grads.append(t.grad if t.grad is not None else torch.zeros_like(t))
-        p2p.send_many(grads, self.prev_stage, fp32_comm=self._fp32_comm())
+        self._track_send(p2p.send_many(grads, self.prev_stage, fp32_comm=self._fp32_comm(),
+                                       async_op=self._async_p2p))
         self.pipe_buffers["inputs"][buffer_id] = None
         if self.wall_clock_breakdown():
             self.timers("pipe_send_grad").stop()
@@ -516,16 +531,17 @@ class PipelineEngine(DeepSpeedEngine):
             self.timers("pipe_recv_input").start()
         if self._recv_meta is None:
             self._recv_meta = self._recv_tensor_meta(self.prev_stage)
-        is_tuple, specs = self._recv_meta
-        bufs = []
-        for dt, shape in specs:
-            tgt = self.precision() if (dt == torch.float32 and self._fp32_comm()) else dt
-            bufs.append(torch.empty(shape, dtype=tgt, device=self.device))
-        p2p.recv_many(bufs, self.prev_stage, fp32_comm=self._fp32_comm())
+        is_tuple, _ = self._recv_meta
+        pre = self._prefetched.pop(("act", buffer_id), None)
+        handle, bufs = pre if pre is not None else self._post_recv_activations()
+        if handle is not None:
+            self._recv_handles[("act", buffer_id)] = handle
         for b in bufs:
             if b.is_floating_point():
                 b.requires_grad_(True)
         if self.has_attention_mask and is_tuple:
+            # the bool mask travels as a half tensor: converted once it has arrived
+            self._wait_recv(("act", buffer_id))
             bufs[-1] = bufs[-1].detach().bool()
         self.pipe_buffers["inputs"][buffer_id] = tuple(bufs) if is_tuple else bufs[0]
         if self.wall_clock_breakdown():
@@ -540,10 +556,96 @@ class PipelineEngine(DeepSpeedEngine):
                 outputs[2:] if isinstance(outputs, tuple) else ())
         targets = [t for t in self._as_list(outputs) if torch.is_tensor(t) and t.is_floating_point() and
                    t.requires_grad]
-        self.grad_layer = [torch.empty_like(t) for t in targets]
-        p2p.recv_many(self.grad_layer, self.next_stage, fp32_comm=self._fp32_comm())
+        pre = self._prefetched.pop(("grad", buffer_id), None)
+        if pre is not None:
+            handle, self.grad_layer = pre
+        else:
+            self.grad_layer = [torch.empty_like(t) for t in targets]
+            handle = p2p.recv_many(self.grad_layer, self.next_stage, fp32_comm=self._fp32_comm(),
+                                   async_op=self._async_p2p)
+        if handle is not None:
+            self._recv_handles[("grad", buffer_id)] = handle
         if self.wall_clock_breakdown():
             self.timers("pipe_recv_grad").stop()
+
+    # ------------------------------------------------------------------ asynchronous p2p
+    def _post_recv_activations(self):
+        _, specs = self._recv_meta
+        bufs = []
+        for dt, shape in specs:
+            tgt = self.precision() if (dt == torch.float32 and self._fp32_comm()) else dt
+            bufs.append(torch.empty(shape, dtype=tgt, device=self.device))
+        handle = p2p.recv_many(bufs, self.prev_stage, fp32_comm=self._fp32_comm(), async_op=self._async_p2p)
+        return handle, bufs
+
+    def _post_recv_grads(self, buffer_id):
+        outputs = self.pipe_buffers["outputs"][buffer_id]
+        if outputs is None:
+            return None
+        if self.is_pipe_partitioned:
+            outputs = (self.pipe_buffers["output_tensors"][buffer_id],) + tuple(
+                outputs[2:] if isinstance(outputs, tuple) else ())
+        targets = [t for t in self._as_list(outputs) if torch.is_tensor(t) and t.is_floating_point() and
+                   t.requires_grad]
+        bufs = [torch.empty_like(t) for t in targets]
+        return p2p.recv_many(bufs, self.next_stage, fp32_comm=self._fp32_comm(), async_op=True), bufs
+
+    def _prefetch(self, cmd):
+        """Post a later receive now (its buffers are installed by the instruction itself)."""
+        bid = cmd.kwargs["buffer_id"]
+        if isinstance(cmd, schedule.RecvActivation):
+            if self._recv_meta is not None and ("act", bid) not in self._prefetched:
+                self._prefetched[("act", bid)] = self._post_recv_activations()
+        elif isinstance(cmd, schedule.RecvGrad) and ("grad", bid) not in self._prefetched:
+            pre = self._post_recv_grads(bid)
+            if pre is not None:
+                self._prefetched[("grad", bid)] = pre
+
+    def _wait_recv(self, key):
+        h = self._recv_handles.pop(key, None)
+        if h is not None:
+            h.wait()
+
+    def _track_send(self, handle):
+        if handle is None or handle.done:
+            return
+        self._pending_sends.append(handle)
+        while len(self._pending_sends) > 4:  # bound the activations kept alive by transfers
+            self._pending_sends.pop(0).wait()
+
+    def _drain_p2p(self):
+        for h in self._pending_sends:
+            h.wait()
+        self._pending_sends = []
+        for h in self._recv_handles.values():
+            h.wait()
+        self._recv_handles = {}
+
+    @staticmethod
+    def _plan_prefetch(flat):
+        """{i: [j, ...]}: receive instruction j is posted just before compute instruction i.
+        A receive moves up over compute / data-loading instructions only, never over another
+        p2p op or a collective, so both ranks of every pair keep issuing their transfers in the
+        schedule's order."""
+        compute = (schedule.ForwardPass, schedule.BackwardPass)
+        movable = compute + (schedule.LoadMicroBatch,)
+        plan = {}
+        for j, cmd in enumerate(flat):
+            if not isinstance(cmd, (schedule.RecvActivation, schedule.RecvGrad)):
+                continue
+            k, target = j - 1, None
+            while k >= 0 and isinstance(flat[k], movable):
+                if isinstance(flat[k], compute):
+                    target = k
+                    break
+                k -= 1
+            if target is not None:
+                # a gradient receive needs its forward's outputs: never above that forward
+                if isinstance(cmd, schedule.RecvGrad) and isinstance(flat[target], schedule.ForwardPass) and \
+                        flat[target].kwargs["buffer_id"] == cmd.kwargs["buffer_id"]:
+                    continue
+                plan.setdefault(target, []).append(j)
+        return plan
 
     def _exec_optimizer_step(self, lr_kwargs=None):
         if self.wall_clock_breakdown():
@@ -632,12 +734,24 @@ class PipelineEngine(DeepSpeedEngine):
     def _exec_schedule(self, pipe_schedule):
         self._reserve_pipe_buffers(pipe_schedule.num_pipe_buffers())
         self._compute_loss = True
-        for step_cmds in pipe_schedule:
-            for cmd in step_cmds:
+        flat = [cmd for step_cmds in pipe_schedule for cmd in step_cmds]
+        plan = self._plan_prefetch(flat) if (self._async_p2p and self.is_pipe_parallel) else {}
+        try:
+            for i, cmd in enumerate(flat):
                 if type(cmd) not in self._INSTRUCTION_MAP:
                     raise RuntimeError(f"{self.__class__.__name__} does not understand instruction {repr(cmd)}")
+                if isinstance(cmd, schedule.OptimizerStep):
+                    self._drain_p2p()
+                for j in plan.get(i, ()):
+                    self._prefetch(flat[j])
+                if self.p2p_trace is not None and isinstance(cmd, (schedule.ForwardPass, schedule.BackwardPass)):
+                    self.p2p_trace.append((type(cmd).__name__, cmd.kwargs["buffer_id"], len(self._pending_sends),
+                                           len(self._prefetched) + len(self._recv_handles)))
                 self._exec_instr = self._INSTRUCTION_MAP[type(cmd)].__get__(self, PipelineEngine)
                 self._exec_instr(**cmd.kwargs)
+        finally:
+            self._drain_p2p()
+            self._prefetched = {}
 
 
 class PipelineError(Exception):

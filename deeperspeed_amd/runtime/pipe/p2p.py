@@ -77,12 +77,42 @@ def recv(tensor, src_stage, async_op=False, fp32_comm=False):
     return None
 
 
-def send_many(tensors: List[torch.Tensor], dest_stage, fp32_comm=False):
-    """Send a list of tensors in one batched call (one RCCL group launch)."""
+class P2PHandle:
+    """Outstanding batched transfer.  `wait()` makes the caller's stream wait for it (RCCL: a
+    stream dependency, no host block) and finishes an fp32-staged receive by casting into the
+    target buffers.  The handle keeps every tensor of the transfer alive until then."""
+
+    __slots__ = ("works", "keep", "staged", "done")
+
+    def __init__(self, works, keep=(), staged=()):
+        self.works = list(works or [])
+        self.keep = list(keep)
+        self.staged = list(staged)
+        self.done = False
+
+    def wait(self):
+        if self.done:
+            return
+        for w in self.works:
+            w.wait()
+        with torch.no_grad():  # targets may already be leaves that require grad
+            for t, b in self.staged:
+                t.copy_(b)
+        self.works, self.keep, self.staged = [], [], []
+        self.done = True
+
+
+_DONE = P2PHandle(())
+_DONE.done = True
+
+
+def send_many(tensors: List[torch.Tensor], dest_stage, fp32_comm=False, async_op=False):
+    """Send a list of tensors in one batched call (one RCCL group launch).  async_op=True
+    returns a P2PHandle to wait on later (the engine overlaps the transfer with compute)."""
     if tensors and _host_staged(tensors[0]):
         for t in tensors:
             send(t, dest_stage, fp32_comm=fp32_comm)
-        return
+        return _DONE if async_op else None
     ops = []
     peer = _peer(dest_stage)
     keep = []
@@ -90,16 +120,20 @@ def send_many(tensors: List[torch.Tensor], dest_stage, fp32_comm=False):
         x = t.float() if (fp32_comm and t.dtype == torch.bfloat16) else t.contiguous()
         keep.append(x)
         ops.append(dist.P2POp(dist.isend, x, peer))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+    h = P2PHandle(dist.batch_isend_irecv(ops) if ops else [], keep=keep)
+    if async_op:
+        return h
+    h.wait()
+    return None
 
 
-def recv_many(tensors: List[torch.Tensor], src_stage, fp32_comm=False):
+def recv_many(tensors: List[torch.Tensor], src_stage, fp32_comm=False, async_op=False):
+    """Receive into `tensors` (one batched call).  With fp32_comm the bf16 targets receive
+    through fp32 staging buffers, cast when the handle is waited: non-blocking too."""
     if tensors and _host_staged(tensors[0]):
         for t in tensors:
             recv(t, src_stage, fp32_comm=fp32_comm)
-        return
+        return _DONE if async_op else None
     ops, staged = [], []
     peer = _peer(src_stage)
     for t in tensors:
@@ -109,11 +143,11 @@ def recv_many(tensors: List[torch.Tensor], src_stage, fp32_comm=False):
             ops.append(dist.P2POp(dist.irecv, b, peer))
         else:
             ops.append(dist.P2POp(dist.irecv, t, peer))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-    for t, b in staged:
-        t.copy_(b)
+    h = P2PHandle(dist.batch_isend_irecv(ops) if ops else [], keep=tensors, staged=staged)
+    if async_op:
+        return h
+    h.wait()
+    return None
 
 
 def barrier(stage_id):
