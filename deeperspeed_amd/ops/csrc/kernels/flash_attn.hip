@@ -771,7 +771,11 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
 // index per value from the C layout, LSE/Delta broadcast from LDS), then
 //   dV^T += dO^T P   (A = dO^T via tr reads, B = P from registers)
 //   dK^T += Q^T dS   (A = Q^T via tr reads,  B = dS from registers)
-template <typename T, int D, bool CAUSAL, int EX = 0, bool FQ = false, bool BUF = true>
+// V3 (no dropout): the row constants enter as the MFMAs' initial accumulators -- S starts at
+// -LSE / scale and dP at -Delta (the "row constants as initial accumulator" idiom), read from
+// LDS as one float4 per 4 C-layout rows instead of 16 scalar broadcasts per 32-query half --
+// so P = exp2(S' * scale * log2e) and dS = P * dP' need no per-element subtraction.
+template <typename T, int D, bool CAUSAL, int EX = 0, bool FQ = false, bool BUF = true, bool V3 = false>
 __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint16_t* __restrict__ Q,
                                              const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                                              const uint16_t* __restrict__ dO, const float* __restrict__ LSE,
@@ -793,6 +797,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   const int64_t obase = o_base<D>(bh, S, onh);
   const float sl2 = scale * 1.4426950408889634f;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
+  constexpr bool INIT = V3 && !DROP;
   // this lane's key bias (log2 units) and which 16-bit half of a pair draw is its key's
   const float kb2 = (BIAS && mykey < S) ? ex.kbias[(bh / ex.hdiv) * (int64_t)S + mykey] * LOG2E : 0.f;
   const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
@@ -837,8 +842,8 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
     }
     if (threadIdx.x < BN2) {
       const int q = i0 + threadIdx.x;
-      st_l = q < S ? LSE[bh * (int64_t)S + q] * 1.4426950408889634f : 0.f;
-      st_d = q < S ? DELTA[bh * (int64_t)S + q] : 0.f;
+      st_l = q < S ? LSE[bh * (int64_t)S + q] * (INIT ? -1.f / scale : 1.4426950408889634f) : 0.f;
+      st_d = q < S ? (INIT ? -DELTA[bh * (int64_t)S + q] : DELTA[bh * (int64_t)S + q]) : 0.f;
     }
   };
   auto store_tile = [&](int stage) {
@@ -858,26 +863,66 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   for (int it = 0; it < ntiles; ++it) {
     const int i0 = qstart + it * BN2;
     const bool has_next = it + 1 < ntiles;
-    if (has_next) load_tile(i0 + BN2);
+    // V3 stages the next tile in two halves (Q during the first 32-query half, dO during the
+    // second) so only one half's registers are live at a time
+    if (has_next) {
+      if constexpr (V3) {
+        tile_load_buf<D>(qr, q_rs, i0 + BN2, (int)ldi);
+        if (threadIdx.x < BN2) {
+          const int q = i0 + BN2 + threadIdx.x;
+          // stored negated: they become the initial accumulators as they are
+          st_l = q < S ? LSE[bh * (int64_t)S + q] * (INIT ? -1.f / scale : 1.4426950408889634f) : 0.f;
+          st_d = q < S ? (INIT ? -DELTA[bh * (int64_t)S + q] : DELTA[bh * (int64_t)S + q]) : 0.f;
+        }
+      } else {
+        load_tile(i0 + BN2);
+      }
+    }
     const uint16_t* Qs = smem + (it & 1) * 2 * TS;
     const uint16_t* Os = Qs + TS;
     const float* lse_s = stats + (it & 1) * 2 * BN2;
     const float* del_s = lse_s + BN2;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      if constexpr (V3) {
+        if (t == 1 && has_next) {
+          const int nx = (it + 1) & 1;
+          tile_store<D>(smem + nx * 2 * TS, qr);
+          if (threadIdx.x < BN2) {
+            stats[nx * 2 * BN2 + threadIdx.x] = st_l;
+            stats[nx * 2 * BN2 + BN2 + threadIdx.x] = st_d;
+          }
+          tile_load_buf<D>(orr, o_rs, i0 + BN2, o_ld<D>(onh));
+        }
+      }
       f32x16 sacc, pacc;
+      if constexpr (INIT) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
+        for (int rb = 0; rb < 4; ++rb) {
+          const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 32 * t + 8 * rb + 4 * h);
+          const float4 d4 = *reinterpret_cast<const float4*>(del_s + 32 * t + 8 * rb + 4 * h);
+          sacc[4 * rb + 0] = l4.x; sacc[4 * rb + 1] = l4.y; sacc[4 * rb + 2] = l4.z; sacc[4 * rb + 3] = l4.w;
+          pacc[4 * rb + 0] = d4.x; pacc[4 * rb + 1] = d4.y; pacc[4 * rb + 2] = d4.z; pacc[4 * rb + 3] = d4.w;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
+      }
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
         sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), kf[ks], sacc);
         pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), vf[ks], pacc);
       }
       float pv[16], dsv[16];
+      if constexpr (INIT) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-        pv[r] = fast_exp2(fmaf(sacc[r], sl2, BIAS ? kb2 - lse_s[qi] : -lse_s[qi]));
+        for (int r = 0; r < 16; ++r) pv[r] = fast_exp2(BIAS ? fmaf(sacc[r], sl2, kb2) : sacc[r] * sl2);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          pv[r] = fast_exp2(fmaf(sacc[r], sl2, BIAS ? kb2 - lse_s[qi] : -lse_s[qi]));
+        }
       }
       // wave-uniform: ragged tail or a query of this sub-tile before the wave's last key
       if ((i0 + 32 * t + 32 > S) || (kb + 32 * w + 32 > S) || (CAUSAL && kb + 32 * w + 31 > i0 + 32 * t)) {
@@ -907,6 +952,9 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
           dsv[r] = pv[r] * fmaf(pacc[r], zr, -del_s[qi]);
           pv[r] *= zr;
         }
+      } else if constexpr (INIT) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dsv[r] = pv[r] * pacc[r];
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -935,6 +983,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
           const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * (D + 8) + col));
           dk[dt] = Mfma32<T>::run(s16x8{qx[0], qx[1], qx[2], qx[3], qy[0], qy[1], qy[2], qy[3]}, sf, dk[dt]);
         }
+        if constexpr (V3) __builtin_amdgcn_sched_barrier(0);  // bounds the tr-read hoisting: 0 spills vs 12
       }
     }
     if constexpr (FQ) {
@@ -974,7 +1023,12 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
         }
       }
     }
-    if (has_next) store_tile((it + 1) & 1);
+    if (has_next) {
+      if constexpr (V3)
+        tile_store<D>(smem + ((it + 1) & 1) * 2 * TS + TS, orr);
+      else
+        store_tile((it + 1) & 1);
+    }
     __syncthreads();
   }
   if (mykey < S) {
@@ -998,12 +1052,16 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
 // dQ: one wave = 32 queries (lane = query column of S^T = K Q^T); Q and dO are B operands in
 // registers; per 64-key tile: S^T, dP^T (A = K / V rows from LDS), dS^T in registers, then
 //   dQ^T += K^T dS^T   (A = K^T via tr reads, B = dS^T from registers)
-template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true>
+// FD (fused delta): the workgroup that owns a query row also forms its Delta = rowsum(dO * O)
+// from the dO fragments it holds anyway plus the matching O fragments, uses it, and stores it
+// for the dK/dV kernel that runs after it -- no separate Delta pass over dO and O.
+template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true, bool FD = false>
 __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_t* __restrict__ Q,
                                            const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                                            const uint16_t* __restrict__ dO, const float* __restrict__ LSE,
                                            const float* __restrict__ DELTA, uint16_t* __restrict__ dQ, int S,
-                                           float scale, int onh, const Extra& ex) {
+                                           float scale, int onh, const Extra& ex,
+                                           const uint16_t* __restrict__ O = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * (D + 8);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1029,7 +1087,28 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
                      : s16x8{};
   }
   const float lse2 = myq < S ? LSE[bh * (int64_t)S + myq] * 1.4426950408889634f : 0.f;
-  const float dl = myq < S ? DELTA[bh * (int64_t)S + myq] : 0.f;
+  float dl;
+  if constexpr (FD) {
+    // this lane holds half of its query's dO row (dims 16ks + 8h .. +7); the lane pair sums
+    float part = 0.f;
+    if (myq < S) {
+      const uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh) + 8 * h;
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) {
+        float a[8], b[8];
+        Vec16<T>::load(reinterpret_cast<const T*>(orow) + 16 * ks, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a[j] = __is_same(T, bf16_t) ? bf16_to_f32((uint16_t)of[ks][j]) : f16_to_f32((uint16_t)of[ks][j]);
+          part = fmaf(a[j], b[j], part);
+        }
+      }
+    }
+    dl = xhalf_sum(part);
+    if (myq < S && h == 0) const_cast<float*>(DELTA)[bh * (int64_t)S + myq] = dl;
+  } else {
+    dl = myq < S ? DELTA[bh * (int64_t)S + myq] : 0.f;
+  }
   f32x16 dq[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -1156,6 +1235,27 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh, Extra ex = Extra()) {
   dkdv_v2_body<T, D, CAUSAL, EX, false, BUF>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh,
                                              ex);
+}
+
+// dQ that also forms and stores Delta (runs before the dK/dV kernel, which reads it)
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) bwd_dq_v3_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const uint16_t* __restrict__ O, const float* __restrict__ LSE,
+    float* __restrict__ DELTA, uint16_t* __restrict__ dQ, int S, float scale, int onh) {
+  dq_v2_body<T, D, CAUSAL, 0, true, true>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh, Extra(),
+                                          O);
+}
+
+// dK/dV with the initial-accumulator row constants (V3); OCC = waves per SIMD the launch
+// bounds allow (1: the whole 512-register file per wave, no spills; 2: latency hiding)
+template <typename T, int D, bool CAUSAL, int OCC>
+__global__ void __launch_bounds__(256, OCC) bwd_dkdv_v3_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh) {
+  dkdv_v2_body<T, D, CAUSAL, 0, false, true, true>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S,
+                                                   scale, onh, Extra());
 }
 
 template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true>
@@ -1791,9 +1891,28 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
   static const bool merge = getenv("DSA_FLASH_BWD_MERGE") && getenv("DSA_FLASH_BWD_MERGE")[0] == '1';
   const bool v1 = v1_env && onh == 0;  // the v1 kernels read dO head-major only
   static const bool bufload = !(getenv("DSA_FA_BUFLOAD") && getenv("DSA_FA_BUFLOAD")[0] == '0');
+  static const int dkdv = getenv("DSA_FA_DKDV") ? atoi(getenv("DSA_FA_DKDV")) : 3;
   // the buffer resources of the dK/dV tile loads address one head's rows with 32-bit offsets
   if ((int64_t)S * (onh ? onh * D : D) * 2 >= (1LL << 31))
     throw std::runtime_error("flash bwd: S * row stride too large for 32-bit buffer offsets");
+  static const bool fdelta = !(getenv("DSA_FA_FUSED_DELTA") && getenv("DSA_FA_FUSED_DELTA")[0] == '0');
+  if (!v1 && !merge && bufload && fdelta && (dkdv == 3 || dkdv == 31)) {
+    // dQ (+ Delta) first, then dK/dV reading that Delta: two launches, no Delta pass
+    const unsigned g = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
+    FA_DISPATCH(dt, D, causal,
+      hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
+                         (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
+      if (dkdv == 3)
+        hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 2>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
+                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
+                           delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh);
+      else
+        hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 1>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
+                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
+                           delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh));
+    return;
+  }
   FA_DISPATCH(dt, D, causal,
     hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
                        (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
@@ -1803,8 +1922,19 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
                          delta, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, fa::Extra());
     } else if (!v1) {
-      // DSA_FA_BUFLOAD=0: the dK/dV kernel stages its Q / dO tiles with pointer loads (A/B only)
-      if (bufload)
+      // DSA_FA_DKDV: 3 (default) initial-accumulator row constants, 31 the same at one wave per
+      // SIMD, 2 the v2 body; DSA_FA_BUFLOAD=0: pointer-form Q / dO tile loads (A/B only)
+      if (dkdv == 3 && bufload)
+        hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 2>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
+                           dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
+                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
+                           scale, onh);
+      else if (dkdv == 31 && bufload)
+        hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 1>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
+                           dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
+                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
+                           scale, onh);
+      else if (bufload)
         hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC, 0, true>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
                            dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
                            (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
