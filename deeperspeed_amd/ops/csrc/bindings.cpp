@@ -852,8 +852,41 @@ static void check_lut(const Tensor& ptr, const Tensor& idx, const Tensor& msk, i
   TORCH_CHECK(idx.numel() == msk.numel(), what, ": index / mask length mismatch");
 }
 
+// Score biases of the fused sparse kernels: kbias [B, S] fp32 (key padding, additive), ebias a
+// 16-bit [B|1, H|1, S, S] view in q's dtype (relative position embedding + attention mask) whose
+// batch / head strides may be 0.  Returns (kbias ptr, ebias ptr, ez, eh, er).
+struct SBias {
+  const float* kb = nullptr;
+  const void* eb = nullptr;
+  int64_t ez = 0, eh = 0, er = 0;
+};
+static SBias sparse_bias(const OptT& kbias, const OptT& ebias, const Tensor& q) {
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2);
+  SBias b;
+  if (kbias.has_value()) {
+    check_dev(*kbias, "sparse_flash kbias");
+    TORCH_CHECK(kbias->scalar_type() == at::kFloat && kbias->is_contiguous() && kbias->dim() == 2 &&
+                    kbias->size(0) == B && kbias->size(1) == S, "sparse_flash: kbias must be contiguous fp32 [B, S]");
+    b.kb = kbias->data_ptr<float>();
+  }
+  if (ebias.has_value()) {
+    const Tensor& e = *ebias;
+    check_dev(e, "sparse_flash ebias");
+    TORCH_CHECK(e.scalar_type() == q.scalar_type() && e.dim() == 4 && (e.size(0) == B || e.size(0) == 1) &&
+                    (e.size(1) == H || e.size(1) == 1) && e.size(2) == S && e.size(3) == S && e.stride(3) == 1 &&
+                    e.stride(2) % 4 == 0, "sparse_flash: ebias must be [B|1, H|1, S, S] in q's dtype, unit key stride");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(e.data_ptr()) % 8 == 0, "sparse_flash: ebias must be 8-byte aligned");
+    b.eb = e.data_ptr();
+    b.ez = e.size(0) == 1 ? 0 : e.stride(0);
+    b.eh = e.size(1) == 1 ? 0 : e.stride(1);
+    b.er = e.stride(2);
+  }
+  return b;
+}
+
 std::vector<Tensor> sparse_flash_fwd(Tensor q, Tensor k, Tensor v, Tensor rowptr, Tensor cols, Tensor masks,
-                                     int64_t Hl, bool causal, double scale, int64_t shift, bool out_bshd) {
+                                     int64_t Hl, bool causal, double scale, int64_t shift, bool out_bshd,
+                                     OptT kbias, OptT ebias) {
   check_dev(q, "q"); check_dev(k, "k"); check_dev(v, "v");
   TORCH_CHECK(q.dim() == 4 && q.sizes() == k.sizes() && q.sizes() == v.sizes(), "sparse_flash: q/k/v shape mismatch");
   TORCH_CHECK(q.scalar_type() != at::kFloat && q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(),
@@ -868,11 +901,12 @@ std::vector<Tensor> sparse_flash_fwd(Tensor q, Tensor k, Tensor v, Tensor rowptr
   c10::hip::HIPGuardMasqueradingAsCUDA guard(q.device());
   Tensor o = out_bshd ? at::empty({B, S, H, D}, q.options()) : at::empty_like(q);
   Tensor lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  const SBias sb = sparse_bias(kbias, ebias, q);
   dsa::launch_sparse_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                                rowptr.data_ptr<int>(), cols.data_ptr<int>(),
                                reinterpret_cast<const uint32_t*>(masks.data_ptr<int>()), (int)(B * H), (int)H, (int)Hl,
                                (int)S, (int)D, causal, (float)scale, (int)shift, dcode(q), cur_stream(),
-                               out_bshd ? (int)H : 0);
+                               out_bshd ? (int)H : 0, sb.kb, sb.eb, sb.ez, sb.eh, sb.er);
   return {o, lse};
 }
 
@@ -881,7 +915,8 @@ std::vector<Tensor> sparse_flash_fwd(Tensor q, Tensor k, Tensor v, Tensor rowptr
 // nslot = partial slots per (batch, head).
 std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor rowptr,
                                      Tensor cols, Tensor masks, Tensor rows, Tensor masks_t, Tensor tasks, Tensor fin,
-                                     int64_t nslot, int64_t Hl, bool causal, double scale, int64_t shift, bool o_bshd) {
+                                     int64_t nslot, int64_t Hl, bool causal, double scale, int64_t shift, bool o_bshd,
+                                     OptT kbias, OptT ebias) {
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
   for (auto* t : {&q, &k, &v}) {
     check_dev(*t, "sparse_flash_bwd");
@@ -910,6 +945,7 @@ std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, 
   Tensor dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
   Tensor delta = at::empty_like(lse);
   Tensor ws = at::empty({std::max<int64_t>(1, B * H * nslot * 2 * 64 * D)}, q.options().dtype(at::kFloat));
+  const SBias sb = sparse_bias(kbias, ebias, q);
   dsa::launch_sparse_flash_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
                                lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
                                dv.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(),
@@ -917,7 +953,7 @@ std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, 
                                reinterpret_cast<const uint32_t*>(masks_t.data_ptr<int>()), tasks.data_ptr<int>(),
                                (int)ntask, fin.data_ptr<int>(), (int)nfin, ws.data_ptr<float>(), (int)nslot,
                                (int)(B * H), (int)H, (int)Hl, (int)S, (int)D, causal, (float)scale, (int)shift,
-                               dcode(q), cur_stream(), o_bshd ? (int)H : 0);
+                               dcode(q), cur_stream(), o_bshd ? (int)H : 0, sb.kb, sb.eb, sb.ez, sb.eh, sb.er);
   return {dq, dk, dv};
 }
 

@@ -1346,12 +1346,45 @@ __device__ __forceinline__ uint32_t full_mask(int nsub_l2) {
   return bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
 }
 
-template <typename T, int D, bool CAUSAL, bool RP>
-__global__ void __launch_bounds__(128, RP ? 2 : 3) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+// Score biases of the reference sparse softmax (softmax_fwd.tr:46-129), compiled in by SX = 1:
+//   kbias [Z, S] fp32: the key-padding mask (additive; 'mul' masks arrive as 0 / -inf), z = bh / H
+//   ebias [Z|1, H|1, S, S] in the input dtype: relative position embedding + attention mask
+//         (additive, pre-summed on the host), element (bh, q, k) at (bh / H) * ez + (bh % H) * eh
+//         + q * er + k (ez / eh = 0 broadcast)
+// either pointer may be null.  Scores enter the softmax as s * scale + kbias + ebias.
+struct SExtra {
+  const float* kbias = nullptr;
+  const uint16_t* ebias = nullptr;
+  int64_t ez = 0, eh = 0, er = 0;
+};
+template <typename T> __device__ __forceinline__ float h16f(uint16_t v);
+template <> __device__ __forceinline__ float h16f<bf16_t>(uint16_t v) { return bf16_to_f32(v); }
+template <> __device__ __forceinline__ float h16f<f16_t>(uint16_t v) { return f16_to_f32(v); }
+__device__ __forceinline__ const uint16_t* ebias_head(const SExtra& sx, int64_t bh, int H) {
+  return sx.ebias + (bh / H) * sx.ez + (bh % H) * sx.eh;
+}
+// log2-domain bias of 4 consecutive keys key0..key0+3 of query row `q` (fwd / dQ layouts)
+template <typename T, int SX>
+__device__ __forceinline__ float4 sbias4(const SExtra& sx, const uint16_t* eh, int64_t z, int S, int q, int key0) {
+  float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (SX != 0) {
+    if (sx.kbias) b = *reinterpret_cast<const float4*>(sx.kbias + z * S + key0);
+    if (sx.ebias) {
+      const ushort4 e = *reinterpret_cast<const ushort4*>(eh + (int64_t)q * sx.er + key0);
+      b.x += h16f<T>(e.x); b.y += h16f<T>(e.y); b.z += h16f<T>(e.z); b.w += h16f<T>(e.w);
+    }
+    b.x *= LOG2E; b.y *= LOG2E; b.z *= LOG2E; b.w *= LOG2E;
+  }
+  return b;
+}
+
+template <typename T, int D, bool CAUSAL, bool RP, int SX = 0>
+__global__ void __launch_bounds__(128, RP ? 1 : 3) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                       const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                       float* __restrict__ LSE, const int* __restrict__ rowptr,
                                                       const int* __restrict__ cols, const uint32_t* __restrict__ masks,
-                                                      int S, float scale, int onh, int H, int Hl, int shift) {
+                                                      int S, float scale, int onh, int H, int Hl, int shift,
+                                                      SExtra sx = SExtra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = STILE * (D + 8);
   constexpr int NT = 128;
@@ -1434,11 +1467,24 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sfwd_kernel(const uint16_t* _
           if (!((mask >> bit) & 1u) || (CAUSAL && j0 + kc > myq)) sv[16 * t + r] = -INFINITY;
         }
     }
+    if constexpr (SX != 0) {  // scores to the log2 domain with the biases folded in
+      const uint16_t* ehd = sx.ebias ? ebias_head(sx, bh, H) : nullptr;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const float4 b4 = sbias4<T, SX>(sx, ehd, bh / H, S, myq, j0 + 32 * t + 8 * rb + 4 * h);
+          float* s4 = sv + 16 * t + 4 * rb;
+          s4[0] = fmaf(s4[0], sl2, b4.x); s4[1] = fmaf(s4[1], sl2, b4.y);
+          s4[2] = fmaf(s4[2], sl2, b4.z); s4[3] = fmaf(s4[3], sl2, b4.w);
+        }
+    }
+    const float a2 = SX != 0 ? 1.f : sl2;
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 32; ++i) mx = fmaxf(mx, sv[i]);
     mx = xhalf_max(mx);
-    const float mt = mx * sl2;
+    const float mt = mx * a2;
     if (__any(mt > m + LAZY_TH)) {
       const float mn = fmaxf(m, mt);
       const float alpha = fast_exp2(m - ((mn == -INFINITY) ? 0.f : mn));
@@ -1453,8 +1499,8 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sfwd_kernel(const uint16_t* _
     float ps = 0.f, ps1 = 0.f;
 #pragma unroll
     for (int i = 0; i < 32; i += 2) {
-      sv[i] = fast_exp2(fmaf(sv[i], sl2, -mu));
-      sv[i + 1] = fast_exp2(fmaf(sv[i + 1], sl2, -mu));
+      sv[i] = fast_exp2(fmaf(sv[i], a2, -mu));
+      sv[i + 1] = fast_exp2(fmaf(sv[i + 1], a2, -mu));
       ps += sv[i];
       ps1 += sv[i + 1];
     }
@@ -1495,12 +1541,15 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sfwd_kernel(const uint16_t* _
       v4.w = to16<T>(o[dt][4 * rb + 3] * inv);
       *reinterpret_cast<ushort4*>(orow + 32 * dt + 8 * rb + 4 * h) = v4;
     }
-  if (h == 0) LSE[bh * (int64_t)S + myq] = (l > 0.f) ? (m + log2f(l)) * 0.6931471805599453f : -INFINITY;
+  // a row with no unmasked key stores +inf: the backward then recomputes P = 0 for it
+  if (h == 0) LSE[bh * (int64_t)S + myq] = (l > 0.f) ? (m + log2f(l)) * 0.6931471805599453f : INFINITY;
 }
 
 // dK / dV over the query tiles listed for this key tile (transposed LUT)
-template <typename T, int D, bool CAUSAL, bool RP>
-__global__ void __launch_bounds__(128, RP ? 2 : 3) sdkdv_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+// Row constants enter as the MFMAs' initial accumulators (S at -LSE / scale, dP at -Delta,
+// stored negated in LDS and read as one float4 per 4 C-layout rows), as in dkdv_v2_body V3.
+template <typename T, int D, bool CAUSAL, bool RP, int SX = 0>
+__global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                        const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
                                                        const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                        uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
@@ -1508,7 +1557,7 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sdkdv_kernel(const uint16_t* 
                                                        const uint32_t* __restrict__ masks,
                                                        const int4* __restrict__ tasks, int ntask,
                                                        float* __restrict__ ws, int nslot, int S, float scale, int onh,
-                                                       int H, int Hl, int shift) {
+                                                       int H, int Hl, int shift, SExtra sx = SExtra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = STILE * (D + 8);
   constexpr int NT = 128;
@@ -1552,10 +1601,17 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sdkdv_kernel(const uint16_t* 
     stile_load<D, NT>(qr, Q + base, i0, S);
     stile_load<D, NT>(orr, dO + obase, i0, S, o_ld<D>(onh));
     if (threadIdx.x < STILE) {
-      st_l = LSE[bh * (int64_t)S + i0 + threadIdx.x] * 1.4426950408889634f;
-      st_d = DELTA[bh * (int64_t)S + i0 + threadIdx.x];
+      st_l = LSE[bh * (int64_t)S + i0 + threadIdx.x] * (-1.f / scale);
+      st_d = -DELTA[bh * (int64_t)S + i0 + threadIdx.x];
     }
   };
+  // this lane's key: key-padding bias (log2 units) and its column of the element bias
+  float kb2 = 0.f;
+  const uint16_t* ecol = nullptr;
+  if constexpr (SX != 0) {
+    if (sx.kbias) kb2 = sx.kbias[(bh / H) * (int64_t)S + mykey] * LOG2E;
+    if (sx.ebias) ecol = ebias_head(sx, bh, H) + mykey;
+  }
   auto store_tile = [&](int stage) {
     uint16_t* b = smem + stage * 2 * TS;
     stile_store<D, NT>(b, qr);
@@ -1590,17 +1646,28 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sdkdv_kernel(const uint16_t* 
     for (int t = 0; t < 2; ++t) {
       f32x16 sacc, pacc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
+      for (int rb = 0; rb < 4; ++rb) {
+        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 32 * t + 8 * rb + 4 * h);
+        const float4 d4 = *reinterpret_cast<const float4*>(del_s + 32 * t + 8 * rb + 4 * h);
+        sacc[4 * rb + 0] = l4.x; sacc[4 * rb + 1] = l4.y; sacc[4 * rb + 2] = l4.z; sacc[4 * rb + 3] = l4.w;
+        pacc[4 * rb + 0] = d4.x; pacc[4 * rb + 1] = d4.y; pacc[4 * rb + 2] = d4.z; pacc[4 * rb + 3] = d4.w;
+      }
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
         sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), kf[ks], sacc);
         pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), vf[ks], pacc);
       }
       float pv[16], dsv[16];
+      if constexpr (SX != 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-        pv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse_s[qi]));
+        for (int r = 0; r < 16; ++r) {
+          float b = kb2;
+          if (ecol) b += h16f<T>(ecol[(int64_t)(i0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3)) * sx.er]) * LOG2E;
+          pv[r] = fast_exp2(fmaf(sacc[r], sl2, b));
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pv[r] = fast_exp2(sacc[r] * sl2);
       }
       if (mask != full || (CAUSAL && kt * STILE + 32 * w + 31 > i0 + 32 * t)) {
 #pragma unroll
@@ -1611,10 +1678,7 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sdkdv_kernel(const uint16_t* 
         }
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-        dsv[r] = pv[r] * (pacc[r] - del_s[qi]);
-      }
+      for (int r = 0; r < 16; ++r) dsv[r] = pv[r] * pacc[r];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ks = 2 * t + kk;
@@ -1671,17 +1735,25 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sdkdv_kernel(const uint16_t* 
 
 // Sum the fp32 partials of each split key tile and write its bf16/fp16 dK (scaled) and dV.
 // fin[lh][j] = (key tile, first slot, chunk count, -), padded with key tile -1.
+// One workgroup per 256 float4 granules of one split key tile (SDKDV_FPARTS per tile): the
+// partial sums spread over the whole chip instead of one workgroup per tile.
+template <int D> constexpr int sdkdv_fparts() { return (2 * STILE * D / 4 + 255) / 256; }
 template <typename T, int D>
 __global__ void __launch_bounds__(256) sdkdv_finish_kernel(const float* __restrict__ ws, const int4* __restrict__ fin,
                                                            int nfin, int nslot, uint16_t* __restrict__ dK,
                                                            uint16_t* __restrict__ dV, int S, float scale, int H,
                                                            int Hl) {
-  const int64_t bh = blockIdx.x / nfin;
+  constexpr int NP = sdkdv_fparts<D>();
+  const int part = blockIdx.x % NP;
+  const int tile = blockIdx.x / NP;
+  const int64_t bh = tile / nfin;
   const int lh = Hl == 1 ? 0 : (int)(bh % H);
-  const int4 f = fin[lh * nfin + (blockIdx.x - (int)bh * nfin)];
+  const int4 f = fin[lh * nfin + (tile - (int)bh * nfin)];
   if (f.x < 0) return;
   const int64_t base = bh * (int64_t)S * D;
-  for (int i = threadIdx.x; i < 2 * STILE * D / 4; i += blockDim.x) {  // float4 granules of dK | dV
+  {
+    const int i = part * 256 + threadIdx.x;  // float4 granule of dK | dV
+    if (i >= 2 * STILE * D / 4) return;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int c = 0; c < f.z; ++c) {
       const float4 v = reinterpret_cast<const float4*>(ws + (bh * nslot + f.y + c) * 2 * STILE * (int64_t)D)[i];
@@ -1699,13 +1771,15 @@ __global__ void __launch_bounds__(256) sdkdv_finish_kernel(const float* __restri
 }
 
 // dQ over the key tiles listed for this query tile (forward LUT)
-template <typename T, int D, bool CAUSAL, bool RP>
-__global__ void __launch_bounds__(128, RP ? 2 : 3) sdq_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+// FD: also forms Delta = rowsum(dO * O) for its rows and stores it (runs before sdkdv_kernel)
+template <typename T, int D, bool CAUSAL, bool RP, int SX = 0, bool FD = false>
+__global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                      const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                      uint16_t* __restrict__ dQ, const int* __restrict__ rowptr,
                                                      const int* __restrict__ cols, const uint32_t* __restrict__ masks,
-                                                     int S, float scale, int onh, int H, int Hl, int shift) {
+                                                     int S, float scale, int onh, int H, int Hl, int shift,
+                                                     SExtra sx = SExtra(), const uint16_t* __restrict__ O = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = STILE * (D + 8);
   constexpr int NT = 128;
@@ -1733,7 +1807,23 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sdq_kernel(const uint16_t* __
     of[ks] = *reinterpret_cast<const s16x8*>(dO + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh) + 16 * ks + 8 * h);
   }
   const float lse2 = LSE[bh * (int64_t)S + myq] * 1.4426950408889634f;
-  const float dl = DELTA[bh * (int64_t)S + myq];
+  float dl;
+  if constexpr (FD) {
+    float part = 0.f;
+    const uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh) + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      float b[8];
+      Vec16<T>::load(reinterpret_cast<const T*>(orow) + 16 * ks, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part = fmaf(h16f<T>((uint16_t)of[ks][j]), b[j], part);
+    }
+    dl = xhalf_sum(part);
+    if (h == 0) const_cast<float*>(DELTA)[bh * (int64_t)S + myq] = dl;
+  } else {
+    dl = DELTA[bh * (int64_t)S + myq];
+  }
+  const uint16_t* ehd = (SX != 0 && sx.ebias) ? ebias_head(sx, bh, H) : nullptr;
   f32x16 dq[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -1778,8 +1868,19 @@ __global__ void __launch_bounds__(128, RP ? 2 : 3) sdq_kernel(const uint16_t* __
         pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), of[ks], pacc);
       }
       float dsv[16];
+      if constexpr (SX != 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dsv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse2));
+        for (int rb = 0; rb < 4; ++rb) {
+          const float4 b4 = sbias4<T, SX>(sx, ehd, bh / H, S, myq, j0 + 32 * t + 8 * rb + 4 * h);
+          dsv[4 * rb + 0] = fast_exp2(fmaf(sacc[4 * rb + 0], sl2, b4.x - lse2));
+          dsv[4 * rb + 1] = fast_exp2(fmaf(sacc[4 * rb + 1], sl2, b4.y - lse2));
+          dsv[4 * rb + 2] = fast_exp2(fmaf(sacc[4 * rb + 2], sl2, b4.z - lse2));
+          dsv[4 * rb + 3] = fast_exp2(fmaf(sacc[4 * rb + 3], sl2, b4.w - lse2));
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dsv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse2));
+      }
       if (mask != full || (CAUSAL && j0 + 32 * t + 31 > qt * STILE + 32 * w)) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -2062,57 +2163,82 @@ static bool sparse_rp() {
   return rp;
 }
 
+// kbias / ebias (SExtra): null when absent; either one selects the SX = 1 kernels
 void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
                              const int* cols, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
-                             float scale, int shift, int dt, hipStream_t s, int onh) {
+                             float scale, int shift, int dt, hipStream_t s, int onh, const float* kbias,
+                             const void* ebias, int64_t ez, int64_t eh, int64_t er) {
   const unsigned grid = (unsigned)(BH * (S / fa::STILE));
   const bool rp = sparse_rp();
+  fa::SExtra sx;
+  sx.kbias = kbias;
+  sx.ebias = (const uint16_t*)ebias;
+  sx.ez = ez; sx.eh = eh; sx.er = er;
+  const bool ex = kbias || ebias;
   FA_DISPATCH(dt, D, causal,
-    if (rp)
+    if (ex)
+      hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, true, 1>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
+                         masks, S, scale, onh, H, Hl, shift, sx);
+    else if (rp)
       hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
-                         masks, S, scale, onh, H, Hl, shift);
+                         masks, S, scale, onh, H, Hl, shift, fa::SExtra());
     else
       hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, false>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(false), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
-                         masks, S, scale, onh, H, Hl, shift));
+                         masks, S, scale, onh, H, Hl, shift, fa::SExtra()));
 }
 
+// Backward: dQ first (it also forms Delta for its rows), then dK / dV reading that Delta, then the
+// sums of split key tiles' partials.
 void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
                              const float* lse, float* delta, void* dq, void* dk, void* dv, const int* rowptr,
                              const int* cols, const uint32_t* masks, const int* rows, const uint32_t* masks_t,
                              const int* tasks, int ntask, const int* fin, int nfin, float* ws, int nslot, int BH,
                              int H, int Hl, int S, int D, bool causal, float scale, int shift, int dt, hipStream_t s,
-                             int onh) {
-  const int64_t nrows = (int64_t)BH * S;
+                             int onh, const float* kbias, const void* ebias, int64_t ez, int64_t eh, int64_t er) {
   const unsigned grid = (unsigned)(BH * (S / fa::STILE));
   const unsigned tgrid = (unsigned)(BH * ntask);
   const bool rp = sparse_rp();
   const int4* tk = reinterpret_cast<const int4*>(tasks);
+  fa::SExtra sx;
+  sx.kbias = kbias;
+  sx.ebias = (const uint16_t*)ebias;
+  sx.ez = ez; sx.eh = eh; sx.er = er;
+  const bool ex = kbias || ebias;
   FA_DISPATCH(dt, D, causal,
-    hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((nrows * 8 + 255) / 256)), dim3(256), 0, s,
-                       (const uint16_t*)dout, (const uint16_t*)o, delta, nrows, S, onh);
-    if (rp) {
+    if (ex) {
+      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true, 1, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, sx, (const uint16_t*)o);
+      hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, true, 1>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
+                         shift, sx);
+    } else if (rp) {
+      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true, 0, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, fa::SExtra(),
+                         (const uint16_t*)o);
       hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, true>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                          (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
-                         shift);
-      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
-                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift);
+                         shift, fa::SExtra());
     } else {
+      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, false, 0, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(false),
+                         s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
+                         delta, (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, fa::SExtra(),
+                         (const uint16_t*)o);
       hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, false>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(false), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                          (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
-                         shift);
-      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, false>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(false), s,
-                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift);
+                         shift, fa::SExtra());
     }
     if (nfin > 0)
-      hipLaunchKernelGGL((fa::sdkdv_finish_kernel<T, DD>), dim3((unsigned)(BH * nfin)), dim3(256), 0, s, ws,
-                         reinterpret_cast<const int4*>(fin), nfin, nslot, (uint16_t*)dk, (uint16_t*)dv, S, scale, H,
-                         Hl));
+      hipLaunchKernelGGL((fa::sdkdv_finish_kernel<T, DD>), dim3((unsigned)(BH * nfin * fa::sdkdv_fparts<DD>())),
+                         dim3(256), 0, s, ws, reinterpret_cast<const int4*>(fin), nfin, nslot, (uint16_t*)dk,
+                         (uint16_t*)dv, S, scale, H, Hl));
 }
 
 }  // namespace dsa

@@ -11,7 +11,10 @@ softmax); the backward is the same walk for dQ and the transposed walk for dK / 
 per layout head, a CSR list of active key tiles per query tile and the transposed list, each
 entry with a bitmask of the active layout sub-blocks when the layout block is smaller than the
 64-element tile (block 16 -> 4x4 sub-blocks, 32 -> 2x2).  Tiles above the diagonal are dropped
-for causal attention.  Shapes outside the kernel's domain (S % 64, head dim, masks / RPE) fall
+for causal attention.  The reference softmax's score terms run inside the same kernels
+(`score_biases`): the key-padding mask as a per-key fp32 bias, the relative position embedding
+and the attention mask pre-summed into one [B|1, H|1, S, S] element bias read only on active
+tiles ('mul' masks become 0 / -inf).  Shapes outside the kernel's domain (S % 64, head dim) fall
 back to the SDD / softmax / DSD path.
 """
 
@@ -129,17 +132,53 @@ def supported(q: torch.Tensor, lut: Optional[SparseFlashLUT]) -> bool:
     return True
 
 
+def _as4(t):
+    while t.dim() < 4:
+        t = t.unsqueeze(0)
+    return t
+
+
+def _additive(mask: torch.Tensor, mode: str) -> torch.Tensor:
+    m = mask.float()
+    return torch.where(m == 0, float("-inf"), 0.0) if mode == "mul" else m
+
+
+def score_biases(q, rpe=None, key_padding_mask=None, attn_mask=None, key_padding_mask_mode="add",
+                 attn_mask_mode="add"):
+    """(kbias, ebias) for the fused kernels from the reference Softmax's optional terms
+    (softmax.py:230-315): kbias = key-padding mask [B, S] fp32, ebias = rpe [Z|1, H|1, S, S] +
+    attention mask [S, S] in q's dtype (broadcast dims kept as stride-0 views)."""
+    B, H, S, _ = q.shape
+    kbias = ebias = None
+    if key_padding_mask is not None:
+        kp = key_padding_mask.reshape(-1, S) if key_padding_mask.dim() != 2 else key_padding_mask
+        kbias = _additive(kp, key_padding_mask_mode).expand(B, S).contiguous()
+    if rpe is not None or attn_mask is not None:
+        e = None
+        if rpe is not None:
+            e = _as4(rpe).float()
+        if attn_mask is not None:
+            a = _additive(attn_mask.reshape(S, S), attn_mask_mode)[None, None]
+            e = a if e is None else e + a
+        if e.shape[0] not in (1, B) or e.shape[1] not in (1, H) or tuple(e.shape[2:]) != (S, S):
+            raise ValueError(f"relative position embedding / attention mask of shape {tuple(e.shape)} does not "
+                             f"broadcast to [{B}, {H}, {S}, {S}]")
+        ebias = e.to(q.dtype).contiguous()
+    return kbias, ebias
+
+
 class _SparseFlash(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, lut, scale, out_bshd):
+    def forward(ctx, q, k, v, lut, scale, out_bshd, kbias, ebias):
         from .. import native
         ops = native.hip_ops()
         rp, cols, masks = lut.device_tensors(q.device)[:3]
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         o, lse = ops.sparse_flash_fwd(q, k, v, rp, cols, masks, lut.heads, lut.causal, float(scale), lut.shift,
-                                      bool(out_bshd))
+                                      bool(out_bshd), kbias, ebias)
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.lut, ctx.scale, ctx.out_bshd = lut, float(scale), bool(out_bshd)
+        ctx.kbias, ctx.ebias = kbias, ebias  # constants: no gradient (as in the reference softmax)
         return o
 
     @staticmethod
@@ -150,11 +189,13 @@ class _SparseFlash(torch.autograd.Function):
         rp, cols, masks, _cp, rows, masks_t, tasks, fin = lut.device_tensors(q.device)
         dq, dk, dv = native.hip_ops().sparse_flash_bwd(do.contiguous(), q, k, v, o, lse, rp, cols, masks, rows,
                                                        masks_t, tasks, fin, lut.nslot, lut.heads, lut.causal,
-                                                       ctx.scale, lut.shift, ctx.out_bshd)
-        return dq, dk, dv, None, None, None
+                                                       ctx.scale, lut.shift, ctx.out_bshd, ctx.kbias, ctx.ebias)
+        return dq, dk, dv, None, None, None, None, None
 
 
-def sparse_flash_attention(q, k, v, lut: SparseFlashLUT, scale: float = 1.0, out_bshd: bool = False):
-    """softmax(scale * Q K^T restricted to the layout [+ causal]) V for q, k, v [B, H, S, D];
-    returns [B, H, S, D], or [B, S, H, D] with out_bshd."""
-    return _SparseFlash.apply(q, k, v, lut, scale, out_bshd)
+def sparse_flash_attention(q, k, v, lut: SparseFlashLUT, scale: float = 1.0, out_bshd: bool = False,
+                           kbias: Optional[torch.Tensor] = None, ebias: Optional[torch.Tensor] = None):
+    """softmax(scale * Q K^T [+ kbias[b, key] + ebias[b, h, q, key]] restricted to the layout
+    [+ causal]) V for q, k, v [B, H, S, D]; returns [B, H, S, D], or [B, S, H, D] with out_bshd.
+    kbias / ebias: see `score_biases` (rows with no unmasked key give 0)."""
+    return _SparseFlash.apply(q, k, v, lut, scale, out_bshd, kbias, ebias)

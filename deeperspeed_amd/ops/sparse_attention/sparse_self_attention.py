@@ -1,8 +1,10 @@
 """Block-sparse self-attention module (reference parity:
 deepspeed/ops/sparse_attention/sparse_self_attention.py:14-174).
 
-softmax(scale * Q K^T (+rpe, masks)) V with Q K^T sampled on the layout (SDD), the sparse
-softmax, and a sparse x dense product (DSD).  The layout is built once for
+softmax(scale * Q K^T (+rpe, masks)) V.  On the GPU one fused kernel per direction walks the
+layout's active tiles with the masks / RPE as score biases (ops/sparse_attention/flash.py);
+elsewhere Q K^T is sampled on the layout (SDD), then the sparse softmax and a sparse x dense
+product (DSD).  The layout is built once for
 `max_seq_length` and broadcast from rank 0 on first use (random patterns stay identical on
 every rank); shorter sequences use its top-left sub-layout."""
 
@@ -26,6 +28,8 @@ class SparseSelfAttention(nn.Module):
         self.key_padding_mask_mode = key_padding_mask_mode
         self.attn_mask_mode = attn_mask_mode
         self.ops = {}
+        # False: masked / RPE calls take the SDD / softmax / DSD kernels (A/B and parity tests)
+        self.fused_masks = True
 
     def get_layout(self, L):
         if self._need_layout_synchronization and dist.is_available() and dist.is_initialized():
@@ -87,10 +91,13 @@ class SparseSelfAttention(nn.Module):
         if attn_mask is not None:
             attn_mask = self.transpose_mask_for_sparse(query.dtype, attn_mask)
         scaling = float(head_dim) ** -0.5
-        if rpe is None and key_padding_mask is None and attn_mask is None:
+        plain = rpe is None and key_padding_mask is None and attn_mask is None
+        if plain or self.fused_masks:
             lut = self.get_lut(tgt_len)
             if flash.supported(query, lut):  # one fused kernel per query tile (ops/sparse_attention/flash.py)
-                return flash.sparse_flash_attention(query, key, value, lut, scaling)
+                kbias, ebias = flash.score_biases(query, rpe, key_padding_mask, attn_mask,
+                                                  self.key_padding_mask_mode, self.attn_mask_mode)
+                return flash.sparse_flash_attention(query, key, value, lut, scaling, kbias=kbias, ebias=ebias)
         sdd_nt, dsd_nn, softmax = self.get_ops(num_heads, tgt_len)
         w = sdd_nt(query, key)
         w = softmax(w, scale=scaling, rpe=rpe, key_padding_mask=key_padding_mask, attn_mask=attn_mask,

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--mode", default="bigbird")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--unfused", action="store_true", help="also time the SDD/softmax/DSD path")
+    ap.add_argument("--masked", action="store_true",
+                    help="also time the fused kernels with a BERT-style key-padding mask (score bias)")
     a = ap.parse_args()
     from deeperspeed_amd.ops import native
     from deeperspeed_amd.ops.sparse_attention import sparsity_config as sc
@@ -55,13 +57,15 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / a.iters
 
+    # autograd.grad, not backward(): accumulating into q/k/v.grad would add three elementwise
+    # passes over [B, H, S, D] per call to the timed region
     def dense():
         o = native.flash_attention(q, k, v, True, D ** -0.5, out_layout="bshd")
-        o.backward(g)
+        torch.autograd.grad(o, (q, k, v), g)
 
     def sparse():
         o = sparse_flash_attention(q, k, v, lut, D ** -0.5, out_bshd=True)
-        o.backward(g)
+        torch.autograd.grad(o, (q, k, v), g)
 
     def sparse_fwd():
         with torch.no_grad():
@@ -82,6 +86,19 @@ def main():
             "ms_fwd": round(t_sparse_f, 3),
             "tile_density": round(lut.density, 4), "speedup_vs_dense": round(t_dense / t_sparse, 2),
             "effective_tflops": round(flops_dense * lut.density * 2 / t_sparse / 1e9, 1)}]
+    if a.masked:
+        from deeperspeed_amd.ops.sparse_attention.flash import score_biases
+        kpm = torch.zeros(B, S, device=dev, dtype=torch.bfloat16)
+        kpm[:, S - S // 8:] = -10000.0  # the last eighth of every sequence is padding
+        kbias, _ = score_biases(q, key_padding_mask=kpm)
+
+        def masked():
+            o = sparse_flash_attention(q, k, v, lut, D ** -0.5, out_bshd=True, kbias=kbias)
+            torch.autograd.grad(o, (q, k, v), g)
+        t_m = time_it(masked)
+        res.append({"variant": f"block-sparse flash ({a.mode}, block {a.block}) + key-padding mask",
+                    "ms_fwd_bwd": round(t_m, 3), "vs_unmasked": round(t_m / t_sparse, 3),
+                    "speedup_vs_dense": round(t_dense / t_m, 2)})
     if a.unfused:
         lay = layout.cpu()
         sdd, dsd, sm = MatMul(lay, a.block, "sdd", trans_b=True), MatMul(lay, a.block, "dsd"), Softmax(lay, a.block)
@@ -89,7 +106,7 @@ def main():
         def unfused():
             w = sm(sdd(q * D ** -0.5, k), scale=1.0, causal=True)
             o = dsd(w, v)
-            o.backward(g.transpose(1, 2))
+            torch.autograd.grad(o, (q, k, v), g.transpose(1, 2))
         t_u = time_it(unfused)
         res.append({"variant": "block-sparse SDD/softmax/DSD (unfused)", "ms_fwd_bwd": round(t_u, 3),
                     "speedup_vs_dense": round(t_dense / t_u, 2)})

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 3: block-sparse kernels at one wave per SIMD (no spills), fused Delta, parallel finish,
+# masks / RPE inside the fused kernels.
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+set -o pipefail
+timeout -k 10 300 python -u -m pytest tests/test_sparse_flash.py tests/test_sparse_attention.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r3f_tests.log 2>&1 || { tail -40 gpurun_out/r3f_tests.log; exit 1; }
+tail -1 gpurun_out/r3f_tests.log
+timeout -k 10 200 python scripts/bench_sparse_attn.py --masked > gpurun_out/r3f_sparse.jsonl 2> gpurun_out/r3f_sparse.err || { tail -20 gpurun_out/r3f_sparse.err; exit 1; }
+cat gpurun_out/r3f_sparse.jsonl
+timeout -k 10 200 python scripts/bench_sparse_attn.py --masked --seq 4096 --heads 16 --dim 64 --batch 4 --mode fixed --block 16 > gpurun_out/r3f_sparse_bert.jsonl 2> gpurun_out/r3f_sparse_bert.err || { tail -20 gpurun_out/r3f_sparse_bert.err; exit 1; }
+cat gpurun_out/r3f_sparse_bert.jsonl
+cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r3f_prof -o sp --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/bench_sparse_attn.py --iters 5 > /dev/null 2>&1 || { echo "rocprof failed"; exit 1; }
+cd $GRAFT_REPO_ROOT; f=$(find gpurun_out/r3f_prof -name "*kernel_stats.csv" | head -1); cp $f gpurun_out/r3f_kernel_stats.csv; python3 -c "
+import csv
+for r in csv.DictReader(open('gpurun_out/r3f_kernel_stats.csv')):
+    print(r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1000,1),'us')"

@@ -164,7 +164,9 @@ def test_sparse_self_attention_fused_matches_unfused():
     q, k, v = (torch.randn(B, H, S, D, device=dev, dtype=torch.float16, requires_grad=True) for _ in range(3))
     fused = attn(q, k, v)
     assert attn.get_lut(S) is not None
+    attn.fused_masks = False  # an all-ones 'mul' attention mask through SDD / softmax / DSD
     unfused = attn(q, k, v, attn_mask=torch.ones(S, S, device=dev, dtype=torch.float16))
+    attn.fused_masks = True
     assert (fused.float() - unfused.float()).abs().max().item() < 1e-2
     fused.float().sum().backward()
     assert all(t.grad is not None and torch.isfinite(t.grad).all() for t in (q, k, v))
@@ -185,3 +187,75 @@ def test_neox_bigbird_fused_path_trains():
     att = m.layers[0].attention
     assert att._sp_ops[1024][3] is not None  # the fused LUT was built and used
     assert torch.isfinite(loss) and all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+
+
+def _masked_reference(q, k, v, lay, block, scale, kbias, ebias):
+    S = q.shape[2]
+    m = lay.bool().repeat_interleave(block, 1).repeat_interleave(block, 2)[:, :S, :S].to(q.device)
+    if m.shape[0] == 1:
+        m = m.expand(q.shape[1], S, S)
+    s = (q.float() @ k.float().transpose(-1, -2)) * scale
+    if kbias is not None:
+        s = s + kbias.float()[:, None, None, :]
+    if ebias is not None:
+        s = s + ebias.float()
+    s = s.masked_fill(~m[None], float("-inf"))
+    p = torch.softmax(s, dim=-1).nan_to_num(0.0)
+    return p @ v.float()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("block,D,dtype,kp_mode,attn_mode", [
+    (32, 64, torch.bfloat16, "mul", "mul"), (64, 96, torch.float16, "add", "add"),
+    (16, 128, torch.bfloat16, "add", "mul")])
+def test_sparse_flash_masks_and_rpe_match_reference(block, D, dtype, kp_mode, attn_mode):
+    """Key-padding mask, attention mask and relative position embedding inside the fused
+    kernels (reference Softmax semantics, add / mul modes) against the fp32 dense reference."""
+    from deeperspeed_amd.ops.sparse_attention.flash import score_biases, sparse_flash_attention
+    torch.manual_seed(4)
+    B, H, S = 2, 4, 512
+    dev = torch.device("cuda")
+    lay = _rand_layout(H, S // block, 0.35, 5)
+    lut = SparseFlashLUT(lay, block)
+    q, k, v = (torch.randn(B, H, S, D, device=dev, dtype=dtype, requires_grad=True) for _ in range(3))
+    if kp_mode == "mul":  # batch 1 pads its last 100 keys
+        kpm = torch.ones(B, S, device=dev, dtype=dtype)
+        kpm[1, -100:] = 0
+    else:
+        kpm = (torch.randn(B, S, device=dev) * 0.5).to(dtype)
+    attn = (torch.rand(S, S, device=dev) > 0.2).to(dtype) if attn_mode == "mul" else \
+        (torch.randn(S, S, device=dev) * 0.3).to(dtype)
+    rpe = (torch.randn(1, H, S, S, device=dev) * 0.2).to(dtype)
+    kbias, ebias = score_biases(q, rpe, kpm, attn, kp_mode, attn_mode)
+    scale = D ** -0.5
+    o = sparse_flash_attention(q, k, v, lut, scale, kbias=kbias, ebias=ebias)
+    g = torch.randn_like(o)
+    o.backward(g)
+    qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
+    ref = _masked_reference(qr, kr, vr, lay, block, scale, kbias, ebias)
+    ref.backward(g.float())
+    tol = 2e-2 if dtype == torch.bfloat16 else 5e-3
+    assert (o.float() - ref).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+    for a, b in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        err = (a.float() - b).abs().max().item()
+        assert err < 4 * tol * max(1.0, b.abs().max().item()), err
+
+
+@pytest.mark.gpu
+def test_sparse_self_attention_masked_fused_matches_unfused():
+    """SparseSelfAttention / BertSparseSelfAttention with masks: the fused kernels agree with the
+    SDD / softmax / DSD path given the same masks and RPE."""
+    from deeperspeed_amd.ops.sparse_attention import FixedSparsityConfig, SparseSelfAttention
+    random.seed(0)
+    torch.manual_seed(6)
+    B, H, S, D = 2, 4, 512, 64
+    attn = SparseSelfAttention(FixedSparsityConfig(num_heads=H, block=16, num_local_blocks=4), max_seq_length=S)
+    dev = torch.device("cuda")
+    q, k, v = (torch.randn(B, H, S, D, device=dev, dtype=torch.bfloat16) for _ in range(3))
+    kpm = torch.zeros(B, 1, 1, S, device=dev, dtype=torch.bfloat16)
+    kpm[0, ..., -64:] = -10000.0  # HF-style additive padding mask
+    rpe = (torch.randn(H, S, S, device=dev) * 0.1).to(torch.bfloat16)
+    fused = attn(q, k, v, rpe=rpe, key_padding_mask=kpm)
+    attn.fused_masks = False
+    unfused = attn(q, k, v, rpe=rpe, key_padding_mask=kpm)
+    assert (fused.float() - unfused.float()).abs().max().item() < 3e-2
