@@ -1346,7 +1346,8 @@ __device__ __forceinline__ uint32_t full_mask(int nsub_l2) {
   return bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
 }
 
-// Score biases of the reference sparse softmax (softmax_fwd.tr:46-129), compiled in by SX = 1:
+// Score biases of the reference sparse softmax (softmax_fwd.tr:46-129), compiled in by SX bits
+// (1: key-padding bias only -- BERT's case, no per-element loads; 3: both):
 //   kbias [Z, S] fp32: the key-padding mask (additive; 'mul' masks arrive as 0 / -inf), z = bh / H
 //   ebias [Z|1, H|1, S, S] in the input dtype: relative position embedding + attention mask
 //         (additive, pre-summed on the host), element (bh, q, k) at (bh / H) * ez + (bh % H) * eh
@@ -1368,8 +1369,8 @@ template <typename T, int SX>
 __device__ __forceinline__ float4 sbias4(const SExtra& sx, const uint16_t* eh, int64_t z, int S, int q, int key0) {
   float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
   if constexpr (SX != 0) {
-    if (sx.kbias) b = *reinterpret_cast<const float4*>(sx.kbias + z * S + key0);
-    if (sx.ebias) {
+    if ((SX & 1) && sx.kbias) b = *reinterpret_cast<const float4*>(sx.kbias + z * S + key0);
+    if ((SX & 2) && sx.ebias) {
       const ushort4 e = *reinterpret_cast<const ushort4*>(eh + (int64_t)q * sx.er + key0);
       b.x += h16f<T>(e.x); b.y += h16f<T>(e.y); b.z += h16f<T>(e.z); b.w += h16f<T>(e.w);
     }
@@ -1379,7 +1380,7 @@ __device__ __forceinline__ float4 sbias4(const SExtra& sx, const uint16_t* eh, i
 }
 
 template <typename T, int D, bool CAUSAL, bool RP, int SX = 0>
-__global__ void __launch_bounds__(128, RP ? 1 : 3) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+__global__ void __launch_bounds__(128, RP ? (SX ? 1 : 2) : 3) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                       const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                       float* __restrict__ LSE, const int* __restrict__ rowptr,
                                                       const int* __restrict__ cols, const uint32_t* __restrict__ masks,
@@ -1468,7 +1469,7 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sfwd_kernel(const uint16_t* _
         }
     }
     if constexpr (SX != 0) {  // scores to the log2 domain with the biases folded in
-      const uint16_t* ehd = sx.ebias ? ebias_head(sx, bh, H) : nullptr;
+      const uint16_t* ehd = ((SX & 2) && sx.ebias) ? ebias_head(sx, bh, H) : nullptr;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1610,7 +1611,7 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
   const uint16_t* ecol = nullptr;
   if constexpr (SX != 0) {
     if (sx.kbias) kb2 = sx.kbias[(bh / H) * (int64_t)S + mykey] * LOG2E;
-    if (sx.ebias) ecol = ebias_head(sx, bh, H) + mykey;
+    if ((SX & 2) && sx.ebias) ecol = ebias_head(sx, bh, H) + mykey;
   }
   auto store_tile = [&](int stage) {
     uint16_t* b = smem + stage * 2 * TS;
@@ -1662,7 +1663,8 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float b = kb2;
-          if (ecol) b += h16f<T>(ecol[(int64_t)(i0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3)) * sx.er]) * LOG2E;
+          if ((SX & 2) && ecol)
+            b += h16f<T>(ecol[(int64_t)(i0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3)) * sx.er]) * LOG2E;
           pv[r] = fast_exp2(fmaf(sacc[r], sl2, b));
         }
       } else {
@@ -1823,7 +1825,7 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
   } else {
     dl = DELTA[bh * (int64_t)S + myq];
   }
-  const uint16_t* ehd = (SX != 0 && sx.ebias) ? ebias_head(sx, bh, H) : nullptr;
+  const uint16_t* ehd = ((SX & 2) && sx.ebias) ? ebias_head(sx, bh, H) : nullptr;
   f32x16 dq[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -2174,9 +2176,12 @@ void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* 
   sx.kbias = kbias;
   sx.ebias = (const uint16_t*)ebias;
   sx.ez = ez; sx.eh = eh; sx.er = er;
-  const bool ex = kbias || ebias;
   FA_DISPATCH(dt, D, causal,
-    if (ex)
+    if (ebias)
+      hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, true, 3>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
+                         masks, S, scale, onh, H, Hl, shift, sx);
+    else if (kbias)
       hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, true, 1>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
                          masks, S, scale, onh, H, Hl, shift, sx);
@@ -2206,9 +2211,16 @@ void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, con
   sx.kbias = kbias;
   sx.ebias = (const uint16_t*)ebias;
   sx.ez = ez; sx.eh = eh; sx.er = er;
-  const bool ex = kbias || ebias;
   FA_DISPATCH(dt, D, causal,
-    if (ex) {
+    if (ebias) {
+      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true, 3, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, sx, (const uint16_t*)o);
+      hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, true, 3>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(true), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
+                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
+                         shift, sx);
+    } else if (kbias) {
       hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true, 1, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                          (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, sx, (const uint16_t*)o);
