@@ -512,44 +512,81 @@ void onebit_unpack(Tensor signs, Tensor scales, Tensor out) {
 }
 
 // ----------------------------------------------------------------------------- block-sparse attention
-// sdd: A [Z,H,Mr,K], B [Z,H,Nr,K] (B given row-major by N: C = A B^T), nz int32 [nnz,3] -> C [Z,nnz,blk,blk]
+// A 16-bit [Z,H,R,K] operand of the sparse products, unit stride along K (returns false) or
+// along R (returns true), every other stride and the base 16-byte aligned (sparse_attn.hip
+// stages 16-byte chunks along the unit-stride dim).  The Python side normalises anything else.
+static bool sparse_mat(const Tensor& x, const char* name, int64_t* st) {
+  TORCH_CHECK(x.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(x.dim() == 4 && x.scalar_type() != at::kFloat, "sparse ", name, ": 16-bit [Z,H,R,K]");
+  for (int d = 0; d < 4; ++d) st[d] = x.size(d) == 1 ? 0 : x.stride(d);
+  const bool t = x.stride(3) != 1 || x.size(3) == 1;
+  const int u = t ? 2 : 3;
+  TORCH_CHECK(x.stride(u) == 1 || x.size(u) == 1, "sparse ", name, ": needs a unit-stride last or second-last dim");
+  st[u] = 1;
+  bool ok = x.size(u) % 8 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0;
+  for (int d = 0; d < 4; ++d)
+    if (d != u) ok = ok && st[d] % 8 == 0;
+  TORCH_CHECK(ok, "sparse ", name, ": unit-stride extent, strides and base must be multiples of 8 elements");
+  return t;
+}
+
+// sdd: C[z][n] = alpha * A[rows of r] . B[rows of c]^T; A [Z,H,Mr,K], B [Z,H,Nr,K] (views)
 Tensor sparse_sdd(Tensor A, Tensor B, Tensor nz, int64_t blk, double alpha) {
-  check_dev(A, "A"); check_dev(B, "B"); check_dev(nz, "nz");
-  TORCH_CHECK(A.dim() == 4 && B.dim() == 4 && A.size(0) == B.size(0) && A.size(1) == B.size(1) &&
-              A.size(3) == B.size(3) && A.scalar_type() == B.scalar_type() && A.scalar_type() != at::kFloat,
-              "sparse_sdd: A/B must be 16-bit [Z,H,*,K] with matching Z,H,K");
-  TORCH_CHECK(A.size(3) % 32 == 0 && blk % 16 == 0 && A.size(2) % blk == 0 && B.size(2) % blk == 0,
-              "sparse_sdd: K % 32, block % 16 and rows % block must be 0");
-  TORCH_CHECK(nz.scalar_type() == at::kInt && nz.dim() == 2 && nz.size(1) == 3, "sparse_sdd: nz int32 [nnz,3]");
+  int64_t sa[4], sb[4];
+  const bool at = sparse_mat(A, "A", sa), bt = sparse_mat(B, "B", sb);
+  check_dev(nz, "nz");
+  TORCH_CHECK(A.size(0) == B.size(0) && A.size(1) == B.size(1) && A.size(3) == B.size(3) &&
+              A.scalar_type() == B.scalar_type(), "sparse_sdd: A/B must match in Z, H, K and dtype");
+  TORCH_CHECK((blk == 16 || blk == 32 || blk == 64 || blk == 128) && A.size(2) % blk == 0 && B.size(2) % blk == 0,
+              "sparse_sdd: block in {16,32,64,128} dividing the rows");
+  TORCH_CHECK(nz.scalar_type() == at::kInt && nz.dim() == 2 && nz.size(1) == 3 && nz.is_contiguous(),
+              "sparse_sdd: nz int32 [nnz,3]");
   const int64_t nnz = nz.size(0);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
   Tensor C = at::empty({A.size(0), nnz, blk, blk}, A.options());
-  dsa::launch_sparse_sdd(A.data_ptr(), B.data_ptr(), C.data_ptr(), nz.data_ptr<int>(), (int)nnz, (int)A.size(0),
-                         (int)A.size(1), (int)A.size(2), (int)B.size(2), (int)A.size(3), (int)blk, (float)alpha,
-                         dcode(A), cur_stream());
+  dsa::launch_sparse_sdd(A.data_ptr(), sa, at, B.data_ptr(), sb, bt, C.data_ptr(), nz.data_ptr<int>(), (int)nnz,
+                         (int)A.size(0), (int)A.size(3), (int)blk, (float)alpha, dcode(A), cur_stream());
   return C;
 }
 
-// dsd: S [Z,nnz,blk,blk] with CSR (rowptr [H*nbr+1], cols [nnz]); Dt [Z,H,N,Kd] -> C [Z,H,nbr*blk,N]
-Tensor sparse_dsd(Tensor S, Tensor rowptr, Tensor cols, Tensor Dt, int64_t H, int64_t nbr, int64_t blk) {
-  check_dev(S, "S"); check_dev(Dt, "Dt"); check_dev(rowptr, "rowptr"); check_dev(cols, "cols");
-  TORCH_CHECK(S.dim() == 4 && S.size(2) == blk && S.size(3) == blk && S.scalar_type() == Dt.scalar_type() &&
-              Dt.dim() == 4 && Dt.size(0) == S.size(0) && Dt.size(1) == H, "sparse_dsd: shapes");
-  TORCH_CHECK(Dt.size(2) % 16 == 0 && Dt.size(3) % blk == 0 && blk % 16 == 0, "sparse_dsd: N % 16, K % block");
-  TORCH_CHECK(rowptr.scalar_type() == at::kInt && rowptr.numel() == H * nbr + 1 && cols.scalar_type() == at::kInt &&
-              cols.numel() == S.size(1), "sparse_dsd: CSR");
+// dsd: C[z,h, rows of r, :] = sum over the row's blocks of S_eff . D[rows of col, :]; S [Z,nnz,blk,blk]
+// contiguous; seg int32 [nseg,4] = (h*nbr + r, first, end, partial slot | -1) covering every row,
+// fin int32 [nfin,4] = (h*nbr + r, slot0, nslots, 0) for split rows; perm (optional) = walk of
+// layout^T (S_eff = stored block perm[p] transposed); D [Z,H,Kd,N] and the preallocated
+// C [Z,H,nbr*blk,N] are views of either orientation.
+void sparse_dsd(Tensor S, Tensor seg, Tensor fin, int64_t nslots, Tensor cols, OptT perm, Tensor D, Tensor C,
+                int64_t H, int64_t nbr, int64_t blk) {
+  check_dev(S, "S"); check_dev(seg, "seg"); check_dev(fin, "fin"); check_dev(cols, "cols");
+  int64_t sd[4], sc[4];
+  const bool dtr = sparse_mat(D, "D", sd), ctr = sparse_mat(C, "C", sc);
+  TORCH_CHECK(S.dim() == 4 && S.is_contiguous() && S.size(2) == blk && S.size(3) == blk &&
+              S.scalar_type() == D.scalar_type() && C.scalar_type() == D.scalar_type(), "sparse_dsd: S");
+  TORCH_CHECK((blk == 16 || blk == 32 || blk == 64 || blk == 128) && D.size(0) == S.size(0) && D.size(1) == H &&
+              D.size(2) % blk == 0 && C.size(0) == S.size(0) && C.size(1) == H && C.size(2) == nbr * blk &&
+              C.size(3) == D.size(3), "sparse_dsd: shapes");
+  TORCH_CHECK(seg.scalar_type() == at::kInt && seg.dim() == 2 && seg.size(1) == 4 && fin.scalar_type() == at::kInt &&
+              fin.dim() == 2 && fin.size(1) == 4 && cols.scalar_type() == at::kInt && cols.numel() == S.size(1),
+              "sparse_dsd: LUTs");
+  if (perm.has_value()) {
+    check_dev(*perm, "perm");
+    TORCH_CHECK(perm->scalar_type() == at::kInt && perm->numel() == S.size(1), "sparse_dsd: perm int32 [nnz]");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
-  Tensor C = at::empty({S.size(0), H, nbr * blk, Dt.size(2)}, S.options());
-  dsa::launch_sparse_dsd(S.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(), Dt.data_ptr(), C.data_ptr(),
-                         (int)S.size(1), (int)S.size(0), (int)H, (int)nbr, (int)Dt.size(2), (int)Dt.size(3), (int)blk,
-                         dcode(S), cur_stream());
-  return C;
+  const int64_t N = D.size(3), Np = (N + 63) / 64 * 64;
+  Tensor ws;
+  if (nslots > 0) ws = at::empty({S.size(0), nslots, blk, Np}, S.options().dtype(at::kFloat));
+  dsa::launch_sparse_dsd(S.data_ptr(), seg.data_ptr<int>(), (int)seg.size(0), fin.data_ptr<int>(), (int)fin.size(0),
+                         cols.data_ptr<int>(), perm.has_value() ? perm->data_ptr<int>() : nullptr, D.data_ptr(), sd,
+                         dtr, C.data_ptr(), sc, ctr, nslots > 0 ? ws.data_ptr<float>() : nullptr, (int)nslots,
+                         (int)S.size(1), (int)S.size(0), (int)nbr, (int)N, (int)blk, dcode(S), cur_stream());
 }
 
-// in-place softmax over the non-zero blocks of each row
-void sparse_softmax_fwd(Tensor x, Tensor rowptr, Tensor cols, int64_t H, int64_t nbr, double scale, OptT rpe,
-                        OptT kpm, OptT attn, bool kpm_mul, bool attn_mul, bool causal) {
-  check_dev(x, "x");
+// softmax over the non-zero blocks of each row, x -> y (may alias); max_row = longest row (elements)
+void sparse_softmax_fwd(Tensor x, Tensor y, Tensor rowptr, Tensor cols, int64_t H, int64_t nbr, int64_t max_row,
+                        double scale, OptT rpe, OptT kpm, OptT attn, bool kpm_mul, bool attn_mul, bool causal) {
+  check_dev(x, "x"); check_dev(y, "y");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous() && y.is_contiguous() && x.sizes() == y.sizes() &&
+              x.scalar_type() == y.scalar_type() && x.size(2) % 16 == 0, "sparse softmax: x/y [Z,nnz,blk,blk]");
   const int64_t blk = x.size(2), S = nbr * blk;
   int64_t rsz = 0, rsh = 0, rsr = 0, ksz = 0, asr = 0;
   if (rpe.has_value()) {
@@ -570,20 +607,24 @@ void sparse_softmax_fwd(Tensor x, Tensor rowptr, Tensor cols, int64_t H, int64_t
     asr = attn->stride(0);
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  dsa::launch_sparse_softmax_fwd(x.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(), (int)x.size(1),
-                                 (int)x.size(0), (int)H, (int)nbr, (int)blk,
+  dsa::launch_sparse_softmax_fwd(x.data_ptr(), y.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(),
+                                 (int)x.size(1), (int)x.size(0), (int)H, (int)nbr, (int)blk, (int)max_row,
                                  rpe.has_value() ? rpe->data_ptr() : nullptr, rsz, rsh, rsr,
                                  kpm.has_value() ? kpm->data_ptr() : nullptr, ksz,
                                  attn.has_value() ? attn->data_ptr() : nullptr, asr, kpm_mul ? 1 : 0,
                                  attn_mul ? 1 : 0, (float)scale, causal ? 1 : 0, dcode(x), cur_stream());
 }
 
-void sparse_softmax_bwd(Tensor y, Tensor dy, Tensor rowptr, int64_t H, int64_t nbr, double scale) {
-  check_dev(y, "y"); check_dev(dy, "dy");
-  TORCH_CHECK(y.sizes() == dy.sizes() && y.scalar_type() == dy.scalar_type(), "sparse softmax bwd: shapes");
+void sparse_softmax_bwd(Tensor y, Tensor dy, Tensor dx, Tensor rowptr, int64_t H, int64_t nbr, int64_t max_row,
+                        double scale) {
+  check_dev(y, "y"); check_dev(dy, "dy"); check_dev(dx, "dx");
+  TORCH_CHECK(y.sizes() == dy.sizes() && y.sizes() == dx.sizes() && y.scalar_type() == dy.scalar_type() &&
+              dx.scalar_type() == y.scalar_type() && y.is_contiguous() && dy.is_contiguous() && dx.is_contiguous() &&
+              y.size(2) % 16 == 0, "sparse softmax bwd: shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
-  dsa::launch_sparse_softmax_bwd(y.data_ptr(), dy.data_ptr(), rowptr.data_ptr<int>(), (int)y.size(1), (int)y.size(0),
-                                 (int)H, (int)nbr, (int)y.size(2), (float)scale, dcode(y), cur_stream());
+  dsa::launch_sparse_softmax_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), rowptr.data_ptr<int>(), (int)y.size(1),
+                                 (int)y.size(0), (int)H, (int)nbr, (int)y.size(2), (int)max_row, (float)scale,
+                                 dcode(y), cur_stream());
 }
 
 // ----------------------------------------------------------------------------- dropout

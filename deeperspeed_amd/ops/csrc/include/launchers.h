@@ -108,16 +108,19 @@ void launch_onebit_unpack(const uint8_t* signs, const float* scales, int P, int6
                           hipStream_t s);
 
 // sparse_attn.hip: block-sparse attention (LUTs from ops/sparse_attention)
-void launch_sparse_sdd(const void* A, const void* B, void* C, const int* nz, int nnz, int Z, int H, int Mr, int Nr,
-                       int K, int blk, float alpha, int dt, hipStream_t s);
-void launch_sparse_dsd(const void* S, const int* rowptr, const int* cols, const void* Dt, void* C, int nnz, int Z,
-                       int H, int nbr, int N, int Kd, int blk, int dt, hipStream_t s);
-void launch_sparse_softmax_fwd(void* x, const int* rowptr, const int* cols, int nnz, int Z, int H, int nbr, int blk,
-                               const void* rpe, int64_t rpe_sz, int64_t rpe_sh, int64_t rpe_sr, const void* kpm,
-                               int64_t kpm_sz, const void* attn, int64_t attn_sr, int kpm_mul, int attn_mul,
-                               float scale, int causal, int dt, hipStream_t s);
-void launch_sparse_softmax_bwd(const void* y, void* dy, const int* rowptr, int nnz, int Z, int H, int nbr, int blk,
-                               float scale, int dt, hipStream_t s);
+// strides are {z, h, row, k} in elements; at/bt/dtr/ctr = the row dim (not k) is the unit-stride one
+void launch_sparse_sdd(const void* A, const int64_t* sa, bool at, const void* B, const int64_t* sb, bool bt, void* C,
+                       const int* nz, int nnz, int Z, int K, int blk, float alpha, int dt, hipStream_t s);
+void launch_sparse_dsd(const void* S, const int* seg, int nseg, const int* fin, int nfin, const int* cols,
+                       const int* perm, const void* D, const int64_t* sd, bool dtr, void* C, const int64_t* sc,
+                       bool ctr, float* ws, int nslots, int nnz, int Z, int nbr, int N, int blk, int dt,
+                       hipStream_t s);
+void launch_sparse_softmax_fwd(const void* x, void* y, const int* rowptr, const int* cols, int nnz, int Z, int H,
+                               int nbr, int blk, int max_row, const void* rpe, int64_t rpe_sz, int64_t rpe_sh,
+                               int64_t rpe_sr, const void* kpm, int64_t kpm_sz, const void* attn, int64_t attn_sr,
+                               int kpm_mul, int attn_mul, float scale, int causal, int dt, hipStream_t s);
+void launch_sparse_softmax_bwd(const void* y, const void* dy, void* dx, const int* rowptr, int nnz, int Z, int H,
+                               int nbr, int blk, int max_row, float scale, int dt, hipStream_t s);
 
 // dropout.hip: counter-based Philox dropout (seed, offset) with uint8 keep-masks
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed, uint64_t offset,

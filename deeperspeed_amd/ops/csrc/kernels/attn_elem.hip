@@ -200,6 +200,103 @@ __global__ void __launch_bounds__(256) rotary_split_bwd_row_kernel(const T* __re
   for (int i = 0; i < NVEC; ++i) Vec16<T>::store(dst + 8 * i, g[i]);
 }
 
+// LDS-tiled rotary split: one workgroup per (b, 16 positions, 4 heads).  The QKV projection
+// output is read as its [s][h][which] runs (2.3 KB contiguous at HD 96) and q/k/v are written
+// as [which][h][s] runs (3 KB contiguous), both with one 16-byte chunk per lane per instruction;
+// the row-per-thread kernels above make every lane walk its own 192-byte row, which spreads each
+// load/store instruction over 64 separate cache lines (3.2 TB/s on the 20B shapes).  BWD runs the
+// same tile the other way round (dq/dk/dv -> dqkv with the inverse rotation).
+constexpr int ROT_SB = 16, ROT_HB = 4;
+constexpr int which_chunks(int hd, int rot) { return hd / 8 > (rot + 7) / 8 ? hd / 8 : (rot + 7) / 8; }
+
+template <typename T, int HD, int ROT, bool BWD>
+__global__ void __launch_bounds__(256) rotary_split_tiled_kernel(const T* __restrict__ qkv_in, T* __restrict__ qkv_out,
+                                                                 const T* __restrict__ q_in, const T* __restrict__ k_in,
+                                                                 const T* __restrict__ v_in, T* __restrict__ q_out,
+                                                                 T* __restrict__ k_out, T* __restrict__ v_out,
+                                                                 const float2* __restrict__ cs, int S, int NH,
+                                                                 float qscale) {
+  constexpr int CPR = HD / 8, HALF = ROT / 2;
+  constexpr int ROWS = 3 * ROT_HB * ROT_SB, CHUNKS = ROWS * CPR;
+  __shared__ __attribute__((aligned(16))) uint16_t tile[ROWS * HD];  // [which][h][s][HD]
+  const int tid = threadIdx.x;
+  const int nsb = S / ROT_SB, nhb = NH / ROT_HB;
+  const int hb = blockIdx.x % nhb, sb = (blockIdx.x / nhb) % nsb, b = blockIdx.x / (nhb * nsb);
+  const int s0 = sb * ROT_SB, h0 = hb * ROT_HB;
+  auto lds_off = [](int which, int hl, int sl) { return ((which * ROT_HB + hl) * ROT_SB + sl) * HD; };
+  // packed side ([B,S,NH,3,HD], GPT-NeoX's per-head interleave) chunk order: s, h, which, chunk
+  auto packed_chunk = [&](int c, int& which, int& hl, int& sl, int& ch) {
+    ch = c % CPR; int r = c / CPR;
+    which = r % 3; r /= 3;
+    hl = r % ROT_HB; sl = r / ROT_HB;
+  };
+  // split side ([B,NH,S,HD] x 3) chunk order: which, h, s, chunk
+  auto split_chunk = [&](int c, int& which, int& hl, int& sl, int& ch) {
+    ch = c % CPR; int r = c / CPR;
+    sl = r % ROT_SB; r /= ROT_SB;
+    hl = r % ROT_HB; which = r / ROT_HB;
+  };
+  for (int c = tid; c < CHUNKS; c += 256) {
+    int which, hl, sl, ch;
+    uint4 v;
+    if constexpr (!BWD) {
+      packed_chunk(c, which, hl, sl, ch);
+      v = *reinterpret_cast<const uint4*>(qkv_in + ((((int64_t)b * S + s0 + sl) * NH + h0 + hl) * 3 + which) * HD + ch * 8);
+    } else {
+      split_chunk(c, which, hl, sl, ch);
+      const T* src = which == 0 ? q_in : (which == 1 ? k_in : v_in);
+      v = *reinterpret_cast<const uint4*>(src + (((int64_t)b * NH + h0 + hl) * S + s0 + sl) * HD + ch * 8);
+    }
+    *reinterpret_cast<uint4*>(tile + lds_off(which, hl, sl) + ch * 8) = v;
+  }
+  __syncthreads();
+  if (tid < ROWS) {
+    const int which = tid / (ROT_HB * ROT_SB), hl = (tid / ROT_SB) % ROT_HB, sl = tid % ROT_SB;
+    if (which < 2) {
+      uint16_t* row = tile + lds_off(which, hl, sl);
+      constexpr int NV = which_chunks(HD, ROT);
+      float x[NV][8];
+      const int nv = which == 0 ? CPR : (ROT + 7) / 8;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        if (i < nv) Vec16<T>::load(reinterpret_cast<const T*>(row) + 8 * i, x[i]);
+      if constexpr (ROT > 0) {
+        const float2* c = cs + (int64_t)(s0 + sl) * HALF;
+#pragma unroll
+        for (int i = 0; i < HALF; ++i) {
+          const float2 cc = c[i];
+          const float a = x[i / 8][i % 8], p = x[(i + HALF) / 8][(i + HALF) % 8];
+          // forward: y1 = x1 c - x2 s, y2 = x2 c + x1 s; backward: the transposed rotation
+          x[i / 8][i % 8] = BWD ? a * cc.x + p * cc.y : a * cc.x - p * cc.y;
+          x[(i + HALF) / 8][(i + HALF) % 8] = BWD ? p * cc.x - a * cc.y : p * cc.x + a * cc.y;
+        }
+      }
+      if (which == 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[i][j] *= qscale;
+      }
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        if (i < nv) Vec16<T>::store(reinterpret_cast<T*>(row) + 8 * i, x[i]);
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < CHUNKS; c += 256) {
+    int which, hl, sl, ch;
+    if constexpr (!BWD) split_chunk(c, which, hl, sl, ch);
+    else packed_chunk(c, which, hl, sl, ch);
+    const uint4 v = *reinterpret_cast<const uint4*>(tile + lds_off(which, hl, sl) + ch * 8);
+    if constexpr (!BWD) {
+      T* dst = which == 0 ? q_out : (which == 1 ? k_out : v_out);
+      *reinterpret_cast<uint4*>(dst + (((int64_t)b * NH + h0 + hl) * S + s0 + sl) * HD + ch * 8) = v;
+    } else {
+      *reinterpret_cast<uint4*>(qkv_out + ((((int64_t)b * S + s0 + sl) * NH + h0 + hl) * 3 + which) * HD + ch * 8) = v;
+    }
+  }
+}
+
 // (HD, ROT) pairs of the GPT-NeoX / GPT-3 presets; anything else takes the vector kernels.
 #define DSA_ROTARY_ROW_CASES(X) X(64, 16) X(64, 64) X(80, 20) X(96, 24) X(96, 96) X(128, 32) X(128, 64) X(128, 128)
 
@@ -455,6 +552,11 @@ static inline bool softmax_rows_shape(int C, int& G, int& NV) {
     default: { constexpr int NV = 16; __VA_ARGS__; } break;          \
   }
 
+static int os_env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
 static int elem_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   if (g > 16384) g = 16384;
@@ -465,6 +567,17 @@ void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const f
                              int HD, int ROT, float qscale, int dt, hipStream_t s) {
   const int rows = B * S * NH;
   const int grid = (rows * 3 + 255) / 256;
+  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0 && os_env_int("DSA_ROTARY_TILED", 1) != 0;
+#define DSA_ROT_TILED_FWD(hd, rot)                                                                             \
+  if (tiled && HD == hd && ROT == rot) {                                                                       \
+    DSA_DISPATCH_16(dt, T,                                                                                     \
+      hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, false>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
+                         dim3(256), 0, s, (const T*)qkv, nullptr, nullptr, nullptr, nullptr, (T*)q, (T*)k, (T*)v, \
+                         (const float2*)cs, S, NH, qscale));                                                   \
+    return;                                                                                                    \
+  }
+  DSA_ROTARY_ROW_CASES(DSA_ROT_TILED_FWD)
+#undef DSA_ROT_TILED_FWD
 #define DSA_ROT_FWD(hd, rot)                                                                                   \
   if (HD == hd && ROT == rot) {                                                                                \
     DSA_DISPATCH_16(dt, T,                                                                                     \
@@ -484,6 +597,17 @@ void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, voi
                              int S, int NH, int HD, int ROT, float qscale, int dt, hipStream_t s) {
   const int rows = B * S * NH;
   const int grid = (rows * 3 + 255) / 256;
+  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0 && os_env_int("DSA_ROTARY_TILED", 1) != 0;
+#define DSA_ROT_TILED_BWD(hd, rot)                                                                             \
+  if (tiled && HD == hd && ROT == rot) {                                                                       \
+    DSA_DISPATCH_16(dt, T,                                                                                     \
+      hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, true>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
+                         dim3(256), 0, s, nullptr, (T*)dqkv, (const T*)dq, (const T*)dk, (const T*)dv, nullptr,  \
+                         nullptr, nullptr, (const float2*)cs, S, NH, qscale));                                 \
+    return;                                                                                                    \
+  }
+  DSA_ROTARY_ROW_CASES(DSA_ROT_TILED_BWD)
+#undef DSA_ROT_TILED_BWD
 #define DSA_ROT_BWD(hd, rot)                                                                                   \
   if (HD == hd && ROT == rot) {                                                                                \
     DSA_DISPATCH_16(dt, T,                                                                                     \

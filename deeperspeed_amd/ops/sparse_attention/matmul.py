@@ -3,11 +3,14 @@
 
 Sparse operands/results use the reference storage: [Z, nnz, block, block], blocks in
 torch.nonzero(layout) order.  Everything reduces to two HIP kernels
-(ops/csrc/kernels/sparse_attn.hip): an NT "dense x dense -> sampled sparse" product and a
-CSR-driven "sparse x dense -> dense" product; transposed sparse operands use a transposed
-LUT plus a block gather/transpose, and backward passes are the same two products with the
-roles exchanged.  CPU tensors run an equivalent PyTorch gather/scatter implementation (the
-numerics reference of the GPU tests).
+(ops/csrc/kernels/sparse_attn.hip): a "dense x dense^T -> sampled sparse" product and a
+CSR-driven "sparse x dense -> dense" product.  Both take their dense operands as strided
+views of either orientation (unit stride along the last or the second-last dim) and stage
+tiles into LDS as they lie in memory, so trans_a/trans_b, dds and every backward product run
+without transpose or gather copies; a transposed sparse operand is a walk of layout^T whose
+blocks the kernel reads transposed, and dds writes its output through a transposed view.
+CPU tensors run an equivalent PyTorch gather/scatter implementation (the numerics reference
+of the GPU tests).
 """
 
 import torch
@@ -39,14 +42,44 @@ class SparseLayout:
         self.rowptr_t = torch.cat([torch.zeros(1, dtype=torch.int64), lt.sum(-1).reshape(-1).cumsum(0)]).to(torch.int32)
         self.cols_t = nzt[:, 2].to(torch.int32)
         self.nz_t = nzt.to(torch.int32)
+        self.max_row = int(layout.sum(-1).max().item()) * self.block if self.nnz else 0
         self._dev = {}
+
+    def segments(self, trans: bool):
+        """Row-segment LUT of the dsd kernel for one orientation: every (head, block-row) row as
+        (row, first, end, slot) with slot -1, except rows much longer than the mean (e.g. BigBird's
+        global columns walked transposed), which are cut into segments with their own fp32
+        partial slots plus a finish entry (row, slot0, nslots, 0).  Longest segments first."""
+        rowptr = (self.rowptr_t if trans else self.rowptr).long()
+        lens = rowptr[1:] - rowptr[:-1]
+        cap = max(2 * int(torch.ceil(lens.float().mean()).item()) if lens.numel() else 1, max(1, 512 // self.block))
+        seg, fin, slot = [], [], 0
+        long_rows = set((lens > cap).nonzero().flatten().tolist())
+        for row in range(lens.numel()):
+            a, b = int(rowptr[row]), int(rowptr[row + 1])
+            if row not in long_rows:
+                seg.append((row, a, b, -1))
+                continue
+            k = -(-(b - a) // cap)
+            step = -(-(b - a) // k)
+            fin.append((row, slot, k, 0))
+            for j in range(k):
+                seg.append((row, a + j * step, min(b, a + (j + 1) * step), slot))
+                slot += 1
+        seg.sort(key=lambda t: t[1] - t[2])  # longest first
+        as_t = lambda x: torch.tensor(x, dtype=torch.int32).reshape(-1, 4)  # noqa: E731
+        return as_t(seg), as_t(fin), slot
 
     def dev(self, device):
         key = str(device)
         if key not in self._dev:
             t = lambda x: x.contiguous().to(device)  # noqa: E731 (nonzero() results are column-major)
             self._dev[key] = dict(nz=t(self.nz), rowptr=t(self.rowptr), cols=t(self.cols), perm_t=t(self.perm_t),
-                                  rowptr_t=t(self.rowptr_t), cols_t=t(self.cols_t), nz_t=t(self.nz_t))
+                                  rowptr_t=t(self.rowptr_t), cols_t=t(self.cols_t), nz_t=t(self.nz_t),
+                                  perm_t32=t(self.perm_t.to(torch.int32)))
+            for name, tr in (("seg", False), ("seg_t", True)):
+                sg, fn, ns = self.segments(tr)
+                self._dev[key][name] = (t(sg), t(fn), ns)
         return self._dev[key]
 
 
@@ -59,13 +92,33 @@ def _use_hip(*ts):
     return all(t.is_cuda for t in ts) and ts[0].dtype in (torch.bfloat16, torch.float16)
 
 
+def _stageable(x):
+    """Can the HIP products read this [Z,H,R,K] view in place?  (unit stride along the last or
+    second-last dim; that extent, the other strides and the base 16-byte aligned)."""
+    if x.stride(-1) == 1 and x.shape[-1] > 1:
+        u = 3
+    elif x.stride(-2) == 1:
+        u = 2
+    else:
+        return False
+    if x.shape[u] % 8 or x.data_ptr() % 16:
+        return False
+    return all(x.shape[d] == 1 or x.stride(d) % 8 == 0 for d in range(4) if d != u)
+
+
+def _hip_operand(x):
+    return x if _stageable(x) else x.contiguous()
+
+
 def sdd(a: torch.Tensor, bn: torch.Tensor, L: SparseLayout, alpha: float = 1.0) -> torch.Tensor:
-    """Sampled (a @ bn^T) on L: a [Z,H,nbr*blk,K], bn [Z,H,nbc*blk,K] -> [Z,nnz,blk,blk]."""
+    """Sampled (a @ bn^T) on L: a [Z,H,nbr*blk,K], bn [Z,H,nbc*blk,K] -> [Z,nnz,blk,blk].
+    a / bn may be transposed views (e.g. trans_a, or the backward's dc^T)."""
     blk = L.block
     if _use_hip(a, bn):
         d = L.dev(a.device)
-        return native.hip_ops().sparse_sdd(_pad_last(a, 32).contiguous(), _pad_last(bn, 32).contiguous(), d["nz"], blk,
-                                           alpha)
+        if a.shape[-1] % 8:
+            a, bn = _pad_last(a, 8), _pad_last(bn, 8)
+        return native.hip_ops().sparse_sdd(_hip_operand(a), _hip_operand(bn), d["nz"], blk, alpha)
     Z, K = a.shape[0], a.shape[-1]
     nz = L.nz.long().to(a.device)
     av = a.reshape(Z, L.H, L.nbr, blk, K)[:, nz[:, 0], nz[:, 1]]
@@ -73,25 +126,30 @@ def sdd(a: torch.Tensor, bn: torch.Tensor, L: SparseLayout, alpha: float = 1.0) 
     return (torch.matmul(av.float(), bv.float().transpose(-1, -2)) * alpha).to(a.dtype)
 
 
-def dsd(s: torch.Tensor, L: SparseLayout, trans: bool, d: torch.Tensor) -> torch.Tensor:
-    """(S or S^T as dense) @ d; s [Z,nnz,blk,blk] on L, d [Z,H,K,N] -> [Z,H,M,N]."""
+def dsd(s: torch.Tensor, L: SparseLayout, trans: bool, d: torch.Tensor, out_t: bool = False) -> torch.Tensor:
+    """(S or S^T as dense) @ d; s [Z,nnz,blk,blk] on L, d [Z,H,K,N] (any orientation) ->
+    [Z,H,M,N].  out_t: the result is a transposed view of a contiguous [Z,H,N,M] tensor."""
     blk = L.block
     Z, N = d.shape[0], d.shape[-1]
-    if trans:
-        perm = L.perm_t.to(s.device)
-        s = s[:, perm].transpose(-1, -2)
-        nbr, nbc = L.nbc, L.nbr
-    else:
-        nbr, nbc = L.nbr, L.nbc
+    nbr, nbc = (L.nbc, L.nbr) if trans else (L.nbr, L.nbc)
     if _use_hip(s, d):
         dv = L.dev(s.device)
-        rowptr, cols = (dv["rowptr_t"], dv["cols_t"]) if trans else (dv["rowptr"], dv["cols"])
-        dt = d.transpose(-1, -2)
-        npad = (-N) % 16
+        seg, fin, nslots = dv["seg_t"] if trans else dv["seg"]
+        cols = dv["cols_t"] if trans else dv["cols"]
+        npad = (-N) % 8
         if npad:
-            dt = F.pad(dt, (0, 0, 0, npad))
-        out = native.hip_ops().sparse_dsd(s.contiguous(), rowptr, cols, dt.contiguous(), L.H, nbr, blk)
+            d = F.pad(d, (0, npad))
+        d = _hip_operand(d)
+        Np, M = N + npad, nbr * blk
+        if out_t:
+            out = torch.empty(Z, L.H, Np, M, dtype=d.dtype, device=d.device).transpose(-1, -2)
+        else:
+            out = torch.empty(Z, L.H, M, Np, dtype=d.dtype, device=d.device)
+        native.hip_ops().sparse_dsd(s.contiguous(), seg, fin, nslots, cols, dv["perm_t32"] if trans else None, d,
+                                    out, L.H, nbr, blk)
         return out[..., :N] if npad else out
+    if trans:
+        s = s[:, L.perm_t.to(s.device)].transpose(-1, -2)
     nzt = (L.nz_t if trans else L.nz).long().to(s.device)
     dv = d.reshape(Z, L.H, nbc, blk, N)[:, nzt[:, 0], nzt[:, 2]]  # [Z,nnz,blk,N]
     contrib = torch.matmul(s.float(), dv.float())
@@ -101,8 +159,9 @@ def dsd(s: torch.Tensor, L: SparseLayout, trans: bool, d: torch.Tensor) -> torch
 
 
 def dds(d: torch.Tensor, s: torch.Tensor, L: SparseLayout, trans: bool) -> torch.Tensor:
-    """d @ (S or S^T as dense); d [Z,H,M,K] -> [Z,H,M,N]."""
-    return dsd(s, L, not trans, d.transpose(-1, -2)).transpose(-1, -2)
+    """d @ (S or S^T as dense); d [Z,H,M,K] -> [Z,H,M,N] (= (S_eff^T @ d^T)^T, written in place
+    through a transposed output view on the GPU)."""
+    return dsd(s, L, not trans, d.transpose(-1, -2), out_t=True).transpose(-1, -2)
 
 
 def _t(x):

@@ -1,7 +1,8 @@
 """Block-sparse softmax (reference parity: deepspeed/ops/sparse_attention/softmax.py `Softmax`):
 scale, relative position embedding [Z|1, H|1, S, S], key-padding mask [Z, S] and attention
 mask [S, S], each mask in 'add' or 'mul' (0 -> -inf) mode, over the non-zero blocks of every
-row.  One wave64 per row on the GPU (sparse_attn.hip)."""
+row.  One wave64 per row on the GPU (sparse_attn.hip): the row is held in registers, so x is
+read once and every bias evaluated once, written out of place."""
 
 import torch
 
@@ -20,8 +21,9 @@ class _SparseSoftmaxFn(torch.autograd.Function):
     def forward(ctx, x, L, scale, rpe, kpm, attn, kpm_mode, attn_mode, causal=False):
         if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16):
             d = L.dev(x.device)
-            y = x.contiguous().clone()
-            native.hip_ops().sparse_softmax_fwd(y, d["rowptr"], d["cols"], L.H, L.nbr, scale,
+            x = x.contiguous()
+            y = torch.empty_like(x)
+            native.hip_ops().sparse_softmax_fwd(x, y, d["rowptr"], d["cols"], L.H, L.nbr, L.max_row, scale,
                                                 None if rpe is None else _as4(rpe).contiguous(),
                                                 None if kpm is None else kpm.contiguous(),
                                                 None if attn is None else attn.contiguous(),
@@ -37,8 +39,10 @@ class _SparseSoftmaxFn(torch.autograd.Function):
         (y,) = ctx.saved_tensors
         L = ctx.L
         if y.is_cuda and y.dtype in (torch.bfloat16, torch.float16):
-            dx = dy.contiguous().clone()
-            native.hip_ops().sparse_softmax_bwd(y, dx, L.dev(y.device)["rowptr"], L.H, L.nbr, ctx.scale)
+            dy = dy.contiguous()
+            dx = torch.empty_like(dy)
+            native.hip_ops().sparse_softmax_bwd(y, dy, dx, L.dev(y.device)["rowptr"], L.H, L.nbr, L.max_row,
+                                                ctx.scale)
         else:
             dx = _softmax_bwd_ref(y, dy, L, ctx.scale)
         return dx, None, None, None, None, None, None, None, None

@@ -1,6 +1,6 @@
-"""rotary_split fwd/bwd at the GPT-NeoX-20B shape (B4 S2048 64 heads x 96, rotary 24):
-achieved HBM bandwidth of the HIP kernels (bytes = read + write of q, k, v)."""
-
+"""Rotary + QKV split fwd/bwd at the GPT-NeoX-20B shape (B4 S2048 NH64 HD96 rotary 24): the
+LDS-tiled kernels vs the row-per-thread kernels (DSA_ROTARY_TILED=0), HIP events, one JSON line
+per variant with the achieved HBM bandwidth (read + write of the full QKV tensor)."""
 import json
 import os
 import sys
@@ -13,26 +13,37 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     from deeperspeed_amd.ops import attention as A
     B, S, NH, HD, ROT = 4, 2048, 64, 96, 24
-    dev = torch.device("cuda", 0)
-    qkv = torch.randn(B, S, NH * 3 * HD, device=dev, dtype=torch.bfloat16)
-    cs = A.rotary_table(S, ROT, 10000.0, dev)
-    from deeperspeed_amd.ops import native
-    ops = native.hip_ops()
-    q, k, v = ops.rotary_split_fwd(qkv, cs, NH, HD, ROT, 0.1)
+    qkv = torch.randn(B, S, 3 * NH * HD, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     nbytes = 2 * qkv.numel() * 2
-    for name, fn in (("fwd", lambda: ops.rotary_split_fwd(qkv, cs, NH, HD, ROT, 0.1)),
-                     ("bwd", lambda: ops.rotary_split_bwd(q, k, v, cs, ROT, 0.1))):
-        for _ in range(5):
-            fn()
+
+    def run(tiled):
+        os.environ["DSA_ROTARY_TILED"] = "1" if tiled else "0"
+        q, k, v = A.rotary_split(qkv, NH, HD, ROT, qscale=HD ** -0.5)
+        g = [torch.randn_like(t) for t in (q, k, v)]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        for _ in range(3):
+            A.rotary_split(qkv, NH, HD, ROT, qscale=HD ** -0.5)
         torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(50):
-            fn()
-        e.record()
+        e[0].record()
+        for _ in range(20):
+            out = A.rotary_split(qkv, NH, HD, ROT, qscale=HD ** -0.5)
+        e[1].record()
+        e[2].record()
+        for _ in range(20):
+            torch.autograd.grad(out, qkv, g, retain_graph=True)
+        e[3].record()
         torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / 50
-        print(json.dumps({"op": f"rotary_split_{name}", "us": round(ms * 1e3, 1), "TB/s": round(nbytes / ms / 1e9, 2)}))
+        fwd, fb = e[0].elapsed_time(e[1]) / 20, e[2].elapsed_time(e[3]) / 20
+        return out, fwd, fb
+
+    res = {}
+    for tiled in (False, True):
+        out, fwd, bwd = run(tiled)
+        res[tiled] = out
+        print(json.dumps({"variant": "tiled" if tiled else "row-per-thread", "fwd_us": round(fwd * 1e3, 1),
+                          "bwd_us": round(bwd * 1e3, 1), "fwd_TBps": round(nbytes / fwd / 1e9, 2),
+                          "bwd_TBps": round(nbytes / bwd / 1e9, 2)}), flush=True)
+    assert all(torch.equal(a, b) for a, b in zip(res[False], res[True]))
 
 
 if __name__ == "__main__":

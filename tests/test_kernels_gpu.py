@@ -97,7 +97,8 @@ def test_sumsq_and_colsum():
 
 
 @pytest.mark.parametrize("hd,rot", [(96, 24), (128, 32), (64, 64), (96, 96), (32, 8), (64, 16), (128, 128), (80, 20)])
-@pytest.mark.parametrize("S,NH", [(40, 4), (41, 5)])  # 41 x 5: the last chunk-kernel block is partial
+# 41 x 5: the last chunk-kernel block is partial; 48 x 8: the LDS-tiled kernels (S % 16, NH % 4)
+@pytest.mark.parametrize("S,NH", [(40, 4), (41, 5), (48, 8)])
 def test_rotary_split_matches_reference(hd, rot, S, NH):
     from deeperspeed_amd.ops import attention as A
     torch.manual_seed(3)
@@ -287,14 +288,21 @@ def _sp_layout(H, nb, seed):
     return lay
 
 
+_SP_MODES = [("sdd", ta, tb) for ta in (False, True) for tb in (False, True)] + \
+    [(m, ta, tb) for m in ("dsd", "dds") for ta, tb in ((False, False), (True, False), (False, True), (True, True))]
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("blk", [16, 32, 64])
-@pytest.mark.parametrize("mode,ta,tb", [("sdd", False, True), ("sdd", True, False), ("dsd", False, False),
-                                        ("dsd", True, False), ("dds", False, False), ("dds", False, True)])
+@pytest.mark.parametrize("blk", [16, 32, 64, 128])
+@pytest.mark.parametrize("mode,ta,tb", _SP_MODES)
 def test_block_sparse_matmul_hip_vs_cpu(dtype, blk, mode, ta, tb):
+    """Every mode x transpose on the LDS-staged kernels: transposed operands are read in place
+    (no copies), the dense width 40 exercises partial K stages / output column tiles."""
+    if dtype == torch.float16 and blk in (32, 128):
+        pytest.skip("fp16 covered at blocks 16/64")
     import deeperspeed_amd.ops.sparse_attention as sa
     torch.manual_seed(0)
-    H, nb, Z, D = 3, 6, 2, 64
+    H, nb, Z, D = 3, 6 if blk < 128 else 3, 2, 40
     S = nb * blk
     lay = _sp_layout(H, nb, blk)
     nnz = int(lay.sum())
@@ -320,6 +328,48 @@ def test_block_sparse_matmul_hip_vs_cpu(dtype, blk, mode, ta, tb):
     ra, rb = torch.autograd.grad(mm(ar, br), (ar, br), g.to(dtype).float())
     torch.testing.assert_close(ga.float().cpu(), ra, atol=tol * 8, rtol=tol)
     torch.testing.assert_close(gb.float().cpu(), rb, atol=tol * 8, rtol=tol)
+
+
+def test_block_sparse_matmul_strided_views():
+    """Operands that are transposed or sliced views go to the kernels as they are."""
+    import deeperspeed_amd.ops.sparse_attention as sa
+    torch.manual_seed(1)
+    H, nb, Z, blk = 2, 4, 2, 32
+    S = nb * blk
+    lay = _sp_layout(H, nb, 3)
+    mm = sa.MatMul(lay, blk, "sdd", trans_a=False, trans_b=True)
+    big = torch.randn(Z, H, S, 128, dtype=torch.bfloat16)
+    a, b = big[..., :64], big[..., 64:]  # row stride 128, unit k stride
+    ref = mm(a.float(), b.float())
+    out = mm(a.to(_dev()), b.to(_dev()))
+    torch.testing.assert_close(out.float().cpu(), ref, atol=0.2, rtol=5e-2)
+    dd = sa.MatMul(lay, blk, "dsd")
+    s = torch.randn(Z, int(lay.sum()), blk, blk, dtype=torch.bfloat16) * 0.2
+    d = torch.randn(Z, H, 64, S, dtype=torch.bfloat16).transpose(-1, -2)  # [Z,H,S,64], k unit-stride
+    torch.testing.assert_close(dd(s.to(_dev()), d.to(_dev())).float().cpu(), dd(s.float(), d.float()),
+                               atol=0.2, rtol=5e-2)
+
+
+@pytest.mark.parametrize("blk,nb,dense", [(16, 8, False), (64, 20, False), (64, 80, True)])
+def test_block_sparse_softmax_row_lengths(blk, nb, dense):
+    """Rows held in registers (<= 4096 elements) and the online two-pass path (longer rows)."""
+    import deeperspeed_amd.ops.sparse_attention as sa
+    torch.manual_seed(2)
+    H, Z = 1, 1
+    S = nb * blk
+    lay = torch.ones(H, nb, nb, dtype=torch.long) if dense else _sp_layout(H, nb, 5)
+    x = (torch.randn(Z, int(lay.sum()), blk, blk) * 3).to(torch.bfloat16)
+    kpm = torch.randn(Z, S).to(torch.bfloat16)
+    sm = sa.Softmax(lay, blk)
+    ref = sm(x.float(), scale=0.7, key_padding_mask=kpm.float())
+    xg = x.to(_dev()).requires_grad_(True)
+    y = sm(xg, scale=0.7, key_padding_mask=kpm.to(_dev()))
+    torch.testing.assert_close(y.float().cpu(), ref, atol=1e-2, rtol=2e-2)
+    g = torch.randn_like(ref).to(torch.bfloat16)
+    (gx,) = torch.autograd.grad(y, xg, g.to(_dev()))
+    xr = x.float().requires_grad_(True)
+    (rx,) = torch.autograd.grad(sm(xr, scale=0.7, key_padding_mask=kpm.float()), xr, g.float())
+    torch.testing.assert_close(gx.float().cpu(), rx, atol=2e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("blk", [16, 64])

@@ -198,3 +198,29 @@ def test_neox_sparse_attention_dense_layout_matches_dense_model():
     ids2 = ids.clone()
     ids2[:, 40:] = (ids2[:, 40:] + 1) % cfg.vocab_size
     torch.testing.assert_close(m3(ids)[:, :40], m3(ids2)[:, :40], atol=1e-5, rtol=1e-5)
+
+
+def test_dsd_row_segments_cover_every_block_once():
+    """The dsd row-segment LUT (long rows of layout^T split with partial slots) covers each
+    non-zero block exactly once, every row appears, and split rows own contiguous slots."""
+    import random
+    from deeperspeed_amd.ops.sparse_attention import sparsity_config as sc
+    from deeperspeed_amd.ops.sparse_attention.matmul import SparseLayout
+    random.seed(0)
+    lay = sc.BigBirdSparsityConfig(num_heads=2, block=16, attention="unidirectional").make_layout(1024)
+    L = SparseLayout(lay, 16)
+    for trans in (False, True):
+        seg, fin, nslots = L.segments(trans)
+        cov = torch.zeros(L.nnz, dtype=torch.long)
+        rows = set()
+        for r, a, b, slot in seg.tolist():
+            cov[a:b] += 1
+            rows.add(r)
+        assert (cov == 1).all() and rows == set(range(L.H * (L.nbc if trans else L.nbr)))
+        slots = sorted(sl for *_, sl in seg.tolist() if sl >= 0)
+        assert slots == list(range(nslots))
+        for r, s0, k, _ in fin.tolist():
+            assert sorted(sl for rr, _, _, sl in seg.tolist() if rr == r) == list(range(s0, s0 + k))
+        lens = (seg[:, 2] - seg[:, 1]).tolist()
+        assert lens == sorted(lens, reverse=True)
+    assert L.segments(True)[2] > 0  # the global key columns are split when walked transposed
