@@ -268,6 +268,36 @@ __global__ void __launch_bounds__(256) lamb_apply_kernel(TW* __restrict__ w, con
   }
 }
 
+// 4 consecutive elements as one vector access (16 bytes fp32, 8 bytes 16-bit)
+template <typename T> struct V4;
+template <> struct V4<float> {
+  __device__ __forceinline__ static void load(const float* p, float* f) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    f[0] = x.x; f[1] = x.y; f[2] = x.z; f[3] = x.w;
+  }
+  __device__ __forceinline__ static void store(float* p, const float* f) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  }
+};
+template <typename T, float (*LD)(uint16_t), uint16_t (*ST)(float)>
+struct V4Half {
+  __device__ __forceinline__ static void load(const T* p, float* f) {
+    const uint2 x = *reinterpret_cast<const uint2*>(p);
+    f[0] = LD(x.x & 0xffff); f[1] = LD(x.x >> 16); f[2] = LD(x.y & 0xffff); f[3] = LD(x.y >> 16);
+  }
+  __device__ __forceinline__ static void store(T* p, const float* f) {
+    *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)ST(f[0]) | ((uint32_t)ST(f[1]) << 16),
+                                              (uint32_t)ST(f[2]) | ((uint32_t)ST(f[3]) << 16));
+  }
+};
+template <> struct V4<bf16_t> : V4Half<bf16_t, bf16_to_f32, f32_to_bf16> {};
+template <> struct V4<f16_t> : V4Half<f16_t, f16_to_f32, f32_to_f16> {};
+
+template <typename... P>
+__device__ __forceinline__ bool aligned16(const P*... p) {
+  return ((reinterpret_cast<uintptr_t>(p) | ...) & 15) == 0;
+}
+
 // Multi-tensor LAMB: the whole parameter list in three launches (meta table as adam_multi:
 // w, g, m, v, out pointers, numel, chunk prefix).  Stage 1 writes per-chunk partial ||w||^2,
 // ||u||^2; finish reduces each tensor's chunks to its clamped trust ratio; apply recomputes
@@ -293,16 +323,37 @@ __global__ void __launch_bounds__(256) lamb_multi_stage1_kernel(const int64_t* _
   const int64_t start = (c - pref[t]) * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
   float sw = 0.f, su = 0.f;
-  for (int64_t e = start + threadIdx.x; e < end; e += blockDim.x) {
-    const float wf = Conv<TW>::load(w, e);
-    const float gf = Conv<TG>::load(g, e) * a.grad_scale;
-    const float mf = fmaf(a.beta1, m[e], (1.f - a.beta1) * gf);
-    const float vf = fmaf(a.beta2, v[e], (1.f - a.beta2) * gf * gf);
-    m[e] = mf; v[e] = vf;
+  auto elem = [&](float wf, float gf, float& mf, float& vf) {
+    gf *= a.grad_scale;
+    mf = fmaf(a.beta1, mf, (1.f - a.beta1) * gf);
+    vf = fmaf(a.beta2, vf, (1.f - a.beta2) * gf * gf);
     const float denom = a.adamw ? sqrtf(vf) + a.eps : sqrtf(vf + a.eps);
     const float u = mf / denom + a.weight_decay * wf;
     sw = fmaf(wf, wf, sw);
     su = fmaf(u, u, su);
+  };
+  // 4-wide vector body when every stream is 16-byte aligned (always for whole allocations)
+  int64_t e0 = start;
+  if (aligned16(w, g, m, v)) {
+    const int64_t vend = start + ((end - start) & ~(int64_t)3);
+    for (int64_t e = start + 4 * threadIdx.x; e < vend; e += 4 * blockDim.x) {
+      float wf[4], gf[4];
+      V4<TW>::load(w + e, wf);
+      V4<TG>::load(g + e, gf);
+      float4 mm = *reinterpret_cast<const float4*>(m + e), vv = *reinterpret_cast<const float4*>(v + e);
+      elem(wf[0], gf[0], mm.x, vv.x);
+      elem(wf[1], gf[1], mm.y, vv.y);
+      elem(wf[2], gf[2], mm.z, vv.z);
+      elem(wf[3], gf[3], mm.w, vv.w);
+      *reinterpret_cast<float4*>(m + e) = mm;
+      *reinterpret_cast<float4*>(v + e) = vv;
+    }
+    e0 = vend;
+  }
+  for (int64_t e = e0 + threadIdx.x; e < end; e += blockDim.x) {
+    float mf = m[e], vf = v[e];
+    elem(Conv<TW>::load(w, e), Conv<TG>::load(g, e), mf, vf);
+    m[e] = mf; v[e] = vf;
   }
   block_sum2(sw, su, red);
   if (threadIdx.x == 0) { partial[2 * c] = sw; partial[2 * c + 1] = su; }
@@ -348,12 +399,28 @@ __global__ void __launch_bounds__(256) lamb_multi_apply_kernel(const int64_t* __
   const int64_t start = (c - pref[t]) * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
   const float s = a.lr * coeff[t];
-  for (int64_t e = start + threadIdx.x; e < end; e += blockDim.x) {
-    const float wf = Conv<TW>::load(w, e);
-    const float vf = v[e];
+  auto step = [&](float wf, float mf, float vf) {
     const float denom = a.adamw ? sqrtf(vf) + a.eps : sqrtf(vf + a.eps);
-    const float u = m[e] / denom + a.weight_decay * wf;
-    const float nw = wf - s * u;
+    return wf - s * (mf / denom + a.weight_decay * wf);
+  };
+  int64_t e0 = start;
+  if (aligned16(w, m, v, out)) {
+    const int64_t vend = start + ((end - start) & ~(int64_t)3);
+    for (int64_t e = start + 4 * threadIdx.x; e < vend; e += 4 * blockDim.x) {
+      float wf[4];
+      V4<TW>::load(w + e, wf);
+      const float4 mm = *reinterpret_cast<const float4*>(m + e), vv = *reinterpret_cast<const float4*>(v + e);
+      wf[0] = step(wf[0], mm.x, vv.x);
+      wf[1] = step(wf[1], mm.y, vv.y);
+      wf[2] = step(wf[2], mm.z, vv.z);
+      wf[3] = step(wf[3], mm.w, vv.w);
+      V4<TW>::store(w + e, wf);
+      if (out) V4<TO>::store(out + e, wf);
+    }
+    e0 = vend;
+  }
+  for (int64_t e = e0 + threadIdx.x; e < end; e += blockDim.x) {
+    const float nw = step(Conv<TW>::load(w, e), m[e], v[e]);
     Conv<TW>::store(w, e, nw);
     if (out) Conv<TO>::store(out, e, nw);
   }

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--torch-profile", default="", help="write a torch.profiler op table of one step here")
     args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29541")
@@ -77,6 +78,17 @@ def main():
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = (time.time() - t0) / args.steps
+    if args.torch_profile:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+            step()
+            torch.cuda.synchronize()
+        with open(args.torch_profile, "w") as f:
+            ka = prof.key_averages()
+            f.write(ka.table(sort_by="self_device_time_total", row_limit=60, max_name_column_width=60) + "\n")
+            f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="count", row_limit=60,
+                                                                        max_name_column_width=50,
+                                                                        max_shapes_column_width=90))
     sps = B / dt
     tflops = sps * cfg.flops_per_sample(S, npred) / 1e12
     ref = REF.get(S)
