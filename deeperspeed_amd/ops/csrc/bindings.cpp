@@ -143,14 +143,20 @@ void lamb(Tensor w, Tensor g, Tensor m, Tensor v, Tensor upd, OptT out, double l
 // multi-tensor LAMB over a meta table (layout of adam_multi); partial >= 2*total_chunks, coeff >= T
 void lamb_multi(Tensor meta, int64_t T, int64_t total_chunks, int64_t chunk, int64_t wt, int64_t gt, int64_t ot,
                 double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2,
-                double grad_scale, double max_coeff, double min_coeff, bool adamw, Tensor partial, Tensor coeff) {
+                double grad_scale, double max_coeff, double min_coeff, bool adamw, Tensor partial, Tensor coeff,
+                OptT scale) {
   check_dev(meta, "meta"); check_dev(partial, "partial"); check_dev(coeff, "coeff");
+  if (scale.has_value()) {
+    check_dev(*scale, "scale");
+    TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1, "lamb_multi: scale must be one fp32");
+  }
   TORCH_CHECK(meta.scalar_type() == at::kLong && meta.numel() == 7 * T + 1, "lamb_multi: bad meta table");
   TORCH_CHECK(partial.scalar_type() == at::kFloat && partial.numel() >= 2 * total_chunks, "lamb_multi: partial");
   TORCH_CHECK(coeff.scalar_type() == at::kFloat && coeff.numel() >= T, "lamb_multi: coeff");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(meta.device());
   dsa::LambArgs a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2,
-                  (float)grad_scale, (float)max_coeff, (float)min_coeff, adamw ? 1 : 0};
+                  (float)grad_scale, (float)max_coeff, (float)min_coeff, adamw ? 1 : 0,
+                  scale.has_value() ? scale->data_ptr<float>() : nullptr};
   dsa::launch_lamb_multi(meta.data_ptr<int64_t>(), (int)T, total_chunks, chunk, (int)wt, (int)gt, (int)ot, a,
                          partial.data_ptr<float>(), coeff.data_ptr<float>(), cur_stream());
 }
@@ -1039,7 +1045,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq_accum", &sumsq_accum);
   m.def("scale_copy", &scale_copy);
   m.def("lamb", &lamb);
-  m.def("lamb_multi", &lamb_multi);
+  m.def("lamb_multi", &lamb_multi, py::arg("meta"), py::arg("T"), py::arg("total_chunks"), py::arg("chunk"),
+        py::arg("wt"), py::arg("gt"), py::arg("ot"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
+        py::arg("wd"), py::arg("bc1"), py::arg("bc2"), py::arg("grad_scale"), py::arg("max_coeff"), py::arg("min_coeff"),
+        py::arg("adamw"), py::arg("partial"), py::arg("coeff"), py::arg("scale") = py::none());
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);

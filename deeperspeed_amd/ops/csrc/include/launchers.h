@@ -20,6 +20,9 @@ struct LambArgs {
   float lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale;
   float max_coeff, min_coeff;
   int adamw;
+  // optional device-resident factor multiplied into grad_scale (unscale x clip computed on the
+  // GPU after backward, no host round trip); a non-finite value skips the whole update
+  const float* scale_ptr = nullptr;
 };
 
 // optim.hip

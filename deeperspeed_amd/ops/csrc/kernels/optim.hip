@@ -323,8 +323,16 @@ __global__ void __launch_bounds__(256) lamb_multi_stage1_kernel(const int64_t* _
   const int64_t start = (c - pref[t]) * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
   float sw = 0.f, su = 0.f;
+  float gscale = a.grad_scale;
+  if (a.scale_ptr) {
+    gscale *= *a.scale_ptr;
+    if (!isfinite(gscale)) {  // skipped step: moments untouched
+      if (threadIdx.x == 0) { partial[2 * c] = 0.f; partial[2 * c + 1] = 0.f; }
+      return;
+    }
+  }
   auto elem = [&](float wf, float gf, float& mf, float& vf) {
-    gf *= a.grad_scale;
+    gf *= gscale;
     mf = fmaf(a.beta1, mf, (1.f - a.beta1) * gf);
     vf = fmaf(a.beta2, vf, (1.f - a.beta2) * gf * gf);
     const float denom = a.adamw ? sqrtf(vf) + a.eps : sqrtf(vf + a.eps);
@@ -398,6 +406,7 @@ __global__ void __launch_bounds__(256) lamb_multi_apply_kernel(const int64_t* __
   const int64_t n = meta[5 * T + t];
   const int64_t start = (c - pref[t]) * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
+  if (a.scale_ptr && !isfinite(a.grad_scale * *a.scale_ptr)) return;  // skipped step
   const float s = a.lr * coeff[t];
   auto step = [&](float wf, float mf, float vf) {
     const float denom = a.adamw ? sqrtf(vf) + a.eps : sqrtf(vf + a.eps);

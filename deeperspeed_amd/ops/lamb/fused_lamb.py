@@ -78,7 +78,33 @@ class FusedLamb(torch.optim.Optimizer):
                 self.lamb_coeffs.append(self._multi_step(dev, pdt, gdt, odt, step, items, group, 1.0 / scale))
         return loss
 
-    def _multi_step(self, dev, pdt, gdt, odt, step, items, group, grad_scale):
+    @torch.no_grad()
+    def step_subset(self, gi, idxs, grads, output_params=None, scale_tensor=None):
+        """Update only parameters `idxs` of param group `gi` (one bucket of an overlapped step,
+        runtime/overlap_step.py).  grads / output_params: lists aligned with those indices.
+        scale_tensor: one fp32 on the device multiplied into the gradients (unscale x clip formed
+        on the GPU); a non-finite value makes the kernels skip the update.  Returns the trust
+        ratios of the bucket (device tensors)."""
+        group = self.param_groups[gi]
+        buckets = {}
+        for i, g, o in zip(idxs, grads, output_params or [None] * len(idxs)):
+            p = group["params"][i]
+            if g is None:
+                continue
+            if o is not None and o.data_ptr() == p.data_ptr():
+                o = None
+            st = self.state[p]
+            if len(st) == 0:
+                st["step"] = 0
+                st["exp_avg"] = torch.zeros(p.numel(), dtype=torch.float32, device=p.device)
+                st["exp_avg_sq"] = torch.zeros(p.numel(), dtype=torch.float32, device=p.device)
+            st["step"] += 1
+            key = (p.device, p.dtype, g.dtype, o.dtype if o is not None else None, st["step"])
+            buckets.setdefault(key, []).append((p, g.contiguous(), o))
+        return [self._multi_step(dev, pdt, gdt, odt, step, items, group, 1.0, scale_tensor)
+                for (dev, pdt, gdt, odt, step), items in buckets.items()]
+
+    def _multi_step(self, dev, pdt, gdt, odt, step, items, group, grad_scale, scale_tensor=None):
         import math
         ws = [p.data for p, _, _ in items]
         gs = [g for _, g, _ in items]
@@ -109,7 +135,7 @@ class FusedLamb(torch.optim.Optimizer):
         native.hip_ops().lamb_multi(meta, T, total, _CHUNK, code[pdt], code[gdt], code[odt or pdt],
                                     group["lr"] * math.sqrt(bc2) / bc1, b1, b2, group["eps"], group["weight_decay"],
                                     bc1, bc2, grad_scale, group["max_coeff"], group["min_coeff"],
-                                    self.eps_mode == 1, partial, coeff)
+                                    self.eps_mode == 1, partial, coeff, scale_tensor)
         return coeff
 
     def get_lamb_coeffs(self):

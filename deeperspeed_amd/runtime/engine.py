@@ -586,7 +586,9 @@ class DeepSpeedEngine(Module):
             return FP16_UnfusedOptimizer(optimizer, static_loss_scale=self.loss_scale() or 1.0,
                                          dynamic_loss_scale=dynamic, dynamic_loss_args=self._dynamic_args(),
                                          mpu=self.mpu, clip_grad=self.gradient_clipping(),
-                                         verbose=self.global_rank == 0)
+                                         verbose=self.global_rank == 0,
+                                         overlap_step=bool(getattr(self._config.zero_config, "overlap_step", False)),
+                                         module=self.module)
         return DeepSpeedZeroOptimizer(optimizer, stage=0, dp_process_group=self.data_parallel_group, mpu=self.mpu,
                                       clip_grad=self.gradient_clipping(), static_loss_scale=self.loss_scale() or 1.0,
                                       dynamic_loss_scale=dynamic, dynamic_loss_args=self._dynamic_args(),

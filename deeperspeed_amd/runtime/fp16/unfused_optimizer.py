@@ -21,7 +21,8 @@ from .loss_scaler import DynamicLossScaler, LossScaler
 
 class FP16_UnfusedOptimizer:
     def __init__(self, init_optimizer, static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None,
-                 verbose=True, mpu=None, clip_grad=0.0, fused_lamb_legacy=False):
+                 verbose=True, mpu=None, clip_grad=0.0, fused_lamb_legacy=False, overlap_step=False, module=None,
+                 overlap_bucket_numel=8_000_000):
         self.optimizer = init_optimizer
         self.mpu = mpu
         self.clip_grad = float(clip_grad or 0.0)
@@ -46,6 +47,9 @@ class FP16_UnfusedOptimizer:
         self.overflow = False
         self.overflow_checker = CheckOverflow(self.fp16_groups, mpu=mpu)
         self._global_grad_norm = 0.0
+        self._overlap = None
+        if overlap_step:
+            self._setup_overlap(module, overlap_bucket_numel, verbose)
         if verbose:
             logger.info(f"FP16_UnfusedOptimizer: {sum(len(g) for g in self.fp16_groups)} params with fp32 masters")
 
@@ -68,6 +72,55 @@ class FP16_UnfusedOptimizer:
 
     def get_global_grad_norm(self):
         return self._global_grad_norm
+
+    # ----------------------------------------------------------------- overlapped step
+    def _setup_overlap(self, module, bucket_numel, verbose):
+        """zero_optimization.overlap_step on the per-tensor path (runtime/overlap_step.py): the
+        fused LAMB of a step runs on a side stream in forward-ordered buckets while the next
+        forward starts; each module waits only for its own bucket."""
+        params = [p for g in self.fp16_groups for p in g]
+        ok = (module is not None and getattr(self.optimizer, "supports_fused_lp_step", False)
+              and hasattr(self.optimizer, "step_subset") and torch.cuda.is_available() and params
+              and all(p.is_cuda for p in params))
+        if not ok:
+            if verbose:
+                logger.info("overlap_step: needs a fused low-precision optimizer (FusedLamb) on the GPU; "
+                            "running the step serially")
+            return
+        from ..overlap_step import OverlapStep, forward_order_buckets
+        where = [(gi, i) for gi, g in enumerate(self.fp16_groups) for i in range(len(g))]
+        flat_buckets = forward_order_buckets(module, params, bucket_numel)
+        # per bucket: {group index: [param index within the group]}
+        self._overlap_buckets = []
+        for idxs in flat_buckets:
+            by_group = {}
+            for k in idxs:
+                gi, i = where[k]
+                by_group.setdefault(gi, []).append(i)
+            self._overlap_buckets.append(by_group)
+        self._overlap = OverlapStep(module, params, flat_buckets, params[0].device)
+        if verbose:
+            logger.info(f"overlap_step: {len(flat_buckets)} forward-ordered optimizer buckets on a side stream")
+
+    def synchronize_step(self):
+        """Order the current stream after an overlapped step (checkpointing, state access)."""
+        if self._overlap is not None:
+            self._overlap.synchronize()
+
+    def _overlapped_fused_step(self, coef_t):
+        ov = self._overlap
+        with ov.launch():
+            for key, by_group in enumerate(self._overlap_buckets):
+                for gi, idxs in by_group.items():
+                    lp = self.fp16_groups[gi]
+                    grads = [lp[i].grad for i in idxs]
+                    self.optimizer.step_subset(gi, idxs, grads, [lp[i].data for i in idxs], coef_t)
+                ov.bucket_done(key)
+        for g in self.fp16_groups:  # the side stream still reads the gradients
+            for p in g:
+                if p.grad is not None:
+                    p.grad.record_stream(ov.stream)
+        self.zero_grad()
 
     # ----------------------------------------------------------------- steps
     def zero_grad(self, set_to_none=True):
@@ -101,6 +154,9 @@ class FP16_UnfusedOptimizer:
         coef = 1.0 / prev
         if self.clip_grad > 0 and norm > self.clip_grad:
             coef *= self.clip_grad / (norm + 1e-6)
+        if self._overlap is not None:
+            self._overlapped_fused_step(torch.full((1,), coef, dtype=torch.float32, device=params[0].device))
+            return self.overflow
         if getattr(self.optimizer, "supports_fused_lp_step", False):
             # fused LAMB: low-precision grads read with the unscale/clip factor folded in, the
             # updated master written back to the low-precision params by the same kernel
@@ -127,12 +183,14 @@ class FP16_UnfusedOptimizer:
 
     # ----------------------------------------------------------------- checkpoints
     def state_dict(self):
+        self.synchronize_step()
         return {"dynamic_loss_scale": self.dynamic_loss_scale, "cur_scale": self.loss_scale,
                 "loss_scaler": self.loss_scaler.state_dict(), "overflow": self.overflow,
                 "optimizer_state_dict": self.optimizer.state_dict(),
                 "fp32_groups": [[m.detach().cpu() for m in g] for g in self.fp32_groups]}
 
     def load_state_dict(self, sd, load_optimizer_states=True):
+        self.synchronize_step()
         self.dynamic_loss_scale = sd.get("dynamic_loss_scale", self.dynamic_loss_scale)
         if "loss_scaler" in sd:
             self.loss_scaler.load_state_dict(sd["loss_scaler"])
@@ -147,6 +205,7 @@ class FP16_UnfusedOptimizer:
                 p.data.copy_(m.data)
 
     def refresh_fp32_params(self):
+        self.synchronize_step()
         for lp_group, fp_group in zip(self.fp16_groups, self.fp32_groups):
             for p, m in zip(lp_group, fp_group):
                 m.data.copy_(p.data.float())
