@@ -525,7 +525,9 @@ def main():
 
     if args.profile_steps > 0:
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        stacks = os.environ.get("DSA_PROFILE_STACK", "0") == "1"
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                     with_stack=stacks) as prof:
             for _ in range(args.profile_steps):
                 train_step()
             sync()
@@ -537,6 +539,13 @@ def main():
                 f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=120,
                                                                            max_name_column_width=60,
                                                                            max_shapes_column_width=120))
+                if stacks:  # where the fills / copies come from (python call sites)
+                    f.write("\n\nfill / zero / copy call sites\n")
+                    for e in prof.key_averages(group_by_stack_n=6):
+                        if any(k in e.key for k in ("fill_", "zero_", "copy_", "aten::zeros", "aten::cat")):
+                            f.write(f"{e.key} count={e.count} device_us={e.device_time_total:.0f}\n")
+                            for fr in e.stack:
+                                f.write(f"    {fr}\n")
 
     global_batch = mb * ga * world
     tokens = global_batch * args.seq * args.steps

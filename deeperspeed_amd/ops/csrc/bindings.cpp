@@ -1008,7 +1008,30 @@ std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, 
 
 void register_gemm_lt(pybind11::module& m);  // gemm_lt.cpp
 
+// ----------------------------------------------------------------------------- streams
+// A HIP stream whose kernels may only occupy the CUs set in `mask` (bit i = CU i of the
+// runtime's CU enumeration).  Side-stream work (an overlapped optimizer step) placed on a
+// subset of the CUs leaves the rest of the chip to the compute stream's GEMMs instead of
+// interleaving workgroups on every CU.  Returned as the raw handle for torch.cuda.ExternalStream;
+// the stream lives for the process.
+int64_t cu_masked_stream(std::vector<int64_t> mask_words) {
+  std::vector<uint32_t> words(mask_words.begin(), mask_words.end());
+  hipStream_t st = nullptr;
+  TORCH_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)words.size(), words.data()) == hipSuccess,
+              "hipExtStreamCreateWithCUMask failed");
+  return reinterpret_cast<int64_t>(st);
+}
+
+int64_t device_cu_count() {
+  int dev = 0, n = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+  return n;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("cu_masked_stream", &cu_masked_stream);
+  m.def("device_cu_count", &device_cu_count);
   register_gemm_lt(m);
   m.def("sum_slices", &sum_slices);
   m.def("dropout_bwd_db", &dropout_bwd_db);

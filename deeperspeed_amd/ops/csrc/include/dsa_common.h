@@ -94,13 +94,19 @@ template <> struct Vec16<float> {
   __device__ __forceinline__ static void store(float* p, const float (&o)[4]) {
     *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
   }
+  // the elements of a raw 16-byte vector already in registers (software-pipelined loads)
+  __device__ __forceinline__ static void unpack(const uint4& v, float (&o)[4]) {
+    o[0] = __uint_as_float(v.x); o[1] = __uint_as_float(v.y); o[2] = __uint_as_float(v.z); o[3] = __uint_as_float(v.w);
+  }
 };
 
 template <typename T16, float (*TO)(uint16_t), uint16_t (*FROM)(float)>
 struct Vec16Half {
   static constexpr int N = 8;
   __device__ __forceinline__ static void load(const T16* p, float (&o)[8]) {
-    uint4 v = *reinterpret_cast<const uint4*>(p);
+    unpack(*reinterpret_cast<const uint4*>(p), o);
+  }
+  __device__ __forceinline__ static void unpack(const uint4& v, float (&o)[8]) {
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

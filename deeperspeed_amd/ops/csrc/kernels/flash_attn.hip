@@ -648,6 +648,15 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     }
     const uint16_t* Ks = smem + (it & 1) * 2 * TS;
     const uint16_t* Vs = Ks + TS;
+    // key biases of this tile issued before the score MFMAs (their latency hides behind them)
+    float4 kb4[BIAS ? 8 : 1];
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int key0 = j0 + 32 * (i >> 2) + 8 * (i & 3) + 4 * h;
+        kb4[i] = key0 < S ? *reinterpret_cast<const float4*>(kbrow + key0) : make_float4(0, 0, 0, 0);
+      }
+    }
     float sv[32];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -676,8 +685,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-          const int key0 = j0 + 32 * t + 8 * rb + 4 * h;
-          const float4 b4 = key0 < S ? *reinterpret_cast<const float4*>(kbrow + key0) : make_float4(0, 0, 0, 0);
+          const float4 b4 = kb4[4 * t + rb];
           float* s4 = sv + 16 * t + 4 * rb;
           s4[0] = fmaf(s4[0], sl2, b4.x * LOG2E);
           s4[1] = fmaf(s4[1], sl2, b4.y * LOG2E);
@@ -1143,6 +1151,14 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
     }
     const uint16_t* Ks = smem + (it & 1) * 2 * TS;
     const uint16_t* Vs = Ks + TS;
+    float4 kb4[BIAS ? 8 : 1];  // key biases of the tile, issued ahead of the MFMAs
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int key0 = j0 + 32 * (i >> 2) + 8 * (i & 3) + 4 * h;
+        kb4[i] = key0 < S ? *reinterpret_cast<const float4*>(kbrow + key0) : make_float4(0, 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       f32x16 sacc, pacc;
@@ -1157,8 +1173,7 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
       if constexpr (BIAS) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-          const int key0 = j0 + 32 * t + 8 * rb + 4 * h;
-          const float4 b4 = key0 < S ? *reinterpret_cast<const float4*>(kbrow + key0) : make_float4(0, 0, 0, 0);
+          const float4 b4 = kb4[4 * t + rb];
           dsv[4 * rb + 0] = fast_exp2(fmaf(sacc[4 * rb + 0], sl2, fmaf(b4.x, LOG2E, -lse2)));
           dsv[4 * rb + 1] = fast_exp2(fmaf(sacc[4 * rb + 1], sl2, fmaf(b4.y, LOG2E, -lse2)));
           dsv[4 * rb + 2] = fast_exp2(fmaf(sacc[4 * rb + 2], sl2, fmaf(b4.z, LOG2E, -lse2)));

@@ -251,16 +251,43 @@ __global__ void __launch_bounds__(256) ln_bwd_wave_kernel(const T* __restrict__ 
     for (int j = 0; j < VN; ++j) { dg[k][j] = 0.f; db[k][j] = 0.f; gm[k][j] = 0.f; }
     if (vi < nvec) Vec16<T>::load(gamma + vi * VN, gm[k]);
   }
-  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
-    const float mu = mean[row], rs = rstd[row];
-    float xh[WV][VN], g[WV][VN];
+  // the row loop is software-pipelined: the next row's x / dy / dres / statistics are loaded
+  // (raw 16-byte vectors) before the current row's reductions, so each wave keeps two rows of
+  // loads in flight -- with ~2 waves per SIMD the loop was latency-bound at ~2.8 TB/s
+  const int64_t rstep = (int64_t)gridDim.x * 4;
+  int64_t row = (int64_t)blockIdx.x * 4 + w;
+  uint4 nx[WV], ng[WV], nr[WV];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int64_t r) {
+    if (r >= rows) return;
+    nmu = mean[r];
+    nrs = rstd[r];
+#pragma unroll
+    for (int k = 0; k < WV; ++k) {
+      const int vi = lane + 64 * k;
+      if (vi < nvec) {
+        nx[k] = *reinterpret_cast<const uint4*>(x + r * H + vi * VN);
+        ng[k] = *reinterpret_cast<const uint4*>(dy + r * H + vi * VN);
+        if (dres) nr[k] = *reinterpret_cast<const uint4*>(dres + r * H + vi * VN);
+      }
+    }
+  };
+  fetch(row);
+  for (; row < rows; row += rstep) {
+    const float mu = nmu, rs = nrs;
+    float xh[WV][VN], g[WV][VN], rr[WV][VN];
+#pragma unroll
+    for (int k = 0; k < WV; ++k) {
+      Vec16<T>::unpack(nx[k], xh[k]);
+      Vec16<T>::unpack(ng[k], g[k]);
+      if (dres) Vec16<T>::unpack(nr[k], rr[k]);
+    }
+    fetch(row + rstep);
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int k = 0; k < WV; ++k) {
       const int vi = lane + 64 * k;
       if (vi < nvec) {
-        Vec16<T>::load(x + row * H + vi * VN, xh[k]);
-        Vec16<T>::load(dy + row * H + vi * VN, g[k]);
 #pragma unroll
         for (int j = 0; j < VN; ++j) {
           xh[k][j] = (xh[k][j] - mu) * rs;
@@ -282,10 +309,8 @@ __global__ void __launch_bounds__(256) ln_bwd_wave_kernel(const T* __restrict__ 
 #pragma unroll
         for (int j = 0; j < VN; ++j) o[j] = rs * (g[k][j] * gm[k][j] - a - xh[k][j] * b);
         if (dres) {
-          float r[VN];
-          Vec16<T>::load(dres + row * H + vi * VN, r);
 #pragma unroll
-          for (int j = 0; j < VN; ++j) o[j] += r[j];
+          for (int j = 0; j < VN; ++j) o[j] += rr[k][j];
         }
         Vec16<T>::store(dx + row * H + vi * VN, o);
       }

@@ -19,9 +19,31 @@ Used by the per-tensor mixed-precision wrapper (runtime/fp16/unfused_optimizer.p
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, List, Sequence
 
 import torch
+
+# DSA_OVERLAP_CUS=n: the side stream may only use n of the CUs (spread evenly over the
+# enumeration, so every XCD keeps most of its CUs for the compute stream); 0 = all CUs
+OVERLAP_CUS = int(os.environ.get("DSA_OVERLAP_CUS", "0"))
+
+
+def side_stream(device, num_cus: int = 0) -> torch.cuda.Stream:
+    """A side stream; with num_cus > 0 one restricted to that many CUs (ops/csrc/bindings.cpp
+    cu_masked_stream)."""
+    if num_cus <= 0:
+        return torch.cuda.Stream(device=device)
+    from ..ops import native
+    hip = native.hip_ops()
+    total = int(hip.device_cu_count())
+    num_cus = min(num_cus, total)
+    step = total / num_cus
+    bits = {int(i * step) for i in range(num_cus)}
+    words = [0] * ((total + 31) // 32)
+    for b in bits:
+        words[b // 32] |= 1 << (b % 32)
+    return torch.cuda.ExternalStream(hip.cu_masked_stream(words), device=device)
 
 
 def _in_backward() -> bool:
@@ -61,7 +83,7 @@ class OverlapStep:
 
     def __init__(self, module: torch.nn.Module, params: Sequence[torch.nn.Parameter], buckets: List[List[int]],
                  device):
-        self.stream = torch.cuda.Stream(device=device)
+        self.stream = side_stream(device, OVERLAP_CUS)
         owner = {id(params[i]): b for b, idxs in enumerate(buckets) for i in idxs}
         self._module_buckets: Dict[torch.nn.Module, list] = {}
         self._handles = []

@@ -511,7 +511,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self._bucket_events: Dict[tuple, torch.cuda.Event] = {}
         if not self._overlap_step:
             return
-        self._step_stream = torch.cuda.Stream(device=self.device)
+        from ..overlap_step import OVERLAP_CUS, side_stream
+        self._step_stream = side_stream(self.device, OVERLAP_CUS)  # DSA_OVERLAP_CUS: CU-masked
         self._bucket_key = {}
         owner = {}
         for gi, g in enumerate(self.groups):

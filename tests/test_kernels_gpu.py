@@ -40,6 +40,29 @@ def test_layernorm_fwd_bwd(dtype, H):
     assert torch.allclose(b.grad.float(), br.grad, atol=gtol * 10, rtol=gtol)
 
 
+@pytest.mark.parametrize("rows", [3, 4100, 8192])
+@pytest.mark.parametrize("H", [768, 1024])
+def test_layernorm_residual_wave_bwd(rows, H):
+    """Wave-per-row LayerNorm backward with the fused residual-gradient add (pre-LN blocks):
+    rows beyond one grid pass exercise the software-pipelined row loop and its tail."""
+    from deeperspeed_amd.ops.native import layer_norm_residual
+    torch.manual_seed(3)
+    x = torch.randn(rows, H, device=_dev(), dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(H, device=_dev())).to(torch.bfloat16).requires_grad_(True)
+    b = (0.1 * torch.randn(H, device=_dev())).to(torch.bfloat16).requires_grad_(True)
+    y, res = layer_norm_residual(x, w, b, 1e-5)
+    dy, dr = torch.randn_like(y), torch.randn_like(res)
+    torch.autograd.backward((y, res), (dy, dr))
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    br = b.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (H,), wr, br, 1e-5)
+    torch.autograd.backward((yr, xr), (dy.float(), dr.float()))
+    assert torch.allclose(x.grad.float(), xr.grad, atol=0.1, rtol=2e-2)
+    assert torch.allclose(w.grad.float(), wr.grad, atol=2e-2 * rows ** 0.5, rtol=2e-2)
+    assert torch.allclose(b.grad.float(), br.grad, atol=2e-2 * rows ** 0.5, rtol=2e-2)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("approx", [False, True])
 def test_bias_gelu(dtype, approx):
