@@ -513,12 +513,16 @@ def main():
 
     dist.barrier()
     sync()
+    if on_gpu:  # trace markers around the timed steps (scripts/prof_summary.py --timed)
+        native.hip_ops().profile_marker(1)
     t_start = time.time()
     for i in range(args.steps):
         loss = train_step()
     sync()
     dist.barrier()
     elapsed = time.time() - t_start
+    if on_gpu:
+        native.hip_ops().profile_marker(2)
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())

@@ -1029,7 +1029,10 @@ int64_t device_cu_count() {
   return n;
 }
 
+void profile_marker(int64_t tag) { dsa::launch_profile_marker((int)tag, cur_stream()); }
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("profile_marker", &profile_marker);
   m.def("cu_masked_stream", &cu_masked_stream);
   m.def("device_cu_count", &device_cu_count);
   register_gemm_lt(m);

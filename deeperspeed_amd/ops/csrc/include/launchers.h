@@ -66,6 +66,8 @@ void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C
                    hipStream_t s);
 // out[c] (+)= sum_r partial[r][c] (fp32 partials, out in dtype dt)
 void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s);
+// empty trace-marker kernel (timed-region boundaries in a rocprofv3 kernel trace)
+void launch_profile_marker(int tag, hipStream_t s);
 
 // transpose.hip: y[C][R] = x[R][C] (16-bit; R % 128 == 0, C % 64 == 0, x row stride ldx).  With
 // `partial` ([R/128, C] fp32 scratch) the column sums of x are also (accumulated) into colsum_out[C].

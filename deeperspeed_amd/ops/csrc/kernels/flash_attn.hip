@@ -584,6 +584,17 @@ __device__ __forceinline__ uint32_t drop_pair(uint32_t hb, int q, int half_s, in
   return drop_mix(((uint32_t)q * (uint32_t)half_s + (uint32_t)j) * 0x85ebca6bu ^ hb);
 }
 
+// EX_BIAS: the head's key-bias row (S fp32) is staged once in LDS behind the K/V double buffer
+// and read per tile with broadcast LDS loads: per-tile global float4 loads of it tripled the
+// vector-memory instructions of the encoder kernels (fwd 31 -> 51 us at B16 H16 S512 D64)
+template <int D>
+__device__ __forceinline__ float* stage_kbias(uint16_t* smem, const float* __restrict__ kbrow, int S) {
+  float* kbs = reinterpret_cast<float*>(smem + 4 * BN2 * (D + 8));
+  for (int i = threadIdx.x; i < S / 4; i += blockDim.x)
+    reinterpret_cast<float4*>(kbs)[i] = reinterpret_cast<const float4*>(kbrow)[i];
+  return kbs;  // visible after the caller's first __syncthreads()
+}
+
 template <typename T, int D, bool CAUSAL, bool LAZY = true, int EX = 0, bool BUF = true>
 __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
@@ -607,6 +618,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
   const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
   const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
+  const float* kbs = BIAS ? stage_kbias<D>(smem, kbrow, S) : nullptr;
 
   s16x8 qf[D / 16];
 #pragma unroll
@@ -648,13 +660,12 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     }
     const uint16_t* Ks = smem + (it & 1) * 2 * TS;
     const uint16_t* Vs = Ks + TS;
-    // key biases of this tile issued before the score MFMAs (their latency hides behind them)
-    float4 kb4[BIAS ? 8 : 1];
+    float4 kb4[BIAS ? 8 : 1];  // this tile's key biases from the LDS-staged row
     if constexpr (BIAS) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int key0 = j0 + 32 * (i >> 2) + 8 * (i & 3) + 4 * h;
-        kb4[i] = key0 < S ? *reinterpret_cast<const float4*>(kbrow + key0) : make_float4(0, 0, 0, 0);
+        kb4[i] = key0 < S ? *reinterpret_cast<const float4*>(kbs + key0) : make_float4(0, 0, 0, 0);
       }
     }
     float sv[32];
@@ -1085,6 +1096,7 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
   const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
   const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
+  const float* kbs = BIAS ? stage_kbias<D>(smem, kbrow, S) : nullptr;
 
   s16x8 qf[D / 16], of[D / 16];
 #pragma unroll
@@ -1151,12 +1163,12 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
     }
     const uint16_t* Ks = smem + (it & 1) * 2 * TS;
     const uint16_t* Vs = Ks + TS;
-    float4 kb4[BIAS ? 8 : 1];  // key biases of the tile, issued ahead of the MFMAs
+    float4 kb4[BIAS ? 8 : 1];  // the tile's key biases from the LDS-staged row
     if constexpr (BIAS) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int key0 = j0 + 32 * (i >> 2) + 8 * (i & 3) + 4 * h;
-        kb4[i] = key0 < S ? *reinterpret_cast<const float4*>(kbrow + key0) : make_float4(0, 0, 0, 0);
+        kb4[i] = key0 < S ? *reinterpret_cast<const float4*>(kbs + key0) : make_float4(0, 0, 0, 0);
       }
     }
 #pragma unroll
@@ -2127,10 +2139,13 @@ void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, f
                          int onh, int inh, int64_t ild) {
   const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild);
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
+  const int kb_lds = kbias ? 4 * S : 0;  // the LDS-staged key-bias row
+  if (kb_lds && fa::fwd_v2_lds<128>() + kb_lds > 160 * 1024)
+    throw std::runtime_error("flash fwd: key-bias row too long for LDS staging");
   if ((int64_t)S * (ild > 0 ? ild : D) * 2 >= (1LL << 31))
     throw std::runtime_error("flash fwd: S * row stride too large for 32-bit buffer offsets");
   FA_EX_DISPATCH(dt, D, kbias, pdrop,
-    hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, false, true, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
+    hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, false, true, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>() + kb_lds, s,
                        (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale, onh,
                        ex));
 }
@@ -2141,6 +2156,9 @@ void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const v
                          int onh, int inh, int64_t ild) {
   const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild);
   const int64_t rows = (int64_t)BH * S;
+  const int kb_lds = kbias ? 4 * S : 0;  // the dQ kernel's LDS-staged key-bias row
+  if (kb_lds && fa::fwd_v2_lds<128>() + kb_lds > 160 * 1024)
+    throw std::runtime_error("flash bwd: key-bias row too long for LDS staging");
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
   // DSA_FLASH_BWD_MERGE=1: dK/dV and dQ workgroups in one launch (measured neutral, r2v)
   static const bool merge = getenv("DSA_FLASH_BWD_MERGE") && getenv("DSA_FLASH_BWD_MERGE")[0] == '1';
@@ -2159,14 +2177,14 @@ void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const v
                          (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex);
     else if (merge)
       hipLaunchKernelGGL((fa::bwd_both_v2_kernel<T, DD, false, EE>), dim3(2 * grid), dim3(256),
-                         fa::dkdv_v2_lds<DD>(), s, (int)grid, (const uint16_t*)q, (const uint16_t*)k,
+                         std::max(fa::dkdv_v2_lds<DD>(), fa::fwd_v2_lds<DD>() + kb_lds), s, (int)grid, (const uint16_t*)q, (const uint16_t*)k,
                          (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq, (uint16_t*)dk,
                          (uint16_t*)dv, S, scale, onh, ex);
     else {
       hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::dkdv_v2_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                          (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex);
-      hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
+      hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>() + kb_lds, s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                          (uint16_t*)dq, S, scale, onh, ex);
     });

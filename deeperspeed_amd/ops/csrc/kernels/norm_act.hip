@@ -727,4 +727,13 @@ void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C
                        accum));
 }
 
+// Empty kernel whose only purpose is its name in a kernel trace: bench.py launches it with
+// tag 1 right before and tag 2 right after the timed steps, so scripts/prof_summary.py --timed
+// can restrict a rocprofv3 trace to the timed region (no init / warmup / memory-fit kernels).
+__global__ void dsa_profile_marker_kernel(int tag) { (void)tag; }
+
+void launch_profile_marker(int tag, hipStream_t s) {
+  hipLaunchKernelGGL(dsa_profile_marker_kernel, dim3(1), dim3(64), 0, s, tag);
+}
+
 }  // namespace dsa

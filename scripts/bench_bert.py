@@ -78,12 +78,16 @@ def main():
         loss = step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+        from deeperspeed_amd.ops import native
+        native.hip_ops().profile_marker(1)  # timed-region trace markers (scripts/prof_summary.py --timed)
     t0 = time.time()
     for _ in range(args.steps):
         loss = step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = (time.time() - t0) / args.steps
+    if dev.type == "cuda":
+        native.hip_ops().profile_marker(2)
     if args.torch_profile:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
