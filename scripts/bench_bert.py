@@ -90,7 +90,8 @@ def main():
         native.hip_ops().profile_marker(2)
     if args.torch_profile:
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                     with_stack=True) as prof:
             step()
             torch.cuda.synchronize()
         with open(args.torch_profile, "w") as f:
@@ -99,6 +100,14 @@ def main():
             f.write(prof.key_averages(group_by_input_shape=True).table(sort_by="count", row_limit=60,
                                                                         max_name_column_width=50,
                                                                         max_shapes_column_width=90))
+            f.write("\n\nsmall copy / fill / memset call sites (python frames)\n")
+            for e in prof.key_averages(group_by_stack_n=8):
+                if any(k in e.key for k in ("copy_", "fill_", "zero_", "aten::zeros", "aten::cat", "contiguous",
+                                            "aten::to", "_foreach", "aten::empty_like")) and e.count:
+                    f.write(f"{e.key} count={e.count} device_us={e.device_time_total:.0f} "
+                            f"cpu_us={e.cpu_time_total:.0f}\n")
+                    for fr in e.stack:
+                        f.write(f"    {fr}\n")
     sps = B / dt
     tflops = sps * cfg.flops_per_sample(S, npred) / 1e12
     ref = REF.get(S)

@@ -13,4 +13,5 @@ timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r3o_prof20b 
 grep -o '"value": [0-9.]*' $R/gpurun_out/r3o_prof20b.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r3o_profbert -o bert --output-format csv -- python3 $R/scripts/bench_bert.py --seq 128 --batch 64 --steps 20 --warmup 5 > $R/gpurun_out/r3o_profbert.json 2> $R/gpurun_out/r3o_profbert.log || { echo "bert rocprof failed"; tail -20 $R/gpurun_out/r3o_profbert.log; exit 1; }
 grep -o '"value": [0-9.]*' $R/gpurun_out/r3o_profbert.json
+cd $R && timeout -k 10 200 python scripts/bench_bert.py --seq 128 --batch 64 --steps 5 --warmup 3 --torch-profile gpurun_out/r3o_bert_torchprof.txt > gpurun_out/r3o_bert_tp.json 2> gpurun_out/r3o_bert_tp.log || { tail -20 gpurun_out/r3o_bert_tp.log; exit 1; }
 echo done
