@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import native
-from ..ops.linear import Linear, grad_only_linear, linear, nt_wgrad_planned
+from ..ops.linear import Linear, grad_only_linear, linear, nt_wgrad_planned, zero_placeholder
 from ..ops.attention import attention, rotary_split
 from ..runtime.activation_checkpointing import checkpointing as ds_ckpt
 
@@ -162,7 +162,7 @@ class _GradOnlySum(torch.autograd.Function):
     @staticmethod
     def forward(ctx, *xs):
         ctx.n = len(xs)
-        return xs[0].new_zeros(1).expand(xs[0].shape)
+        return zero_placeholder(xs[0], xs[0].shape)
 
     @staticmethod
     def backward(ctx, g):

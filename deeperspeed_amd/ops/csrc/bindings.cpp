@@ -192,7 +192,10 @@ std::vector<Tensor> ln_fwd(Tensor x, Tensor gamma, OptT beta, double eps, OptT r
 }
 
 // Returns (dx, dgamma, dbeta)
-std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, bool has_beta, OptT dres) {
+// dgamma_acc / dbeta_acc: existing gradient buffers the parameter gradients are accumulated into
+// (the engine's bound p.grad views) instead of fresh tensors for autograd to add
+std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, bool has_beta, OptT dres,
+                           OptT dgamma_acc, OptT dbeta_acc) {
   check_dev(dy, "dy"); check_dev(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "ln_bwd: dy/x mismatch");
   const int64_t H = x.size(-1);
@@ -201,14 +204,22 @@ std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tenso
   if (dres.has_value()) TORCH_CHECK(dres->sizes() == x.sizes() && dres->is_contiguous(), "ln_bwd: dres");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Tensor dx = at::empty_like(x);
-  Tensor dgamma = at::empty_like(gamma);
-  Tensor dbeta = has_beta ? at::empty_like(gamma) : Tensor();
+  const bool acc = dgamma_acc.has_value();
+  if (acc) {
+    TORCH_CHECK(dgamma_acc->sizes() == gamma.sizes() && dgamma_acc->scalar_type() == gamma.scalar_type() &&
+                dgamma_acc->is_contiguous(), "ln_bwd: dgamma_acc must match gamma");
+    TORCH_CHECK(!has_beta || (dbeta_acc.has_value() && dbeta_acc->sizes() == gamma.sizes() &&
+                              dbeta_acc->scalar_type() == gamma.scalar_type() && dbeta_acc->is_contiguous()),
+                "ln_bwd: dbeta_acc must match gamma");
+  }
+  Tensor dgamma = acc ? *dgamma_acc : at::empty_like(gamma);
+  Tensor dbeta = has_beta ? (acc ? *dbeta_acc : at::empty_like(gamma)) : Tensor();
   const int grid = dsa::ln_bwd_grid(rows);
   Tensor partial = at::empty({2 * (int64_t)grid * H}, x.options().dtype(at::kFloat));
   dsa::launch_ln_bwd(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                      dres.has_value() ? dres->data_ptr() : nullptr, dx.data_ptr(), dgamma.data_ptr(),
                      has_beta ? dbeta.data_ptr() : nullptr, partial.data_ptr<float>(), rows, (int)H, dcode(x),
-                     cur_stream());
+                     cur_stream(), acc ? 1 : 0);
   return {dx, dgamma, dbeta};
 }
 
@@ -1076,7 +1087,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("wd"), py::arg("bc1"), py::arg("bc2"), py::arg("grad_scale"), py::arg("max_coeff"), py::arg("min_coeff"),
         py::arg("adamw"), py::arg("partial"), py::arg("coeff"), py::arg("scale") = py::none());
   m.def("ln_fwd", &ln_fwd);
-  m.def("ln_bwd", &ln_bwd);
+  m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("has_beta"), py::arg("dres") = py::none(), py::arg("dgamma_acc") = py::none(),
+        py::arg("dbeta_acc") = py::none());
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("bias_gelu_fwd_t", &bias_gelu_fwd_t);

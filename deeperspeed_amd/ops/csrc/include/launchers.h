@@ -48,7 +48,7 @@ void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_o
                    hipStream_t s);
 void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    const void* dres, void* dx, void* dgamma, void* dbeta, float* partial, int64_t rows, int H,
-                   int dt, hipStream_t s);
+                   int dt, hipStream_t s, int accum = 0);  // accum: dgamma / dbeta += the new sums
 // y = a + b (+ c), n % (16 B / elem) == 0
 void launch_sum_slices(const void* part, int S, int64_t n, void* out, bool out_f32, int accum, int dt,
                        hipStream_t s);

@@ -524,7 +524,7 @@ int ln_bwd_grid(int64_t rows) { return (int)(rows < 512 ? rows : 512); }
 // partial workspace: 2 * ln_bwd_grid(rows) * H floats
 void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    const void* dres, void* dx, void* dgamma, void* dbeta, float* partial, int64_t rows, int H,
-                   int dt, hipStream_t s) {
+                   int dt, hipStream_t s, int accum) {
   if (rows <= 0) return;
   const bool wave = ln_wave(H, dt);
   // partial rows: one per block (<= ln_bwd_grid(rows), the caller's workspace)
@@ -540,7 +540,7 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
                          (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
                          partial, rows, H));
     hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 15) / 16, dbeta ? 2 : 1), dim3(256), 0, s, partial, grid, H,
-                       (T*)dgamma, 0, (int64_t)grid * H, (T*)dbeta));
+                       (T*)dgamma, accum, (int64_t)grid * H, (T*)dbeta));
 }
 
 void launch_add3(const void* a, const void* b, const void* c, void* y, int64_t n, int dt, hipStream_t s) {

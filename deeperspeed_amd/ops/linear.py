@@ -284,6 +284,20 @@ class _AccumLinear(torch.autograd.Function):
         return dx, dw, db, None
 
 
+_ZERO = {}
+
+
+def zero_placeholder(like: torch.Tensor, shape) -> torch.Tensor:
+    """A zero-stride view of one cached zero element (per dtype / device) expanded to `shape`:
+    the value of an output nobody reads.  Reusing the element avoids a one-element fill kernel
+    per call (~600 launches per 20B step from the recompute's gradient-only ops)."""
+    key = (like.dtype, like.device)
+    z = _ZERO.get(key)
+    if z is None:
+        z = _ZERO[key] = torch.zeros(1, dtype=like.dtype, device=like.device)
+    return z.expand(*shape)
+
+
 class _GradOnlyLinear(torch.autograd.Function):
     """y = x W^T + b whose VALUE is never read: forward returns a zero-stride placeholder and
     costs nothing; backward produces the exact input / weight / bias gradients."""
@@ -293,7 +307,7 @@ class _GradOnlyLinear(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
         ctx.share_gt = share_gt
-        return x.new_zeros(1).expand(*x.shape[:-1], weight.shape[0])
+        return zero_placeholder(x, (*x.shape[:-1], weight.shape[0]))
 
     @staticmethod
     def backward(ctx, g):

@@ -49,6 +49,21 @@ def _ln_ref(x, gamma, beta, eps):
     return y.to(x.dtype), mean.reshape(-1), rstd.reshape(-1)
 
 
+def _ln_param_acc(ctx):
+    """(gamma.grad, beta.grad) when both are bound gradient buffers the LN-backward column sums
+    can accumulate into (the engine's p.grad views; ops/linear.py does the same for weights):
+    autograd then gets None for them and its AccumulateGrad add over the parameter disappears."""
+    from .linear import FUSE_WGRAD, _bound_grad
+    g, b = ctx.params
+    if not (FUSE_WGRAD and ctx.needs_input_grad[1]) or (b is not None and not ctx.needs_input_grad[2]):
+        return None
+    gg = _bound_grad(g)
+    gb = _bound_grad(b) if b is not None else None
+    if gg is None or not gg.is_contiguous() or (b is not None and (gb is None or not gb.is_contiguous())):
+        return None
+    return gg, gb
+
+
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, eps):
@@ -60,12 +75,17 @@ class _LayerNormFn(torch.autograd.Function):
             y, mean, rstd = _ln_ref(x, gamma, beta, eps)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.has_beta = beta is not None
+        ctx.params = (gamma, beta)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, gamma, mean, rstd = ctx.saved_tensors
         dy = dy.contiguous()
+        acc = _ln_param_acc(ctx) if x.is_cuda else None
+        if acc is not None:
+            dx, _, _ = hip_ops().ln_bwd(dy, x, gamma, mean, rstd, ctx.has_beta, None, acc[0], acc[1])
+            return dx, None, None, None
         if x.is_cuda:
             dx, dg, db = hip_ops().ln_bwd(dy, x, gamma, mean, rstd, ctx.has_beta, None)
         else:
@@ -101,6 +121,7 @@ class _LayerNormResidualFn(torch.autograd.Function):
             y, mean, rstd = _ln_ref(x, gamma, beta, eps)
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.has_beta = beta is not None
+        ctx.params = (gamma, beta)
         return y, x
 
     @staticmethod
@@ -110,6 +131,10 @@ class _LayerNormResidualFn(torch.autograd.Function):
             dx, dg, db, _ = _LayerNormFn.backward(ctx, dy)
             return (dx if dres is None else dx + dres), dg, db, None
         dres = None if dres is None else dres.contiguous()
+        acc = _ln_param_acc(ctx)
+        if acc is not None:
+            dx, _, _ = hip_ops().ln_bwd(dy.contiguous(), x, gamma, mean, rstd, ctx.has_beta, dres, acc[0], acc[1])
+            return dx, None, None, None
         dx, dg, db = hip_ops().ln_bwd(dy.contiguous(), x, gamma, mean, rstd, ctx.has_beta, dres)
         return dx, dg, (db if ctx.has_beta else None), None
 

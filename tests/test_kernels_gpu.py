@@ -63,6 +63,33 @@ def test_layernorm_residual_wave_bwd(rows, H):
     assert torch.allclose(b.grad.float(), br.grad, atol=2e-2 * rows ** 0.5, rtol=2e-2)
 
 
+@pytest.mark.parametrize("residual", [False, True])
+@pytest.mark.parametrize("H", [1024, 6144])
+def test_layernorm_accumulates_into_bound_param_grads(residual, H):
+    """With gamma.grad / beta.grad already bound (engine gradient views), the LN backward adds
+    its column sums into them in the colsum kernel (autograd gets None): same result as autograd
+    adding fresh gradients."""
+    from deeperspeed_amd.ops.native import FusedLayerNorm
+    torch.manual_seed(5)
+    ln = FusedLayerNorm(H, 1e-5, dtype=torch.bfloat16, device=_dev())
+    with torch.no_grad():
+        ln.weight.add_(0.1 * torch.randn_like(ln.weight))
+        ln.bias.add_(0.1 * torch.randn_like(ln.bias))
+    x = torch.randn(512, H, device=_dev(), dtype=torch.bfloat16, requires_grad=True)
+    dy = torch.randn(512, H, device=_dev(), dtype=torch.bfloat16)
+
+    def run():
+        out = ln(x, residual_out=True)[0] if residual else ln(x)
+        out.backward(dy)
+
+    run()  # first use: fresh gradients through autograd
+    g1, b1 = ln.weight.grad.clone(), ln.bias.grad.clone()
+    x.grad = None
+    run()  # bound gradients: accumulated in place by the kernel
+    assert torch.allclose(ln.weight.grad.float(), 2 * g1.float(), rtol=2e-2, atol=2e-2)
+    assert torch.allclose(ln.bias.grad.float(), 2 * b1.float(), rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("approx", [False, True])
 def test_bias_gelu(dtype, approx):
