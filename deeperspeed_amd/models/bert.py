@@ -71,9 +71,9 @@ class BertForPreTraining(nn.Module):
         super().__init__()
         self.cfg = cfg
         H = cfg.hidden_size
-        self.word_embeddings = nn.Embedding(cfg.vocab_size, H)
-        self.position_embeddings = nn.Embedding(cfg.max_position, H)
-        self.token_type_embeddings = nn.Embedding(cfg.type_vocab_size, H)
+        self.word_embeddings = native.Embedding(cfg.vocab_size, H)
+        self.position_embeddings = native.Embedding(cfg.max_position, H)
+        self.token_type_embeddings = native.Embedding(cfg.type_vocab_size, H)
         self.embeddings_ln = native.FusedLayerNorm(H, cfg.layer_norm_eps)
         lcfg = DeepSpeedTransformerConfig(batch_size=-1, hidden_size=H, intermediate_size=cfg.intermediate_size,
                                           heads=cfg.num_heads, attn_dropout_ratio=cfg.attn_dropout,

@@ -123,8 +123,8 @@ class GPT2(nn.Module):
     def __init__(self, cfg: GPT2Config, device=None, dtype=None):
         super().__init__()
         self.cfg = cfg
-        self.wte = nn.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
-        self.wpe = nn.Embedding(cfg.n_positions, cfg.hidden_size, device=device, dtype=dtype)
+        self.wte = native.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
+        self.wpe = native.Embedding(cfg.n_positions, cfg.hidden_size, device=device, dtype=dtype)
         self.h = nn.ModuleList([GPT2Block(cfg, device, dtype) for _ in range(cfg.num_layers)])
         self.head = GPT2LMHead(cfg, self.wte, device, dtype)
         self.reset_parameters()

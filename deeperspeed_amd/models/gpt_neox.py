@@ -406,7 +406,7 @@ class GPTNeoX(nn.Module):
     def __init__(self, cfg: GPTNeoXConfig, device=None, dtype=None):
         super().__init__()
         self.cfg = cfg
-        self.embed_in = nn.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
+        self.embed_in = native.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
         self.layers = nn.ModuleList([NeoXTransformerLayer(cfg, i, device, dtype) for i in range(cfg.num_layers)])
         link_stash_prefetch([l.attention for l in self.layers])
         self.final_layer_norm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
@@ -446,7 +446,7 @@ def lm_loss(logits, labels, internal=False):
 class _EmbedPipe(nn.Module):
     def __init__(self, cfg, device=None, dtype=None):
         super().__init__()
-        self.embed_in = nn.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
+        self.embed_in = native.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
         nn.init.normal_(self.embed_in.weight, 0.0, cfg.init_std)
 
     def forward(self, input_ids):

@@ -1042,8 +1042,30 @@ int64_t device_cu_count() {
 
 void profile_marker(int64_t tag) { dsa::launch_profile_marker((int)tag, cur_stream()); }
 
+// dw[V, H] (+)= scatter-sum of dy[n, H] rows by token id, from ids sorted on the device (values and
+// the permutation of torch.sort): no device -> host read anywhere (ops/csrc/kernels/embedding.hip)
+Tensor embedding_bwd(Tensor sorted_ids, Tensor perm, Tensor dy, Tensor dw, int64_t padding_idx, bool accumulate) {
+  check_dev(sorted_ids, "sorted_ids"); check_dev(perm, "perm"); check_dev(dy, "dy"); check_dev(dw, "dw");
+  TORCH_CHECK(sorted_ids.scalar_type() == at::kLong && perm.scalar_type() == at::kLong &&
+              sorted_ids.is_contiguous() && perm.is_contiguous() && sorted_ids.numel() == perm.numel(),
+              "embedding_bwd: int64 sorted ids / permutation of equal length");
+  TORCH_CHECK(dy.dim() == 2 && dw.dim() == 2 && dy.size(1) == dw.size(1) && dy.size(0) == sorted_ids.numel(),
+              "embedding_bwd: dy [n, H], dw [V, H]");
+  TORCH_CHECK(dy.is_contiguous() && dw.is_contiguous() && dy.scalar_type() == dw.scalar_type() &&
+              dy.element_size() == 2 && dw.size(1) % 8 == 0, "embedding_bwd: contiguous 16-bit rows, H % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  const int64_t n = dy.size(0), H = dy.size(1);
+  const int64_t nc = dsa::embedding_bwd_chunks(n);
+  Tensor ws = at::empty({2 * nc * H}, dy.options().dtype(at::kFloat));
+  dsa::launch_embedding_bwd_sorted(sorted_ids.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dy.data_ptr(),
+                                   dw.data_ptr(), ws.data_ptr<float>(), ws.data_ptr<float>() + nc * H, n, (int)H,
+                                   padding_idx, accumulate ? 1 : 0, dcode(dy), cur_stream());
+  return dw;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("profile_marker", &profile_marker);
+  m.def("embedding_bwd", &embedding_bwd);
   m.def("cu_masked_stream", &cu_masked_stream);
   m.def("device_cu_count", &device_cu_count);
   register_gemm_lt(m);

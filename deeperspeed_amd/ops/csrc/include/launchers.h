@@ -66,6 +66,11 @@ void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C
                    hipStream_t s);
 // out[c] (+)= sum_r partial[r][c] (fp32 partials, out in dtype dt)
 void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s);
+// embedding.hip: sync-free deterministic embedding backward over sorted ids (H % 8 == 0)
+int64_t embedding_bwd_chunks(int64_t n);
+void launch_embedding_bwd_sorted(const int64_t* sorted_ids, const int64_t* perm, const void* dy, void* dw,
+                                 float* head, float* cont, int64_t n, int H, int64_t padding_idx, int accumulate,
+                                 int dt, hipStream_t s);
 // empty trace-marker kernel (timed-region boundaries in a rocprofv3 kernel trace)
 void launch_profile_marker(int tag, hipStream_t s);
 

@@ -37,8 +37,13 @@ class FusedLamb(torch.optim.Optimizer):
 
     supports_fused_lp_step = True  # FP16_UnfusedOptimizer passes low-precision grads/outputs
 
+    @property
+    def supports_device_scale(self):
+        """step(scale_tensor=...) is honoured (the multi-tensor GPU kernels read it)."""
+        return self.multi_tensor
+
     @torch.no_grad()
-    def step(self, closure=None, grads=None, output_params=None, scale=1.0, grad_norms=None):
+    def step(self, closure=None, grads=None, output_params=None, scale=1.0, grad_norms=None, scale_tensor=None):
         """`grads`/`output_params`/`scale` follow the reference's legacy fused interface:
         optional explicit gradient lists, low-precision output copies and a loss scale the
         gradients are divided by.  GPU tensors of one (dtype, step) bucket are updated by the
@@ -65,6 +70,8 @@ class FusedLamb(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros(p.numel(), dtype=torch.float32, device=p.device)
                     st["exp_avg_sq"] = torch.zeros(p.numel(), dtype=torch.float32, device=p.device)
                 st["step"] += 1
+                if scale_tensor is not None and not (p.is_cuda and self.multi_tensor):
+                    raise RuntimeError("FusedLamb: scale_tensor needs the multi-tensor GPU path")
                 if p.is_cuda and self.multi_tensor:
                     key = (p.device, p.dtype, g.dtype, o.dtype if o is not None else None, st["step"])
                     buckets.setdefault(key, []).append((p, g.contiguous(), o))
@@ -75,7 +82,8 @@ class FusedLamb(torch.optim.Optimizer):
                                  group["max_coeff"], group["min_coeff"], self.eps_mode == 1)
                 self.lamb_coeffs.append(c)
             for (dev, pdt, gdt, odt, step), items in buckets.items():
-                self.lamb_coeffs.append(self._multi_step(dev, pdt, gdt, odt, step, items, group, 1.0 / scale))
+                self.lamb_coeffs.append(self._multi_step(dev, pdt, gdt, odt, step, items, group, 1.0 / scale,
+                                                         scale_tensor))
         return loss
 
     @torch.no_grad()

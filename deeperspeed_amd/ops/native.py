@@ -857,3 +857,53 @@ def bias_dropout_residual(x, bias, residual, p, training=True, generator=None):
     if not training or p <= 0:
         return residual + (x + bias)
     return _BiasDropoutResidualFn.apply(x, bias, residual, float(p), _draw_seed(generator))
+
+
+# --------------------------------------------------------------------------- embedding
+class _EmbeddingFn(torch.autograd.Function):
+    """Embedding lookup whose backward never reads anything back to the host: ids are sorted on
+    the device and ops/csrc/kernels/embedding.hip sums the rows of equal ids in fp32 (fixed
+    order: deterministic), launches sized by the token count.  PyTorch's dense embedding backward
+    reads the number of distinct ids back to the host, which drains the GPU queue at the end of
+    every backward.  With a bound weight gradient (the engine's p.grad view) the rows are added
+    into it in place, like the fused weight gradients of ops/linear.py."""
+
+    @staticmethod
+    def forward(ctx, ids, weight, padding_idx):
+        ctx.save_for_backward(ids)
+        ctx.weight = weight
+        ctx.padding_idx = padding_idx
+        return torch.nn.functional.embedding(ids, weight, padding_idx if padding_idx >= 0 else None)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ids,) = ctx.saved_tensors
+        w = ctx.weight
+        H = w.shape[1]
+        sorted_ids, perm = torch.sort(ids.reshape(-1), stable=True)
+        g2 = g.reshape(-1, H).contiguous()
+        from .linear import FUSE_WGRAD, _bound_grad
+        bound = _bound_grad(w) if FUSE_WGRAD else None
+        if bound is not None and bound.is_contiguous():
+            hip_ops().embedding_bwd(sorted_ids, perm, g2, bound, ctx.padding_idx, True)
+            return None, None, None
+        dw = torch.zeros(w.shape, dtype=g2.dtype, device=g2.device)
+        hip_ops().embedding_bwd(sorted_ids, perm, g2, dw, ctx.padding_idx, False)
+        return None, dw, None
+
+
+def embedding_supported(weight: torch.Tensor) -> bool:
+    return (weight.is_cuda and weight.dtype in (torch.bfloat16, torch.float16) and weight.dim() == 2
+            and weight.shape[1] % 8 == 0 and weight.is_contiguous())
+
+
+class Embedding(torch.nn.Embedding):
+    """nn.Embedding (same parameters / state dict) with the sync-free HIP backward on the GPU
+    (16-bit weights, width % 8 == 0, dense gradients); otherwise torch's embedding."""
+
+    def forward(self, ids):
+        if (embedding_supported(self.weight) and self.max_norm is None and not self.sparse
+                and not self.scale_grad_by_freq and torch.is_grad_enabled() and self.weight.requires_grad):
+            pad = -1 if self.padding_idx is None else int(self.padding_idx)
+            return _EmbeddingFn.apply(ids, self.weight, pad)
+        return super().forward(ids)

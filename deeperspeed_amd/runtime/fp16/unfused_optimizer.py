@@ -10,6 +10,7 @@ buffered_allreduce_fallback), exactly like the reference.
 """
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -17,6 +18,10 @@ import torch.distributed as dist
 from ...utils.logging import logger
 from ..utils import CheckOverflow, get_grad_norm, grad_norm_sq_tensor
 from .loss_scaler import DynamicLossScaler, LossScaler
+
+
+# bf16 / static-scale steps without a host read of the gradient norm (DSA_SYNC_FREE_STEP=0: off)
+SYNC_FREE_STEP = os.environ.get("DSA_SYNC_FREE_STEP", "1") != "0"
 
 
 class FP16_UnfusedOptimizer:
@@ -71,7 +76,28 @@ class FP16_UnfusedOptimizer:
         return self.loss_scaler.loss_scale
 
     def get_global_grad_norm(self):
+        if torch.is_tensor(self._global_grad_norm):  # sync-free step: read on demand only
+            self._global_grad_norm = float(self._global_grad_norm)
         return self._global_grad_norm
+
+    def _sync_free(self, params):
+        """Static loss scale 1 (bf16) with the fused multi-tensor LAMB: the unscale x clip factor
+        is formed on the device and a non-finite gradient norm makes the kernels skip the update
+        (LambArgs.scale_ptr), so the step needs no host read and the host keeps queueing the next
+        forward.  The host-side overflow flag then stays False (the skipped-step count and the LR
+        schedule are not rolled back on the -- for bf16 diverged -- non-finite step)."""
+        return (SYNC_FREE_STEP and not self.dynamic_loss_scale and self.loss_scale == 1.0
+                and getattr(self.optimizer, "supports_device_scale", False) and params
+                and all(p.is_cuda for p in params))
+
+    def _device_coef(self, params):
+        sq = grad_norm_sq_tensor(params, mpu=self.mpu)
+        norm = sq.sqrt()
+        self._global_grad_norm = norm
+        coef = torch.ones_like(norm)
+        if self.clip_grad > 0:
+            coef = torch.where(norm > self.clip_grad, self.clip_grad / (norm + 1e-6), coef)
+        return torch.where(torch.isfinite(sq), coef, torch.full_like(coef, float("nan")))
 
     # ----------------------------------------------------------------- overlapped step
     def _setup_overlap(self, module, bucket_numel, verbose):
@@ -137,6 +163,19 @@ class FP16_UnfusedOptimizer:
 
     def step(self, closure=None):
         params = [p for g in self.fp16_groups for p in g]
+        if self._sync_free(params):
+            coef_t = self._device_coef(params)
+            self.overflow = False
+            if self._overlap is not None:
+                self._overlapped_fused_step(coef_t)
+                return self.overflow
+            grads, outs = [], []
+            for lp_group in self.fp16_groups:
+                grads.append([p.grad for p in lp_group])
+                outs.append([p.data for p in lp_group])
+            self.optimizer.step(grads=grads, output_params=outs, scale=1.0, scale_tensor=coef_t)
+            self.zero_grad()
+            return self.overflow
         # one multi-tensor reduction gives both the global norm and the overflow flag (the sum
         # of squares is inf/nan iff some gradient entry is): no per-tensor isinf/isnan passes
         sq = grad_norm_sq_tensor(params, mpu=self.mpu).item()

@@ -100,3 +100,24 @@ def test_lamb_device_scale_skips_non_finite():
         assert torch.equal(a, w)
     for m in m_nan:
         assert torch.count_nonzero(m).item() == 0
+
+
+@pytest.mark.parametrize("clip", [0.0, 0.05])
+def test_sync_free_step_matches_host_checked_step(monkeypatch, clip):
+    """bf16 LAMB step with the clip factor formed on the device (no host read of the norm) vs the
+    host-checked step: identical without clipping, equal to fp32 rounding of the factor with."""
+    from deeperspeed_amd.runtime.fp16 import unfused_optimizer as uo
+    monkeypatch.setattr(uo, "SYNC_FREE_STEP", False)
+    host_l, host_w, _, host_n, _ = _train(False, clip, steps=3)
+    monkeypatch.setattr(uo, "SYNC_FREE_STEP", True)
+    dev_l, dev_w, _, dev_n, _ = _train(False, clip, steps=3)
+    assert abs(host_n - dev_n) <= 1e-3 * host_n
+    if clip == 0.0:
+        assert host_l == dev_l
+        for a, b in zip(host_w, dev_w):
+            assert torch.equal(a, b)
+    else:
+        for a, b in zip(host_l, dev_l):
+            assert abs(a - b) <= 1e-3 * abs(a)
+        for a, b in zip(host_w, dev_w):
+            assert torch.allclose(a, b, rtol=1e-2, atol=1e-3)
