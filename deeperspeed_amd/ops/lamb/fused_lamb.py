@@ -129,7 +129,9 @@ class FusedLamb(torch.optim.Optimizer):
             rows = ([t.data_ptr() for t in ws] + [t.data_ptr() for t in gs] + [t.data_ptr() for t in ms] +
                     [t.data_ptr() for t in vs] + [(o.data_ptr() if o is not None else 0) for o in outs] + numels
                     + pref)
-            meta = torch.tensor(rows, dtype=torch.int64).to(dev)
+            # pinned staging + async copy: a pageable H2D copy would wait for the whole stream
+            # (the gradients are new tensors every step, so this runs every step)
+            meta = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
             hit = (meta, len(ws), pref[-1], torch.empty(2 * pref[-1], dtype=torch.float32, device=dev))
             if len(self._meta_cache) > 64:
                 self._meta_cache.clear()
