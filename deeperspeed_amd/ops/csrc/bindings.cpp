@@ -645,18 +645,27 @@ void sparse_softmax_bwd(Tensor y, Tensor dy, Tensor dx, Tensor rowptr, int64_t H
 }
 
 // ----------------------------------------------------------------------------- dropout
-std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, int64_t offset) {
+// optional device RNG state int64 [seed, step] (graph-replayable dropout, dropout.hip rng_apply)
+static const int64_t* rng_ptr(const OptT& rng, const Tensor& like) {
+  if (!rng.has_value()) return nullptr;
+  TORCH_CHECK(rng->scalar_type() == at::kLong && rng->numel() == 2 && rng->is_contiguous() &&
+              rng->device() == like.device(), "rng must be a contiguous int64 [seed, step] on the tensor's device");
+  return rng->data_ptr<int64_t>();
+}
+
+std::vector<Tensor> dropout_fwd(Tensor x, double p, int64_t seed, int64_t offset, OptT rng) {
   check_dev(x, "x");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   Tensor y = at::empty_like(x);
   Tensor mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
   dsa::launch_dropout_fwd(x.data_ptr(), y.data_ptr(), mask.data_ptr<uint8_t>(), x.numel(), (float)p, (uint64_t)seed,
-                          (uint64_t)offset, dcode(x), cur_stream());
+                          (uint64_t)offset, dcode(x), cur_stream(), rng_ptr(rng, x));
   return {y, mask};
 }
 
 // y = res + dropout(x + bias); x/res [rows, C], bias [C]
-std::vector<Tensor> bias_dropout_residual(Tensor x, Tensor bias, Tensor res, double p, int64_t seed, int64_t offset) {
+std::vector<Tensor> bias_dropout_residual(Tensor x, Tensor bias, Tensor res, double p, int64_t seed, int64_t offset,
+                                          OptT rng) {
   check_dev(x, "x"); check_dev(bias, "bias"); check_dev(res, "res");
   const int64_t C = x.size(-1);
   TORCH_CHECK(bias.numel() == C && res.sizes() == x.sizes() && x.scalar_type() == res.scalar_type() &&
@@ -666,7 +675,7 @@ std::vector<Tensor> bias_dropout_residual(Tensor x, Tensor bias, Tensor res, dou
   Tensor mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
   dsa::launch_bias_dropout_residual(x.data_ptr(), bias.data_ptr(), res.data_ptr(), y.data_ptr(),
                                     mask.data_ptr<uint8_t>(), x.numel() / C, (int)C, (float)p, (uint64_t)seed,
-                                    (uint64_t)offset, dcode(x), cur_stream());
+                                    (uint64_t)offset, dcode(x), cur_stream(), rng_ptr(rng, x));
   return {y, mask};
 }
 
@@ -847,7 +856,7 @@ static void check_qkv(const Tensor& qkv, const char* what) {
 }
 
 std::vector<Tensor> flash_attn_qkv_fwd(Tensor qkv, c10::optional<Tensor> kbias, double scale, double p_drop,
-                                       int64_t seed) {
+                                       int64_t seed, OptT rng) {
   check_qkv(qkv, "flash_attn_qkv_fwd");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
   TORCH_CHECK(S % 8 == 0 && (D == 64 || D == 128), "flash_attn_qkv_fwd: S % 8 == 0 and head dim 64 or 128");
@@ -864,12 +873,12 @@ std::vector<Tensor> flash_attn_qkv_fwd(Tensor qkv, c10::optional<Tensor> kbias, 
   const int64_t hd = H * D * qkv.element_size();
   dsa::launch_flash_fwd_ex(base, base + hd, base + 2 * hd, o.data_ptr(), lse.data_ptr<float>(), (int)(B * H), (int)S,
                            (int)D, (float)scale, kbias ? kbias->data_ptr<float>() : nullptr, (int)H, (float)p_drop,
-                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D);
+                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D, rng_ptr(rng, qkv));
   return {o, lse};
 }
 
 Tensor flash_attn_qkv_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, c10::optional<Tensor> kbias, double scale,
-                          double p_drop, int64_t seed) {
+                          double p_drop, int64_t seed, OptT rng) {
   check_qkv(qkv, "flash_attn_qkv_bwd");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
   for (auto* t : {&dout, &o}) {
@@ -893,7 +902,7 @@ Tensor flash_attn_qkv_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, c10::op
   dsa::launch_flash_bwd_ex(dout.data_ptr(), base, base + hd, base + 2 * hd, o.data_ptr(), lse.data_ptr<float>(),
                            delta.data_ptr<float>(), dbase, dbase + hd, dbase + 2 * hd, (int)(B * H), (int)S, (int)D,
                            (float)scale, kbias ? kbias->data_ptr<float>() : nullptr, (int)H, (float)p_drop,
-                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D);
+                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D, rng_ptr(rng, qkv));
   return dqkv;
 }
 
@@ -1075,8 +1084,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sparse_flash_fwd", &sparse_flash_fwd);
   m.def("flash_attn_fwd_ex", &flash_attn_fwd_ex);
   m.def("flash_attn_bwd_ex", &flash_attn_bwd_ex);
-  m.def("flash_attn_qkv_fwd", &flash_attn_qkv_fwd);
-  m.def("flash_attn_qkv_bwd", &flash_attn_qkv_bwd);
+  m.def("flash_attn_qkv_fwd", &flash_attn_qkv_fwd, py::arg("qkv"), py::arg("kbias"), py::arg("scale"), py::arg("p_drop"),
+        py::arg("seed"), py::arg("rng") = py::none());
+  m.def("flash_attn_qkv_bwd", &flash_attn_qkv_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"), py::arg("lse"),
+        py::arg("kbias"), py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("rng") = py::none());
   m.def("sparse_flash_bwd", &sparse_flash_bwd);
   m.def("onebit_worker_compress", &onebit_worker_compress);
   m.def("onebit_server_compress", &onebit_server_compress);
@@ -1085,8 +1096,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sparse_dsd", &sparse_dsd);
   m.def("sparse_softmax_fwd", &sparse_softmax_fwd);
   m.def("sparse_softmax_bwd", &sparse_softmax_bwd);
-  m.def("dropout_fwd", &dropout_fwd);
-  m.def("bias_dropout_residual", &bias_dropout_residual);
+  m.def("dropout_fwd", &dropout_fwd, py::arg("x"), py::arg("p"), py::arg("seed"), py::arg("offset"),
+        py::arg("rng") = py::none());
+  m.def("bias_dropout_residual", &bias_dropout_residual, py::arg("x"), py::arg("bias"), py::arg("res"), py::arg("p"),
+        py::arg("seed"), py::arg("offset"), py::arg("rng") = py::none());
   m.def("dropout_bwd", &dropout_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd, py::arg("logits"), py::arg("labels"), py::arg("lse"), py::arg("dloss"),

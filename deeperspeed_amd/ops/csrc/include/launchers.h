@@ -133,10 +133,12 @@ void launch_sparse_softmax_bwd(const void* y, const void* dy, void* dx, const in
                                int nbr, int blk, int max_row, float scale, int dt, hipStream_t s);
 
 // dropout.hip: counter-based Philox dropout (seed, offset) with uint8 keep-masks
+// rng: optional device int64 [seed, step] read by the kernels (graph-replayable masks, dropout.hip)
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed, uint64_t offset,
-                        int dt, hipStream_t s);
+                        int dt, hipStream_t s, const int64_t* rng = nullptr);
 void launch_bias_dropout_residual(const void* x, const void* bias, const void* res, void* y, uint8_t* mask,
-                                  int64_t rows, int C, float p, uint64_t seed, uint64_t offset, int dt, hipStream_t s);
+                                  int64_t rows, int C, float p, uint64_t seed, uint64_t offset, int dt, hipStream_t s,
+                                  const int64_t* rng = nullptr);
 void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, int dt, hipStream_t s);
 
 // flash_attn.hip: q,k,v,o [BH, S, D] (D in 64/96/128), lse/delta [BH, S] fp32
@@ -150,11 +152,11 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
 // min(6, log2(layout block))
 void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh = 0, int64_t ild = 0);
+                         int onh, int inh = 0, int64_t ild = 0, const int64_t* rng = nullptr);
 void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const void* v, const void* o,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh = 0, int64_t ild = 0);
+                         int onh, int inh = 0, int64_t ild = 0, const int64_t* rng = nullptr);
 void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
                              const int* cols, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
                              float scale, int shift, int dt, hipStream_t s, int onh = 0,

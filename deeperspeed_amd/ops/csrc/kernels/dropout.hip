@@ -32,10 +32,21 @@ __device__ __forceinline__ void uniform4(uint64_t seed, uint64_t offset, uint64_
   u[0] = r.x * k; u[1] = r.y * k; u[2] = r.z * k; u[3] = r.w * k;
 }
 
+// Graph-replayable seeds: with `rng` (device int64 [seed, step]) the seed is read on the GPU and
+// the step shifts the Philox counter by 2^40 per increment, so a captured HIP graph draws fresh
+// masks on every replay (the host-side seed / offset then only separate the call sites).
+__device__ __forceinline__ void rng_apply(const int64_t* __restrict__ rng, uint64_t& seed, uint64_t& offset) {
+  if (rng) {
+    seed ^= (uint64_t)rng[0];
+    offset += (uint64_t)rng[1] << 40;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) dropout_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ mask, int64_t n, float p,
-                                                          uint64_t seed, uint64_t offset) {
+                                                          uint64_t seed, uint64_t offset, const int64_t* __restrict__ rng = nullptr) {
+  rng_apply(rng, seed, offset);
   const float scale = 1.f / (1.f - p);
   const int64_t ngroups = (n + 3) / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -58,7 +69,8 @@ template <typename T>
 __global__ void __launch_bounds__(256) bias_dropout_residual_kernel(const T* __restrict__ x, const T* __restrict__ b,
                                                                     const T* __restrict__ res, T* __restrict__ y,
                                                                     uint8_t* __restrict__ mask, int64_t n, int C,
-                                                                    float p, uint64_t seed, uint64_t offset) {
+                                                                    float p, uint64_t seed, uint64_t offset, const int64_t* __restrict__ rng = nullptr) {
+  rng_apply(rng, seed, offset);
   const float scale = 1.f / (1.f - p);
   const int64_t ngroups = (n + 3) / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -127,7 +139,8 @@ __device__ __forceinline__ void load_mask(const uint8_t* m, bool (&keep)[VN]) {
 template <typename T>
 __global__ void __launch_bounds__(256) dropout_fwd_vec_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                               uint8_t* __restrict__ mask, int64_t n, float p,
-                                                              uint64_t seed, uint64_t offset) {
+                                                              uint64_t seed, uint64_t offset, const int64_t* __restrict__ rng = nullptr) {
+  rng_apply(rng, seed, offset);
   constexpr int VN = Vec16<T>::N;
   const float scale = 1.f / (1.f - p);
   const int64_t nvec = n / VN, stride = (int64_t)gridDim.x * blockDim.x;
@@ -152,7 +165,8 @@ __global__ void __launch_bounds__(256) bias_dropout_residual_vec_kernel(const T*
                                                                         const T* __restrict__ res,
                                                                         T* __restrict__ y, uint8_t* __restrict__ mask,
                                                                         int64_t n, int C, float p, uint64_t seed,
-                                                                        uint64_t offset) {
+                                                                        uint64_t offset, const int64_t* __restrict__ rng = nullptr) {
+  rng_apply(rng, seed, offset);
   constexpr int VN = Vec16<T>::N;
   const float scale = 1.f / (1.f - p);
   const int64_t nvec = n / VN, stride = (int64_t)gridDim.x * blockDim.x;
@@ -265,35 +279,35 @@ static inline unsigned dgrid(int64_t work) {
 }
 
 void launch_dropout_fwd(const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed, uint64_t offset,
-                        int dt, hipStream_t s) {
+                        int dt, hipStream_t s, const int64_t* rng) {
   if (n <= 0) return;
   const int vn = dt == kF32 ? 4 : 8;
   if (vec_ok(n, vn, {x, y}) && (reinterpret_cast<uintptr_t>(mask) & 7) == 0) {
     DSA_DISPATCH_T(dt, T,
       hipLaunchKernelGGL((dropout_fwd_vec_kernel<T>), dim3(dgrid(n / vn)), dim3(256), 0, s, (const T*)x, (T*)y, mask,
-                         n, p, seed, offset));
+                         n, p, seed, offset, rng));
     return;
   }
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((dropout_fwd_kernel<T>), dim3(dgrid((n + 3) / 4)), dim3(256), 0, s, (const T*)x, (T*)y, mask,
-                       n, p, seed, offset));
+                       n, p, seed, offset, rng));
 }
 
 void launch_bias_dropout_residual(const void* x, const void* bias, const void* res, void* y, uint8_t* mask,
                                   int64_t rows, int C, float p, uint64_t seed, uint64_t offset, int dt,
-                                  hipStream_t s) {
+                                  hipStream_t s, const int64_t* rng) {
   const int64_t n = rows * C;
   if (n <= 0) return;
   const int vn = dt == kF32 ? 4 : 8;
   if (vec_ok(n, vn, {x, bias, res, y}) && C % vn == 0 && (reinterpret_cast<uintptr_t>(mask) & 7) == 0) {
     DSA_DISPATCH_T(dt, T,
       hipLaunchKernelGGL((bias_dropout_residual_vec_kernel<T>), dim3(dgrid(n / vn)), dim3(256), 0, s, (const T*)x,
-                         (const T*)bias, (const T*)res, (T*)y, mask, n, C, p, seed, offset));
+                         (const T*)bias, (const T*)res, (T*)y, mask, n, C, p, seed, offset, rng));
     return;
   }
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((bias_dropout_residual_kernel<T>), dim3(dgrid((n + 3) / 4)), dim3(256), 0, s, (const T*)x,
-                       (const T*)bias, (const T*)res, (T*)y, mask, n, C, p, seed, offset));
+                       (const T*)bias, (const T*)res, (T*)y, mask, n, C, p, seed, offset, rng));
 }
 
 void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, int dt, hipStream_t s) {

@@ -554,6 +554,8 @@ struct Extra {
   // the [B*H, S, D] layout
   int inh = 0;
   int64_t ild = 0;
+  // optional device int64 [seed, step] mixed into `seed` on the GPU (graph-replayable dropout)
+  const int64_t* rng = nullptr;
 };
 // compile-time layout switch: the head-major kernels keep constant row strides (immediate load
 // offsets); only EX_QKV instantiations pay for the runtime stride
@@ -578,6 +580,11 @@ __device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t drop_head(uint32_t seed, int64_t bh) {
   return drop_mix(seed ^ drop_mix((uint32_t)bh * 0x9e3779b1u + 0x632be5abu));
+}
+// the kernel's dropout seed: the host value, mixed with the device [seed, step] when present
+__device__ __forceinline__ uint32_t ex_seed(const Extra& ex) {
+  if (!ex.rng) return ex.seed;
+  return ex.seed ^ drop_mix((uint32_t)ex.rng[0] ^ drop_mix((uint32_t)ex.rng[1] * 0x85ebca6bu + 0x27d4eb2fu));
 }
 // draws of (q, 2j) in the low and (q, 2j+1) in the high 16 bits
 __device__ __forceinline__ uint32_t drop_pair(uint32_t hb, int q, int half_s, int j) {
@@ -617,7 +624,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
   const uint16_t* Vb = V + ib;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
   const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
-  const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
+  const uint32_t hb = DROP ? drop_head(ex_seed(ex), bh) : 0u;
   const float* kbs = BIAS ? stage_kbias<D>(smem, kbrow, S) : nullptr;
 
   s16x8 qf[D / 16];
@@ -819,7 +826,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   constexpr bool INIT = V3 && !DROP;
   // this lane's key bias (log2 units) and which 16-bit half of a pair draw is its key's
   const float kb2 = (BIAS && mykey < S) ? ex.kbias[(bh / ex.hdiv) * (int64_t)S + mykey] * LOG2E : 0.f;
-  const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
+  const uint32_t hb = DROP ? drop_head(ex_seed(ex), bh) : 0u;
   const int dshift = (mykey & 1) * 16;
   // FQ (S <= BM2: this workgroup owns every key of the head): K [BM2][D+8] and the tile's dS
   // [BN2 queries][BM2 + 8 keys] also live in LDS, and dQ = dS K is formed per query tile here
@@ -1095,7 +1102,7 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
   const float sl2 = scale * 1.4426950408889634f;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
   const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
-  const uint32_t hb = DROP ? drop_head(ex.seed, bh) : 0u;
+  const uint32_t hb = DROP ? drop_head(ex_seed(ex), bh) : 0u;
   const float* kbs = BIAS ? stage_kbias<D>(smem, kbrow, S) : nullptr;
 
   s16x8 qf[D / 16], of[D / 16];
@@ -2122,8 +2129,9 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
   } while (0)
 
 static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t seed, int inh = 0,
-                            int64_t ild = 0) {
+                            int64_t ild = 0, const int64_t* rng = nullptr) {
   fa::Extra ex;
+  ex.rng = rng;
   ex.inh = inh;
   ex.ild = ild;
   ex.kbias = kbias;
@@ -2136,8 +2144,8 @@ static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t 
 
 void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh, int64_t ild) {
-  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild);
+                         int onh, int inh, int64_t ild, const int64_t* rng) {
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng);
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
   const int kb_lds = kbias ? 4 * S : 0;  // the LDS-staged key-bias row
   if (kb_lds && fa::fwd_v2_lds<128>() + kb_lds > 160 * 1024)
@@ -2153,8 +2161,8 @@ void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, f
 void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const void* v, const void* o,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh, int64_t ild) {
-  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild);
+                         int onh, int inh, int64_t ild, const int64_t* rng) {
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng);
   const int64_t rows = (int64_t)BH * S;
   const int kb_lds = kbias ? 4 * S : 0;  // the dQ kernel's LDS-staged key-bias row
   if (kb_lds && fa::fwd_v2_lds<128>() + kb_lds > 160 * 1024)

@@ -76,6 +76,8 @@ def nt_wgrad_count() -> int:
 
 
 def _bound_grad(p: torch.Tensor):
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return None  # a HIP-graph capture must not bake one step's gradient buffer into the graph
     g = p.grad
     if g is None or g.shape != p.shape or g.dtype != p.dtype or g.device != p.device:
         return None

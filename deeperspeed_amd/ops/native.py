@@ -538,22 +538,24 @@ def flash_attention_encoder(q, k, v, key_bias=None, scale=1.0, dropout_p=0.0, tr
 
 class _FlashAttnQkvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv5, kbias, scale, p, seed):
+    def forward(ctx, qkv5, kbias, scale, p, seed, rng=None):
         B, S, _, H, D = qkv5.shape
         _macs(2 * B * H * S * S * D)
-        o, lse = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed)
+        o, lse = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed, rng)
         ctx.save_for_backward(qkv5, o, lse, kbias)
-        ctx.scale, ctx.p, ctx.seed = scale, p, seed
+        ctx.scale, ctx.p, ctx.seed, ctx.rng = scale, p, seed, rng
         return o
 
     @staticmethod
     def backward(ctx, do):
         qkv5, o, lse, kbias = ctx.saved_tensors
-        dqkv = hip_ops().flash_attn_qkv_bwd(do.contiguous(), qkv5, o, lse, kbias, ctx.scale, ctx.p, ctx.seed)
-        return dqkv, None, None, None, None
+        dqkv = hip_ops().flash_attn_qkv_bwd(do.contiguous(), qkv5, o, lse, kbias, ctx.scale, ctx.p, ctx.seed,
+                                            ctx.rng)
+        return dqkv, None, None, None, None, None
 
 
-def flash_attention_qkv(qkv, num_heads, key_bias=None, scale=1.0, dropout_p=0.0, training=True, generator=None):
+def flash_attention_qkv(qkv, num_heads, key_bias=None, scale=1.0, dropout_p=0.0, training=True, generator=None,
+                        rng=None, site=0):
     """Encoder attention straight from the fused QKV projection: qkv [B, S, 3*H*D] (q | k | v,
     heads contiguous inside each) -> context [B, S, H*D], same math as flash_attention_encoder
     (same keep mask for the same seed) without the head split / merge copies; the backward
@@ -563,8 +565,12 @@ def flash_attention_qkv(qkv, num_heads, key_bias=None, scale=1.0, dropout_p=0.0,
     p = float(dropout_p) if training else 0.0
     if key_bias is not None:
         key_bias = key_bias.reshape(B, S).float().contiguous()
-    seed = (_draw_seed(generator) if p > 0.0 else 0) & ((1 << 63) - 1)
-    o = _FlashAttnQkvFn.apply(qkv.contiguous().view(B, S, 3, num_heads, D), key_bias, float(scale), p, int(seed))
+    if rng is not None:  # device [seed, step] (graph-replayable): the host value only names the call site
+        seed = site
+    else:
+        seed = (_draw_seed(generator) if p > 0.0 else 0) & ((1 << 63) - 1)
+    o = _FlashAttnQkvFn.apply(qkv.contiguous().view(B, S, 3, num_heads, D), key_bias, float(scale), p, int(seed),
+                              rng if p > 0.0 else None)
     return o.view(B, S, num_heads * D)
 
 
@@ -825,9 +831,9 @@ def dropout_matmul(probs, v, p, training=True, generator=None):
 
 class _BiasDropoutResidualFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, res, p, seed):
+    def forward(ctx, x, bias, res, p, seed, rng=None):
         if x.is_cuda:
-            y, mask = hip_ops().bias_dropout_residual(x.contiguous(), bias, res.contiguous(), p, seed, 0)
+            y, mask = hip_ops().bias_dropout_residual(x.contiguous(), bias, res.contiguous(), p, seed, 0, rng)
         else:
             g = torch.Generator().manual_seed(seed)
             mask = (torch.rand(x.shape, generator=g) >= p).to(torch.uint8)
@@ -849,13 +855,17 @@ class _BiasDropoutResidualFn(torch.autograd.Function):
         else:
             dx = (dy.float() * mask / (1 - ctx.p)).to(dy.dtype)
             db = dx.reshape(-1, dx.shape[-1]).float().sum(0).to(dy.dtype)
-        return dx, db, dy, None, None
+        return dx, db, dy, None, None, None
 
 
-def bias_dropout_residual(x, bias, residual, p, training=True, generator=None):
-    """residual + dropout(x + bias), one fused pass (reference dropout_kernels.cu ForwardWithBias)."""
+def bias_dropout_residual(x, bias, residual, p, training=True, generator=None, rng=None, site=0):
+    """residual + dropout(x + bias), one fused pass (reference dropout_kernels.cu ForwardWithBias).
+    rng: device int64 [seed, step] read by the kernel (graph-replayable masks); `site` then
+    separates the call sites that share it."""
     if not training or p <= 0:
         return residual + (x + bias)
+    if rng is not None and x.is_cuda:
+        return _BiasDropoutResidualFn.apply(x, bias, residual, float(p), int(site) << 20, rng)
     return _BiasDropoutResidualFn.apply(x, bias, residual, float(p), _draw_seed(generator))
 
 

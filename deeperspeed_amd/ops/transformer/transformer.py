@@ -154,13 +154,14 @@ class DeepSpeedTransformerFunction:
             if mask.dim() == 2:
                 mask = mask[:, None, None, :]
             mask = mask.reshape(B, 1, -1, S)
+        rng = getattr(layer, "_rng", None) if (layer is not None and training) else None
         if (fast and _ENCODER_FLASH and native.qkv_flash_supported(qkv, nh)
                 and (mask is None or mask.shape[2] == 1)):
             # one fused kernel per direction reading q, k, v straight out of the QKV projection:
             # scores, key-padding bias, softmax, dropout and P V stay on chip, the context is
             # written token-major [B, S, nh * hd] for the output projection, dqkv in qkv's layout
             ctx = native.flash_attention_qkv(qkv, nh, None if mask is None else mask.reshape(B, S),
-                                             1.0 / math.sqrt(hd), cfg.attn_dropout_ratio, training, gen)
+                                             1.0 / math.sqrt(hd), cfg.attn_dropout_ratio, training, gen, rng=rng, site=1)
         else:
             if fast:
                 q, k, v = _SplitHeads.apply(qkv, nh)  # contiguous [B, nh, S, hd]: batched GEMMs without copies
@@ -177,7 +178,8 @@ class DeepSpeedTransformerFunction:
                 ctx = torch.matmul(probs, v)
             ctx = _MergeHeads.apply(ctx) if fast else ctx.transpose(1, 2).reshape(B, S, Hd)
         attn_out = _linear(ctx, attn_ow)
-        add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen)
+        add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen, rng=rng,
+                                               site=2)
         if fuse_res:
             ff1_inp, add_res = native.layer_norm_residual(add_res, attn_nw, attn_nb, eps)
         else:
@@ -185,9 +187,11 @@ class DeepSpeedTransformerFunction:
         inter = _gelu_tanh(_linear(ff1_inp, inter_w), inter_b)
         out = _linear(inter, output_w)
         if cfg.pre_layer_norm:
-            out = native.bias_dropout_residual(out, output_b, add_res, cfg.hidden_dropout_ratio, training, gen)
+            out = native.bias_dropout_residual(out, output_b, add_res, cfg.hidden_dropout_ratio, training, gen, rng=rng,
+                                               site=3)
         else:
-            out = native.bias_dropout_residual(out, output_b, ff1_inp, cfg.hidden_dropout_ratio, training, gen)
+            out = native.bias_dropout_residual(out, output_b, ff1_inp, cfg.hidden_dropout_ratio, training, gen, rng=rng,
+                                               site=3)
             out = ln(out, norm_w, norm_b, eps)
         if grads is not None:  # reference test hook: collect gradients of the intermediates
             for t in (out, add_res, ff1_inp):
@@ -264,8 +268,21 @@ class DeepSpeedTransformerLayer(nn.Module):
         self.norm_w.fill_(1.0)
         self.norm_b.zero_()
 
+    def enable_device_rng(self, seed: int, device=None):
+        """Dropout seeds from a device int64 [seed, step] that the layer's forward advances with
+        a kernel: a HIP graph captured around the layer then draws fresh masks on every replay
+        (host-drawn seeds would be frozen into the graph).  Needed for graphed training
+        (`make_graphed_encoder`); the eager masks differ from the host-seeded ones."""
+        dev = device or self.attn_qkvw.device
+        self._rng = torch.tensor([int(seed), 0], dtype=torch.int64, device=dev)
+
     def forward(self, hidden_states, attention_mask=None, head_mask=None, encoder_hidden_states=None,
                 encoder_attention_mask=None, output_attentions=False, grads=None):
+        rng = getattr(self, "_rng", None)
+        if rng is not None and self.training and torch.is_grad_enabled():
+            from ...runtime.activation_checkpointing import checkpointing as ds_ckpt
+            if not ds_ckpt.is_recomputing():  # a recompute must redraw the forward's masks
+                rng[1:].add_(1)
         self.config.training = self.training
         self.config.is_grad_enabled = torch.is_grad_enabled()
         out = DeepSpeedTransformerFunction.apply(hidden_states, attention_mask, self, grads, self.config.layer_id,
@@ -273,3 +290,28 @@ class DeepSpeedTransformerLayer(nn.Module):
                                                  self.attn_nw, self.attn_nb, self.inter_w, self.inter_b,
                                                  self.output_w, self.output_b, self.norm_w, self.norm_b, self.config)
         return (out,) if self.config.huggingface else out
+
+
+def make_graphed_encoder(layers, sample_hidden, sample_mask=None, seed: int = 1234, warmup: int = 3):
+    """Capture every DeepSpeedTransformerLayer of `layers` (an nn.ModuleList, replaced in place)
+    as HIP graphs -- one forward and one backward graph per layer (torch.cuda.make_graphed_callables)
+    -- so a training step replays 2 x num_layers graphs instead of launching ~30 kernels per
+    layer and direction from Python.  The layers' dropout then draws from device RNG state
+    (`enable_device_rng`), advanced by a kernel inside the forward graph, so every replay gets
+    fresh masks.  Shapes (batch, sequence) and the attention-mask layout are fixed by the
+    samples; parameters keep receiving ordinary .grad tensors.
+
+    The reference has no graph capture (CUDA graphs postdate DeepSpeed v0.3.15); the BERT layer it
+    benchmarks is its ds_transformer_cuda op (csrc/transformer/ds_transformer_cuda.cpp)."""
+    for i, layer in enumerate(layers):
+        if not isinstance(layer, DeepSpeedTransformerLayer):
+            raise TypeError("make_graphed_encoder: every layer must be a DeepSpeedTransformerLayer")
+        layer.enable_device_rng(seed + 7919 * i)
+    args = []
+    for _ in layers:
+        h = sample_hidden.detach().clone().requires_grad_(True)
+        args.append((h,) if sample_mask is None else (h, sample_mask.detach()))
+    graphed = torch.cuda.make_graphed_callables(tuple(layers), tuple(args), num_warmup_iters=warmup)
+    for i, g in enumerate(graphed):
+        layers[i] = g
+    return layers

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--torch-profile", default="", help="write a torch.profiler op table of one step here")
+    ap.add_argument("--hip-graphs", choices=["on", "off"], default="off",
+                    help="capture every encoder layer's forward / backward as HIP graphs "
+                         "(ops/transformer make_graphed_encoder; dropout from device RNG state)")
     ap.add_argument("--overlap-step", choices=["on", "off"], default="off",
                     help="run the LAMB step on a side stream overlapped with the next forward "
                          "(zero_optimization.overlap_step; identical math)")
@@ -67,6 +70,13 @@ def main():
     pos = torch.stack([torch.randperm(S, device=dev, generator=g)[:npred].sort().values for _ in range(B)])
     lab = torch.randint(0, cfg.vocab_size, (B, npred), device=dev, generator=g)
     nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
+
+    if args.hip_graphs == "on" and dev.type == "cuda":
+        from deeperspeed_amd.ops.transformer.transformer import make_graphed_encoder
+        m = engine.module
+        ext = ((1.0 - am.to(torch.bfloat16)) * -10000.0)[:, None, None, :]
+        make_graphed_encoder(m.layers, torch.randn(B, S, cfg.hidden_size, device=dev, dtype=torch.bfloat16), ext)
+        torch.cuda.synchronize()
 
     def step():
         loss = engine(ids, tt, am, pos, lab, nsp)
@@ -115,6 +125,7 @@ def main():
                       "unit": "samples/s", "ms_per_step": round(dt * 1e3, 2), "batch": B, "seq": S,
                       "masked_per_seq": npred, "model_tflops": round(tflops, 1), "dtype": "bf16",
                       "optimizer": "FusedLamb", "overlap_step": args.overlap_step == "on",
+                      "hip_graphs": args.hip_graphs == "on",
                       "gradient_clipping": 1.0, "data": "synthetic", "final_loss": round(float(loss.detach()), 4),
                       "ref_v100_samples_per_s": ref[0] if ref else None,
                       "vs_ref_v100": round(sps / ref[0], 2) if ref else None}), flush=True)
