@@ -76,8 +76,11 @@ def nt_wgrad_count() -> int:
 
 
 def _bound_grad(p: torch.Tensor):
-    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-        return None  # a HIP-graph capture must not bake one step's gradient buffer into the graph
+    if (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+            and not getattr(p, "_dsa_persistent_grad", False)):
+        # a HIP-graph capture may only bake in gradient buffers that outlive the step
+        # (make_graphed_encoder's persistent .grad, zeroed in place by the optimizer)
+        return None
     g = p.grad
     if g is None or g.shape != p.shape or g.dtype != p.dtype or g.device != p.device:
         return None

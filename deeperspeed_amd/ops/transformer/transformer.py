@@ -292,7 +292,8 @@ class DeepSpeedTransformerLayer(nn.Module):
         return (out,) if self.config.huggingface else out
 
 
-def make_graphed_encoder(layers, sample_hidden, sample_mask=None, seed: int = 1234, warmup: int = 3):
+def make_graphed_encoder(layers, sample_hidden, sample_mask=None, seed: int = 1234, warmup: int = 3,
+                         persistent_grads: bool = True):
     """Capture every DeepSpeedTransformerLayer of `layers` (an nn.ModuleList, replaced in place)
     as HIP graphs -- one forward and one backward graph per layer (torch.cuda.make_graphed_callables)
     -- so a training step replays 2 x num_layers graphs instead of launching ~30 kernels per
@@ -307,11 +308,21 @@ def make_graphed_encoder(layers, sample_hidden, sample_mask=None, seed: int = 12
         if not isinstance(layer, DeepSpeedTransformerLayer):
             raise TypeError("make_graphed_encoder: every layer must be a DeepSpeedTransformerLayer")
         layer.enable_device_rng(seed + 7919 * i)
+        if persistent_grads:
+            # the backward graphs accumulate weight / bias / LayerNorm gradients straight into these
+            # buffers (ops/linear.py, native LayerNorm): no static gradient outputs to copy into .grad
+            # after every replay; the optimizer zeroes them in place (FP16_UnfusedOptimizer.zero_grad)
+            for p in layer.parameters():
+                p.grad = torch.zeros_like(p)
+                p._dsa_persistent_grad = True
     args = []
     for _ in layers:
         h = sample_hidden.detach().clone().requires_grad_(True)
         args.append((h,) if sample_mask is None else (h, sample_mask.detach()))
-    graphed = torch.cuda.make_graphed_callables(tuple(layers), tuple(args), num_warmup_iters=warmup)
+    graphed = torch.cuda.make_graphed_callables(tuple(layers), tuple(args), num_warmup_iters=warmup,
+                                                allow_unused_input=persistent_grads)
     for i, g in enumerate(graphed):
         layers[i] = g
+    if persistent_grads:  # the warmup iterations accumulated into the persistent buffers
+        torch._foreach_zero_([p.grad for layer in layers for p in layer.parameters()])
     return layers

@@ -150,13 +150,18 @@ class FP16_UnfusedOptimizer:
 
     # ----------------------------------------------------------------- steps
     def zero_grad(self, set_to_none=True):
+        keep = []
         for group in self.fp16_groups:
             for p in group:
-                if set_to_none:
+                if getattr(p, "_dsa_persistent_grad", False) and p.grad is not None:
+                    keep.append(p.grad)  # a captured HIP graph accumulates into this buffer
+                elif set_to_none:
                     p.grad = None
                 elif p.grad is not None:
                     p.grad.detach_()
                     p.grad.zero_()
+        if keep:
+            torch._foreach_zero_(keep)
 
     def backward(self, loss, retain_graph=False):
         (loss.float() * self.loss_scale).backward(retain_graph=retain_graph)

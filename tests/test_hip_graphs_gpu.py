@@ -47,9 +47,12 @@ def _train(graphs, steps=4):
         # the comparison from the same state as the eager run
         for layer in engine.module.layers:
             layer._rng[1] = 0
-    else:
+    else:  # eager reference with the same device RNG and the same persistent, in-place-accumulated grads
         for i, layer in enumerate(engine.module.layers):
             layer.enable_device_rng(77 + 7919 * i)
+            for p in layer.parameters():
+                p.grad = torch.zeros_like(p)
+                p._dsa_persistent_grad = True
     losses = []
     for _ in range(steps):
         loss = engine(ids, None, am, pos, lab, nsp)
