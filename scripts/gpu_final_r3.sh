@@ -9,3 +9,4 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/final_smoke.log
 timeout -k 10 420 python bench.py > gpurun_out/final_bench.json 2> gpurun_out/final_bench.log || { tail -30 gpurun_out/final_bench.log; exit 1; }
 grep -o '"value": [0-9.]*' gpurun_out/final_bench.json
+bash scripts/gpu_r3w.sh
