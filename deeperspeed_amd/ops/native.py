@@ -882,6 +882,7 @@ class _EmbeddingFn(torch.autograd.Function):
     def forward(ctx, ids, weight, padding_idx):
         ctx.save_for_backward(ids)
         ctx.weight = weight
+        ctx.wshape = tuple(weight.shape)  # a ZeRO-3 parameter may be released (empty) until re-gathered
         ctx.padding_idx = padding_idx
         return torch.nn.functional.embedding(ids, weight, padding_idx if padding_idx >= 0 else None)
 
@@ -889,7 +890,7 @@ class _EmbeddingFn(torch.autograd.Function):
     def backward(ctx, g):
         (ids,) = ctx.saved_tensors
         w = ctx.weight
-        H = w.shape[1]
+        H = ctx.wshape[1]
         sorted_ids, perm = torch.sort(ids.reshape(-1), stable=True)
         g2 = g.reshape(-1, H).contiguous()
         from .linear import FUSE_WGRAD, _bound_grad
@@ -897,7 +898,7 @@ class _EmbeddingFn(torch.autograd.Function):
         if bound is not None and bound.is_contiguous():
             hip_ops().embedding_bwd(sorted_ids, perm, g2, bound, ctx.padding_idx, True)
             return None, None, None
-        dw = torch.zeros(w.shape, dtype=g2.dtype, device=g2.device)
+        dw = torch.zeros(ctx.wshape, dtype=g2.dtype, device=g2.device)
         hip_ops().embedding_bwd(sorted_ids, perm, g2, dw, ctx.padding_idx, False)
         return None, dw, None
 
