@@ -118,6 +118,58 @@ def log(msg):
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+# A rank that hangs (an RCCL collective that never completes, a stuck kernel) must not burn a
+# multi-GPU slot for the process-group timeout: every rank beats a heartbeat per phase / warmup /
+# timed step (one stderr line + a file the spawning parent watches) and a watchdog thread ends
+# the rank -- after printing its last heartbeat and every thread's Python stack -- when no beat
+# came for DSA_BENCH_WATCHDOG_S seconds.  Its non-zero exit makes torchrun, or spawn_ranks
+# below, stop the whole job.
+WATCHDOG_S = float(os.environ.get("DSA_BENCH_WATCHDOG_S", "480"))
+PG_TIMEOUT_S = float(os.environ.get("DSA_BENCH_PG_TIMEOUT_S", "600"))
+
+
+class Heartbeat:
+    def __init__(self, rank, limit_s=WATCHDOG_S):
+        import threading
+        self.rank = rank
+        self.limit = limit_s
+        self.last = "start"
+        self.t = time.time()
+        self.path = None
+        d = os.environ.get("DSA_BENCH_HB_DIR")
+        if d:
+            self.path = os.path.join(d, f"rank{rank}")
+        self._write()
+        if limit_s > 0:
+            threading.Thread(target=self._watch, name="bench-watchdog", daemon=True).start()
+
+    def _write(self):
+        if self.path:
+            tmp = self.path + ".tmp"
+            with open(tmp, "w") as f:
+                f.write(f"{self.t:.3f} {self.last}\n")
+            os.replace(tmp, self.path)
+
+    def beat(self, what, **info):
+        self.last = what + "".join(f" {k}={v}" for k, v in info.items())
+        self.t = time.time()
+        print(f"[hb] rank={self.rank} {self.last}", file=sys.stderr, flush=True)
+        self._write()
+
+    def _watch(self):
+        import faulthandler
+        while True:
+            time.sleep(min(5.0, self.limit / 4))
+            idle = time.time() - self.t
+            if idle > self.limit:
+                print(f"[bench] WATCHDOG rank {self.rank}: no progress for {idle:.0f}s "
+                      f"(limit {self.limit:.0f}s, DSA_BENCH_WATCHDOG_S); last heartbeat: {self.last}; "
+                      f"Python stacks follow", file=sys.stderr, flush=True)
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                sys.stderr.flush()
+                os._exit(124)
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -134,13 +186,15 @@ def spawn_ranks(n):
     import signal
     import subprocess
     import threading
+    import tempfile
     port = os.environ.get("MASTER_PORT") or str(_free_port())
     addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
     cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    hb_dir = tempfile.mkdtemp(prefix="dsa_bench_hb_")
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR=addr, MASTER_PORT=port)
+                   GROUP_RANK="0", MASTER_ADDR=addr, MASTER_PORT=port, DSA_BENCH_HB_DIR=hb_dir)
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else 2,
                                       start_new_session=True))
     lines = []
@@ -157,6 +211,7 @@ def spawn_ranks(n):
 
     def stop_all(grace=30.0):
         signal_all(signal.SIGTERM)
+        signal_all(signal.SIGCONT)  # a stopped rank handles its SIGTERM only once resumed
         deadline = time.time() + grace
         while any(p.poll() is None for p in procs) and time.time() < deadline:
             time.sleep(0.2)
@@ -166,9 +221,24 @@ def spawn_ranks(n):
         stop_all(10.0)
         sys.exit(128 + signum)
 
+    def heartbeats():
+        out = {}
+        for r in range(n):
+            try:
+                with open(os.path.join(hb_dir, f"rank{r}")) as f:
+                    t, _, what = f.read().strip().partition(" ")
+                out[r] = (float(t), what)
+            except (OSError, ValueError):
+                out[r] = (None, "no heartbeat yet")
+        return out
+
     signal.signal(signal.SIGINT, on_signal)
     signal.signal(signal.SIGTERM, on_signal)
     rc = 0
+    # parent-side watchdog: covers a rank that cannot run its own (stopped, wedged in a driver
+    # call holding the GIL); a little longer than the ranks' own limit so theirs fires first
+    limit = WATCHDOG_S + 60.0 if WATCHDOG_S > 0 else 0.0
+    started = time.time()
     while True:
         codes = [p.poll() for p in procs]
         bad = next(((r, c) for r, c in enumerate(codes) if c not in (None, 0)), None)
@@ -176,14 +246,31 @@ def spawn_ranks(n):
             r, c = bad
             rc = c if c > 0 else 128 - c
             print(f"[bench] rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr, flush=True)
+            for rr, (t, what) in heartbeats().items():
+                print(f"[bench]   rank {rr} last heartbeat: {what}", file=sys.stderr, flush=True)
             stop_all()
             break
         if all(c == 0 for c in codes):
             break
+        if limit > 0:
+            now = time.time()
+            hb = heartbeats()
+            stale = [r for r, (t, _) in hb.items() if codes[r] is None and now - (t or started) > limit]
+            if stale:
+                print(f"[bench] WATCHDOG: rank(s) {stale} made no progress for {limit:.0f}s; stopping all ranks",
+                      file=sys.stderr, flush=True)
+                for rr, (t, what) in hb.items():
+                    age = f"{now - t:.0f}s ago" if t else "never"
+                    print(f"[bench]   rank {rr} last heartbeat ({age}): {what}", file=sys.stderr, flush=True)
+                stop_all(10.0)
+                rc = 124
+                break
         time.sleep(0.2)
     for p in procs:
         p.wait()
     reader.join(timeout=10)
+    import shutil
+    shutil.rmtree(hb_dir, ignore_errors=True)
     if rc == 0:
         for ln in lines:
             os.write(_RESULT_FD, ln)
@@ -211,8 +298,24 @@ def main():
     from deeperspeed_amd.runtime import memory_fit
 
     on_gpu = torch.cuda.is_available()
-    ds.init_distributed(dist_backend=args.dist_backend if on_gpu else "gloo")
+    hb = Heartbeat(int(os.environ["RANK"]))
+    if world > 1 and int(os.environ["RANK"]) == 0 and on_gpu:
+        # rank 0 logs RCCL's version, topology, channel and ring setup once (stdout of the C
+        # library is redirected to stderr above), so a multi-GPU record shows how it was wired
+        os.environ.setdefault("NCCL_DEBUG", "INFO")
+        os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,GRAPH,ENV")
+    from datetime import timedelta
+    ds.init_distributed(dist_backend=args.dist_backend if on_gpu else "gloo", timeout=timedelta(seconds=PG_TIMEOUT_S))
     rank = dist.get_rank()
+    hb.beat("process group up", backend=dist.get_backend(), world=world)
+    if rank == 0 and world > 1:
+        try:
+            rccl = ".".join(map(str, torch.cuda.nccl.version())) if on_gpu else None
+        except Exception:  # noqa: BLE001 - informational only
+            rccl = "unknown"
+        log(f"world={world} backend={dist.get_backend()} rccl={rccl} pg_timeout={PG_TIMEOUT_S:.0f}s "
+            f"watchdog={WATCHDOG_S:.0f}s HSA_ENABLE_IPC_MODE_LEGACY={os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY')} "
+            + " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_"))))
     if os.environ.get("DSA_BENCH_FAIL_RANK") == str(rank):  # teardown test hook (tests/test_bench_contract.py)
         raise SystemExit(7)
     if on_gpu:
@@ -344,15 +447,20 @@ def main():
         f"measured_fit={fit is not None} force_sharded={args.force_sharded} hbm={hbm / 2**30:.0f} GiB "
         f"planned={planned / 2**30:.0f} GiB")
     if args.pipe > 1:
-        return run_pipeline(args, cfg, mb, ga, world, rank, dev)
+        return run_pipeline(args, cfg, mb, ga, world, rank, dev, hb)
     t0 = time.time()
     torch.manual_seed(1234)
     model = GPTNeoX(cfg, device=dev, dtype=torch.bfloat16)
     log(f"model built in {time.time() - t0:.1f}s")
+    hb.beat("model built")
     engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
     del model
     log(f"engine ready in {time.time() - t0:.1f}s" +
         (f", mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB" if on_gpu else ""))
+    hb.beat("engine ready")
+
+    def peak_gib():
+        return round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else 0.0
 
     g = torch.Generator(device=dev)
     g.manual_seed(4321 + rank)
@@ -492,6 +600,10 @@ def main():
 
     i, extra = 0, 0
     while i < args.warmup + extra:
+        if os.environ.get("DSA_BENCH_STOP_RANK") == str(rank) and i == 1:
+            # watchdog test hook (tests/test_bench_contract.py): this rank freezes mid-run
+            import signal
+            os.kill(os.getpid(), signal.SIGSTOP)
         ts = time.time()
         loss, ph = timed_step()
         log(f"warmup {i} loss={float(loss.detach()):.4f} {time.time() - ts:.2f}s "
@@ -500,6 +612,8 @@ def main():
                f" reserved={reserved_peak() / 2**30:.1f} GiB device={device_peak() / 2**30:.1f} GiB" if on_gpu else "")
             + (f" zero3_pool={engine.optimizer._pool.held * 2 / 2**30:.1f} GiB"
                if hasattr(engine.optimizer, "_pool") else ""))
+        hb.beat(f"warmup {i} done", peak_gib=peak_gib(),
+                fit=[list(x) for x in fit.actions] if fit is not None else None)
         changed = False
         if fit is not None:
             changed = refit(i)
@@ -518,9 +632,11 @@ def main():
     t_start = time.time()
     for i in range(args.steps):
         loss = train_step()
+        hb.beat(f"timed step {i} queued", peak_gib=peak_gib())  # host-side only: no sync in the loop
     sync()
     dist.barrier()
     elapsed = time.time() - t_start
+    hb.beat("timed steps done", seconds=round(elapsed, 2))
     if on_gpu:
         native.hip_ops().profile_marker(2)
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -616,7 +732,7 @@ def _optimizer_block(args):
     return {"type": name, "params": {"lr": 1e-4, "freeze_step": args.freeze_step, "comm_backend_name": "nccl"}}
 
 
-def run_pipeline(args, cfg, mb, ga, world, rank, dev):
+def run_pipeline(args, cfg, mb, ga, world, rank, dev, hb):
     """BASELINE config 4: GPT-NeoX/GPT-3 as a PipelineModule, PP=args.pipe x DP=world/pipe,
     1F1B schedule with `ga` micro-batches per step, p2p activations over RCCL, ZeRO-1 (Adam)
     or 1-bit Adam/LAMB on the data-parallel group."""
@@ -654,17 +770,20 @@ def run_pipeline(args, cfg, mb, ga, world, rank, dev):
         if on_gpu:
             torch.cuda.synchronize()
 
+    hb.beat("pipeline engine ready")
     for i in range(args.warmup):
         ts = time.time()
         loss = train_step()
         sync()
         log(f"warmup {i} loss={float(loss):.4f} {time.time() - ts:.2f}s"
             + (f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB" if on_gpu else ""))
+        hb.beat(f"warmup {i} done", peak_gib=round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else 0.0)
     dist.barrier()
     sync()
     t_start = time.time()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         loss = train_step()
+        hb.beat(f"timed step {i} done")
     sync()
     dist.barrier()
     t = torch.tensor([time.time() - t_start], device=dev, dtype=torch.float64)

@@ -106,7 +106,7 @@ void sumsq_accum(Tensor x, Tensor workspace, Tensor out) {
                           cur_stream());
 }
 
-void scale_copy(Tensor x, Tensor y, OptT scale_t, double scale) {
+void scale_copy(Tensor x, Tensor y, OptT scale_t, double scale, bool accumulate) {
   check_dev(x, "x"); check_dev(y, "y");
   TORCH_CHECK(x.numel() == y.numel(), "scale_copy: size mismatch");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & (x.element_size() * 4 - 1)) == 0 &&
@@ -119,7 +119,7 @@ void scale_copy(Tensor x, Tensor y, OptT scale_t, double scale) {
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   dsa::launch_scale_copy(x.data_ptr(), dcode(x), y.data_ptr(), dcode(y), x.numel(), sp, (float)scale,
-                         cur_stream());
+                         cur_stream(), accumulate ? 1 : 0);
 }
 
 void lamb(Tensor w, Tensor g, Tensor m, Tensor v, Tensor upd, OptT out, double lr, double beta1, double beta2,
@@ -1115,7 +1115,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam_compact", &adam_compact);
   m.def("adam_multi", &adam_multi);
   m.def("sumsq_accum", &sumsq_accum);
-  m.def("scale_copy", &scale_copy);
+  m.def("scale_copy", &scale_copy, pybind11::arg("x"), pybind11::arg("y"), pybind11::arg("scale_t"),
+        pybind11::arg("scale"), pybind11::arg("accumulate") = false);
   m.def("lamb", &lamb);
   m.def("lamb_multi", &lamb_multi, py::arg("meta"), py::arg("T"), py::arg("total_chunks"), py::arg("chunk"),
         py::arg("wt"), py::arg("gt"), py::arg("ot"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),

@@ -2040,7 +2040,9 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
       hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
                          (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
-      if (dkdv == 3)
+      // D = 128 at two waves per SIMD spills ~160 VGPRs to scratch (hipcc resource usage): one
+      // wave per SIMD keeps the whole working set in VGPR + AGPR (4.7x -> see profiles/r4b_*)
+      if (dkdv == 3 && DD < 128)
         hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 2>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
                            (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
                            delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh);
@@ -2061,12 +2063,12 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     } else if (!v1) {
       // DSA_FA_DKDV: 3 (default) initial-accumulator row constants, 31 the same at one wave per
       // SIMD, 2 the v2 body; DSA_FA_BUFLOAD=0: pointer-form Q / dO tile loads (A/B only)
-      if (dkdv == 3 && bufload)
+      if (dkdv == 3 && bufload && DD < 128)
         hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 2>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
                            dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
                            (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
                            scale, onh);
-      else if (dkdv == 31 && bufload)
+      else if ((dkdv == 31 || dkdv == 3) && bufload)
         hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 1>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
                            dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
                            (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,

@@ -185,8 +185,9 @@ __global__ void __launch_bounds__(256) sum_finish_kernel(const float* __restrict
   if (threadIdx.x == 0) out[0] += acc;
 }
 
-// y = x * scale (in place or out of place, mixed dtype)
-template <typename TI, typename TO>
+// y = x * scale, or y += x * scale (ACC: e.g. a bf16 micro-batch gradient accumulated into an
+// fp32 shard in one pass instead of a cast kernel plus an add kernel); mixed dtypes
+template <typename TI, typename TO, bool ACC>
 __global__ void __launch_bounds__(256) scale_copy_kernel(const TI* __restrict__ x, TO* __restrict__ y,
                                                          int64_t n, const float* __restrict__ scale_ptr,
                                                          float scale) {
@@ -196,13 +197,20 @@ __global__ void __launch_bounds__(256) scale_copy_kernel(const TI* __restrict__ 
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
     float f[4];
     load_n<TI, 4>(x + i * 4, f);
+    if constexpr (ACC) {
+      float o[4];
+      load_n<TO, 4>(y + i * 4, o);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) f[k] *= s;
+      for (int k = 0; k < 4; ++k) f[k] = o[k] + f[k] * s;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) f[k] *= s;
+    }
     store_n<TO, 4>(y + i * 4, f);
   }
   if (blockIdx.x == 0)
     for (int64_t e = nvec * 4 + threadIdx.x; e < n; e += blockDim.x)
-      Conv<TO>::store(y, e, Conv<TI>::load(x, e) * s);
+      Conv<TO>::store(y, e, (ACC ? Conv<TO>::load(y, e) : 0.f) + Conv<TI>::load(x, e) * s);
 }
 
 // ---------------------------------------------------------------------------
@@ -480,12 +488,16 @@ void launch_sumsq_accum(const void* x, int xt, int64_t n, float* workspace, floa
 }
 
 void launch_scale_copy(const void* x, int xt, void* y, int yt, int64_t n, const float* scale_ptr,
-                       float scale, hipStream_t s) {
+                       float scale, hipStream_t s, int accumulate) {
   if (n <= 0) return;
   const int grid = grid_for(n / 4, 256, 4096);
   DSA_DISPATCH_T(xt, TI, DSA_DISPATCH_T(yt, TO,
-    hipLaunchKernelGGL((scale_copy_kernel<TI, TO>), dim3(grid), dim3(256), 0, s,
-                       (const TI*)x, (TO*)y, n, scale_ptr, scale)));
+    if (accumulate)
+      hipLaunchKernelGGL((scale_copy_kernel<TI, TO, true>), dim3(grid), dim3(256), 0, s,
+                         (const TI*)x, (TO*)y, n, scale_ptr, scale);
+    else
+      hipLaunchKernelGGL((scale_copy_kernel<TI, TO, false>), dim3(grid), dim3(256), 0, s,
+                         (const TI*)x, (TO*)y, n, scale_ptr, scale)));
 }
 
 // workspace: >= 2*1024 + 1 floats; upd: n floats

@@ -433,12 +433,17 @@ def adam_compact_(hi, res, g, m, v, lr, beta1, beta2, eps, weight_decay, step, b
     res.copy_(r)
 
 
-def scale_copy_(x: torch.Tensor, y: torch.Tensor, scale: float = 1.0, scale_tensor: Optional[torch.Tensor] = None):
+def scale_copy_(x: torch.Tensor, y: torch.Tensor, scale: float = 1.0, scale_tensor: Optional[torch.Tensor] = None,
+                accumulate: bool = False):
+    """y = x * scale (accumulate: y += x * scale), one pass for any dtype pair."""
     if x.is_cuda and x.data_ptr() % (x.element_size() * 4) == 0 and y.data_ptr() % (y.element_size() * 4) == 0:
-        hip_ops().scale_copy(x, y, scale_tensor, scale)
+        hip_ops().scale_copy(x, y, scale_tensor, scale, accumulate)
     else:
         s = scale if scale_tensor is None else scale * scale_tensor.float()
-        y.copy_(x.float() * s)
+        if accumulate:
+            y.add_((x.float() * s).to(y.dtype))
+        else:
+            y.copy_(x.float() * s)
     return y
 
 
@@ -891,7 +896,8 @@ class _EmbeddingFn(torch.autograd.Function):
         (ids,) = ctx.saved_tensors
         w = ctx.weight
         H = ctx.wshape[1]
-        sorted_ids, perm = torch.sort(ids.reshape(-1), stable=True)
+        # the kernel takes int64 ids (nn.Embedding also accepts int32: widen before the sort)
+        sorted_ids, perm = torch.sort(ids.reshape(-1).long(), stable=True)
         g2 = g.reshape(-1, H).contiguous()
         from .linear import FUSE_WGRAD, _bound_grad
         bound = _bound_grad(w) if FUSE_WGRAD else None

@@ -279,9 +279,13 @@ class DeepSpeedTransformerLayer(nn.Module):
     def forward(self, hidden_states, attention_mask=None, head_mask=None, encoder_hidden_states=None,
                 encoder_attention_mask=None, output_attentions=False, grads=None):
         rng = getattr(self, "_rng", None)
-        if rng is not None and self.training and torch.is_grad_enabled():
+        if rng is not None and self.training:
             from ...runtime.activation_checkpointing import checkpointing as ds_ckpt
-            if not ds_ckpt.is_recomputing():  # a recompute must redraw the forward's masks
+            # a new training forward draws new masks -- including the first (no_grad) forward of
+            # an activation checkpoint; its recompute inside backward must redraw the same masks,
+            # so it does not advance (the recompute follows its own forward before the next
+            # forward of this layer, as in gradient accumulation)
+            if (torch.is_grad_enabled() or ds_ckpt.is_checkpoint_forward()) and not ds_ckpt.is_recomputing():
                 rng[1:].add_(1)
         self.config.training = self.training
         self.config.is_grad_enabled = torch.is_grad_enabled()

@@ -120,6 +120,7 @@ class DeepSpeedEngine(Module):
         self.training_dataloader = self.deepspeed_io(training_data) if training_data else None
 
         self.optimizer = None
+        self.amp = None  # runtime/amp.py AmpState when "amp": {"enabled": true}
         self.basic_optimizer = None
         self.lr_scheduler = None
         if model_parameters or optimizer:
@@ -500,7 +501,8 @@ class DeepSpeedEngine(Module):
             self.data_parallel_group = self.mpu.get_data_parallel_group()
             self.dp_world_size = self.mpu.get_data_parallel_world_size()
             self.mp_world_size = self.mpu.get_model_parallel_world_size()
-        if not self.amp_enabled() and dist.is_initialized() and self.dp_world_size > 1 and \
+        # (amp included: the reference broadcasts after amp.initialize, REF engine.py:693-694)
+        if dist.is_initialized() and self.dp_world_size > 1 and \
                 os.environ.get("DSA_SKIP_MODEL_BROADCAST", "0") != "1":
             self._broadcast_model()
 
@@ -526,8 +528,17 @@ class DeepSpeedEngine(Module):
         if name in (ONEBIT_ADAM_OPTIMIZER, ONEBIT_LAMB_OPTIMIZER) and self.zero_optimization():
             raise AssertionError("1-bit optimizers are not compatible with ZeRO")
         if self.zero_optimization():
-            assert not self.amp_enabled(), "Amp and ZeRO are not currently compatible"
+            assert not self.amp_enabled(), ("Amp and ZeRO are not currently compatible: use the bf16 / fp16 "
+                                            "config blocks (\"fp16\": {\"enabled\": true, \"type\": \"bfloat16\"})")
             self.optimizer = self._configure_zero_optimizer(basic_optimizer)
+        elif self.amp_enabled():
+            assert not self.fp16_enabled(), "Cannot enable both amp with (legacy) fp16 mode"
+            from .amp import AmpState
+            self.amp = AmpState(self.amp_params() or {}, self.device)
+            log_dist(f"amp: fp32 master parameters, forward under autocast({self.amp.dtype}), "
+                     f"opt_level {self.amp.opt_level}, loss scaling "
+                     f"{'dynamic' if self.amp.scaler is not None else 'off'}", ranks=[0])
+            self.optimizer = basic_optimizer
         elif self.fp16_enabled():
             self.optimizer = self._configure_fp16_optimizer(basic_optimizer)
         else:
@@ -721,7 +732,11 @@ class DeepSpeedEngine(Module):
             self.timers("forward").start()
         if self.training_dataloader is None:
             self.tput_timer.start()
-        loss = self.module(*inputs, **kwargs)
+        if self.amp is not None:
+            with self.amp.autocast():
+                loss = self.module(*inputs, **kwargs)
+        else:
+            loss = self.module(*inputs, **kwargs)
         if self.wall_clock_breakdown():
             self.timers("forward").stop()
             self.timers("forward_microstep").stop()
@@ -768,6 +783,9 @@ class DeepSpeedEngine(Module):
             self.optimizer.is_gradient_accumulation_boundary = self.is_gradient_accumulation_boundary()
         if hasattr(self.optimizer, "backward") and (self.zero_optimization() or self.fp16_enabled()):
             self.optimizer.backward(loss)
+        elif self.amp is not None:
+            # the unscale is delayed to the accumulation boundary (apex delay_unscale)
+            self.amp.scale(loss).backward()
         else:
             loss.backward()
         _linear_ops.clear_transposed()  # pre-transposed operands never outlive their backward
@@ -829,12 +847,19 @@ class DeepSpeedEngine(Module):
     def _take_model_step(self, lr_kwargs):
         if self.gradient_clipping() > 0.0 and not self.fp16_enabled() and not hasattr(self.optimizer, "groups"):
             self.timers("_step_clipping").start()
+            if self.amp is not None:
+                self.amp.unscale(self.optimizer)  # clip the unscaled fp32 masters (REF engine.py:1148-1153)
             self.clip_fp32_gradients()
             self.timers("_step_clipping").stop()
         if self.store_gradients:
+            if self.amp is not None:
+                self.amp.unscale(self.optimizer)
             self.stored_gradients = self._snapshot_gradients()
         self.timers("_step_step").start()
-        self.optimizer.step()
+        if self.amp is not None:
+            self.amp.step(self.optimizer)
+        else:
+            self.optimizer.step()
         self.timers("_step_step").stop()
         self.timers("_step_zero_grad").start()
         if hasattr(self.optimizer, "groups"):
@@ -845,12 +870,13 @@ class DeepSpeedEngine(Module):
             self.optimizer.zero_grad()
         self.timers("_step_zero_grad").stop()
         report_progress = self.global_rank == 0
-        overflow = bool(getattr(self.optimizer, "overflow", False))
+        overflow = bool(self.amp.overflow if self.amp is not None else getattr(self.optimizer, "overflow", False))
         if overflow:
             self.skipped_steps += 1
         elif self.lr_scheduler is not None:
             self.lr_scheduler.step(**(lr_kwargs or {}))
         if report_progress and (self.global_steps + 1) % self.steps_per_print() == 0:
+            self._reconcile_device_skips()
             self._report_progress(self.global_steps + 1)
         self.global_steps += 1
         self.global_samples += self.train_batch_size()
@@ -904,6 +930,11 @@ class DeepSpeedEngine(Module):
 
     def get_pld_theta(self):
         return self.progressive_layer_drop.get_theta() if self.progressive_layer_drop else None
+
+    def _reconcile_device_skips(self):
+        """Steps the optimizer skipped on the device without a host sync (sync-free LAMB)."""
+        if hasattr(self.optimizer, "reconcile_skipped_steps"):
+            self.skipped_steps += self.optimizer.reconcile_skipped_steps()
 
     def _report_progress(self, step):
         log_dist(f"step={step}, skipped={self.skipped_steps}, lr={self.get_lr()}, mom={self.get_mom()}", ranks=[0])
@@ -1073,6 +1104,7 @@ class DeepSpeedEngine(Module):
                 "layout": layout_signature(opt.groups), "dp_world_size": opt.dp_world}
 
     def _save_checkpoint(self, save_dir, tag, client_state=None):
+        self._reconcile_device_skips()
         save_path = self._get_ckpt_name(save_dir, tag)
         if self.zero_optimization_partition_weights():
             module_sd = self._zero3_module_payload()
@@ -1084,6 +1116,8 @@ class DeepSpeedEngine(Module):
                      csr_tensor_module_names=self.csr_tensor_module_names, skipped_steps=self.skipped_steps,
                      global_steps=self.global_steps, global_samples=self.global_samples,
                      dp_world_size=self.dp_world_size, mp_world_size=self.mp_world_size, ds_version=__version__)
+        if self.amp is not None:
+            state["amp"] = self.amp.state_dict()
         state.update(client_state or {})
         log_dist(message=f"Saving model checkpoint: {save_path}", ranks=[0])
         torch.save(state, save_path)
@@ -1206,6 +1240,8 @@ class DeepSpeedEngine(Module):
         if not self.zero_optimization() and load_optimizer_states and self.optimizer is not None and \
                 checkpoint.get("optimizer") is not None:
             self.optimizer.load_state_dict(checkpoint["optimizer"])
+        if self.amp is not None and load_optimizer_states and checkpoint.get("amp"):
+            self.amp.load_state_dict(checkpoint["amp"])
         if load_lr_scheduler_states and self.lr_scheduler is not None and checkpoint.get("lr_scheduler"):
             self.lr_scheduler.load_state_dict(checkpoint["lr_scheduler"])
         self.csr_tensor_module_names = checkpoint.get("csr_tensor_module_names", set())
@@ -1214,7 +1250,7 @@ class DeepSpeedEngine(Module):
         self.skipped_steps = checkpoint.get("skipped_steps", 0)
         self.loaded_checkpoint_mp_world_size = checkpoint.get("mp_world_size")
         self.loaded_checkpoint_dp_world_size = checkpoint.get("dp_world_size")
-        deepspeed_states = ["module", "optimizer", "lr_scheduler", "csr_tensor_module_names", "skipped_steps",
+        deepspeed_states = ["module", "optimizer", "amp", "lr_scheduler", "csr_tensor_module_names", "skipped_steps",
                             "global_steps", "dp_world_size", "mp_world_size", "global_samples", "ds_version"]
         client_state = {k: v for k, v in checkpoint.items() if k not in deepspeed_states}
         return load_path, client_state

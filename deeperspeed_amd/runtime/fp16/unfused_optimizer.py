@@ -53,6 +53,9 @@ class FP16_UnfusedOptimizer:
         self.overflow_checker = CheckOverflow(self.fp16_groups, mpu=mpu)
         self._global_grad_norm = 0.0
         self._overlap = None
+        self._persistent_zeroed = False  # set by an overlapped step that zeroed them itself
+        self._dev_skipped = None  # device count of sync-free steps skipped as non-finite
+        self._skips_seen = 0
         if overlap_step:
             self._setup_overlap(module, overlap_bucket_numel, verbose)
         if verbose:
@@ -74,6 +77,26 @@ class FP16_UnfusedOptimizer:
     @property
     def cur_scale(self):
         return self.loss_scaler.loss_scale
+
+    def reconcile_skipped_steps(self) -> int:
+        """Sync-free steps skip a non-finite update inside the kernels, unseen by the host.  This
+        reads the device-side count (one host sync: call it at print / checkpoint boundaries),
+        rolls the per-parameter step counters back by the newly skipped steps so later bias
+        corrections are right again, and returns that number for the engine's skipped-step
+        accounting.  Steps taken between a skip and this call used a bias correction one step
+        ahead (documented drift; the LR schedule is not rolled back either)."""
+        if self._dev_skipped is None:
+            return 0
+        n = int(self._dev_skipped.item()) - self._skips_seen
+        if n <= 0:
+            return 0
+        self._skips_seen += n
+        for st in self.optimizer.state.values():
+            if "step" in st:
+                st["step"] = max(0, st["step"] - n)
+        logger.warning(f"[deepspeed] {n} sync-free LAMB step(s) had a non-finite gradient norm and were skipped "
+                       f"on the device; optimizer step counters rolled back")
+        return n
 
     def get_global_grad_norm(self):
         if torch.is_tensor(self._global_grad_norm):  # sync-free step: read on demand only
@@ -137,24 +160,43 @@ class FP16_UnfusedOptimizer:
         ov = self._overlap
         with ov.launch():
             for key, by_group in enumerate(self._overlap_buckets):
+                persistent = []
                 for gi, idxs in by_group.items():
                     lp = self.fp16_groups[gi]
                     grads = [lp[i].grad for i in idxs]
                     self.optimizer.step_subset(gi, idxs, grads, [lp[i].data for i in idxs], coef_t)
+                    persistent += [g for i, g in zip(idxs, grads)
+                                   if g is not None and getattr(lp[i], "_dsa_persistent_grad", False)]
+                # persistent (HIP-graph-captured) gradient buffers are zeroed in place HERE, on the
+                # side stream behind the kernels that read them and before the bucket's event:
+                # the next forward / graph replay waits for that event before it accumulates
+                # into them again.  Zeroing them on the compute stream would race the step.
+                if persistent:
+                    torch._foreach_zero_(persistent)
                 ov.bucket_done(key)
         for g in self.fp16_groups:  # the side stream still reads the gradients
             for p in g:
                 if p.grad is not None:
                     p.grad.record_stream(ov.stream)
-        self.zero_grad()
+        self.zero_grad(skip_persistent=True)
 
     # ----------------------------------------------------------------- steps
-    def zero_grad(self, set_to_none=True):
+    def zero_grad(self, set_to_none=True, skip_persistent=False):
+        """skip_persistent: the persistent buffers were already zeroed on the overlapped step's
+        side stream (_overlapped_fused_step); that holds until the next backward."""
+        skip_persistent = skip_persistent or self._persistent_zeroed
+        if skip_persistent:
+            self._persistent_zeroed = True
+        elif self._overlap is not None and self._overlap._done is not None:
+            # an overlapped step may still read the persistent buffers on its side stream: order
+            # the in-place zeroing after it (a stream wait, no host sync)
+            torch.cuda.current_stream().wait_event(self._overlap._done)
         keep = []
         for group in self.fp16_groups:
             for p in group:
                 if getattr(p, "_dsa_persistent_grad", False) and p.grad is not None:
-                    keep.append(p.grad)  # a captured HIP graph accumulates into this buffer
+                    if not skip_persistent:
+                        keep.append(p.grad)  # a captured HIP graph accumulates into this buffer
                 elif set_to_none:
                     p.grad = None
                 elif p.grad is not None:
@@ -164,12 +206,16 @@ class FP16_UnfusedOptimizer:
             torch._foreach_zero_(keep)
 
     def backward(self, loss, retain_graph=False):
+        self._persistent_zeroed = False  # new gradients accumulate into the persistent buffers
         (loss.float() * self.loss_scale).backward(retain_graph=retain_graph)
 
     def step(self, closure=None):
         params = [p for g in self.fp16_groups for p in g]
         if self._sync_free(params):
             coef_t = self._device_coef(params)
+            if self._dev_skipped is None:
+                self._dev_skipped = torch.zeros(1, dtype=torch.int32, device=coef_t.device)
+            self._dev_skipped.add_(torch.isfinite(coef_t).logical_not())  # read lazily
             self.overflow = False
             if self._overlap is not None:
                 self._overlapped_fused_step(coef_t)

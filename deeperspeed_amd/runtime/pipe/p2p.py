@@ -17,6 +17,49 @@ import torch.distributed as dist
 
 _grid = None
 
+# Optional log of every p2p transfer this rank issues, in issue order:
+# (kind "send" | "recv", peer global rank, shape, dtype).  RCCL serialises the send/recv of a
+# rank pair on one communicator stream, so the two ranks of every pair must issue complementary
+# sequences (rank a's k-th op towards b is the mirror of b's k-th op towards a) or the pair can
+# deadlock; gloo queues both directions independently and cannot show such a bug.  The log lets
+# a test (tests/test_pipe_p2p_order.py) or a debugging run check the invariant on any backend.
+_op_log = None
+
+
+def record_ops(enable: bool = True):
+    """Start (clearing) or stop the transfer log."""
+    global _op_log
+    _op_log = [] if enable else None
+
+
+def op_log():
+    return list(_op_log or [])
+
+
+def _log(kind, peer, t):
+    if _op_log is not None:
+        _op_log.append((kind, int(peer), tuple(t.shape), str(t.dtype)))
+
+
+def check_pair_order(logs):
+    """logs: {global rank: op_log()}.  Returns a list of human-readable violations (empty if every
+    pair issues complementary send/recv sequences)."""
+    errs = []
+    flip = {"send": "recv", "recv": "send"}
+    for a, la in logs.items():
+        for b, lb in logs.items():
+            if b <= a:
+                continue
+            ab = [(k, sh, dt) for k, peer, sh, dt in la if peer == b]
+            ba = [(flip[k], sh, dt) for k, peer, sh, dt in lb if peer == a]
+            if ab == ba:
+                continue
+            n = next((i for i, (x, y) in enumerate(zip(ab, ba)) if x != y), min(len(ab), len(ba)))
+            errs.append(f"ranks {a}<->{b}: op {n} differs: rank {a} issues "
+                        f"{ab[n] if n < len(ab) else None}, rank {b} mirrors {ba[n] if n < len(ba) else None} "
+                        f"({len(ab)} vs {len(ba)} ops)")
+    return errs
+
 
 def init_process_groups(grid):
     global _grid
@@ -45,6 +88,7 @@ def send(tensor, dest_stage, async_op=False, fp32_comm=False):
     src_stage = _grid.get_stage_id()
     _is_valid_send_recv(src_stage, dest_stage)
     t = tensor.float() if (fp32_comm and tensor.dtype == torch.bfloat16) else tensor
+    _log("send", _peer(dest_stage), t)
     if _host_staged(t):
         dist.send(t.detach().cpu().contiguous(), _peer(dest_stage))
         return None
@@ -58,6 +102,7 @@ def send(tensor, dest_stage, async_op=False, fp32_comm=False):
 def recv(tensor, src_stage, async_op=False, fp32_comm=False):
     dest_stage = _grid.get_stage_id()
     _is_valid_send_recv(src_stage, dest_stage)
+    _log("recv", _peer(src_stage), tensor.float() if (fp32_comm and tensor.dtype == torch.bfloat16) else tensor)
     if _host_staged(tensor):
         buf = torch.empty(tensor.shape, dtype=torch.float32 if (fp32_comm and tensor.dtype == torch.bfloat16)
                           else tensor.dtype)
@@ -118,6 +163,7 @@ def send_many(tensors: List[torch.Tensor], dest_stage, fp32_comm=False, async_op
     keep = []
     for t in tensors:
         x = t.float() if (fp32_comm and t.dtype == torch.bfloat16) else t.contiguous()
+        _log("send", peer, x)
         keep.append(x)
         ops.append(dist.P2POp(dist.isend, x, peer))
     h = P2PHandle(dist.batch_isend_irecv(ops) if ops else [], keep=keep)
@@ -140,8 +186,10 @@ def recv_many(tensors: List[torch.Tensor], src_stage, fp32_comm=False, async_op=
         if fp32_comm and t.dtype == torch.bfloat16:
             b = torch.empty(t.shape, dtype=torch.float32, device=t.device)
             staged.append((t, b))
+            _log("recv", peer, b)
             ops.append(dist.P2POp(dist.irecv, b, peer))
         else:
+            _log("recv", peer, t)
             ops.append(dist.P2POp(dist.irecv, t, peer))
     h = P2PHandle(dist.batch_isend_irecv(ops) if ops else [], keep=tensors, staged=staged)
     if async_op:

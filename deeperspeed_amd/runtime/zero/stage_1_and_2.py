@@ -271,13 +271,18 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
             work = comm.all_reduce(src, group=self.dp_group, async_op=True, tag="zero.allreduce")
             out = src[self.dp_rank * b.chunk: (self.dp_rank + 1) * b.chunk]
         else:
-            out.copy_(src[: b.chunk])
+            if out is out_slice:
+                out.copy_(src[: b.chunk])
+            else:  # one rank: finish() reads the bucket itself (no staging copy)
+                out = src[: b.chunk]
             work = None
 
         def finish(out=out, out_slice=out_slice, accumulate=accumulate, st=st, g=g):
             if out is not out_slice:
                 if accumulate:
-                    out_slice.add_(out.to(out_slice.dtype))
+                    # bf16 micro-batch gradient into the fp32 shard: one fused cast-accumulate pass
+                    from ...ops import native
+                    native.scale_copy_(out, out_slice, 1.0, accumulate=True)
                 else:
                     out_slice.copy_(out)
             if st.buffer is not None:

@@ -57,5 +57,20 @@ from deeperspeed_amd import (DeepSpeedConfig, DeepSpeedEngine, __version__, add_
                              checkpointing, init_distributed, initialize, log_dist, logger)
 
 
+# Legacy `deepspeed.pt.*` module paths (REF deepspeed/__init__.py:39-49): the same module objects
+# under their pre-0.3 names.
+import types as _types  # noqa: E402
+
+_LEGACY_PT = {"deepspeed_utils": "deeperspeed_amd.runtime.utils",
+              "deepspeed_config": "deeperspeed_amd.runtime.config",
+              "loss_scaler": "deeperspeed_amd.runtime.fp16.loss_scaler"}
+pt = _types.ModuleType("deepspeed.pt", "legacy deepspeed.pt module paths")
+sys.modules["deepspeed.pt"] = pt
+for _name, _target in _LEGACY_PT.items():
+    _mod = importlib.import_module(_target)
+    setattr(pt, _name, _mod)
+    sys.modules["deepspeed.pt." + _name] = _mod
+
+
 def __getattr__(name):
     return getattr(_impl, name)

@@ -59,3 +59,34 @@ def test_bench_pipeline_onebit_self_spawn():
     assert r.returncode == 0, r.stderr.decode()[-3000:]
     out = json.loads(r.stdout.decode().strip())
     assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "pp2-dp2"
+
+
+def test_bench_watchdog_ends_a_frozen_job():
+    """rank 3 of a 4-rank gloo job freezes (SIGSTOP) at warmup step 1; the
+    other ranks block in its collectives.  Their watchdogs (no heartbeat for
+    DSA_BENCH_WATCHDOG_S) end them with their last heartbeat and stacks, and the parent stops
+    every rank (the stopped one included) and exits non-zero well before any process-group
+    timeout."""
+    import time
+    t0 = time.time()
+    r = _run(["--gpus", "4", "--model", "tiny", "--seq", "64", "--steps", "2", "--warmup", "3",
+              "--dist-backend", "gloo"],
+             extra_env={"DSA_BENCH_STOP_RANK": "3", "DSA_BENCH_WATCHDOG_S": "20"}, timeout=200)
+    took = time.time() - t0
+    err = r.stderr.decode()
+    assert r.returncode != 0, err[-3000:]
+    assert took < 150, took
+    assert "WATCHDOG" in err, err[-3000:]
+    assert "last heartbeat" in err
+    assert "[hb] rank=3" in err  # per-rank heartbeat lines
+    assert r.stdout.decode().strip() == ""
+
+
+def test_bench_heartbeats_per_step():
+    r = _run(["--gpus", "2", "--model", "tiny", "--seq", "64", "--steps", "2", "--warmup", "1",
+              "--dist-backend", "gloo"])
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    err = r.stderr.decode()
+    for rank in (0, 1):
+        assert f"[hb] rank={rank} warmup 0 done" in err
+        assert f"[hb] rank={rank} timed step 1 queued" in err

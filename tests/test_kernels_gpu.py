@@ -863,3 +863,19 @@ def test_embedding_backward_sync_free(V, pattern, padding_idx):
     emb.weight.grad = None
     emb(ids).backward(dy)
     assert torch.equal(emb.weight.grad, g1)  # deterministic
+
+
+def test_embedding_backward_int32_ids():
+    """nn.Embedding accepts int32 ids; the HIP backward (int64 sorted ids) widens them first
+    (ADVICE r3): same gradient as int64 ids."""
+    from deeperspeed_amd.ops.native import Embedding
+    torch.manual_seed(3)
+    V, H = 4096, 256
+    ids = torch.randint(0, V, (8, 512), device=_dev())
+    dy = torch.randn(8, 512, H, device=_dev(), dtype=torch.bfloat16)
+    grads = []
+    for dt in (torch.int64, torch.int32):
+        emb = Embedding(V, H, device=_dev(), dtype=torch.bfloat16)
+        emb(ids.to(dt)).backward(dy)
+        grads.append(emb.weight.grad.clone())
+    assert torch.equal(grads[0], grads[1])

@@ -20,7 +20,7 @@ def _env():
     os.environ.setdefault("WORLD_SIZE", "1")
 
 
-def _train(overlap, clip, steps=4, bucket_numel=None):
+def _train(overlap, clip, steps=4, bucket_numel=None, graphs=False):
     _env()
     import deeperspeed_amd as ds
     from deeperspeed_amd.models.bert import BertForPreTraining, get_config
@@ -46,6 +46,12 @@ def _train(overlap, clip, steps=4, bucket_numel=None):
     pos = torch.stack([torch.randperm(S, device=dev, generator=g)[:npred].sort().values for _ in range(B)])
     lab = torch.randint(0, cfg.vocab_size, (B, npred), device=dev, generator=g)
     nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
+    if graphs:  # persistent gradient buffers, zeroed in place by the optimizer
+        from deeperspeed_amd.ops.transformer.transformer import make_graphed_encoder
+        ext = ((1.0 - am.to(torch.bfloat16)) * -10000.0)[:, None, None, :]
+        make_graphed_encoder(engine.module.layers, torch.randn(B, S, cfg.hidden_size, device=dev,
+                                                               dtype=torch.bfloat16), ext)
+        torch.cuda.synchronize()
     losses = []
     for _ in range(steps):
         loss = engine(ids, tt, am, pos, lab, nsp)
@@ -70,6 +76,20 @@ def test_overlapped_lamb_step_is_exact(clip):
     for a, b in zip(base_s, ov_s):
         assert torch.equal(a, b)
     assert base_l[-1] < base_l[0]
+
+
+def test_overlapped_lamb_with_hip_graph_persistent_grads():
+    """HIP-graphed encoder (persistent .grad buffers zeroed in place) + overlapped step: the side
+    stream zeroes each bucket's persistent buffers behind its own LAMB kernels, so the next
+    replay never accumulates into a buffer the step is still reading.  Must equal
+    graphed + serial step bit for bit."""
+    base_l, base_w, base_s, _, _ = _train(False, 1.0, steps=5, graphs=True)
+    ov_l, ov_w, ov_s, _, _ = _train(True, 1.0, steps=5, graphs=True)
+    assert base_l == ov_l
+    for a, b in zip(base_w, ov_w):
+        assert torch.equal(a, b)
+    for a, b in zip(base_s, ov_s):
+        assert torch.equal(a, b)
 
 
 def test_lamb_device_scale_skips_non_finite():
@@ -121,3 +141,35 @@ def test_sync_free_step_matches_host_checked_step(monkeypatch, clip):
             assert abs(a - b) <= 1e-3 * abs(a)
         for a, b in zip(host_w, dev_w):
             assert torch.allclose(a, b, rtol=1e-2, atol=1e-3)
+
+
+def test_sync_free_skip_is_counted_and_rolled_back():
+    """a sync-free bf16 LAMB step with a non-finite gradient is skipped inside the
+    kernels; the engine learns it at the next print / checkpoint boundary (skipped_steps), and the
+    per-parameter step counters are rolled back so later bias corrections are right."""
+    _env()
+    import torch.nn as nn
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.runtime.fp16 import unfused_optimizer as uo
+    if not uo.SYNC_FREE_STEP:
+        pytest.skip("DSA_SYNC_FREE_STEP=0")
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(256, 512), nn.GELU(), nn.Linear(512, 256)).to(dev, torch.bfloat16)
+    conf = {"train_micro_batch_size_per_gpu": 8, "gradient_accumulation_steps": 1, "steps_per_print": 3,
+            "optimizer": {"type": "Lamb", "params": {"lr": 1e-3}},
+            "fp16": {"enabled": True, "type": "bfloat16"}, "gradient_clipping": 1.0}
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    opt = engine.optimizer
+    assert isinstance(opt, uo.FP16_UnfusedOptimizer) and opt._sync_free([p for g in opt.fp16_groups for p in g])
+    x = torch.randn(8, 256, device=dev, dtype=torch.bfloat16)
+    for i in range(3):
+        loss = engine(x).float().pow(2).mean()
+        engine.backward(loss)
+        if i == 1:
+            next(iter(model.parameters())).grad[0, 0] = float("inf")
+        engine.step()
+    torch.cuda.synchronize()
+    assert engine.skipped_steps == 1  # reconciled at the steps_per_print boundary
+    steps = {st["step"] for st in opt.state.values() if "step" in st}
+    assert steps == {2}

@@ -230,3 +230,25 @@ def test_layer_norm_residual_passthrough_gradients():
         res.append((y.detach(), xi.grad, wi.grad, bi.grad))
     for a, c in zip(*res):
         assert torch.allclose(a, c, atol=1e-4, rtol=1e-4)
+
+
+def test_device_rng_advances_once_per_checkpointed_forward():
+    """Device-RNG dropout step under activation checkpointing: the first (no_grad)
+    forward of the checkpoint advances the step, the recompute inside backward does not (it
+    must redraw the same masks) -- so two checkpointed training steps use two different steps."""
+    from deeperspeed_amd.runtime.activation_checkpointing import checkpointing as ckpt
+    torch.manual_seed(0)
+    cfg = DeepSpeedTransformerConfig(batch_size=2, hidden_size=64, intermediate_size=256, heads=4,
+                                     attn_dropout_ratio=0.1, hidden_dropout_ratio=0.1, num_hidden_layers=1,
+                                     initializer_range=0.02, pre_layer_norm=True, training=True)
+    layer = DeepSpeedTransformerLayer(cfg).train()
+    layer.enable_device_rng(11)
+    x = torch.randn(2, 16, 64, requires_grad=True)
+    m = torch.zeros(2, 1, 1, 16)
+    for step in (1, 2):
+        out = ckpt.checkpoint(lambda h: layer(h, m), x)
+        assert int(layer._rng[1]) == step
+        out.sum().backward()
+        assert int(layer._rng[1]) == step  # the recompute did not advance it
+    layer(x, m)  # plain (non-checkpointed) training forward
+    assert int(layer._rng[1]) == 3
