@@ -379,9 +379,12 @@ def main():
     # without recompute and leaves room to keep every gathered unit resident: hipBLASLt is ~4 %
     # faster at M = 16384 tokens than at 8192 (profiles/aux/gemm_m16k.log) and the
     # per-micro-batch ZeRO-3 gradient reduce-scatters halve.  Otherwise micro-batch 4 x 4.
+    # Smaller models (GPT-NeoX 1.3B, BASELINE config 2) run the 16 sequences as one micro-batch:
+    # 16 x 1 measured 109.7k vs 104.6k tok/s for 8 x 2 on one MI355X (profiles/r4b_*), larger GEMMs
+    # and no accumulation pass
     if args.micro_batch or args.grad_accum or not big:
-        mb = args.micro_batch or (4 if big else 8)
-        ga = args.grad_accum or (4 if big else 2)
+        mb = args.micro_batch or (4 if big else 16 // (args.grad_accum or 1))
+        ga = args.grad_accum or (4 if big else max(1, 16 // mb))
         offload, ckpt, planned = layout(mb, ga)
     else:
         for mb, ga in ((8, 2), (4, 4)):

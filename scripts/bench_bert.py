@@ -59,8 +59,18 @@ def main():
             # the reference's BERT configs clip at 1.0 (tests/model/BingBertSquad/*_config.json)
             "gradient_clipping": 1.0,
             "zero_optimization": {"stage": 0, "overlap_step": args.overlap_step == "on"}}
-    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
     B, S = args.batch, args.seq
+    if args.hip_graphs == "on" and dev.type == "cuda":
+        # captured before initialize: overlap_step registers forward pre-hooks, which
+        # make_graphed_callables refuses on the modules it captures (hooks added later are fine)
+        from deeperspeed_amd.ops.transformer.transformer import make_graphed_encoder
+        ext = torch.zeros(B, 1, 1, S, device=dev, dtype=torch.bfloat16)  # all-ones attention mask
+        make_graphed_encoder(model.layers, torch.randn(B, S, cfg.hidden_size, device=dev, dtype=torch.bfloat16), ext)
+        for p in model.parameters():  # the capture's warmup iterations accumulated into the buffers
+            if p.grad is not None:
+                p.grad.zero_()
+        torch.cuda.synchronize()
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
     npred = max(1, round(0.15 * S / 8) * 8 // 1) if S != 128 else 20
     npred = 20 if S == 128 else (80 if S == 512 else npred)
     g = torch.Generator(device=dev).manual_seed(1)
@@ -70,13 +80,6 @@ def main():
     pos = torch.stack([torch.randperm(S, device=dev, generator=g)[:npred].sort().values for _ in range(B)])
     lab = torch.randint(0, cfg.vocab_size, (B, npred), device=dev, generator=g)
     nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
-
-    if args.hip_graphs == "on" and dev.type == "cuda":
-        from deeperspeed_amd.ops.transformer.transformer import make_graphed_encoder
-        m = engine.module
-        ext = ((1.0 - am.to(torch.bfloat16)) * -10000.0)[:, None, None, :]
-        make_graphed_encoder(m.layers, torch.randn(B, S, cfg.hidden_size, device=dev, dtype=torch.bfloat16), ext)
-        torch.cuda.synchronize()
 
     def step():
         loss = engine(ids, tt, am, pos, lab, nsp)

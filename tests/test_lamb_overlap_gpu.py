@@ -34,6 +34,15 @@ def _train(overlap, clip, steps=4, bucket_numel=None, graphs=False):
             "optimizer": {"type": "Lamb", "params": {"lr": 2e-3, "weight_decay": 0.01}},
             "fp16": {"enabled": True, "type": "bfloat16"}, "gradient_clipping": clip,
             "zero_optimization": {"stage": 0, "overlap_step": overlap}}
+    if graphs:  # graphed before initialize: overlap_step's forward pre-hooks come after the capture
+        from deeperspeed_amd.ops.transformer.transformer import make_graphed_encoder
+        B, S = 8, 128
+        ext = torch.zeros(B, 1, 1, S, device=dev, dtype=torch.bfloat16)
+        make_graphed_encoder(model.layers, torch.randn(B, S, cfg.hidden_size, device=dev, dtype=torch.bfloat16), ext)
+        for p in model.parameters():  # the capture's warmup iterations accumulated into them
+            if p.grad is not None:
+                p.grad.zero_()
+        torch.cuda.synchronize()
     engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
     opt = engine.optimizer
     assert isinstance(opt, FP16_UnfusedOptimizer)
@@ -46,12 +55,6 @@ def _train(overlap, clip, steps=4, bucket_numel=None, graphs=False):
     pos = torch.stack([torch.randperm(S, device=dev, generator=g)[:npred].sort().values for _ in range(B)])
     lab = torch.randint(0, cfg.vocab_size, (B, npred), device=dev, generator=g)
     nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
-    if graphs:  # persistent gradient buffers, zeroed in place by the optimizer
-        from deeperspeed_amd.ops.transformer.transformer import make_graphed_encoder
-        ext = ((1.0 - am.to(torch.bfloat16)) * -10000.0)[:, None, None, :]
-        make_graphed_encoder(engine.module.layers, torch.randn(B, S, cfg.hidden_size, device=dev,
-                                                               dtype=torch.bfloat16), ext)
-        torch.cuda.synchronize()
     losses = []
     for _ in range(steps):
         loss = engine(ids, tt, am, pos, lab, nsp)
