@@ -916,7 +916,7 @@ static void check_lut(const Tensor& ptr, const Tensor& idx, const Tensor& msk, i
                   ptr.is_contiguous() && idx.is_contiguous() && msk.is_contiguous(),
               what, ": int32 contiguous LUT tensors");
   TORCH_CHECK(ptr.numel() == Hl * ntiles + 1, what, ": pointer array must hold Hl * S/64 + 1 entries");
-  TORCH_CHECK(idx.numel() == msk.numel(), what, ": index / mask length mismatch");
+  TORCH_CHECK(idx.numel() == 4 * msk.numel(), what, ": four gathered 16-blocks per mask entry");
 }
 
 // Score biases of the fused sparse kernels: kbias [B, S] fp32 (key padding, additive), ebias a
@@ -982,8 +982,8 @@ std::vector<Tensor> sparse_flash_fwd(Tensor q, Tensor k, Tensor v, Tensor rowptr
 // nslot = partial slots per (batch, head).
 std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor rowptr,
                                      Tensor cols, Tensor masks, Tensor rows, Tensor masks_t, Tensor tasks, Tensor fin,
-                                     int64_t nslot, int64_t Hl, bool causal, double scale, int64_t shift, bool o_bshd,
-                                     OptT kbias, OptT ebias) {
+                                     Tensor kgroups, int64_t nslot, int64_t Hl, bool causal, double scale,
+                                     int64_t shift, bool o_bshd, OptT kbias, OptT ebias) {
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), D = q.size(3);
   for (auto* t : {&q, &k, &v}) {
     check_dev(*t, "sparse_flash_bwd");
@@ -1001,8 +1001,12 @@ std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, 
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * S, "sparse_flash_bwd: lse");
   check_lut(rowptr, cols, masks, Hl, S / 64, "sparse_flash_bwd rowptr/cols/masks");
   check_dev(rows, "rows"); check_dev(masks_t, "masks_t"); check_dev(tasks, "tasks"); check_dev(fin, "fin");
-  TORCH_CHECK(rows.scalar_type() == at::kInt && masks_t.scalar_type() == at::kInt && rows.numel() == masks_t.numel(),
+  TORCH_CHECK(rows.scalar_type() == at::kInt && masks_t.scalar_type() == at::kInt &&
+                  rows.numel() == 4 * masks_t.numel() && rows.is_contiguous() && masks_t.is_contiguous(),
               "sparse_flash_bwd: transposed LUT");
+  check_dev(kgroups, "kgroups");
+  TORCH_CHECK(kgroups.scalar_type() == at::kInt && kgroups.is_contiguous() && kgroups.numel() == Hl * (S / 64) * 4,
+              "sparse_flash_bwd: kgroups [Hl, S/64, 4]");
   TORCH_CHECK(tasks.scalar_type() == at::kInt && tasks.dim() == 3 && tasks.size(0) == Hl && tasks.size(2) == 4 &&
                   tasks.is_contiguous(), "sparse_flash_bwd: tasks [Hl, ntask, 4]");
   TORCH_CHECK(fin.scalar_type() == at::kInt && fin.dim() == 3 && fin.size(0) == Hl && fin.size(2) == 4 &&
@@ -1018,7 +1022,8 @@ std::vector<Tensor> sparse_flash_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, 
                                dv.data_ptr(), rowptr.data_ptr<int>(), cols.data_ptr<int>(),
                                reinterpret_cast<const uint32_t*>(masks.data_ptr<int>()), rows.data_ptr<int>(),
                                reinterpret_cast<const uint32_t*>(masks_t.data_ptr<int>()), tasks.data_ptr<int>(),
-                               (int)ntask, fin.data_ptr<int>(), (int)nfin, ws.data_ptr<float>(), (int)nslot,
+                               (int)ntask, fin.data_ptr<int>(), (int)nfin, kgroups.data_ptr<int>(), ws.data_ptr<float>(),
+                               (int)nslot,
                                (int)(B * H), (int)H, (int)Hl, (int)S, (int)D, causal, (float)scale, (int)shift,
                                dcode(q), cur_stream(), o_bshd ? (int)H : 0, sb.kb, sb.eb, sb.ez, sb.eh, sb.er);
   return {dq, dk, dv};

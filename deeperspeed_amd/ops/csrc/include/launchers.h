@@ -165,9 +165,9 @@ void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* 
 void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
                              const float* lse, float* delta, void* dq, void* dk, void* dv, const int* rowptr,
                              const int* cols, const uint32_t* masks, const int* rows, const uint32_t* masks_t,
-                             const int* tasks, int ntask, const int* fin, int nfin, float* ws, int nslot, int BH,
-                             int H, int Hl, int S, int D, bool causal, float scale, int shift, int dt, hipStream_t s,
-                             int onh = 0, const float* kbias = nullptr, const void* ebias = nullptr, int64_t ez = 0,
+                             const int* tasks, int ntask, const int* fin, int nfin, const int* kgroups, float* ws,
+                             int nslot, int BH, int H, int Hl, int S, int D, bool causal, float scale, int shift,
+                             int dt, hipStream_t s, int onh = 0, const float* kbias = nullptr, const void* ebias = nullptr, int64_t ez = 0,
                              int64_t eh = 0, int64_t er = 0);
 
 }  // namespace dsa

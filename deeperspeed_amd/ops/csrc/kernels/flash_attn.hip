@@ -1339,13 +1339,17 @@ template <int D> constexpr int dq_lds() { return (2 * BN * (D + 8) + 4 * 16 * (B
 // Flash attention restricted to the active blocks of a block-sparse layout (reference:
 // deepspeed/ops/sparse_attention matmul.py SDD/DSD + softmax.py, fused here into one pass per
 // query tile so the sparse score matrix is never written).  Granularity: 64-query x 64-key
-// tiles, 2 waves (32 queries or keys each) per workgroup.  The host builds, per layout head,
-//   fwd / dQ LUT : rowptr[nqt + 1], cols[e] = key tile, masks[e] = active layout sub-blocks
-//   dK / dV LUT  : colptr[nkt + 1], rows[e] = query tile, masks_t[e] (same bit convention)
-// For layout blocks smaller than 64 (16 / 32), a tile holds nsub x nsub sub-blocks; bit
-// (qsub << log2 nsub) + ksub of the mask says whether sub-block (qsub, ksub) is active, and
-// only tiles whose mask is not full are masked element-wise.  `shift` = log2(block) capped at
-// 6.  S must be a multiple of 64.  Causal masking (GPT) is applied on top of the layout.
+// MFMA tiles, 2 waves (32 queries or keys each) per workgroup, whose 64 keys (forward / dQ) or
+// 64 queries (dK / dV) are GATHERED from four 16-row blocks named by the LUT entry, so the work
+// follows the layout's active 16-blocks instead of the 64-tiles they touch
+// (ops/sparse_attention/flash.py builds the walks).  Per layout head:
+//   fwd / dQ LUT : rowptr[nqt + 1]; cols[e] = int4 key 16-blocks; masks[e] bit (qsub * 4 + kslot)
+//   dK / dV LUT  : tasks (key group, entry range, slot); kgroups[g] = int4 key 16-blocks of the
+//                  group (the output rows); rows[e] = int4 query 16-blocks; masks_t[e] bit
+//                  (qslot * 4 + kslot)
+// Block lists are ascending (padding repeats the last block with its mask bits clear); only
+// tiles whose mask is not full, or that reach past the causal diagonal, are masked element-wise.
+// S must be a multiple of 64.  Causal masking (GPT) is applied on top of the layout.
 constexpr int STILE = 64;
 
 // g is one head's base (wave-uniform): the tile loads go through a buffer resource sized to the
@@ -1375,10 +1379,29 @@ __device__ __forceinline__ void stile_store(uint16_t* lds, const uint4 (&r)[8 * 
   }
 }
 
-__device__ __forceinline__ uint32_t full_mask(int nsub_l2) {
-  const int bits = 1 << (2 * nsub_l2);
-  return bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
+// One of the four gathered 16-row blocks of a tile (i is compile-time in every caller but the
+// D = 96 tile loads, where it is a 3-deep select)
+__device__ __forceinline__ int sel4(const int4& b, int i) {
+  return i == 0 ? b.x : (i == 1 ? b.y : (i == 2 ? b.z : b.w));
 }
+
+// stile_load over a gathered tile: tile row `row` is row (row & 15) of 16-row block blk[row >> 4]
+template <int D, int NT>
+__device__ __forceinline__ void gtile_load(uint4 (&r)[8 * D / NT], const uint16_t* __restrict__ g, const int4 blk,
+                                           int S, int ld = D) {
+  constexpr int CH = D / 8;
+  const __amdgpu_buffer_rsrc_t rs = head_rsrc(g, S, ld);
+#pragma unroll
+  for (int k = 0; k < 8 * D / NT; ++k) {
+    const int c = threadIdx.x + NT * k;
+    const int row = c / CH, ch = c - row * CH;
+    const int grow = sel4(blk, row >> 4) * 16 + (row & 15);
+    const fa_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (grow * ld + ch * 8) * 2, 0, 0);
+    r[k] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+
+constexpr uint32_t GFULL = 0xffffu;  // all 4 x 4 (query 16-block, key 16-block) pairs of a tile active
 
 // Score biases of the reference sparse softmax (softmax_fwd.tr:46-129), compiled in by SX bits
 // (1: key-padding bias only -- BERT's case, no per-element loads; 3: both):
@@ -1414,10 +1437,10 @@ __device__ __forceinline__ float4 sbias4(const SExtra& sx, const uint16_t* eh, i
 }
 
 template <typename T, int D, bool CAUSAL, bool RP, int SX = 0>
-__global__ void __launch_bounds__(128, RP ? (SX ? 1 : 2) : 3) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+__global__ void __launch_bounds__(128, RP ? ((SX == 3 || (SX && D >= 128)) ? 1 : 2) : 3) sfwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                       const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                       float* __restrict__ LSE, const int* __restrict__ rowptr,
-                                                      const int* __restrict__ cols, const uint32_t* __restrict__ masks,
+                                                      const int4* __restrict__ cols, const uint32_t* __restrict__ masks,
                                                       int S, float scale, int onh, int H, int Hl, int shift,
                                                       SExtra sx = SExtra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -1434,9 +1457,7 @@ __global__ void __launch_bounds__(128, RP ? (SX ? 1 : 2) : 3) sfwd_kernel(const 
   const int e0 = rowptr[lh * nqt + qt], e1 = rowptr[lh * nqt + qt + 1];
   const int qrow = 32 * w + c32;  // row inside the tile
   const int myq = qt * STILE + qrow;
-  const int nsub_l2 = 6 - shift;
-  const uint32_t full = full_mask(nsub_l2);
-  const int qsub = qrow >> shift;
+  const int qsub = qrow >> 4;
   const uint16_t* Qb = Q + bh * (int64_t)S * D;
   const uint16_t* Kb = K + bh * (int64_t)S * D;
   const uint16_t* Vb = V + bh * (int64_t)S * D;
@@ -1454,24 +1475,24 @@ __global__ void __launch_bounds__(128, RP ? (SX ? 1 : 2) : 3) sfwd_kernel(const 
 
   uint4 kr[8 * D / NT], vr[8 * D / NT];
   if (RP && e0 < e1) {
-    stile_load<D, NT>(kr, Kb, cols[e0] * STILE, S);
-    stile_load<D, NT>(vr, Vb, cols[e0] * STILE, S);
+    gtile_load<D, NT>(kr, Kb, cols[e0], S);
+    gtile_load<D, NT>(vr, Vb, cols[e0], S);
     stile_store<D, NT>(smem, kr);
     stile_store<D, NT>(smem + TS, vr);
   }
   __syncthreads();
   for (int e = e0; e < e1; ++e) {
     const int it = e - e0;
-    const int j0 = cols[e] * STILE;
+    const int4 kb = cols[e];
     const uint32_t mask = masks[e];
     const bool has_next = e + 1 < e1;
     if (RP && has_next) {
-      stile_load<D, NT>(kr, Kb, cols[e + 1] * STILE, S);
-      stile_load<D, NT>(vr, Vb, cols[e + 1] * STILE, S);
+      gtile_load<D, NT>(kr, Kb, cols[e + 1], S);
+      gtile_load<D, NT>(vr, Vb, cols[e + 1], S);
     }
     if (!RP) {  // single LDS stage: more workgroups per CU hide the load instead
-      stile_load<D, NT>(kr, Kb, j0, S);
-      stile_load<D, NT>(vr, Vb, j0, S);
+      gtile_load<D, NT>(kr, Kb, kb, S);
+      gtile_load<D, NT>(vr, Vb, kb, S);
       if (it > 0) __syncthreads();
       stile_store<D, NT>(smem, kr);
       stile_store<D, NT>(smem + TS, vr);
@@ -1492,14 +1513,14 @@ __global__ void __launch_bounds__(128, RP ? (SX ? 1 : 2) : 3) sfwd_kernel(const 
       for (int r = 0; r < 16; ++r) sv[16 * t + r] = acc[r];
     }
     // wave-uniform: a partially active tile, or keys past this wave's first query
-    if (mask != full || (CAUSAL && j0 + STILE - 1 > qt * STILE + 32 * w)) {
+    if (mask != GFULL || (CAUSAL && kb.w * 16 + 15 > qt * STILE + 32 * w)) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int kc = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);  // key column inside the tile
-          const int bit = (qsub << nsub_l2) + (kc >> shift);
-          if (!((mask >> bit) & 1u) || (CAUSAL && j0 + kc > myq)) sv[16 * t + r] = -INFINITY;
+          const int slot = 2 * t + (r >> 3);  // gathered key block of tile column 32t + 8(r>>2) + 4h + (r&3)
+          const int key = sel4(kb, slot) * 16 + 8 * ((r >> 2) & 1) + 4 * h + (r & 3);
+          if (!((mask >> ((qsub << 2) + slot)) & 1u) || (CAUSAL && key > myq)) sv[16 * t + r] = -INFINITY;
         }
     }
     if constexpr (SX != 0) {  // scores to the log2 domain with the biases folded in
@@ -1508,7 +1529,8 @@ __global__ void __launch_bounds__(128, RP ? (SX ? 1 : 2) : 3) sfwd_kernel(const 
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-          const float4 b4 = sbias4<T, SX>(sx, ehd, bh / H, S, myq, j0 + 32 * t + 8 * rb + 4 * h);
+          const int key0 = sel4(kb, 2 * t + (rb >> 1)) * 16 + 8 * (rb & 1) + 4 * h;
+          const float4 b4 = sbias4<T, SX>(sx, ehd, bh / H, S, myq, key0);
           float* s4 = sv + 16 * t + 4 * rb;
           s4[0] = fmaf(s4[0], sl2, b4.x); s4[1] = fmaf(s4[1], sl2, b4.y);
           s4[2] = fmaf(s4[2], sl2, b4.z); s4[3] = fmaf(s4[3], sl2, b4.w);
@@ -1588,9 +1610,10 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
                                                        const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
                                                        const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                        uint16_t* __restrict__ dK, uint16_t* __restrict__ dV,
-                                                       const int* __restrict__ rows,
+                                                       const int4* __restrict__ rows,
                                                        const uint32_t* __restrict__ masks,
                                                        const int4* __restrict__ tasks, int ntask,
+                                                       const int4* __restrict__ kgroups,
                                                        float* __restrict__ ws, int nslot, int S, float scale, int onh,
                                                        int H, int Hl, int shift, SExtra sx = SExtra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -1600,20 +1623,20 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
-  // task = (key tile, entry range of its query-tile list, partial slot or -1): key tiles whose
-  // list is long (the global columns of BigBird / Longformer layouts) are split into chunks
+  // task = (key group, entry range of its query list, partial slot or -1): groups whose list is
+  // long (the global columns of BigBird / Longformer / fixed layouts) are split into chunks
   // that write fp32 partials, summed by sdkdv_finish_kernel -- no single workgroup walks them all
   const int task = xcd_task(blockIdx.x, gridDim.x);
   const int64_t bh = task / ntask;
   const int lh = Hl == 1 ? 0 : (int)(bh % H);
   const int4 tk = tasks[lh * ntask + (task - (int)bh * ntask)];
-  const int kt = tk.x, e0 = tk.y, e1 = tk.z, slot = tk.w;
-  if (kt < 0) return;  // padding task (whole workgroup, before any barrier)
+  const int kg = tk.x, e0 = tk.y, e1 = tk.z, slot = tk.w;
+  if (kg < 0) return;  // padding task (whole workgroup, before any barrier)
+  const int4 kblk = kgroups[lh * (S / STILE) + kg];  // this group's four key 16-blocks (ascending)
   const int kcol = 32 * w + c32;
-  const int mykey = kt * STILE + kcol;
-  const int nsub_l2 = 6 - shift;
-  const uint32_t full = full_mask(nsub_l2);
-  const int ksub = kcol >> shift;
+  const int ksub = kcol >> 4;
+  const int mykey = sel4(kblk, ksub) * 16 + (kcol & 15);
+  const int wmaxkey = sel4(kblk, 2 * w + 1) * 16 + 15;  // this wave's last key
   const int64_t base = bh * (int64_t)S * D;
   const int64_t obase = o_base<D>(bh, S, onh);
   const float sl2 = scale * 1.4426950408889634f;
@@ -1632,12 +1655,13 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
 
   uint4 qr[8 * D / NT], orr[8 * D / NT];
   float st_l = 0.f, st_d = 0.f;
-  auto load_tile = [&](int i0) {
-    stile_load<D, NT>(qr, Q + base, i0, S);
-    stile_load<D, NT>(orr, dO + obase, i0, S, o_ld<D>(onh));
+  auto load_tile = [&](const int4 qb) {
+    gtile_load<D, NT>(qr, Q + base, qb, S);
+    gtile_load<D, NT>(orr, dO + obase, qb, S, o_ld<D>(onh));
     if (threadIdx.x < STILE) {
-      st_l = LSE[bh * (int64_t)S + i0 + threadIdx.x] * (-1.f / scale);
-      st_d = -DELTA[bh * (int64_t)S + i0 + threadIdx.x];
+      const int qp = sel4(qb, threadIdx.x >> 4) * 16 + (threadIdx.x & 15);
+      st_l = LSE[bh * (int64_t)S + qp] * (-1.f / scale);
+      st_d = -DELTA[bh * (int64_t)S + qp];
     }
   };
   // this lane's key: key-padding bias (log2 units) and its column of the element bias
@@ -1657,18 +1681,18 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
     }
   };
   if (RP && e0 < e1) {
-    load_tile(rows[e0] * STILE);
+    load_tile(rows[e0]);
     store_tile(0);
   }
   __syncthreads();
   for (int e = e0; e < e1; ++e) {
     const int it = e - e0;
-    const int i0 = rows[e] * STILE;
+    const int4 qb = rows[e];
     const uint32_t mask = masks[e];
     const bool has_next = e + 1 < e1;
-    if (RP && has_next) load_tile(rows[e + 1] * STILE);
+    if (RP && has_next) load_tile(rows[e + 1]);
     if (!RP) {
-      load_tile(i0);
+      load_tile(qb);
       if (it > 0) __syncthreads();
       store_tile(0);
       __syncthreads();
@@ -1698,19 +1722,20 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
         for (int r = 0; r < 16; ++r) {
           float b = kb2;
           if ((SX & 2) && ecol)
-            b += h16f<T>(ecol[(int64_t)(i0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3)) * sx.er]) * LOG2E;
+            b += h16f<T>(ecol[(int64_t)(sel4(qb, 2 * t + (r >> 3)) * 16 + 8 * ((r >> 2) & 1) + 4 * h + (r & 3)) *
+                              sx.er]) * LOG2E;
           pv[r] = fast_exp2(fmaf(sacc[r], sl2, b));
         }
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) pv[r] = fast_exp2(sacc[r] * sl2);
       }
-      if (mask != full || (CAUSAL && kt * STILE + 32 * w + 31 > i0 + 32 * t)) {
+      if (mask != GFULL || (CAUSAL && wmaxkey > sel4(qb, 2 * t) * 16)) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-          const int bit = ((qi >> shift) << nsub_l2) + ksub;
-          if (!((mask >> bit) & 1u) || (CAUSAL && mykey > i0 + qi)) pv[r] = 0.f;
+          const int qslot = 2 * t + (r >> 3);
+          const int qpos = sel4(qb, qslot) * 16 + 8 * ((r >> 2) & 1) + 4 * h + (r & 3);
+          if (!((mask >> ((qslot << 2) + ksub)) & 1u) || (CAUSAL && mykey > qpos)) pv[r] = 0.f;
         }
       }
 #pragma unroll
@@ -1770,7 +1795,7 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
 }
 
 // Sum the fp32 partials of each split key tile and write its bf16/fp16 dK (scaled) and dV.
-// fin[lh][j] = (key tile, first slot, chunk count, -), padded with key tile -1.
+// fin[lh][j] = (key group, first slot, chunk count, -), padded with key group -1.
 // One workgroup per 256 float4 granules of one split key tile (SDKDV_FPARTS per tile): the
 // partial sums spread over the whole chip instead of one workgroup per tile.
 template <int D> constexpr int sdkdv_fparts() { return (2 * STILE * D / 4 + 255) / 256; }
@@ -1778,7 +1803,7 @@ template <typename T, int D>
 __global__ void __launch_bounds__(256) sdkdv_finish_kernel(const float* __restrict__ ws, const int4* __restrict__ fin,
                                                            int nfin, int nslot, uint16_t* __restrict__ dK,
                                                            uint16_t* __restrict__ dV, int S, float scale, int H,
-                                                           int Hl) {
+                                                           int Hl, const int4* __restrict__ kgroups) {
   constexpr int NP = sdkdv_fparts<D>();
   const int part = blockIdx.x % NP;
   const int tile = blockIdx.x / NP;
@@ -1801,7 +1826,9 @@ __global__ void __launch_bounds__(256) sdkdv_finish_kernel(const float* __restri
     const float sc = is_k ? scale : 1.f;
     ushort4 o4;
     o4.x = to16<T>(acc.x * sc); o4.y = to16<T>(acc.y * sc); o4.z = to16<T>(acc.z * sc); o4.w = to16<T>(acc.w * sc);
-    uint16_t* dst = (is_k ? dK : dV) + base + (int64_t)f.x * STILE * D + off;
+    const int4 kb = kgroups[lh * (S / STILE) + f.x];
+    const int row = off / D;
+    uint16_t* dst = (is_k ? dK : dV) + base + (int64_t)(sel4(kb, row >> 4) * 16 + (row & 15)) * D + (off - row * D);
     *reinterpret_cast<ushort4*>(dst) = o4;
   }
 }
@@ -1813,7 +1840,7 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
                                                      const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
                                                      const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                      uint16_t* __restrict__ dQ, const int* __restrict__ rowptr,
-                                                     const int* __restrict__ cols, const uint32_t* __restrict__ masks,
+                                                     const int4* __restrict__ cols, const uint32_t* __restrict__ masks,
                                                      int S, float scale, int onh, int H, int Hl, int shift,
                                                      SExtra sx = SExtra(), const uint16_t* __restrict__ O = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -1830,9 +1857,7 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
   const int e0 = rowptr[lh * nqt + qt], e1 = rowptr[lh * nqt + qt + 1];
   const int qrow = 32 * w + c32;
   const int myq = qt * STILE + qrow;
-  const int nsub_l2 = 6 - shift;
-  const uint32_t full = full_mask(nsub_l2);
-  const int qsub = qrow >> shift;
+  const int qsub = qrow >> 4;
   const int64_t base = bh * (int64_t)S * D;
   const float sl2 = scale * 1.4426950408889634f;
 
@@ -1868,24 +1893,24 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
 
   uint4 kr[8 * D / NT], vr[8 * D / NT];
   if (RP && e0 < e1) {
-    stile_load<D, NT>(kr, K + base, cols[e0] * STILE, S);
-    stile_load<D, NT>(vr, V + base, cols[e0] * STILE, S);
+    gtile_load<D, NT>(kr, K + base, cols[e0], S);
+    gtile_load<D, NT>(vr, V + base, cols[e0], S);
     stile_store<D, NT>(smem, kr);
     stile_store<D, NT>(smem + TS, vr);
   }
   __syncthreads();
   for (int e = e0; e < e1; ++e) {
     const int it = e - e0;
-    const int j0 = cols[e] * STILE;
+    const int4 kb = cols[e];
     const uint32_t mask = masks[e];
     const bool has_next = e + 1 < e1;
     if (RP && has_next) {
-      stile_load<D, NT>(kr, K + base, cols[e + 1] * STILE, S);
-      stile_load<D, NT>(vr, V + base, cols[e + 1] * STILE, S);
+      gtile_load<D, NT>(kr, K + base, cols[e + 1], S);
+      gtile_load<D, NT>(vr, V + base, cols[e + 1], S);
     }
     if (!RP) {
-      stile_load<D, NT>(kr, K + base, j0, S);
-      stile_load<D, NT>(vr, V + base, j0, S);
+      gtile_load<D, NT>(kr, K + base, kb, S);
+      gtile_load<D, NT>(vr, V + base, kb, S);
       if (it > 0) __syncthreads();
       stile_store<D, NT>(smem, kr);
       stile_store<D, NT>(smem + TS, vr);
@@ -1907,7 +1932,8 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
       if constexpr (SX != 0) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-          const float4 b4 = sbias4<T, SX>(sx, ehd, bh / H, S, myq, j0 + 32 * t + 8 * rb + 4 * h);
+          const int key0 = sel4(kb, 2 * t + (rb >> 1)) * 16 + 8 * (rb & 1) + 4 * h;
+          const float4 b4 = sbias4<T, SX>(sx, ehd, bh / H, S, myq, key0);
           dsv[4 * rb + 0] = fast_exp2(fmaf(sacc[4 * rb + 0], sl2, b4.x - lse2));
           dsv[4 * rb + 1] = fast_exp2(fmaf(sacc[4 * rb + 1], sl2, b4.y - lse2));
           dsv[4 * rb + 2] = fast_exp2(fmaf(sacc[4 * rb + 2], sl2, b4.z - lse2));
@@ -1917,12 +1943,12 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
 #pragma unroll
         for (int r = 0; r < 16; ++r) dsv[r] = fast_exp2(fmaf(sacc[r], sl2, -lse2));
       }
-      if (mask != full || (CAUSAL && j0 + 32 * t + 31 > qt * STILE + 32 * w)) {
+      if (mask != GFULL || (CAUSAL && sel4(kb, 2 * t + 1) * 16 + 15 > qt * STILE + 32 * w)) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int kc = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-          const int bit = (qsub << nsub_l2) + (kc >> shift);
-          if (!((mask >> bit) & 1u) || (CAUSAL && j0 + kc > myq)) dsv[r] = 0.f;
+          const int slot = 2 * t + (r >> 3);
+          const int key = sel4(kb, slot) * 16 + 8 * ((r >> 2) & 1) + 4 * h + (r & 3);
+          if (!((mask >> ((qsub << 2) + slot)) & 1u) || (CAUSAL && key > myq)) dsv[r] = 0.f;
         }
       }
 #pragma unroll
@@ -2210,9 +2236,10 @@ static bool sparse_rp() {
 
 // kbias / ebias (SExtra): null when absent; either one selects the SX = 1 kernels
 void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
-                             const int* cols, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
+                             const int* cols_, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
                              float scale, int shift, int dt, hipStream_t s, int onh, const float* kbias,
                              const void* ebias, int64_t ez, int64_t eh, int64_t er) {
+  const int4* cols = reinterpret_cast<const int4*>(cols_);
   const unsigned grid = (unsigned)(BH * (S / fa::STILE));
   const bool rp = sparse_rp();
   fa::SExtra sx;
@@ -2242,10 +2269,14 @@ void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* 
 // sums of split key tiles' partials.
 void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o,
                              const float* lse, float* delta, void* dq, void* dk, void* dv, const int* rowptr,
-                             const int* cols, const uint32_t* masks, const int* rows, const uint32_t* masks_t,
-                             const int* tasks, int ntask, const int* fin, int nfin, float* ws, int nslot, int BH,
-                             int H, int Hl, int S, int D, bool causal, float scale, int shift, int dt, hipStream_t s,
-                             int onh, const float* kbias, const void* ebias, int64_t ez, int64_t eh, int64_t er) {
+                             const int* cols_, const uint32_t* masks, const int* rows_, const uint32_t* masks_t,
+                             const int* tasks, int ntask, const int* fin, int nfin, const int* kgroups_, float* ws,
+                             int nslot, int BH, int H, int Hl, int S, int D, bool causal, float scale, int shift,
+                             int dt, hipStream_t s, int onh, const float* kbias, const void* ebias, int64_t ez,
+                             int64_t eh, int64_t er) {
+  const int4* cols = reinterpret_cast<const int4*>(cols_);
+  const int4* rows = reinterpret_cast<const int4*>(rows_);
+  const int4* kgroups = reinterpret_cast<const int4*>(kgroups_);
   const unsigned grid = (unsigned)(BH * (S / fa::STILE));
   const unsigned tgrid = (unsigned)(BH * ntask);
   const bool rp = sparse_rp();
@@ -2261,7 +2292,7 @@ void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, con
                          (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, sx, (const uint16_t*)o);
       hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, true, 3>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
+                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, kgroups, ws, nslot, S, scale, onh, H, Hl,
                          shift, sx);
     } else if (kbias) {
       hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true, 1, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
@@ -2269,7 +2300,7 @@ void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, con
                          (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, sx, (const uint16_t*)o);
       hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, true, 1>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
+                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, kgroups, ws, nslot, S, scale, onh, H, Hl,
                          shift, sx);
     } else if (rp) {
       hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true, 0, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
@@ -2278,7 +2309,7 @@ void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, con
                          (const uint16_t*)o);
       hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, true>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
+                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, kgroups, ws, nslot, S, scale, onh, H, Hl,
                          shift, fa::SExtra());
     } else {
       hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, false, 0, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(false),
@@ -2287,13 +2318,13 @@ void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, con
                          (const uint16_t*)o);
       hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, false>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(false), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, ws, nslot, S, scale, onh, H, Hl,
+                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, kgroups, ws, nslot, S, scale, onh, H, Hl,
                          shift, fa::SExtra());
     }
     if (nfin > 0)
       hipLaunchKernelGGL((fa::sdkdv_finish_kernel<T, DD>), dim3((unsigned)(BH * nfin * fa::sdkdv_fparts<DD>())),
                          dim3(256), 0, s, ws, reinterpret_cast<const int4*>(fin), nfin, nslot, (uint16_t*)dk,
-                         (uint16_t*)dv, S, scale, H, Hl));
+                         (uint16_t*)dv, S, scale, H, Hl, kgroups));
 }
 
 }  // namespace dsa

@@ -4,18 +4,29 @@ The reference computes block-sparse attention as three Triton launches -- SDD (Q
 the layout), a sparse row softmax and DSD (P V) -- with the sparse score matrix written to and
 read back from HBM between them (deepspeed/ops/sparse_attention/matmul.py:117-238,
 softmax.py:44-120, trsrc/softmax_fwd.tr:46-129).  Here one kernel walks, per 64-query tile, the
-64-key tiles the layout activates and keeps scores / probabilities in registers (online
-softmax); the backward is the same walk for dQ and the transposed walk for dK / dV.
+key tiles the layout activates and keeps scores / probabilities in registers (online softmax);
+the backward is the same walk for dQ and the transposed walk for dK / dV.
 
-`SparseFlashLUT` turns a layout [H or 1, nb, nb] of `block`-sized blocks into those walks:
-per layout head, a CSR list of active key tiles per query tile and the transposed list, each
-entry with a bitmask of the active layout sub-blocks when the layout block is smaller than the
-64-element tile (block 16 -> 4x4 sub-blocks, 32 -> 2x2).  Tiles above the diagonal are dropped
-for causal attention.  The reference softmax's score terms run inside the same kernels
-(`score_biases`): the key-padding mask as a per-key fp32 bias, the relative position embedding
-and the attention mask pre-summed into one [B|1, H|1, S, S] element bias read only on active
-tiles ('mul' masks become 0 / -inf).  Shapes outside the kernel's domain (S % 64, head dim) fall
-back to the SDD / softmax / DSD path.
+Gathered tiles.  The kernels' unit of work is a 64 x 64 MFMA tile, but a tile's 64 keys (or, in
+the dK / dV walk, its 64 queries) need not be contiguous: every LUT entry names FOUR 16-row
+blocks that are gathered into the tile, and a 16-bit mask says which (query 16-block, key
+16-block) pairs of the 4 x 4 grid are active.  `SparseFlashLUT` builds the walks at that 16-row
+granularity whatever the layout block (16 / 32 / 64 / 128):
+  * forward / dQ: per contiguous 64-query tile, the union of the key 16-blocks its four query
+    blocks activate, packed four at a time -- work scales with the active 16-blocks, not with the
+    64-tiles they touch (the reference's default block 16 "fixed" layout puts one global key
+    block in every 64-key window: 2,080 dense tiles at S = 4096 become 592 gathered ones);
+  * dK / dV: the key 16-blocks are first grouped four at a time into output groups (contiguous,
+    or sorted by how many query blocks attend them when that packs tighter -- the global columns
+    of fixed / Longformer layouts land together), then per group the union of the query 16-blocks
+    that attend it, packed four at a time.
+Blocks above the diagonal are dropped for causal attention (the element-level diagonal is masked
+in the kernels).  Layout blocks of 64 / 128 reproduce the contiguous tiles with full masks.
+
+The reference softmax's score terms run inside the same kernels (`score_biases`): the key-padding
+mask as a per-key fp32 bias, the relative position embedding and the attention mask pre-summed
+into one [B|1, H|1, S, S] element bias read only on active tiles ('mul' masks become 0 / -inf).
+Shapes outside the kernel's domain (S % 64, head dim) fall back to the SDD / softmax / DSD path.
 """
 
 from __future__ import annotations
@@ -26,9 +37,26 @@ import numpy as np
 import torch
 
 TILE = 64
+SUB = 16  # rows per gathered block
+NSUB = TILE // SUB
 
 
 class SparseFlashLUT:
+    """Gathered-tile walks of a block-sparse layout (see the module docstring).
+
+    Host arrays (`_host`, in `device_tensors` order):
+      rowptr  int32 [Hl * nqt + 1]   forward / dQ entries of each query tile
+      cols    int32 [E, 4]           the four key 16-blocks of each entry (ascending; padding repeats
+                                     the last one, its mask bits are 0)
+      masks   int32 [E]              bit (qsub * 4 + kslot): query 16-block qsub of the tile x key slot
+      colptr  int32 [Hl * nkg + 1]   dK / dV entries of each key group
+      rows    int32 [E_t, 4]         the four query 16-blocks of each dK / dV entry
+      masks_t int32 [E_t]            bit (qslot * 4 + kslot)
+      tasks   int32 [Hl, ntask, 4]   (key group or -1, entry begin, entry end, partial slot or -1)
+      fin     int32 [Hl, nfin, 4]    (key group or -1, first slot, chunks, 0) of split groups
+      kgroups int32 [Hl, nkg, 4]     the four key 16-blocks of each group (ascending)
+    """
+
     def __init__(self, layout: torch.Tensor, block: int, causal: bool = False):
         lay = layout.detach().cpu().to(torch.bool)
         if lay.dim() == 2:
@@ -44,30 +72,100 @@ class SparseFlashLUT:
         self.seq = nb * block
         if self.seq % TILE:
             raise ValueError(f"sequence {self.seq} is not a multiple of the {TILE}-element tile")
-        self.shift = min(6, int(block).bit_length() - 1)
-        nt = self.seq // TILE
-        L = lay.numpy()
-        if block >= TILE:  # each tile lies inside one layout block
-            rep = block // TILE
-            act = np.repeat(np.repeat(L, rep, axis=1), rep, axis=2)
-            masks = act.astype(np.int64)
-        else:
-            r = TILE // block
-            sub = L.reshape(self.heads, nt, r, nt, r).transpose(0, 1, 3, 2, 4)  # [h, i, j, qsub, ksub]
-            weights = (1 << np.arange(r * r, dtype=np.int64)).reshape(r, r)
-            masks = (sub.astype(np.int64) * weights).sum(axis=(3, 4))
-            act = masks != 0
+        self.shift = 4  # kept for the kernels' signature: masks are always on the 16-row grid
+        r = block // SUB
+        L = np.repeat(np.repeat(lay.numpy(), r, axis=1), r, axis=2)  # [Hl, n16, n16]
+        n16 = L.shape[-1]
         if self.causal:
-            act = act & np.tril(np.ones((nt, nt), dtype=bool))[None]
-        self.density = float(act.sum()) / act.size
-        self.tiles = int(act.sum())
-        self._host = self._csr(act, masks) + self._csr(act.transpose(0, 2, 1), masks.transpose(0, 2, 1))
-        self._host += self._split_tasks(self._host[3], nt)
+            L = L & np.tril(np.ones((n16, n16), dtype=bool))[None]
+        nqt = n16 // NSUB
+        fwd = [self._fwd_walk(L[h], nqt) for h in range(self.heads)]
+        bwd = [self._bwd_walk(L[h], nqt) for h in range(self.heads)]
+        self.tiles = sum(len(f[1]) for f in fwd)
+        self.density = float(self.tiles) / (self.heads * nqt * nqt)  # gathered 64x64 tiles processed
+        self.block_density = float(L.sum()) / L.size
+        rowptr, cols, masks = self._concat(fwd, nqt)
+        colptr, rows, masks_t = self._concat([b[:3] for b in bwd], nqt)
+        kgroups = np.stack([b[3] for b in bwd]).astype(np.int32)
+        self._host = (rowptr, cols, masks, colptr, rows, masks_t)
+        self._host += self._split_tasks(colptr, nqt)
+        self._host += (kgroups,)
         self.nslot = self._nslot
         self._dev: Dict[torch.device, tuple] = {}
 
-    # query tiles per dK / dV workgroup: longer key-tile lists (global columns) are split into
-    # chunks whose fp32 partials are summed by a finish kernel
+    # ------------------------------------------------------------------ walks
+    @staticmethod
+    def _pack(blocks, act):
+        """Entries of 4 gathered blocks: blocks ascending; act(slot_block) -> [4] bools per
+        gathered block (which of the 4 tile sub-rows / slots it pairs with).  Returns
+        [(blk4, mask16)] with bit (tile_sub * 4 + slot)."""
+        out = []
+        for i in range(0, len(blocks), NSUB):
+            chunk = list(blocks[i:i + NSUB])
+            mask = 0
+            for slot, b in enumerate(chunk):
+                for sub, on in enumerate(act(b)):
+                    if on:
+                        mask |= 1 << (sub * NSUB + slot)
+            chunk += [chunk[-1]] * (NSUB - len(chunk))
+            out.append((chunk, mask))
+        return out
+
+    def _fwd_walk(self, L, nqt):
+        ptr, ents = [0], []
+        for qt in range(nqt):
+            rows = L[qt * NSUB:(qt + 1) * NSUB]  # [4, n16]
+            union = np.nonzero(rows.any(axis=0))[0]
+            ents += self._pack(union, lambda b: rows[:, b])
+            ptr.append(len(ents))
+        return ptr, ents
+
+    def _bwd_walk(self, L, nqt):
+        n16 = L.shape[0]
+        att = [np.nonzero(L[:, k])[0] for k in range(n16)]  # query blocks attending key block k
+        contiguous = [list(range(g * NSUB, (g + 1) * NSUB)) for g in range(nqt)]
+        order = sorted(range(n16), key=lambda k: (-len(att[k]), att[k][0] if len(att[k]) else n16, k))
+        by_count = [sorted(order[g * NSUB:(g + 1) * NSUB]) for g in range(nqt)]
+
+        def walk(groups):
+            ptr, ents = [0], []
+            for grp in groups:
+                cols = L[:, grp]  # [n16, 4]
+                union = np.nonzero(cols.any(axis=1))[0]
+                ents += self._pack(union, lambda q: cols[q])
+                ptr.append(len(ents))
+            return ptr, ents
+
+        a, b = walk(contiguous), walk(by_count)
+        ptr, ents, groups = (a + (contiguous,)) if len(a[1]) <= len(b[1]) else (b + (by_count,))
+        # bits of a dK / dV entry: (query slot * 4 + key slot) -- _pack built (key slot * 4 +
+        # query slot) from the group's point of view, so transpose the 4 x 4 grid
+        fixed = []
+        for blk4, m in ents:
+            t = 0
+            for ks in range(NSUB):
+                for qs in range(NSUB):
+                    if (m >> (ks * NSUB + qs)) & 1:
+                        t |= 1 << (qs * NSUB + ks)
+            fixed.append((blk4, t))
+        return ptr, fixed, None, np.array(groups, dtype=np.int32)
+
+    @staticmethod
+    def _concat(walks, n):
+        ptr = [0]
+        blocks, masks = [], []
+        for w in walks:
+            p, ents = w[0], w[1]
+            base = ptr[-1]
+            ptr += [base + x for x in p[1:]]
+            blocks += [e[0] for e in ents]
+            masks += [e[1] for e in ents]
+        blk = np.array(blocks, dtype=np.int32).reshape(-1, NSUB)
+        m = np.array(masks, dtype=np.int64)
+        return np.array(ptr, dtype=np.int32), blk, m.astype(np.int32)
+
+    # entries per dK / dV workgroup: longer lists (the global columns of BigBird / Longformer /
+    # fixed layouts) are split into chunks whose fp32 partials are summed by a finish kernel
     CHUNK = 8
 
     def _split_tasks(self, colptr, nt):
@@ -85,7 +183,7 @@ class SparseFlashLUT:
                 for c in range(n):
                     heavy.append((kt, e0 + c * self.CHUNK, min(e1, e0 + (c + 1) * self.CHUNK), nslot + c))
                 nslot += n
-            per_head.append(heavy + light)  # split (long) tiles launch first
+            per_head.append(heavy + light)  # split (long) groups launch first
             fins.append(fin)
             slots.append(nslot)
         ntask = max(1, max(len(t) for t in per_head))
@@ -101,17 +199,6 @@ class SparseFlashLUT:
         if nfin == 0:
             fin = fin[:, :0]
         return (tasks, fin)
-
-    @staticmethod
-    def _csr(act, masks):
-        h, n, _ = act.shape
-        counts = act.reshape(h * n, n).sum(axis=1)
-        ptr = np.zeros(h * n + 1, dtype=np.int64)
-        np.cumsum(counts, out=ptr[1:])
-        hi, ri, ci = np.nonzero(act)  # row-major: (head, row) ascending, columns ascending
-        bits = masks[hi, ri, ci].astype(np.int64)
-        bits = np.where(bits >= 2**31, bits - 2**32, bits)  # uint32 bit patterns stored as int32
-        return (ptr.astype(np.int32), ci.astype(np.int32), bits.astype(np.int32))
 
     def device_tensors(self, device):
         t = self._dev.get(device)
@@ -186,10 +273,11 @@ class _SparseFlash(torch.autograd.Function):
         from .. import native
         q, k, v, o, lse = ctx.saved_tensors
         lut = ctx.lut
-        rp, cols, masks, _cp, rows, masks_t, tasks, fin = lut.device_tensors(q.device)
+        rp, cols, masks, _cp, rows, masks_t, tasks, fin, kgroups = lut.device_tensors(q.device)
         dq, dk, dv = native.hip_ops().sparse_flash_bwd(do.contiguous(), q, k, v, o, lse, rp, cols, masks, rows,
-                                                       masks_t, tasks, fin, lut.nslot, lut.heads, lut.causal,
-                                                       ctx.scale, lut.shift, ctx.out_bshd, ctx.kbias, ctx.ebias)
+                                                       masks_t, tasks, fin, kgroups, lut.nslot, lut.heads,
+                                                       lut.causal, ctx.scale, lut.shift, ctx.out_bshd, ctx.kbias,
+                                                       ctx.ebias)
         return dq, dk, dv, None, None, None, None, None
 
 

@@ -746,8 +746,13 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             src = gf
             if g.dtype == torch.float16:
                 src.mul_(1.0 / self.dp_world)
+            cast = None
             if self.fp32_reduce and src.dtype != torch.float32:
-                src = src.float()
+                # the fp32 staging copy of the unit gradient comes from (and returns to) the pool:
+                # it is part of the planned transient memory, not a fresh allocation per unit
+                cast = self._pool.get(src.numel(), torch.float32, src.device)
+                cast.copy_(src)
+                src = cast
             out_slice = g.shard_grad[b.shard_offset: b.shard_offset + b.chunk]
             direct = out_slice.dtype == src.dtype and not self._grads_nonzero
             out = out_slice if direct else self._pool.get(b.chunk, src.dtype, src.device)
@@ -760,7 +765,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
                 mine = src[self.dp_rank * b.chunk: (self.dp_rank + 1) * b.chunk]
                 done = functools.partial(_copy if direct else _accum, out_slice, mine)
             # buffers go back to the pool once the reduction has been waited for
-            back = [gf] if direct else [gf, out]
+            back = ([gf] if direct else [gf, out]) + ([cast] if cast is not None else [])
             fin = functools.partial(_finish_reduce, done, self._pool, back)
             self._reduced_this_pass = True
             self._queue_reduction(work, fin, b.numel, overlap=self.overlap_comm)
