@@ -320,7 +320,7 @@ Tensor colsum(Tensor x, OptT out_opt, bool accumulate) {
 
 // y = x^T for a 2-D 16-bit x [R, C] (unit column stride, any 16-byte aligned row stride).
 // With colsum_out ([C], x's dtype) the column sums of x are also written (accum: added) there.
-Tensor transpose2d(Tensor x, OptT colsum_out, bool accum) {
+Tensor transpose2d(Tensor x, OptT colsum_out, bool accum, OptT out) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "transpose2d: x must be a 2-D GPU tensor, unit column stride");
   const int dt = dcode(x);
   TORCH_CHECK(dt != dsa::kCodeF32, "transpose2d: 16-bit dtypes only");
@@ -328,7 +328,16 @@ Tensor transpose2d(Tensor x, OptT colsum_out, bool accum) {
   TORCH_CHECK(dsa::transpose_supported(R, C), "transpose2d: rows must be a multiple of 128 and cols of 64");
   TORCH_CHECK(aligned16(x.data_ptr()) && ldx % 8 == 0, "transpose2d: rows must be 16-byte aligned");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  Tensor y = at::empty({C, R}, x.options());
+  Tensor y;
+  if (out.has_value()) {  // caller-owned destination (a persistent prefetch buffer)
+    check_dev(*out, "out");
+    TORCH_CHECK(out->dim() == 2 && out->size(0) == C && out->size(1) == R && out->is_contiguous() &&
+                    out->scalar_type() == x.scalar_type() && aligned16(out->data_ptr()),
+                "transpose2d: out must be a contiguous [C, R] tensor of x's dtype, 16-byte aligned");
+    y = *out;
+  } else {
+    y = at::empty({C, R}, x.options());
+  }
   Tensor partial;
   void* cptr = nullptr;
   if (colsum_out.has_value()) {
@@ -1139,5 +1148,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("heads_split", &heads_split);
   m.def("heads_merge", &heads_merge);
   m.def("swap12", &swap12);
-  m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("colsum_out") = py::none(), py::arg("accum") = false);
+  m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("colsum_out") = py::none(), py::arg("accum") = false,
+        py::arg("out") = py::none());
 }

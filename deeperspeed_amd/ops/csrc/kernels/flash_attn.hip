@@ -1391,6 +1391,17 @@ __device__ __forceinline__ void gtile_load(uint4 (&r)[8 * D / NT], const uint16_
                                            int S, int ld = D) {
   constexpr int CH = D / 8;
   const __amdgpu_buffer_rsrc_t rs = head_rsrc(g, S, ld);
+  if (blk.y == blk.x + 1 && blk.z == blk.x + 2 && blk.w == blk.x + 3) {  // one contiguous 64-row tile
+    const int r0 = blk.x * 16;
+#pragma unroll
+    for (int k = 0; k < 8 * D / NT; ++k) {
+      const int c = threadIdx.x + NT * k;
+      const int row = c / CH, ch = c - row * CH;
+      const fa_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ((r0 + row) * ld + ch * 8) * 2, 0, 0);
+      r[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 8 * D / NT; ++k) {
     const int c = threadIdx.x + NT * k;

@@ -378,12 +378,13 @@ def transpose_supported(x: torch.Tensor) -> bool:
             and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0)
 
 
-def transpose2d(x: torch.Tensor, colsum_out: Optional[torch.Tensor] = None, accum: bool = False) -> torch.Tensor:
-    """x [R, C] -> contiguous x^T [C, R]; optionally colsum_out (+)= x.sum(0) from the same read
-    (the bias gradient of a linear whose output gradient is x)."""
+def transpose2d(x: torch.Tensor, colsum_out: Optional[torch.Tensor] = None, accum: bool = False,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [R, C] -> contiguous x^T [C, R] (into `out` when given); optionally colsum_out (+)= x.sum(0)
+    from the same read (the bias gradient of a linear whose output gradient is x)."""
     if x.is_cuda:
-        return hip_ops().transpose2d(x, colsum_out, accum)
-    y = x.t().contiguous()
+        return hip_ops().transpose2d(x, colsum_out, accum, out)
+    y = x.t().contiguous() if out is None else out.copy_(x.t())
     if colsum_out is not None:
         s = x.float().sum(0)
         if accum:

@@ -788,7 +788,7 @@ class DeepSpeedEngine(Module):
             self.amp.scale(loss).backward()
         else:
             loss.backward()
-        _linear_ops.clear_transposed()  # pre-transposed operands never outlive their backward
+        _linear_ops.end_backward_pass()  # pre-transposed operands never outlive their backward
         if self.wall_clock_breakdown():
             self.timers("backward_inner").stop()
             self.timers("backward_inner_microstep").stop()

@@ -425,7 +425,7 @@ class PipelineEngine(DeepSpeedEngine):
                 torch.autograd.backward(tensors=out_t, grad_tensors=grads)
             else:
                 torch.autograd.backward(tensors=(outputs,), grad_tensors=(grads[0],))
-        _linear_ops.clear_transposed()  # pre-transposed operands never outlive their backward
+        _linear_ops.end_backward_pass()  # pre-transposed operands never outlive their backward
         self.pipe_buffers["output_tensors"][buffer_id] = None
         self.pipe_buffers["outputs"][buffer_id] = None
         if self.wall_clock_breakdown():
