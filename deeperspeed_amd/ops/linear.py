@@ -361,6 +361,52 @@ def forward_gemm(x, weight, bias=None):
     return F.linear(x, weight, bias)
 
 
+# Input and weight gradients of one linear on two streams when both GEMMs are too small to fill
+# the chip (BERT-Large at 8k tokens: 48-512 output tiles of 256 x 256 each against 256 CUs): the
+# dgrad runs on the compute stream, the wgrad (+ bias gradient) beside it on a side stream, and
+# the compute stream waits for both before anything else -- autograd's gradient hooks and every
+# later kernel see finished gradients, exactly as with the serial order.  Large linears (GPT-NeoX
+# 20B: 768 + 576 tiles) stay serial: a GEMM that fills every CU gains nothing from company.
+# DSA_PAR_WGRAD=0 turns it off; DSA_PAR_WGRAD_MAX_TILES is the summed tile count below which it runs.
+PAR_WGRAD = os.environ.get("DSA_PAR_WGRAD", "1") != "0"
+PAR_WGRAD_MAX_TILES = int(os.environ.get("DSA_PAR_WGRAD_MAX_TILES", "768"))
+_par_streams = {}
+_par_count = [0]
+
+
+def _tiles(a: int, b: int) -> int:
+    return -(-a // 256) * -(-b // 256)
+
+
+def _linear_backward(ctx, g):
+    x, weight = ctx.saved_tensors
+    bias = ctx.bias
+    g2 = g.reshape(-1, g.shape[-1])
+    x2 = x.reshape(-1, x.shape[-1])
+    need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+    need_b = bias is not None and ctx.needs_input_grad[2]
+    if (PAR_WGRAD and need_x and (need_w or need_b) and g2.is_cuda and not torch.cuda.is_current_stream_capturing()
+            and _tiles(g2.size(0), weight.size(1)) + _tiles(weight.size(0), weight.size(1)) <= PAR_WGRAD_MAX_TILES):
+        dev = g2.device
+        side = _par_streams.get(dev)
+        if side is None:
+            side = _par_streams[dev] = torch.cuda.Stream(device=dev)
+        cur = torch.cuda.current_stream(dev)
+        side.wait_stream(cur)
+        dx = input_grad(g2, weight).view(x.shape)
+        with torch.cuda.stream(side):
+            dw, db = accumulate_param_grads(g2, x2, weight, bias, need_w, need_b, ctx.share_gt)
+        cur.wait_stream(side)
+        for t in (dw, db):  # made on the side stream, consumed by autograd on the compute stream
+            if t is not None:
+                t.record_stream(cur)
+        _par_count[0] += 1
+        return dx, dw, db, None
+    dx = input_grad(g2, weight).view(x.shape) if need_x else None
+    dw, db = accumulate_param_grads(g2, x2, weight, bias, need_w, need_b, ctx.share_gt)
+    return dx, dw, db, None
+
+
 class _AccumLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, share_gt=False):
@@ -371,15 +417,7 @@ class _AccumLinear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        x, weight = ctx.saved_tensors
-        bias = ctx.bias
-        g2 = g.reshape(-1, g.shape[-1])
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = input_grad(g2, weight).view(x.shape)
-        dw, db = accumulate_param_grads(g2, x.reshape(-1, x.shape[-1]), weight, bias, ctx.needs_input_grad[1],
-                                        bias is not None and ctx.needs_input_grad[2], ctx.share_gt)
-        return dx, dw, db, None
+        return _linear_backward(ctx, g)
 
 
 _ZERO = {}
@@ -409,15 +447,7 @@ class _GradOnlyLinear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        x, weight = ctx.saved_tensors
-        bias = ctx.bias
-        g2 = g.reshape(-1, g.shape[-1])
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = input_grad(g2, weight).view(x.shape)
-        dw, db = accumulate_param_grads(g2, x.reshape(-1, x.shape[-1]), weight, bias, ctx.needs_input_grad[1],
-                                        bias is not None and ctx.needs_input_grad[2], ctx.share_gt)
-        return dx, dw, db, None
+        return _linear_backward(ctx, g)
 
 
 def linear(x, weight, bias=None, share_grad_t=False):
