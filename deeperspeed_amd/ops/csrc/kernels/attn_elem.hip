@@ -218,12 +218,16 @@ __global__ void __launch_bounds__(256) rotary_split_tiled_kernel(const T* __rest
                                                                  float qscale) {
   constexpr int CPR = HD / 8, HALF = ROT / 2;
   constexpr int ROWS = 3 * ROT_HB * ROT_SB, CHUNKS = ROWS * CPR;
-  __shared__ __attribute__((aligned(16))) uint16_t tile[ROWS * HD];  // [which][h][s][HD]
+  // rows padded by 16 bytes: in the per-row rotation phase every lane walks its own row, and an
+  // unpadded 256-byte row (HD 128) puts all 64 lanes' accesses on the same banks
+  constexpr int HDP = HD + 8;
+  constexpr int PER = (CHUNKS + 255) / 256;  // 16-byte chunks per thread, all loads issued first
+  __shared__ __attribute__((aligned(16))) uint16_t tile[ROWS * HDP];  // [which][h][s][HD (+8)]
   const int tid = threadIdx.x;
   const int nsb = S / ROT_SB, nhb = NH / ROT_HB;
   const int hb = blockIdx.x % nhb, sb = (blockIdx.x / nhb) % nsb, b = blockIdx.x / (nhb * nsb);
   const int s0 = sb * ROT_SB, h0 = hb * ROT_HB;
-  auto lds_off = [](int which, int hl, int sl) { return ((which * ROT_HB + hl) * ROT_SB + sl) * HD; };
+  auto lds_off = [](int which, int hl, int sl) { return ((which * ROT_HB + hl) * ROT_SB + sl) * HDP; };
   // packed side ([B,S,NH,3,HD], GPT-NeoX's per-head interleave) chunk order: s, h, which, chunk
   auto packed_chunk = [&](int c, int& which, int& hl, int& sl, int& ch) {
     ch = c % CPR; int r = c / CPR;
@@ -236,18 +240,34 @@ __global__ void __launch_bounds__(256) rotary_split_tiled_kernel(const T* __rest
     sl = r % ROT_SB; r /= ROT_SB;
     hl = r % ROT_HB; which = r / ROT_HB;
   };
-  for (int c = tid; c < CHUNKS; c += 256) {
-    int which, hl, sl, ch;
-    uint4 v;
-    if constexpr (!BWD) {
-      packed_chunk(c, which, hl, sl, ch);
-      v = *reinterpret_cast<const uint4*>(qkv_in + ((((int64_t)b * S + s0 + sl) * NH + h0 + hl) * 3 + which) * HD + ch * 8);
-    } else {
-      split_chunk(c, which, hl, sl, ch);
-      const T* src = which == 0 ? q_in : (which == 1 ? k_in : v_in);
-      v = *reinterpret_cast<const uint4*>(src + (((int64_t)b * NH + h0 + hl) * S + s0 + sl) * HD + ch * 8);
+  {
+    uint4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {  // every global load in flight before the first LDS store
+      const int c = tid + 256 * k;
+      if (c < CHUNKS) {
+        int which, hl, sl, ch;
+        if constexpr (!BWD) {
+          packed_chunk(c, which, hl, sl, ch);
+          v[k] = *reinterpret_cast<const uint4*>(qkv_in + ((((int64_t)b * S + s0 + sl) * NH + h0 + hl) * 3 + which) *
+                                                              HD + ch * 8);
+        } else {
+          split_chunk(c, which, hl, sl, ch);
+          const T* src = which == 0 ? q_in : (which == 1 ? k_in : v_in);
+          v[k] = *reinterpret_cast<const uint4*>(src + (((int64_t)b * NH + h0 + hl) * S + s0 + sl) * HD + ch * 8);
+        }
+      }
     }
-    *reinterpret_cast<uint4*>(tile + lds_off(which, hl, sl) + ch * 8) = v;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int c = tid + 256 * k;
+      if (c < CHUNKS) {
+        int which, hl, sl, ch;
+        if constexpr (!BWD) packed_chunk(c, which, hl, sl, ch);
+        else split_chunk(c, which, hl, sl, ch);
+        *reinterpret_cast<uint4*>(tile + lds_off(which, hl, sl) + ch * 8) = v[k];
+      }
+    }
   }
   __syncthreads();
   if (tid < ROWS) {

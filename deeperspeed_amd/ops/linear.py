@@ -367,8 +367,11 @@ def forward_gemm(x, weight, bias=None):
 # the compute stream waits for both before anything else -- autograd's gradient hooks and every
 # later kernel see finished gradients, exactly as with the serial order.  Large linears (GPT-NeoX
 # 20B: 768 + 576 tiles) stay serial: a GEMM that fills every CU gains nothing from company.
-# DSA_PAR_WGRAD=0 turns it off; DSA_PAR_WGRAD_MAX_TILES is the summed tile count below which it runs.
-PAR_WGRAD = os.environ.get("DSA_PAR_WGRAD", "1") != "0"
+# Opt-in (DSA_PAR_WGRAD=1): on BERT-Large it measured 8 % SLOWER than the serial order (2,073 vs
+# 2,258 samples/s at seq 128, 479 vs 519 at seq 512, profiles/r4e_notes.md) -- two hipBLASLt
+# kernels sharing the CUs run each other's tiles into stragglers, and every linear adds two stream
+# waits to a partly launch-bound step.  DSA_PAR_WGRAD_MAX_TILES bounds the summed tile count.
+PAR_WGRAD = os.environ.get("DSA_PAR_WGRAD", "0") == "1"
 PAR_WGRAD_MAX_TILES = int(os.environ.get("DSA_PAR_WGRAD_MAX_TILES", "768"))
 _par_streams = {}
 _par_count = [0]

@@ -11,8 +11,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    import argparse
     from deeperspeed_amd.ops import attention as A
-    B, S, NH, HD, ROT = 4, 2048, 64, 96, 24
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="4,2048,64,96,24", help="B,S,NH,HD,ROT (1.3B at 16x1: 16,2048,16,128,32)")
+    B, S, NH, HD, ROT = (int(x) for x in ap.parse_args().shape.split(","))
     qkv = torch.randn(B, S, 3 * NH * HD, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     nbytes = 2 * qkv.numel() * 2
 
@@ -40,7 +43,7 @@ def main():
     for tiled in (False, True):
         out, fwd, bwd = run(tiled)
         res[tiled] = out
-        print(json.dumps({"variant": "tiled" if tiled else "row-per-thread", "fwd_us": round(fwd * 1e3, 1),
+        print(json.dumps({"variant": "tiled" if tiled else "row-per-thread", "shape": [B, S, NH, HD, ROT], "fwd_us": round(fwd * 1e3, 1),
                           "bwd_us": round(bwd * 1e3, 1), "fwd_TBps": round(nbytes / fwd / 1e9, 2),
                           "bwd_TBps": round(nbytes / bwd / 1e9, 2)}), flush=True)
     assert all(torch.equal(a, b) for a, b in zip(res[False], res[True]))
