@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(256) rotary_split_bwd_row_kernel(const T* __re
 constexpr int ROT_SB = 16, ROT_HB = 4;
 constexpr int which_chunks(int hd, int rot) { return hd / 8 > (rot + 7) / 8 ? hd / 8 : (rot + 7) / 8; }
 
-template <typename T, int HD, int ROT, bool BWD>
+template <typename T, int HD, int ROT, bool BWD, bool PAD = true>
 __global__ void __launch_bounds__(256) rotary_split_tiled_kernel(const T* __restrict__ qkv_in, T* __restrict__ qkv_out,
                                                                  const T* __restrict__ q_in, const T* __restrict__ k_in,
                                                                  const T* __restrict__ v_in, T* __restrict__ q_out,
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256) rotary_split_tiled_kernel(const T* __rest
   constexpr int ROWS = 3 * ROT_HB * ROT_SB, CHUNKS = ROWS * CPR;
   // rows padded by 16 bytes: in the per-row rotation phase every lane walks its own row, and an
   // unpadded 256-byte row (HD 128) puts all 64 lanes' accesses on the same banks
-  constexpr int HDP = HD + 8;
+  constexpr int HDP = PAD ? HD + 8 : HD;
   constexpr int PER = (CHUNKS + 255) / 256;  // 16-byte chunks per thread, all loads issued first
   __shared__ __attribute__((aligned(16))) uint16_t tile[ROWS * HDP];  // [which][h][s][HD (+8)]
   const int tid = threadIdx.x;
@@ -587,13 +587,17 @@ void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const f
                              int HD, int ROT, float qscale, int dt, hipStream_t s) {
   const int rows = B * S * NH;
   const int grid = (rows * 3 + 255) / 256;
-  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0 && os_env_int("DSA_ROTARY_TILED", 1) != 0;
+  const int tiled_mode = os_env_int("DSA_ROTARY_TILED", 1);
+  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0 && tiled_mode != 0;
 #define DSA_ROT_TILED_FWD(hd, rot)                                                                             \
   if (tiled && HD == hd && ROT == rot) {                                                                       \
     DSA_DISPATCH_16(dt, T,                                                                                     \
-      hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, false>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
-                         dim3(256), 0, s, (const T*)qkv, nullptr, nullptr, nullptr, nullptr, (T*)q, (T*)k, (T*)v, \
-                         (const float2*)cs, S, NH, qscale));                                                   \
+      if (tiled_mode == 2)  /* DSA_ROTARY_TILED=2: unpadded LDS rows (A/B) */                              \
+        hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, false, false>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
+                           dim3(256), 0, s, (const T*)qkv, nullptr, nullptr, nullptr, nullptr, (T*)q, (T*)k, (T*)v, (const float2*)cs, S, NH, qscale);                                                     \
+      else                                                                                                     \
+        hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, false>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
+                           dim3(256), 0, s, (const T*)qkv, nullptr, nullptr, nullptr, nullptr, (T*)q, (T*)k, (T*)v, (const float2*)cs, S, NH, qscale));                                                    \
     return;                                                                                                    \
   }
   DSA_ROTARY_ROW_CASES(DSA_ROT_TILED_FWD)
@@ -617,13 +621,17 @@ void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, voi
                              int S, int NH, int HD, int ROT, float qscale, int dt, hipStream_t s) {
   const int rows = B * S * NH;
   const int grid = (rows * 3 + 255) / 256;
-  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0 && os_env_int("DSA_ROTARY_TILED", 1) != 0;
+  const int tiled_mode = os_env_int("DSA_ROTARY_TILED", 1);
+  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0 && tiled_mode != 0;
 #define DSA_ROT_TILED_BWD(hd, rot)                                                                             \
   if (tiled && HD == hd && ROT == rot) {                                                                       \
     DSA_DISPATCH_16(dt, T,                                                                                     \
-      hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, true>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
-                         dim3(256), 0, s, nullptr, (T*)dqkv, (const T*)dq, (const T*)dk, (const T*)dv, nullptr,  \
-                         nullptr, nullptr, (const float2*)cs, S, NH, qscale));                                 \
+      if (tiled_mode == 2)  /* DSA_ROTARY_TILED=2: unpadded LDS rows (A/B) */                              \
+        hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, true, false>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
+                           dim3(256), 0, s, nullptr, (T*)dqkv, (const T*)dq, (const T*)dk, (const T*)dv, nullptr, nullptr, nullptr, (const float2*)cs, S, NH, qscale);                                                     \
+      else                                                                                                     \
+        hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, true>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
+                           dim3(256), 0, s, nullptr, (T*)dqkv, (const T*)dq, (const T*)dk, (const T*)dv, nullptr, nullptr, nullptr, (const float2*)cs, S, NH, qscale));                                                    \
     return;                                                                                                    \
   }
   DSA_ROTARY_ROW_CASES(DSA_ROT_TILED_BWD)

@@ -109,16 +109,44 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(const T* __restrict_
     for (int j = 0; j < VN; ++j) { dg[k][j] = 0.f; db[k][j] = 0.f; gm[k][j] = 0.f; }
     if (vi < nvec) Vec16<T>::load(gamma + vi * VN, gm[k]);
   }
+  // software-pipelined over the block's rows: the next row's x / dy (and its mean / rstd) are in
+  // flight while this row is reduced across the block -- one row per block in flight left the
+  // 512-block grid at ~3.7 TB/s on [32768, 2048] (profiles/r4e_neox13b_zero2_mb16_timed_kernel_stats.md)
+  float nx[NV][VN], ng[NV][VN];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int64_t r) {
+    nmu = mean[r];
+    nrs = rstd[r];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int vi = threadIdx.x + k * LN_THREADS;
+      if (vi < nvec) {
+        Vec16<T>::load(x + r * H + vi * VN, nx[k]);
+        Vec16<T>::load(dy + r * H + vi * VN, ng[k]);
+      }
+    }
+  };
+  if ((int64_t)blockIdx.x < rows) fetch(blockIdx.x);
   for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
-    const float mu = mean[row], rs = rstd[row];
-    float xh[NV][VN], g[NV][VN];
+    const float mu = nmu, rs = nrs;
+    float xh[NV][VN], g[NV][VN], rr[NV][VN];
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int j = 0; j < VN; ++j) { xh[k][j] = nx[k][j]; g[k][j] = ng[k][j]; }
+    if (row + gridDim.x < rows) fetch(row + gridDim.x);
+    if (dres) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int vi = threadIdx.x + k * LN_THREADS;
+        if (vi < nvec) Vec16<T>::load(dres + row * H + vi * VN, rr[k]);
+      }
+    }
     float a = 0.f, b = 0.f;  // sum(dxhat), sum(dxhat * xhat)
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int vi = threadIdx.x + k * LN_THREADS;
       if (vi < nvec) {
-        Vec16<T>::load(x + row * H + vi * VN, xh[k]);
-        Vec16<T>::load(dy + row * H + vi * VN, g[k]);
 #pragma unroll
         for (int j = 0; j < VN; ++j) {
           xh[k][j] = (xh[k][j] - mu) * rs;
@@ -140,10 +168,8 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(const T* __restrict_
 #pragma unroll
         for (int j = 0; j < VN; ++j) o[j] = rs * (g[k][j] * gm[k][j] - a - xh[k][j] * b);
         if (dres) {
-          float r[VN];
-          Vec16<T>::load(dres + row * H + vi * VN, r);
 #pragma unroll
-          for (int j = 0; j < VN; ++j) o[j] += r[j];
+          for (int j = 0; j < VN; ++j) o[j] += rr[k][j];
         }
         Vec16<T>::store(dx + row * H + vi * VN, o);
       }

@@ -20,7 +20,7 @@ def main():
     nbytes = 2 * qkv.numel() * 2
 
     def run(tiled):
-        os.environ["DSA_ROTARY_TILED"] = "1" if tiled else "0"
+        os.environ["DSA_ROTARY_TILED"] = str(int(tiled))
         q, k, v = A.rotary_split(qkv, NH, HD, ROT, qscale=HD ** -0.5)
         g = [torch.randn_like(t) for t in (q, k, v)]
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -40,13 +40,15 @@ def main():
         return out, fwd, fb
 
     res = {}
-    for tiled in (False, True):
+    names = {0: "row-per-thread", 1: "tiled (padded LDS rows)", 2: "tiled (unpadded rows)"}
+    for tiled in (0, 2, 1, 2, 1):
         out, fwd, bwd = run(tiled)
         res[tiled] = out
-        print(json.dumps({"variant": "tiled" if tiled else "row-per-thread", "shape": [B, S, NH, HD, ROT], "fwd_us": round(fwd * 1e3, 1),
+        print(json.dumps({"variant": names[tiled], "shape": [B, S, NH, HD, ROT], "fwd_us": round(fwd * 1e3, 1),
                           "bwd_us": round(bwd * 1e3, 1), "fwd_TBps": round(nbytes / fwd / 1e9, 2),
                           "bwd_TBps": round(nbytes / bwd / 1e9, 2)}), flush=True)
-    assert all(torch.equal(a, b) for a, b in zip(res[False], res[True]))
+    assert all(torch.equal(a, b) for a, b in zip(res[0], res[1]))
+    assert all(torch.equal(a, b) for a, b in zip(res[0], res[2]))
 
 
 if __name__ == "__main__":
