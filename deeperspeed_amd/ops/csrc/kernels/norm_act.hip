@@ -97,7 +97,8 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(const T* __restrict_
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd,
                                                             const T* __restrict__ dres, T* __restrict__ dx,
-                                                            float* __restrict__ partial, int64_t rows, int H) {
+                                                            float* __restrict__ partial, int64_t rows, int H,
+                                                            int pf = 1) {
   __shared__ float red[32];
   constexpr int VN = Vec16<T>::N;
   const int nvec = H / VN;
@@ -128,13 +129,14 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(const T* __restrict_
   };
   if ((int64_t)blockIdx.x < rows) fetch(blockIdx.x);
   for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    if (!pf && row != blockIdx.x) fetch(row);  // DSA_LN_BWD_PREFETCH=0: load the row just in time (A/B)
     const float mu = nmu, rs = nrs;
     float xh[NV][VN], g[NV][VN], rr[NV][VN];
 #pragma unroll
     for (int k = 0; k < NV; ++k)
 #pragma unroll
       for (int j = 0; j < VN; ++j) { xh[k][j] = nx[k][j]; g[k][j] = ng[k][j]; }
-    if (row + gridDim.x < rows) fetch(row + gridDim.x);
+    if (pf && row + gridDim.x < rows) fetch(row + gridDim.x);
     if (dres) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
@@ -547,6 +549,11 @@ void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_o
 
 int ln_bwd_grid(int64_t rows) { return (int)(rows < 512 ? rows : 512); }
 
+static int ln_bwd_prefetch() {
+  const char* v = getenv("DSA_LN_BWD_PREFETCH");
+  return (v && v[0] == '0') ? 0 : 1;
+}
+
 // partial workspace: 2 * ln_bwd_grid(rows) * H floats
 void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    const void* dres, void* dx, void* dgamma, void* dbeta, float* partial, int64_t rows, int H,
@@ -564,7 +571,7 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
     else
       DSA_DISPATCH_NV(nv, NV, hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(grid), dim3(LN_THREADS), 0, s,
                          (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
-                         partial, rows, H));
+                         partial, rows, H, ln_bwd_prefetch()));
     hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 15) / 16, dbeta ? 2 : 1), dim3(256), 0, s, partial, grid, H,
                        (T*)dgamma, accum, (int64_t)grid * H, (T*)dbeta));
 }
