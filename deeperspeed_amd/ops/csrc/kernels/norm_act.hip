@@ -549,6 +549,9 @@ void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_o
 
 int ln_bwd_grid(int64_t rows) { return (int)(rows < 512 ? rows : 512); }
 
+// Row prefetch in the block-per-row backward: +5-9 % at hidden 2048 (one vector per thread), but
+// -15 % at 6144 (three vectors per thread: the doubled row registers cost more than the latency
+// they hide), so only the one-vector instances take it (profiles/r4g_notes.md)
 static int ln_bwd_prefetch() {
   const char* v = getenv("DSA_LN_BWD_PREFETCH");
   return (v && v[0] == '0') ? 0 : 1;
@@ -571,7 +574,7 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
     else
       DSA_DISPATCH_NV(nv, NV, hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(grid), dim3(LN_THREADS), 0, s,
                          (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
-                         partial, rows, H, ln_bwd_prefetch()));
+                         partial, rows, H, (NV == 1) ? ln_bwd_prefetch() : 0));
     hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 15) / 16, dbeta ? 2 : 1), dim3(256), 0, s, partial, grid, H,
                        (T*)dgamma, accum, (int64_t)grid * H, (T*)dbeta));
 }

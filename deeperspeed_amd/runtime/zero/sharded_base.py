@@ -150,6 +150,10 @@ class ShardedOptimizerBase:
         self.device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
             else torch.device("cpu")
         self._copy_streams = None
+        # host-moments groups (param groups with "host_moments": True, see _host_moments_step)
+        self._host_stream = None
+        self._host_staging = None
+        self._host_d2h_done = None
 
     # ------------------------------------------------------------------ properties
     @property
@@ -178,6 +182,16 @@ class ShardedOptimizerBase:
         return self._global_grad_norm
 
     # ------------------------------------------------------------------ setup helpers
+    def _host_moment_group(self, g) -> bool:
+        """Param groups marked `"host_moments": True` keep their Adam moments in pinned host
+        memory while the rest of the optimizer state stays in HBM (MI355X extension: frees
+        8 B / parameter of HBM for the groups a trainer names -- bench.py gives it to the GPT-NeoX
+        LM head and last layers, whose update has the most slack before the next forward reads
+        them).  Needs the fused Adam and a GPU; the step streams the moments through HBM in
+        pieces on copy engines (_host_moments_step)."""
+        return bool(self.optimizer.param_groups[g.group_index].get("host_moments", False)) and self.fused \
+            and torch.cuda.is_available() and self.offload is None
+
     def _split_groups(self):
         """Split each inner param group into (dtype, model-parallel) flat groups."""
         from .layout import split_param_group
@@ -229,8 +243,9 @@ class ShardedOptimizerBase:
             for g in self.groups:
                 st = self.optimizer.state[g.master]
                 st["step"] = 0
-                on_host = (host and self.offload_states == "all") or moments_only
-                kw = dict(dtype=torch.float32, pin_memory=on_host and (pin or moments_only))
+                on_host = (host and self.offload_states == "all") or moments_only or self._host_moment_group(g)
+                kw = dict(dtype=torch.float32, pin_memory=on_host and (pin or moments_only or
+                                                                       self._host_moment_group(g)))
                 if on_host:
                     st["exp_avg"] = torch.zeros(g.shard_numel, **kw)
                     st["exp_avg_sq"] = torch.zeros(g.shard_numel, **kw)
@@ -440,7 +455,12 @@ class ShardedOptimizerBase:
                 st = self.optimizer.state_for(g.master) if isinstance(self.optimizer, FusedAdam) else \
                     self.optimizer.state[g.master]
                 st["step"] = st.get("step", 0) + 1
+            host_groups = [g for g in self.groups if self._host_moment_group(g)]
+            if host_groups:  # their copy pipeline starts first and runs beside the HBM groups
+                self._host_moments_step(host_groups, grad_scale)
             for g in self.groups:
+                if self._host_moment_group(g):
+                    continue
                 grp = self._inner_group(g)
                 for b in g.buckets:
                     out = self._bucket_out(g, b)
@@ -449,6 +469,8 @@ class ShardedOptimizerBase:
                         self.optimizer.update_flat(grp, g.master, g.master, g.shard_grad, out=o,
                                                    grad_scale=grad_scale, lo=lo, hi=hi)
                     self._after_bucket_update(g, b)
+            if host_groups:  # the step's end (and the gradient zeroing after it) follows their kernels
+                torch.cuda.current_stream().wait_stream(self._host_stream)
             return
         # generic torch optimizer over the fp32 master shards
         for g in self.groups:
@@ -463,6 +485,88 @@ class ShardedOptimizerBase:
                 if out is not None and out.data_ptr() != g.master.data_ptr():
                     native.scale_copy_(g.master[b.shard_offset: b.shard_offset + b.chunk], out)
                 self._after_bucket_update(g, b)
+
+    HOST_PIECE = int(16 * 1024 * 1024)  # elements of m / v staged per piece (64 MB each in fp32)
+
+    def _host_moments_step(self, groups, grad_scale):
+        """Adam for the host-moments groups: per piece, H2D of m / v into one of three persistent
+        HBM staging slots (copy stream), the fused Adam kernel on a stream of its own, D2H of m / v
+        (second copy stream).  Nothing waits on the host: the current stream (the overlapped
+        step's side stream, or the compute stream) waits for the kernels at the end, the next
+        step's H2D waits for this step's D2H, and checkpoints wait for it (host_moments_sync).
+        Each bucket's update event is recorded for the forward pre-hooks (overlap_step)."""
+        h2d, d2h = self._streams()
+        if self._host_stream is None:
+            self._host_stream = torch.cuda.Stream(device=self.device)
+        hs, cur = self._host_stream, torch.cuda.current_stream()
+        piece = min(self.HOST_PIECE, max(b.chunk for g in groups for b in g.buckets))
+        if self._host_staging is None or self._host_staging[0][0].numel() < piece:
+            self._host_staging = [(torch.empty(piece, dtype=torch.float32, device=self.device),
+                                   torch.empty(piece, dtype=torch.float32, device=self.device)) for _ in range(3)]
+        stages = self._host_staging
+        start = torch.cuda.Event()
+        start.record(cur)  # gradients are final
+        hs.wait_event(start)
+        h2d.wait_event(start)
+        if self._host_d2h_done is not None:  # the previous step's moments are home
+            h2d.wait_event(self._host_d2h_done)
+        free_ev = list(getattr(self, "_host_free_ev", [None] * 3))
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+        k = 0
+        for g in groups:
+            grp = self._inner_group(g)
+            b1, b2 = grp["betas"]
+            st = self.optimizer.state_for(g.master) if isinstance(self.optimizer, FusedAdam) else \
+                self.optimizer.state[g.master]
+            for b in g.buckets:
+                out_full = self._bucket_out(g, b)
+                for s in range(0, b.chunk, piece):
+                    e = min(s + piece, b.chunk)
+                    lo, hi, n = b.shard_offset + s, b.shard_offset + e, e - s
+                    i = k % 3
+                    k += 1
+                    m_dev, v_dev = stages[i][0][:n], stages[i][1][:n]
+                    with torch.cuda.stream(h2d):
+                        if free_ev[i] is not None:
+                            h2d.wait_event(free_ev[i])
+                        m_dev.copy_(st["exp_avg"][lo:hi], non_blocking=True)
+                        v_dev.copy_(st["exp_avg_sq"][lo:hi], non_blocking=True)
+                        ev_in = torch.cuda.Event()
+                        ev_in.record(h2d)
+                    hs.wait_event(ev_in)
+                    o = None if out_full is None else out_full[s:e]
+                    with torch.cuda.stream(hs):
+                        if self.compact_master:
+                            native.adam_compact_(o, g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, grp["lr"],
+                                                 b1, b2, grp["eps"], grp["weight_decay"], st["step"],
+                                                 grp.get("bias_correction", True), grad_scale, adamw)
+                        else:
+                            native.adam_flat_(g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, o, grp["lr"], b1,
+                                              b2, grp["eps"], grp["weight_decay"], st["step"],
+                                              grp.get("bias_correction", True), grad_scale, adamw)
+                        ev_done = torch.cuda.Event()
+                        ev_done.record(hs)
+                    with torch.cuda.stream(d2h):
+                        d2h.wait_event(ev_done)
+                        st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
+                        st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
+                        ev_free = torch.cuda.Event()
+                        ev_free.record(d2h)
+                    free_ev[i] = ev_free
+                self._after_host_bucket_update(g, b, hs)
+        self._host_free_ev = free_ev
+        done = torch.cuda.Event()
+        done.record(d2h)
+        self._host_d2h_done = done
+
+    def _after_host_bucket_update(self, g, b, stream):
+        """Bucket-update hook for a host-moments bucket updated on `stream` (stage 3 records the
+        overlap_step event there)."""
+
+    def host_moments_sync(self):
+        """Block the host until the last step's host moments are written back (checkpoints)."""
+        if self._host_d2h_done is not None:
+            self._host_d2h_done.synchronize()
 
     # ------------------------------------------------------------------ offload step
     def _streams(self):
@@ -631,6 +735,7 @@ class ShardedOptimizerBase:
         return 0
 
     def state_dict(self):
+        self.host_moments_sync()
         base = self.optimizer.state_dict()
         if self.nvme:  # moments live on NVMe: materialise them for the checkpoint
             for gi in range(len(self.groups)):
@@ -664,6 +769,7 @@ class ShardedOptimizerBase:
         return "dsa_flat_fp32_shards"
 
     def load_state_dict(self, state_dict_list, load_optimizer_states=True, load_from_fp32_weights=True):
+        self.host_moments_sync()  # no write-back of the previous step may land after the load
         if isinstance(state_dict_list, dict):
             state_dict_list = [state_dict_list]
         sd0 = state_dict_list[0]

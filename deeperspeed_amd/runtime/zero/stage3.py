@@ -824,6 +824,12 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             ev.record(self._step_stream)
             self._bucket_events[self._bucket_key[id(b)]] = ev
 
+    def _after_host_bucket_update(self, g, b, stream):
+        if self._overlap_step and self._step_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self._bucket_events[self._bucket_key[id(b)]] = ev
+
     def state_dict(self):
         self.synchronize_step()
         return super().state_dict()
