@@ -83,6 +83,10 @@ def parse():
                         "(auto: when the spare HBM holds a bf16 copy of the gradients)")
     p.add_argument("--dist-backend", type=str, default="nccl",
                    help="nccl (= RCCL); gloo only to rehearse N ranks sharing one GPU (forced on CPU)")
+    p.add_argument("--host-moments-layers", type=str, default="auto",
+                   help="Adam moments of the LM head and the last K transformer layers in pinned host memory, "
+                        "streamed through HBM during the step (frees 8 B/param of HBM for the activation stash); "
+                        "auto: 2 for the 20B single-GPU bound ZeRO-3 run, else 0")
     p.add_argument("--fp32-reduce", type=str, default="off", choices=["on", "off"],
                    help="reduce bf16 gradients in fp32 (DeeperSpeed's bf16 default fp32_allreduce; "
                         "tests/test_zero_reduce_precision.py measures what bf16 reduction costs)")
@@ -456,7 +460,25 @@ def main():
     model = GPTNeoX(cfg, device=dev, dtype=torch.bfloat16)
     log(f"model built in {time.time() - t0:.1f}s")
     hb.beat("model built")
-    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    # Host moments (MI355X extension, runtime/zero/sharded_base.py _host_moments_step): on one GPU
+    # the 20B states leave ~16 GiB for activations, so 18 of 44 layers recompute their attention.
+    # The LM head and the last K layers are the parameters with the most slack between their final
+    # gradient (early in the last micro-batch's backward) and their next read (late in the next
+    # forward): their Adam moments live in pinned host memory and stream through HBM on the copy
+    # engines during the overlapped step, and the 8 B/param freed goes to the attention stash.
+    hm = args.host_moments_layers
+    k_host = (2 if (world == 1 and args.zero == 3 and offload == "compact" and ckpt == "on" and big and on_gpu
+                    and not args.force_sharded and args.pipe == 1) else 0) if hm == "auto" else int(hm)
+    params = model.parameters()
+    host_numel = 0
+    if k_host > 0:
+        tail = {id(p) for m in [model.embed_out] + list(model.layers[-k_host:]) for p in m.parameters()}
+        host_numel = sum(p.numel() for p in model.parameters() if id(p) in tail)
+        params = [{"params": [p for p in model.parameters() if id(p) not in tail]},
+                  {"params": [p for p in model.parameters() if id(p) in tail], "host_moments": True}]
+        log(f"host moments: LM head + last {k_host} layers = {host_numel / 1e9:.2f}B params "
+            f"({8 * host_numel / 2**30:.1f} GiB of Adam moments in pinned host memory)")
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=params, config_params=conf)
     del model
     log(f"engine ready in {time.time() - t0:.1f}s" +
         (f", mem={torch.cuda.memory_allocated() / 2**30:.1f} GiB" if on_gpu else ""))
@@ -716,6 +738,7 @@ def main():
                    "fp32_reduce": args.fp32_reduce == "on",
                    "dist_backend": dist.get_backend(),
                    "overlap_step": bool(zcfg.get("overlap_step", False)),
+                   "host_moments_params": host_numel,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N): BASELINE.md's derived target "
                                     "(reference's best published ZeRO-3 49 TFLOPS/GPU on V100 at 6N FLOPs/token); "
                                     "BASELINE.json publishes no number for this metric"},
