@@ -540,6 +540,7 @@ def main():
             m.register_forward_hook(_mark)
 
     stashed = 0
+    stashed_mlp = 0
 
     def plan_stash():
         """Selective recompute from MEASURED headroom: after a warmup step with full recompute,
@@ -555,8 +556,18 @@ def main():
         n = int(max(0, min(len(layers), free // per_layer)))
         for m in layers[-n:] if n else []:
             m.attention.stash_outputs = True
-        log(f"selective recompute: {n}/{len(layers)} layers keep attention outputs "
-            f"({n * per_layer / 2**30:.1f} GiB; reserved peak {reserved_peak() / 2**30:.1f} GiB)")
+        # then the MLP: the fc1 output u [tokens, 4h] of as many layers as still fit (saves the fc1
+        # GEMM of their recompute; about the same GEMM time per GiB as the attention stash)
+        per_mlp = mb * args.seq * cfg.intermediate_size * 2
+        n_mlp = 0
+        if n == len(layers) and os.environ.get("DSA_MLP_STASH", "1") != "0":
+            n_mlp = int(max(0, min(len(layers), (free - n * per_layer) // per_mlp)))
+            for m in layers[-n_mlp:] if n_mlp else []:
+                m.mlp.stash_outputs = True
+        nonlocal stashed_mlp
+        stashed_mlp = n_mlp
+        log(f"selective recompute: {n}/{len(layers)} layers keep attention outputs, {n_mlp} keep the fc1 output "
+            f"({(n * per_layer + n_mlp * per_mlp) / 2**30:.1f} GiB; reserved peak {reserved_peak() / 2**30:.1f} GiB)")
         # the remaining layers park their stash in pinned host memory (copy engines over PCIe,
         # prefetched back by the recompute of the layers above): opt-in, DSA_STASH_OFFLOAD=1 -- on the
         # measured box the PCIe copies throttled the forward (profiles/aux/host_stash_ab.log)
@@ -578,12 +589,25 @@ def main():
         variance on another box cannot push a timed step into an out-of-memory error."""
         if n <= 0:
             return n
+        nonlocal stashed_mlp
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
         sfloor = float(os.environ.get("DSA_STASH_FLOOR_GIB", "1.5")) * 2**30
         over = reserved_peak() - (hbm / share - sfloor)
         if over <= 0:
             return n
+        if stashed_mlp:  # the MLP stashes go back first
+            per_mlp = mb * args.seq * cfg.intermediate_size * 2
+            drop = min(stashed_mlp, int(-(-over // per_mlp)))
+            for m in layers[len(layers) - stashed_mlp: len(layers) - stashed_mlp + drop]:
+                m.mlp._stash.clear()
+                m.mlp.stash_outputs = False
+            stashed_mlp -= drop
+            over -= drop * per_mlp
+            torch.cuda.empty_cache()
+            log(f"stash safety: {drop} MLP stash(es) given back ({stashed_mlp} kept)")
+            if over <= 0:
+                return n
         drop = min(n, int(-(-over // per_layer)))
         offload = any(l.attention.stash_offload for l in layers)
         for m in layers[len(layers) - n: len(layers) - n + drop]:
@@ -729,6 +753,7 @@ def main():
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None,
                    "planned_hbm_gib": round(planned / 2**30, 1),
                    "stashed_attention_layers": stashed,
+                   "stashed_mlp_layers": stashed_mlp,
                    "host_stashed_attention_layers": sum(1 for m in engine.module.modules()
                                                         if getattr(m, "stash_offload", False)),
                    "zero3_path": zpath,

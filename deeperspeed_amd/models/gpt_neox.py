@@ -121,9 +121,18 @@ class LinearBiasGeLU(nn.Linear):
         # activation is then produced transposed (its only reader is that linear's weight
         # gradient, which wants it reduction-contiguous)
         self.colmajor_in_recompute = False
+        self.keep_u = False  # MLP stash: hand the GEMM output to the caller (kept_u) on this forward
+        self.kept_u = None
+        self.stashed_u = None  # MLP stash: the next forward reuses this GEMM output (gradient-only GEMM)
 
     def forward(self, x):
-        u = linear(x, self.weight)
+        if self.stashed_u is not None:
+            u_st, self.stashed_u = self.stashed_u, None
+            u = _StashInject.apply(grad_only_linear(x, self.weight), u_st)
+        else:
+            u = linear(x, self.weight)
+            if self.keep_u:
+                self.kept_u = u
         if (self.colmajor_in_recompute and _SKIP_OUTPUTS and torch.is_grad_enabled() and COLMAJOR_GELU
                 and native.bias_gelu_t_supported(u)):
             return native.bias_gelu_colmajor(u, self.bias, self.approximate)
@@ -180,6 +189,19 @@ def residual_sum(*xs):
     for x in xs[2:]:
         out = out + x
     return out
+
+
+class _StashInject(torch.autograd.Function):
+    """Value of `stashed`, gradient routed to `placeholder` (a gradient-only GEMM whose output
+    the first forward already computed and kept)."""
+
+    @staticmethod
+    def forward(ctx, placeholder, stashed):
+        return stashed.view(stashed.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
 
 
 class OutputLinear(nn.Linear):
@@ -341,9 +363,33 @@ class NeoXMLP(nn.Module):
                                             device=device, dtype=dtype)
         self.dense_4h_to_h = OutputLinear(cfg.intermediate_size, cfg.hidden_size, device=device, dtype=dtype)
         self.dense_h_to_4h.colmajor_in_recompute = self.dense_4h_to_h.skip_in_recompute
+        # Selective MLP recompute (set per layer by the trainer when HBM allows, after the
+        # attention stash): the first forward of a checkpointed block keeps the fc1 GEMM output
+        # u [tokens, 4h]; the recompute takes it instead of re-running the GEMM (the bias + GeLU
+        # and fc1's gradients run as usual).  Keyed like NeoXAttention's stash.
+        self.stash_outputs = False
+        self._stash = {}
+        self._stash_key = None
 
     def forward(self, x):
-        return self.dense_4h_to_h(self.dense_h_to_4h(x))
+        key, fc1 = self._stash_key, self.dense_h_to_4h
+        if self.stash_outputs and key is not None:
+            if ds_ckpt.is_recomputing() and torch.is_grad_enabled():
+                u = self._stash.pop(key, None)
+                if u is not None:
+                    fc1.stashed_u = u
+            elif ds_ckpt.is_checkpoint_forward():
+                if key in self._stash or len(self._stash) >= NeoXAttention._STASH_LIMIT:
+                    raise RuntimeError("MLP selective-recompute stash for this input was never consumed")
+                fc1.keep_u = True
+                try:
+                    h = fc1(x)
+                finally:
+                    fc1.keep_u = False
+                self._stash[key] = fc1.kept_u
+                fc1.kept_u = None
+                return self.dense_4h_to_h(h)
+        return self.dense_4h_to_h(fc1(x))
 
 
 STASH_PREFETCH_DEPTH = 2  # layers whose host-parked stash a recompute starts bringing back
@@ -385,14 +431,15 @@ class NeoXTransformerLayer(nn.Module):
         return residual_sum(x, self.mlp(h2))
 
     def _block_ckpt(self, x):
-        self.attention._stash_key = (x.untyped_storage().data_ptr(), x.storage_offset(), tuple(x.shape))
+        key = (x.untyped_storage().data_ptr(), x.storage_offset(), tuple(x.shape))
+        self.attention._stash_key = self.mlp._stash_key = key
         try:
             if ds_ckpt.is_recomputing():
                 with skip_unread_outputs():
                     return self._block(x)
             return self._block(x)
         finally:
-            self.attention._stash_key = None
+            self.attention._stash_key = self.mlp._stash_key = None
 
     def forward(self, x):
         if self.cfg.checkpoint_activations and self.training and torch.is_grad_enabled():

@@ -71,3 +71,34 @@ def test_stash_two_forwards_before_backward(offload):
     for n in ra:
         torch.testing.assert_close(sa[n], ra[n], atol=1e-3, rtol=1e-3, msg=n)
         torch.testing.assert_close(sb[n], rb[n], atol=1e-3, rtol=1e-3, msg=n)
+
+
+def test_mlp_stash_matches_full_recompute():
+    """MLP selective recompute (NeoXMLP.stash_outputs): the recompute takes the fc1 output the first
+    forward kept (gradient-only fc1 GEMM) -- same gradients as the full recompute, also combined
+    with the attention stash."""
+    from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
+
+    def run(att, mlp):
+        torch.manual_seed(0)
+        cfg = get_config("tiny", hidden_size=384, num_heads=4, num_layers=3, max_seq_len=128,
+                         checkpoint_activations=True)
+        model = GPTNeoX(cfg, device="cuda", dtype=torch.bfloat16).train()
+        for m in model.layers:
+            m.attention.stash_outputs = att
+            m.mlp.stash_outputs = mlp
+        g = torch.Generator(device="cuda").manual_seed(1)
+        ids = torch.randint(0, cfg.vocab_size, (2, 128), device="cuda", generator=g)
+        for _ in range(2):
+            model.zero_grad(set_to_none=True)
+            loss = model(ids, labels=ids)
+            loss.backward()
+        assert all(not m.mlp._stash and not m.attention._stash for m in model.layers)
+        return float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+    l0, g0 = run(False, False)
+    for att in (False, True):
+        l1, g1 = run(att, True)
+        assert l0 == l1
+        for n in g0:
+            torch.testing.assert_close(g1[n], g0[n], atol=1e-3, rtol=1e-3, msg=n)
