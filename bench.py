@@ -466,7 +466,7 @@ def main():
     # gradient (early in the last micro-batch's backward) and their next read (late in the next
     # forward): their Adam moments live in pinned host memory and stream through HBM on the copy
     # engines during the overlapped step, and the 8 B/param freed goes to the attention stash.
-    hm = args.host_moments_layers
+    hm = os.environ.get("DSA_BENCH_HOST_MOMENTS", args.host_moments_layers)
     k_host = (2 if (world == 1 and args.zero == 3 and offload == "compact" and ckpt == "on" and big and on_gpu
                     and not args.force_sharded and args.pipe == 1) else 0) if hm == "auto" else int(hm)
     params = model.parameters()
