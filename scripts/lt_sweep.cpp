@@ -12,8 +12,12 @@
 //     wgrad  dW[N,K] += dY[M,N]^T . X[M,K]      (col-major NT, beta = 1)
 //     wgradT dW[N,K] += dYt[N,M] . Xt[K,M]^T    (col-major TN after the two transposes, beta = 1)
 //
+//     fwdb   fwd with the BIAS epilogue (what F.linear(x, W, b) asks for)
+//
 // Build: hipcc -O2 --offload-arch=gfx950 scripts/lt_sweep.cpp -lhipblaslt -o lt_sweep
-// Run:   ./lt_sweep <layout> M N K [top]
+// Run:   ./lt_sweep <layout>:M:N:K [<layout>:M:N:K ...]   (one JSON line per problem)
+// Only macro tiles of at least 128 x 128 are timed when both output dims are >= 2048 (the small
+// tiles cannot fill the chip there, and each kernel's first launch loads its code object).
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
@@ -48,14 +52,44 @@ __global__ void fill_rand(uint16_t* p, size_t n, uint32_t seed) {
   }
 }
 
+static bool small_tile(const std::string& name) {
+  const size_t p = name.find("_MT");
+  if (p == std::string::npos) return false;
+  const int a = atoi(name.c_str() + p + 3);
+  const size_t x = name.find('x', p + 3);
+  const int b = x == std::string::npos ? 0 : atoi(name.c_str() + x + 1);
+  return a < 128 || b < 128;
+}
+
+static int sweep(hipblasLtHandle_t h, const std::string& spec, void* ws, size_t wsz);
+
 int main(int argc, char** argv) {
-  if (argc < 5) {
-    fprintf(stderr, "usage: %s fwd|dgrad|wgrad|wgradT M N K [top]\n", argv[0]);
+  if (argc < 2) {
+    fprintf(stderr, "usage: %s layout:M:N:K ...\n", argv[0]);
     return 2;
   }
-  const std::string lay = argv[1];
-  const int64_t M = atoll(argv[2]), N = atoll(argv[3]), K = atoll(argv[4]);
-  const int top = argc > 5 ? atoi(argv[5]) : 5;
+  hipblasLtHandle_t h;
+  CK(hipblasLtCreate(&h));
+  void* ws;
+  const size_t wsz = 64ull << 20;
+  CK(hipMalloc(&ws, wsz));
+  for (int i = 1; i < argc; ++i)
+    if (sweep(h, argv[i], ws, wsz)) return 1;
+  return 0;
+}
+
+static int sweep(hipblasLtHandle_t h, const std::string& spec, void* ws, size_t wsz) {
+  char lbuf[16];
+  long M_, N_, K_;
+  if (sscanf(spec.c_str(), "%15[a-zA-Z]:%ld:%ld:%ld", lbuf, &M_, &N_, &K_) != 4) {
+    fprintf(stderr, "bad problem %s\n", spec.c_str());
+    return 1;
+  }
+  std::string lay = lbuf;
+  const int64_t M = M_, N = N_, K = K_;
+  const int top = 4;
+  const bool bias = lay == "fwdb";
+  if (bias) lay = "fwd";
   // column-major problem D[m,n] = op(A)[m,k] op(B)[k,n]
   hipblasOperation_t ta, tb;
   int64_t m, n, k, lda, ldb, ldd, ar, ac, br, bc;
@@ -74,17 +108,16 @@ int main(int argc, char** argv) {
     ar = M, ac = K, lda = M, br = M, bc = N, ldb = M, ldd = K;
   } else {
     fprintf(stderr, "unknown layout %s\n", lay.c_str());
-    return 2;
+    return 1;
   }
-  hipblasLtHandle_t h;
-  CK(hipblasLtCreate(&h));
-  uint16_t *A, *B, *D;
-  void* ws;
-  const size_t wsz = 64ull << 20;
+  uint16_t *A, *B, *D, *bvec = nullptr;
   CK(hipMalloc(&A, ar * ac * 2));
   CK(hipMalloc(&B, br * bc * 2));
   CK(hipMalloc(&D, m * n * 2));
-  CK(hipMalloc(&ws, wsz));
+  if (bias) {
+    CK(hipMalloc(&bvec, m * 2));
+    fill_rand<<<64, 256>>>(bvec, m, 4);
+  }
   fill_rand<<<2048, 256>>>(A, ar * ac, 1);
   fill_rand<<<2048, 256>>>(B, br * bc, 2);
   fill_rand<<<2048, 256>>>(D, m * n, 3);
@@ -94,6 +127,13 @@ int main(int argc, char** argv) {
   CK(hipblasLtMatmulDescCreate(&op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
   CK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
   CK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
+  if (bias) {
+    const hipblasLtEpilogue_t e = HIPBLASLT_EPILOGUE_BIAS;
+    const hipDataType bt = HIP_R_16BF;
+    CK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e)));
+    CK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bvec, sizeof(void*)));
+    CK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  }
   hipblasLtMatrixLayout_t la, lb, ld;
   CK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, ar, ac, lda));
   CK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, br, bc, ldb));
@@ -124,7 +164,9 @@ int main(int argc, char** argv) {
   std::vector<R> res;
   const double flops = 2.0 * M * N * K;
   int tried = 0;
+  const bool big = m >= 2048 && n >= 2048;
   for (auto& r : all) {
+    if (big && small_tile(hipblaslt_ext::getKernelNameFromAlgo(h, r.algo))) continue;
     size_t need = 0;
     if (hipblaslt_ext::matmulIsAlgoSupported(h, op, &alpha, la, lb, &beta, ld, ld, r.algo, need) !=
             HIPBLAS_STATUS_SUCCESS ||
@@ -132,11 +174,11 @@ int main(int argc, char** argv) {
       continue;
     ++tried;
     bool ok = true;
-    for (int i = 0; i < 2 && ok; ++i)
+    for (int i = 0; i < 1 && ok; ++i)
       ok = hipblasLtMatmul(h, op, &alpha, A, la, B, lb, &beta, D, ld, D, ld, &r.algo, ws, wsz, 0) ==
            HIPBLAS_STATUS_SUCCESS;
     if (!ok) continue;
-    const int reps = 5;
+    const int reps = 3;
     hipEventRecord(e0, 0);
     for (int i = 0; i < reps; ++i) hipblasLtMatmul(h, op, &alpha, A, la, B, lb, &beta, D, ld, D, ld, &r.algo, ws, wsz, 0);
     hipEventRecord(e1, 0);
@@ -149,14 +191,23 @@ int main(int argc, char** argv) {
   float heur_ms = -1;
   for (auto& r : res)
     if (r.idx == heur_idx) heur_ms = r.ms;
-  printf("{\"layout\": \"%s\", \"M\": %ld, \"N\": %ld, \"K\": %ld, \"algos\": %zu, \"supported\": %d, "
+  printf("{\"layout\": \"%s%s\", \"M\": %ld, \"N\": %ld, \"K\": %ld, \"algos\": %zu, \"supported\": %d, "
          "\"heuristic_idx\": %d, \"heuristic_tflops\": %.1f, \"top\": [",
-         lay.c_str(), (long)M, (long)N, (long)K, all.size(), tried, heur_idx,
+         lay.c_str(), bias ? "+bias" : "", (long)M, (long)N, (long)K, all.size(), tried, heur_idx,
          heur_ms > 0 ? flops / heur_ms / 1e9 : -1.0);
   for (int i = 0; i < top && i < (int)res.size(); ++i)
     printf("%s{\"idx\": %d, \"tflops\": %.1f, \"kernel\": \"%s\"}", i ? ", " : "", res[i].idx,
            flops / res[i].ms / 1e9, res[i].name.substr(0, 120).c_str());
   printf("]}\n");
   fflush(stdout);
+  hipFree(A);
+  hipFree(B);
+  hipFree(D);
+  if (bvec) hipFree(bvec);
+  hipblasLtMatrixLayoutDestroy(la);
+  hipblasLtMatrixLayoutDestroy(lb);
+  hipblasLtMatrixLayoutDestroy(ld);
+  hipblasLtMatmulDescDestroy(op);
+  hipblasLtMatmulPreferenceDestroy(pref);
   return 0;
 }
