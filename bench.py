@@ -764,6 +764,7 @@ def main():
                    "dist_backend": dist.get_backend(),
                    "overlap_step": bool(zcfg.get("overlap_step", False)),
                    "host_moments_params": host_numel,
+                   "lt_gemm": _lt_summary() if on_gpu else None,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N): BASELINE.md's derived target "
                                     "(reference's best published ZeRO-3 49 TFLOPS/GPU on V100 at 6N FLOPs/token); "
                                     "BASELINE.json publishes no number for this metric"},
@@ -772,6 +773,20 @@ def main():
         emit_result(out)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _lt_summary():
+    """How many GEMM problems the hipBLASLt wrapper tuned, and how many picked a solution from the
+    measured table (ops/lt_tune.py) over the heuristic's candidates."""
+    try:
+        from deeperspeed_amd.ops import lt_tune, native
+        if not lt_tune.ENABLED:
+            return {"enabled": False}
+        ch = native.hip_ops().lt_choices()
+    except Exception as e:  # diagnostics only
+        return {"error": repr(e)}
+    return {"enabled": True, "problems": len(ch), "table_wins": sum(1 for c in ch if c[10]),
+            "routes": {"fwd": lt_tune.FWD, "dgrad": lt_tune.DGRAD, "wgrad": lt_tune.WGRAD}}
 
 
 def _optimizer_block(args):

@@ -24,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import native
+from ..ops import lt_tune
 from ..ops.linear import Linear, grad_only_linear, linear, nt_wgrad_planned, zero_placeholder
 from ..ops.attention import attention, rotary_split
 from ..runtime.activation_checkpointing import checkpointing as ds_ckpt
@@ -134,7 +135,10 @@ class LinearBiasGeLU(nn.Linear):
             if self.keep_u:
                 self.kept_u = u
         if (self.colmajor_in_recompute and _SKIP_OUTPUTS and torch.is_grad_enabled() and COLMAJOR_GELU
-                and native.bias_gelu_t_supported(u)):
+                and native.bias_gelu_t_supported(u)
+                # fc2's weight gradient reads its input token-major when the measured NT GEMM wins
+                and not lt_tune.wgrad_nt(u.numel() // self.out_features, self.in_features, self.out_features,
+                                         u.element_size())):
             return native.bias_gelu_colmajor(u, self.bias, self.approximate)
         # the backward also writes du^T when this layer's own weight gradient will read it
         offer = u.is_cuda and nt_wgrad_planned(u.numel() // self.out_features, self.out_features, self.in_features,

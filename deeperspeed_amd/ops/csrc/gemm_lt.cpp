@@ -13,12 +13,25 @@
 // Row-major tensors are passed as their column-major transposes: Y^T[N,M] = W[N,K] . X^T[K,M]
 // ("TN"), so the bias runs along D's rows as hipBLASLt requires.  Per (shape, epilogue) the
 // top heuristic algorithms are timed once on the first call and the fastest is cached.
+//
+// Registered candidates: hipBLASLt's heuristic top-16 rarely holds the fastest kernel for the
+// GPT-NeoX shapes on gfx950.  An exhaustive offline sweep (scripts/lt_sweep.cpp over all of
+// hipblaslt_ext::getAllAlgos) found CMS-variant 256x256 kernels 3-13 % faster for the forward
+// and the untransposed input-gradient (NN) layouts, and NT weight-gradient kernels that make the
+// operand transposes unnecessary for some shapes (profiles/r4i_lt_sweep.jsonl).  Those solution
+// indices ship in ops/lt_table.json; lt_register() adds them to the candidates timed on the
+// first call of that problem, so a stale or foreign index can only lose the timing, never be
+// used unverified (each one is checked with matmulIsAlgoSupported first).
+#include <pybind11/stl.h>
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
 
+#include <algorithm>
 #include <map>
+#include <string>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -33,6 +46,7 @@ namespace {
 
 constexpr size_t kWorkspace = 64ull << 20;
 constexpr int kCandidates = 16;  // heuristic algorithms timed once per GEMM shape
+constexpr int kTimedReps = 5;    // launches timed per candidate (after one warm-up launch)
 
 struct Ctx {
   hipblasLtHandle_t handle = nullptr;
@@ -79,11 +93,26 @@ using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int, int, 
 struct Algo {
   hipblasLtMatmulAlgo_t algo;
   size_t ws;
+  int index;       // hipBLASLt solution index (diagnostics)
+  float ms;        // timed per-call time of the winner
+  int candidates;  // how many were timed
+  bool registered; // the winner came from the registered table, not the heuristic
 };
 
 std::map<Key, Algo>& algo_cache() {
   static std::map<Key, Algo> c;
   return c;
+}
+
+// (ta, tb, m, n, k, epi, has_C, ab_type, d_type) -> solution indices from the offline sweep
+using RegKey = std::tuple<int, int, int64_t, int64_t, int64_t, int, bool, int, int>;
+std::map<RegKey, std::vector<int>>& registry() {
+  static std::map<RegKey, std::vector<int>> r;
+  return r;
+}
+std::mutex& cache_mu() {
+  static std::mutex mu;
+  return mu;
 }
 
 void run(const Gemm& g, int device, hipStream_t stream) {
@@ -112,6 +141,7 @@ void run(const Gemm& g, int device, hipStream_t stream) {
   LT_CHECK(hipblasLtMatrixLayoutCreate(&ld, g.d_type, g.m, g.n, g.ldd));
   const float alpha = 1.f, beta = g.C ? 1.f : 0.f;
   const Key key{device, (int)g.epi, g.m, g.n, g.k, (int)g.ta, (int)g.tb, (int)g.ab_type, (int)g.d_type, g.C != nullptr};
+  std::lock_guard<std::mutex> lock(cache_mu());
   auto& cache = algo_cache();
   auto it = cache.find(key);
   if (it == cache.end()) {
@@ -119,14 +149,36 @@ void run(const Gemm& g, int device, hipStream_t stream) {
     LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
     uint64_t wsz = kWorkspace;
     LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz)));
-    hipblasLtMatmulHeuristicResult_t res[kCandidates];
-    int nres = 0;
-    LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(c.handle, op, la, lb, ld, ld, pref, kCandidates, res, &nres));
+    hipblasLtMatmulHeuristicResult_t hres[kCandidates];
+    int nh = 0;
+    LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(c.handle, op, la, lb, ld, ld, pref, kCandidates, hres, &nh));
     hipblasLtMatmulPreferenceDestroy(pref);
+    std::vector<hipblasLtMatmulHeuristicResult_t> res(hres, hres + nh);
+    std::vector<char> from_table(res.size(), 0);
+    const RegKey rk{(int)g.ta, (int)g.tb, g.m, g.n, g.k, (int)g.epi, g.C != nullptr, (int)g.ab_type, (int)g.d_type};
+    auto reg = registry().find(rk);
+    if (reg != registry().end() && !reg->second.empty()) {
+      std::vector<int> idx = reg->second;
+      std::vector<hipblasLtMatmulHeuristicResult_t> extra;
+      if (hipblaslt_ext::getAlgosFromIndex(c.handle, idx, extra) == HIPBLAS_STATUS_SUCCESS) {
+        for (auto& r : extra) {
+          size_t need = 0;
+          if (hipblaslt_ext::matmulIsAlgoSupported(c.handle, op, &alpha, la, lb, &beta, ld, ld, r.algo, need) !=
+                  HIPBLAS_STATUS_SUCCESS || need > kWorkspace)
+            continue;
+          r.workspaceSize = need;
+          r.state = HIPBLAS_STATUS_SUCCESS;
+          res.push_back(r);
+          from_table.push_back(1);
+        }
+      }
+    }
+    const int nres = (int)res.size();
     TORCH_CHECK(nres > 0, "gemm_lt: hipBLASLt has no algorithm for this GEMM / epilogue");
     // time the candidates once (each 3 launches after one warm-up); the output buffers are
     // scratch until the real launch below overwrites them
     int best = 0;
+    float best_ms = 1e30f;
     if (nres > 1) {
       // when accumulating (C = D) the candidates write a scratch D so timing never disturbs
       // the caller's output; otherwise D is overwritten by the final launch anyway
@@ -139,14 +191,13 @@ void run(const Gemm& g, int device, hipStream_t stream) {
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
       hipEventCreate(&e1);
-      float best_ms = 1e30f;
       for (int i = 0; i < nres; ++i) {
         if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
         if (hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, sc ? sc : sd, ld, sd, ld, &res[i].algo,
                             c.workspace.data_ptr(), kWorkspace, stream) != HIPBLAS_STATUS_SUCCESS)
           continue;
         hipEventRecord(e0, stream);
-        for (int r = 0; r < 3; ++r)
+        for (int r = 0; r < kTimedReps; ++r)
           hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, sc ? sc : sd, ld, sd, ld, &res[i].algo,
                           c.workspace.data_ptr(), kWorkspace, stream);
         hipEventRecord(e1, stream);
@@ -161,7 +212,8 @@ void run(const Gemm& g, int device, hipStream_t stream) {
       hipEventDestroy(e0);
       hipEventDestroy(e1);
     }
-    it = cache.emplace(key, Algo{res[best].algo, res[best].workspaceSize}).first;
+    it = cache.emplace(key, Algo{res[best].algo, res[best].workspaceSize, hipblaslt_ext::getIndexFromAlgo(res[best].algo),
+                                 nres > 1 ? best_ms / kTimedReps : -1.f, nres, from_table[best] != 0}).first;
   }
   LT_CHECK(hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, g.C ? g.C : g.D, ld, g.D, ld,
                            &it->second.algo, c.workspace.data_ptr(), kWorkspace, stream));
@@ -308,7 +360,37 @@ int64_t lt_algo_count(int64_t m, int64_t n, int64_t k, int64_t epi, bool with_au
   return st == HIPBLAS_STATUS_SUCCESS ? nres : -(int64_t)st;
 }
 
+// Candidate solution indices for one column-major problem (bf16 operands; d_bf16 false -> fp32 D).
+void lt_register(bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t epi, bool beta, bool d_bf16,
+                 std::vector<int64_t> idx) {
+  std::lock_guard<std::mutex> lock(cache_mu());
+  const RegKey rk{(int)(ta ? HIPBLAS_OP_T : HIPBLAS_OP_N), (int)(tb ? HIPBLAS_OP_T : HIPBLAS_OP_N), m, n, k, (int)epi,
+                  beta, (int)HIP_R_16BF, (int)(d_bf16 ? HIP_R_16BF : HIP_R_32F)};
+  auto& v = registry()[rk];
+  for (int64_t i : idx)
+    if (std::find(v.begin(), v.end(), (int)i) == v.end()) v.push_back((int)i);
+}
+
+// The tuned choices so far: (ta, tb, m, n, k, epi, has_C, solution index, ms per call, candidates
+// timed, winner from the registered table, kernel name).
+std::vector<pybind11::tuple> lt_choices() {
+  std::lock_guard<std::mutex> lock(cache_mu());
+  std::vector<pybind11::tuple> out;
+  for (auto& kv : algo_cache()) {
+    const Key& k = kv.first;
+    Algo a = kv.second;
+    const int dev = std::get<0>(k);
+    std::string name = hipblaslt_ext::getKernelNameFromAlgo(ctx_for(dev).handle, a.algo);
+    out.push_back(pybind11::make_tuple(std::get<5>(k) == (int)HIPBLAS_OP_T, std::get<6>(k) == (int)HIPBLAS_OP_T,
+                                       std::get<2>(k), std::get<3>(k), std::get<4>(k), std::get<1>(k), std::get<9>(k),
+                                       a.index, a.ms, a.candidates, a.registered, name));
+  }
+  return out;
+}
+
 void register_gemm_lt(pybind11::module& m) {
+  m.def("lt_register", &lt_register);
+  m.def("lt_choices", &lt_choices);
   m.def("lt_algo_count", &lt_algo_count);
   m.def("linear_lt", &linear_lt);
   m.def("gemm_lt", &gemm_lt, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("trans_a") = false,

@@ -35,6 +35,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import lt_tune
+
 FUSE_WGRAD = os.environ.get("DSA_FUSE_WGRAD", "1") != "0"
 WGRAD_NT = os.environ.get("DSA_WGRAD_NT", "1") != "0"
 # smallest out*in weight that takes the transposed path (the transposes move ~4*M*(out+in)
@@ -65,6 +67,7 @@ LINEAR_LT = os.environ.get("DSA_LINEAR_LT", "0") == "1"
 
 _count = [0]  # in-place accumulations performed (tests / diagnostics)
 _nt_count = [0]  # wgrads formed from transposed operands
+_lt_nt_count = [0]  # wgrads formed by the measured NT solution on token-major operands
 
 
 def fused_wgrad_count() -> int:
@@ -148,6 +151,8 @@ def nt_wgrad_planned(M: int, out_features: int, in_features: int, elem_size: int
     transposed, so it adds no transient copy."""
     if not WGRAD_NT or out_features * in_features < WGRAD_NT_MIN_NUMEL:
         return False
+    if lt_tune.wgrad_nt(M, out_features, in_features, elem_size):
+        return False  # the measured NT GEMM reads the token-major operands directly
     if (WGRAD_SPLIT > 1 and M >= WGRAD_SPLIT_MIN_TOKENS and M % WGRAD_SPLIT == 0
             and -(-out_features // 256) * -(-in_features // 256) <= WGRAD_SPLIT_MAX_TILES):
         return False  # split-K path (_split_k)
@@ -295,6 +300,9 @@ def end_backward_pass():
 
 def input_grad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """dx = g2 @ W for g2 = dy [M, out], W [out, in]."""
+    if lt_tune.DGRAD and _lt_ok(g2, weight) and lt_tune.use_dgrad(g2.size(0), weight.size(0), weight.size(1)):
+        # a measured NN solution runs at the TN rate: no weight transpose (ops/lt_tune.py)
+        return _lt_ops().gemm_lt(g2, weight)
     if (DGRAD_NT and g2.is_cuda and g2.dtype == weight.dtype and weight.numel() >= DGRAD_NT_MIN_NUMEL
             and g2.size(0) >= 1024):
         from . import native
@@ -327,6 +335,17 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
             _count[0] += 1
             return None, None
         return _wgrad_split(g2, x2, split), (native.colsum(g2) if has_b else None)
+    if (gw is not None and lt_tune.WGRAD and _lt_ok(g2, x2, gw) and (not has_b or _lt_ok(bias.grad))
+            and lt_tune.wgrad_nt(g2.size(0), g2.size(1), x2.size(1), g2.element_size())):
+        # one NT GEMM on the token-major operands, accumulated into the bound gradient: cheaper
+        # than transposing both operands for this shape by the measured rates (ops/lt_tune.py)
+        _lt_ops().gemm_lt(g2, x2, trans_a=True, out=gw, accumulate=True)
+        if has_b:
+            from . import native
+            native.colsum(g2, bias.grad, accumulate=True)
+        _count[0] += 1
+        _lt_nt_count[0] += 1
+        return None, None
     if gw is not None and gw.is_contiguous():
         nt = _nt_operands(g2, x2, bias.grad if has_b else None, offer_gt)
         if nt is not None:
@@ -350,8 +369,26 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     return dw, db
 
 
+def _lt_ops():
+    """The HIP extension with the measured hipBLASLt solutions registered (ops/lt_tune.py)."""
+    from . import lt_tune, native
+    ops = native.hip_ops()
+    lt_tune.register(ops)
+    return ops
+
+
+def _lt_ok(*ts) -> bool:
+    return all(t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() for t in ts)
+
+
 def forward_gemm(x, weight, bias=None):
-    """y = x W^T + b; on the GPU through the autotuned hipBLASLt wrapper."""
+    """y = x W^T + b; through the hipBLASLt wrapper when the measured-solution table covers the
+    problem (ops/lt_tune.py), else torch's F.linear."""
+    if lt_tune.FWD and x.dim() >= 2 and _lt_ok(x, weight) and (bias is None or _lt_ok(bias)):
+        M = x.numel() // x.shape[-1]
+        if M > 0 and lt_tune.use_fwd(M, weight.shape[0], weight.shape[1], bias is not None):
+            y = _lt_ops().linear_lt(x.view(M, x.shape[-1]), weight, bias, None, False, None)
+            return y.view(*x.shape[:-1], weight.shape[0])
     if (LINEAR_LT and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and weight.dtype == x.dtype
             and weight.is_contiguous() and x.is_contiguous() and x.numel() > 0
             and (bias is None or (bias.dtype == x.dtype and bias.is_contiguous()))):

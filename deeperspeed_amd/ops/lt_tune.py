@@ -1,0 +1,140 @@
+"""Measured hipBLASLt solutions for the transformer GEMMs, and the layout choices they imply.
+
+hipBLASLt's heuristic returns a handful of algorithms per problem; on gfx950 the fastest kernel
+for the GPT-NeoX shapes is often not among them.  `scripts/lt_sweep.cpp` times EVERY solution
+`hipblaslt_ext::getAllAlgos` lists for the problems of a linear layer (forward with bias, input
+gradient untransposed "NN", weight gradient token-major "NT", and both gradients after operand
+transposes "TN") and `scripts/make_lt_table.py` keeps the fastest few per problem in
+`ops/lt_table.json` (source data: `profiles/r4i_lt_sweep*.jsonl`).
+
+At run time (`ops/csrc/gemm_lt.cpp`):
+- the table's solution indices join the heuristic candidates that the wrapper times on the first
+  call of each problem (a stale index is checked with matmulIsAlgoSupported and can only lose);
+- `ops/linear.py` routes a linear's forward, input gradient and weight gradient through the
+  wrapper for the problems the table covers, and picks per shape between the untransposed
+  weight gradient (NT) and the transposed-operand one (TN + two HIP transposes) from the measured
+  rates plus the transposes' HBM traffic.
+
+Reference counterpart: the reference calls cuBLAS with the default heuristic
+(`csrc/includes/cublas_wrappers.h`, `cublasGemmEx(..., CUBLAS_GEMM_DEFAULT_TENSOR_OP)`); the
+per-shape algorithm choice is an MI355X addition.
+
+DSA_LT=0 disables every route (torch / heuristic paths as before); DSA_LT_FWD, DSA_LT_DGRAD and
+DSA_LT_WGRAD=0 disable one route each; DSA_LT_TABLE names another table file.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import threading
+from typing import Dict, Optional, Tuple
+
+ENABLED = os.environ.get("DSA_LT", "1") != "0"
+FWD = ENABLED and os.environ.get("DSA_LT_FWD", "1") != "0"
+DGRAD = ENABLED and os.environ.get("DSA_LT_DGRAD", "1") != "0"
+WGRAD = ENABLED and os.environ.get("DSA_LT_WGRAD", "1") != "0"
+TABLE_PATH = os.environ.get("DSA_LT_TABLE", os.path.join(os.path.dirname(__file__), "lt_table.json"))
+# effective HBM rate of the HIP transpose kernel (read + write), bytes/s: profiles/aux transposes
+# stream at 4-4.5 TB/s on MI355X
+TRANSPOSE_BPS = 4.2e12
+
+EPI_DEFAULT, EPI_BIAS = 1, 4
+
+Key = Tuple[int, int, int, int, int, int, int]  # column-major (ta, tb, m, n, k, epilogue, beta)
+
+_lock = threading.Lock()
+_table: Optional[Dict[Key, dict]] = None
+_registered = False
+
+
+def key(kind: str, M: int, N: int, K: int, bias: bool = False) -> Key:
+    """Column-major hipBLASLt problem of a row-major linear over M tokens, N outputs, K inputs:
+    fwd    Y[M,N]   = X[M,K] W[N,K]^T (+ b)
+    dgrad  dX[M,K]  = dY[M,N] W[N,K]
+    wgrad  dW[N,K] += dY[M,N]^T X[M,K]          (token-major operands)
+    wgradT dW[N,K] += dYt[N,M] Xt[K,M]^T        (operands transposed first)"""
+    if kind == "fwd":
+        return (1, 0, N, M, K, EPI_BIAS if bias else EPI_DEFAULT, 0)
+    if kind == "dgrad":
+        return (0, 0, K, M, N, EPI_DEFAULT, 0)
+    if kind == "wgrad":
+        return (0, 1, K, N, M, EPI_DEFAULT, 1)
+    if kind == "wgradT":
+        return (1, 0, K, N, M, EPI_DEFAULT, 1)
+    raise ValueError(kind)
+
+
+def load_table(path: Optional[str] = None) -> Dict[Key, dict]:
+    """{column-major key: {"idx": [solution indices], "tflops": best measured, ...}}."""
+    global _table
+    if path is None and _table is not None:
+        return _table
+    p = path or TABLE_PATH
+    out: Dict[Key, dict] = {}
+    if os.path.exists(p):
+        with open(p) as f:
+            data = json.load(f)
+        for e in data.get("entries", []):
+            c = e["col"]
+            k = (int(c["ta"]), int(c["tb"]), int(c["m"]), int(c["n"]), int(c["k"]), int(c["epi"]), int(c["beta"]))
+            out[k] = e
+    if path is None:
+        _table = out
+    return out
+
+
+def register(hip_ops) -> int:
+    """Hand every table entry's solution indices to the wrapper (once per process)."""
+    global _registered
+    with _lock:
+        if _registered:
+            return 0
+        _registered = True
+        n = 0
+        for (ta, tb, m, n_, k, epi, beta), e in load_table().items():
+            hip_ops.lt_register(bool(ta), bool(tb), m, n_, k, epi, bool(beta), True, [int(i) for i in e["idx"]])
+            n += 1
+        return n
+
+
+def entry(kind: str, M: int, N: int, K: int, bias: bool = False) -> Optional[dict]:
+    if not ENABLED:
+        return None
+    return load_table().get(key(kind, M, N, K, bias))
+
+
+def use_fwd(M: int, N: int, K: int, bias: bool) -> bool:
+    return FWD and entry("fwd", M, N, K, bias) is not None
+
+
+def use_dgrad(M: int, N: int, K: int) -> bool:
+    return DGRAD and entry("dgrad", M, N, K) is not None
+
+
+_nt_cache: Dict[Tuple[int, int, int, int], bool] = {}
+
+
+def wgrad_nt(M: int, N: int, K: int, elem_size: int = 2) -> bool:
+    """True when the weight gradient of an [N, K] linear over M tokens is cheaper as one NT GEMM
+    on the token-major operands than as transposes of both operands plus the TN GEMM, by the
+    table's measured rates."""
+    if not WGRAD:
+        return False
+    ck = (M, N, K, elem_size)
+    r = _nt_cache.get(ck)
+    if r is None:
+        nt, tn = entry("wgrad", M, N, K), entry("wgradT", M, N, K)
+        if nt is None:
+            r = False
+        else:
+            flops = 2.0 * M * N * K
+            cost_nt = flops / (nt["tflops"] * 1e12)
+            if tn is None:
+                r = True  # no TN record: the NT kernel was measured, the transposes were not needed
+            else:
+                t_bytes = 2.0 * elem_size * M * (N + K)  # read + write of dY and X
+                cost_tn = flops / (tn["tflops"] * 1e12) + t_bytes / TRANSPOSE_BPS
+                r = cost_nt < cost_tn
+        _nt_cache[ck] = r
+    return r

@@ -87,7 +87,7 @@ static int sweep(hipblasLtHandle_t h, const std::string& spec, void* ws, size_t 
   }
   std::string lay = lbuf;
   const int64_t M = M_, N = N_, K = K_;
-  const int top = 4;
+  const int top = 6;
   const bool bias = lay == "fwdb";
   if (bias) lay = "fwd";
   // column-major problem D[m,n] = op(A)[m,k] op(B)[k,n]
@@ -192,9 +192,11 @@ static int sweep(hipblasLtHandle_t h, const std::string& spec, void* ws, size_t 
   for (auto& r : res)
     if (r.idx == heur_idx) heur_ms = r.ms;
   printf("{\"layout\": \"%s%s\", \"M\": %ld, \"N\": %ld, \"K\": %ld, \"algos\": %zu, \"supported\": %d, "
-         "\"heuristic_idx\": %d, \"heuristic_tflops\": %.1f, \"top\": [",
+         "\"heuristic_idx\": %d, \"heuristic_tflops\": %.1f, "
+         "\"col\": {\"ta\": %d, \"tb\": %d, \"m\": %ld, \"n\": %ld, \"k\": %ld, \"epi\": %d, \"beta\": %d}, \"top\": [",
          lay.c_str(), bias ? "+bias" : "", (long)M, (long)N, (long)K, all.size(), tried, heur_idx,
-         heur_ms > 0 ? flops / heur_ms / 1e9 : -1.0);
+         heur_ms > 0 ? flops / heur_ms / 1e9 : -1.0, ta == HIPBLAS_OP_T, tb == HIPBLAS_OP_T, (long)m, (long)n, (long)k,
+         bias ? (int)HIPBLASLT_EPILOGUE_BIAS : (int)HIPBLASLT_EPILOGUE_DEFAULT, beta != 0.f);
   for (int i = 0; i < top && i < (int)res.size(); ++i)
     printf("%s{\"idx\": %d, \"tflops\": %.1f, \"kernel\": \"%s\"}", i ? ", " : "", res[i].idx,
            flops / res[i].ms / 1e9, res[i].name.substr(0, 120).c_str());

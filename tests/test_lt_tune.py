@@ -1,0 +1,70 @@
+"""CPU checks of the measured-solution table logic (ops/lt_tune.py, scripts/make_lt_table.py)."""
+
+import json
+import os
+import sys
+
+from deeperspeed_amd.ops import lt_tune
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_keys_are_the_column_major_problems():
+    # Y[M,N] = X W^T  ->  Y^T[N,M] = W(T) X(N)
+    assert lt_tune.key("fwd", 8192, 18432, 6144, bias=True) == (1, 0, 18432, 8192, 6144, 4, 0)
+    # dX[M,K] = dY W  ->  dX^T[K,M] = W(N) dY(N)
+    assert lt_tune.key("dgrad", 8192, 18432, 6144) == (0, 0, 6144, 8192, 18432, 1, 0)
+    # dW[N,K] += dY^T X  ->  dW^T[K,N] = X(N) dY(T), accumulating
+    assert lt_tune.key("wgrad", 8192, 18432, 6144) == (0, 1, 6144, 18432, 8192, 1, 1)
+    assert lt_tune.key("wgradT", 8192, 18432, 6144) == (1, 0, 6144, 18432, 8192, 1, 1)
+
+
+def test_make_table_matches_runtime_keys(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    try:
+        import make_lt_table
+    finally:
+        sys.path.pop(0)
+    for layout, kind, bias in (("fwd+bias", "fwd", True), ("fwd", "fwd", False), ("dgrad", "dgrad", False),
+                               ("wgrad", "wgrad", False), ("wgradT", "wgradT", False)):
+        c = make_lt_table.col_of(layout, 8192, 24576, 6144)
+        assert (c["ta"], c["tb"], c["m"], c["n"], c["k"], c["epi"], c["beta"]) == \
+            lt_tune.key(kind, 8192, 24576, 6144, bias)
+
+
+def _table(tmp_path, rows):
+    p = tmp_path / "t.json"
+    ents = []
+    for kind, M, N, K, tf in rows:
+        k = lt_tune.key(kind, M, N, K)
+        ents.append({"col": dict(zip(("ta", "tb", "m", "n", "k", "epi", "beta"), k)), "idx": [1], "tflops": tf})
+    p.write_text(json.dumps({"entries": ents}))
+    return str(p)
+
+
+def test_nt_choice_counts_transpose_traffic(tmp_path, monkeypatch):
+    M, N, K = 8192, 6144, 6144
+    # NT 10 % slower than TN: the GEMM costs 0.04 ms more, the two transposes ~0.048 ms -> NT
+    path = _table(tmp_path, [("wgrad", M, N, K, 1400.0), ("wgradT", M, N, K, 1540.0)])
+    monkeypatch.setattr(lt_tune, "_table", lt_tune.load_table(path))
+    monkeypatch.setattr(lt_tune, "WGRAD", True)
+    monkeypatch.setattr(lt_tune, "ENABLED", True)
+    lt_tune._nt_cache.clear()
+    assert lt_tune.wgrad_nt(M, N, K)
+    # NT 25 % slower: the transposes are cheaper -> TN
+    path = _table(tmp_path, [("wgrad", M, N, K, 1200.0), ("wgradT", M, N, K, 1600.0)])
+    monkeypatch.setattr(lt_tune, "_table", lt_tune.load_table(path))
+    lt_tune._nt_cache.clear()
+    assert not lt_tune.wgrad_nt(M, N, K)
+    # no NT record -> never NT; switch off -> never NT
+    monkeypatch.setattr(lt_tune, "_table", {})
+    lt_tune._nt_cache.clear()
+    assert not lt_tune.wgrad_nt(M, N, K)
+    lt_tune._nt_cache.clear()
+
+
+def test_shipped_table_parses():
+    t = lt_tune.load_table(lt_tune.TABLE_PATH)
+    assert t, "ops/lt_table.json missing or empty"
+    for k, e in t.items():
+        assert len(k) == 7 and e["idx"] and e["tflops"] > 0
