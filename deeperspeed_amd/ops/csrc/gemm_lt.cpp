@@ -30,6 +30,8 @@
 #include <hipblaslt/hipblaslt.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <mutex>
@@ -110,6 +112,13 @@ std::map<RegKey, std::vector<int>>& registry() {
   static std::map<RegKey, std::vector<int>> r;
   return r;
 }
+bool lt_debug() {
+  static const bool on = [] {
+    const char* e = getenv("DSA_LT_DEBUG");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 std::mutex& cache_mu() {
   static std::mutex mu;
   return mu;
@@ -160,12 +169,19 @@ void run(const Gemm& g, int device, hipStream_t stream) {
     if (reg != registry().end() && !reg->second.empty()) {
       std::vector<int> idx = reg->second;
       std::vector<hipblasLtMatmulHeuristicResult_t> extra;
-      if (hipblaslt_ext::getAlgosFromIndex(c.handle, idx, extra) == HIPBLAS_STATUS_SUCCESS) {
+      const hipblasStatus_t gs = hipblaslt_ext::getAlgosFromIndex(c.handle, idx, extra);
+      if (lt_debug())
+        fprintf(stderr, "[gemm_lt] m=%ld n=%ld k=%ld: %zu registered, getAlgosFromIndex status %d -> %zu\n",
+                (long)g.m, (long)g.n, (long)g.k, idx.size(), (int)gs, extra.size());
+      if (gs == HIPBLAS_STATUS_SUCCESS) {
         for (auto& r : extra) {
           size_t need = 0;
-          if (hipblaslt_ext::matmulIsAlgoSupported(c.handle, op, &alpha, la, lb, &beta, ld, ld, r.algo, need) !=
-                  HIPBLAS_STATUS_SUCCESS || need > kWorkspace)
-            continue;
+          const hipblasStatus_t ss =
+              hipblaslt_ext::matmulIsAlgoSupported(c.handle, op, &alpha, la, lb, &beta, ld, ld, r.algo, need);
+          if (lt_debug())
+            fprintf(stderr, "[gemm_lt]   index %d supported %d ws %zu\n", hipblaslt_ext::getIndexFromAlgo(r.algo),
+                    (int)ss, need);
+          if (ss != HIPBLAS_STATUS_SUCCESS || need > kWorkspace) continue;
           r.workspaceSize = need;
           r.state = HIPBLAS_STATUS_SUCCESS;
           res.push_back(r);
@@ -204,6 +220,10 @@ void run(const Gemm& g, int device, hipStream_t stream) {
         hipEventSynchronize(e1);
         float ms = 0.f;
         hipEventElapsedTime(&ms, e0, e1);
+        if (lt_debug())
+          fprintf(stderr, "[gemm_lt]   candidate %d (index %d, %s) %.3f ms\n", i,
+                  hipblaslt_ext::getIndexFromAlgo(res[i].algo), from_table[i] ? "table" : "heuristic",
+                  ms / kTimedReps);
         if (ms < best_ms) {
           best_ms = ms;
           best = i;
