@@ -19,7 +19,8 @@ Reference counterpart: the reference calls cuBLAS with the default heuristic
 (`csrc/includes/cublas_wrappers.h`, `cublasGemmEx(..., CUBLAS_GEMM_DEFAULT_TENSOR_OP)`); the
 per-shape algorithm choice is an MI355X addition.
 
-DSA_LT=0 disables every route (torch / heuristic paths as before); DSA_LT_FWD, DSA_LT_DGRAD and
+DSA_LT=1 enables the routes (default off until they win in the step: profiles/r4j_notes.md);
+DSA_LT_FWD, DSA_LT_DGRAD and
 DSA_LT_WGRAD=0 disable one route each; DSA_LT_TABLE names another table file.
 """
 
@@ -30,7 +31,7 @@ import os
 import threading
 from typing import Dict, Optional, Tuple
 
-ENABLED = os.environ.get("DSA_LT", "1") != "0"
+ENABLED = os.environ.get("DSA_LT", "0") == "1"  # default off until the in-step A/B wins
 FWD = ENABLED and os.environ.get("DSA_LT_FWD", "1") != "0"
 DGRAD = ENABLED and os.environ.get("DSA_LT_DGRAD", "1") != "0"
 WGRAD = ENABLED and os.environ.get("DSA_LT_WGRAD", "1") != "0"

@@ -34,9 +34,9 @@ def data():
 
 def test_table_covers_the_tested_shape():
     from deeperspeed_amd.ops import lt_tune
-    assert lt_tune.entry("fwd", M, N, K, bias=True) is not None
-    assert lt_tune.entry("dgrad", M, N, K) is not None
-    assert lt_tune.entry("wgrad", M, N, K) is not None
+    t = lt_tune.load_table()
+    for kind, bias in (("fwd", True), ("dgrad", False), ("wgrad", False)):
+        assert lt_tune.key(kind, M, N, K, bias) in t, kind
 
 
 def test_forward_with_bias(data):
@@ -75,6 +75,7 @@ def test_choices_recorded_and_table_candidates_timed(data):
 def test_linear_layer_routes_match_reference(data, monkeypatch):
     """ops.linear forward + backward (bound weight / bias gradients) through the routes."""
     from deeperspeed_amd.ops import linear, lt_tune
+    monkeypatch.setattr(lt_tune, "ENABLED", True)
     monkeypatch.setattr(lt_tune, "FWD", True)
     monkeypatch.setattr(lt_tune, "DGRAD", True)
     monkeypatch.setattr(lt_tune, "WGRAD", True)
