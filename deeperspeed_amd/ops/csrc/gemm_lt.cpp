@@ -19,9 +19,9 @@
 // hipblaslt_ext::getAllAlgos) found CMS-variant 256x256 kernels 3-13 % faster for the forward
 // and the untransposed input-gradient (NN) layouts, and NT weight-gradient kernels that make the
 // operand transposes unnecessary for some shapes (profiles/r4i_lt_sweep.jsonl).  Those solution
-// indices ship in ops/lt_table.json; lt_register() adds them to the candidates timed on the
-// first call of that problem, so a stale or foreign index can only lose the timing, never be
-// used unverified (each one is checked with matmulIsAlgoSupported first).
+// NAMES ship in ops/lt_table.json (indices are not stable across processes); lt_register() adds
+// them to the candidates timed on the first call of that problem, so a stale or foreign name can
+// only lose the timing, never be used unverified (each is checked with matmulIsAlgoSupported).
 #include <pybind11/stl.h>
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
@@ -36,6 +36,7 @@
 #include <string>
 #include <mutex>
 #include <tuple>
+#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -48,7 +49,7 @@ namespace {
 
 constexpr size_t kWorkspace = 64ull << 20;
 constexpr int kCandidates = 16;  // heuristic algorithms timed once per GEMM shape
-constexpr int kTimedReps = 5;    // launches timed per candidate (after one warm-up launch)
+constexpr int kTimedReps = 8;    // launches per finalist in the second timing pass
 
 struct Ctx {
   hipblasLtHandle_t handle = nullptr;
@@ -108,9 +109,32 @@ std::map<Key, Algo>& algo_cache() {
 
 // (ta, tb, m, n, k, epi, has_C, ab_type, d_type) -> solution indices from the offline sweep
 using RegKey = std::tuple<int, int, int64_t, int64_t, int64_t, int, bool, int, int>;
-std::map<RegKey, std::vector<int>>& registry() {
-  static std::map<RegKey, std::vector<int>> r;
+std::map<RegKey, std::vector<std::string>>& registry() {
+  static std::map<RegKey, std::vector<std::string>> r;
   return r;
+}
+
+// Every solution hipBLASLt has for one (transA, transB, operand type, output type), indexed by
+// solution name; listed once per process, the first time a registered problem of that layout is
+// tuned.
+struct LayoutAlgos {
+  std::vector<hipblasLtMatmulHeuristicResult_t> algos;
+  std::unordered_map<std::string, std::vector<int>> by_name;
+};
+
+const LayoutAlgos& layout_algos(hipblasLtHandle_t h, hipblasOperation_t ta, hipblasOperation_t tb, hipDataType ab,
+                                hipDataType d) {
+  static std::map<std::tuple<int, int, int, int>, LayoutAlgos> cache;
+  auto key = std::make_tuple((int)ta, (int)tb, (int)ab, (int)d);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  LayoutAlgos& la = cache[key];
+  if (hipblaslt_ext::getAllAlgos(h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, ta, tb, ab, ab, d, d, HIPBLAS_COMPUTE_32F,
+                                 la.algos) != HIPBLAS_STATUS_SUCCESS)
+    la.algos.clear();
+  for (size_t i = 0; i < la.algos.size(); ++i)
+    la.by_name[hipblaslt_ext::getSolutionNameFromAlgo(h, la.algos[i].algo)].push_back((int)i);
+  return la;
 }
 bool lt_debug() {
   static const bool on = [] {
@@ -167,32 +191,37 @@ void run(const Gemm& g, int device, hipStream_t stream) {
     const RegKey rk{(int)g.ta, (int)g.tb, g.m, g.n, g.k, (int)g.epi, g.C != nullptr, (int)g.ab_type, (int)g.d_type};
     auto reg = registry().find(rk);
     if (reg != registry().end() && !reg->second.empty()) {
-      std::vector<int> idx = reg->second;
-      std::vector<hipblasLtMatmulHeuristicResult_t> extra;
-      const hipblasStatus_t gs = hipblaslt_ext::getAlgosFromIndex(c.handle, idx, extra);
-      if (lt_debug())
-        fprintf(stderr, "[gemm_lt] m=%ld n=%ld k=%ld: %zu registered, getAlgosFromIndex status %d -> %zu\n",
-                (long)g.m, (long)g.n, (long)g.k, idx.size(), (int)gs, extra.size());
-      if (gs == HIPBLAS_STATUS_SUCCESS) {
-        for (auto& r : extra) {
+      // registered solutions are identified by NAME: hipBLASLt's solution indices depend on the
+      // order in which a process loads its solution libraries, names do not
+      const LayoutAlgos& la_all = layout_algos(c.handle, g.ta, g.tb, g.ab_type, g.d_type);
+      int found = 0, supported = 0;
+      for (const std::string& name : reg->second) {
+        auto hit = la_all.by_name.find(name);
+        if (hit == la_all.by_name.end()) continue;
+        for (int pos : hit->second) {
+          ++found;
+          hipblasLtMatmulHeuristicResult_t r = la_all.algos[pos];
           size_t need = 0;
-          const hipblasStatus_t ss =
-              hipblaslt_ext::matmulIsAlgoSupported(c.handle, op, &alpha, la, lb, &beta, ld, ld, r.algo, need);
-          if (lt_debug())
-            fprintf(stderr, "[gemm_lt]   index %d supported %d ws %zu\n", hipblaslt_ext::getIndexFromAlgo(r.algo),
-                    (int)ss, need);
-          if (ss != HIPBLAS_STATUS_SUCCESS || need > kWorkspace) continue;
+          if (hipblaslt_ext::matmulIsAlgoSupported(c.handle, op, &alpha, la, lb, &beta, ld, ld, r.algo, need) !=
+                  HIPBLAS_STATUS_SUCCESS || need > kWorkspace)
+            continue;
+          ++supported;
           r.workspaceSize = need;
           r.state = HIPBLAS_STATUS_SUCCESS;
           res.push_back(r);
           from_table.push_back(1);
         }
       }
+      if (lt_debug())
+        fprintf(stderr, "[gemm_lt] m=%ld n=%ld k=%ld: %zu registered names, %d solutions found, %d supported\n",
+                (long)g.m, (long)g.n, (long)g.k, reg->second.size(), found, supported);
     }
     const int nres = (int)res.size();
     TORCH_CHECK(nres > 0, "gemm_lt: hipBLASLt has no algorithm for this GEMM / epilogue");
-    // time the candidates once (each 3 launches after one warm-up); the output buffers are
-    // scratch until the real launch below overwrites them
+    // Two timing passes (the output buffers are scratch until the real launch below overwrites
+    // them): every candidate 2 launches after a warm-up, then the best 4 again over kTimedReps
+    // launches each; the GPU is first kept busy for ~20 launches so no candidate is timed at a
+    // lower clock than the rest.
     int best = 0;
     float best_ms = 1e30f;
     if (nres > 1) {
@@ -207,23 +236,37 @@ void run(const Gemm& g, int device, hipStream_t stream) {
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
       hipEventCreate(&e1);
-      for (int i = 0; i < nres; ++i) {
-        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
-        if (hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, sc ? sc : sd, ld, sd, ld, &res[i].algo,
-                            c.workspace.data_ptr(), kWorkspace, stream) != HIPBLAS_STATUS_SUCCESS)
-          continue;
+      auto launch = [&](int i) {
+        return hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, sc ? sc : sd, ld, sd, ld, &res[i].algo,
+                               c.workspace.data_ptr(), kWorkspace, stream) == HIPBLAS_STATUS_SUCCESS;
+      };
+      auto time = [&](int i, int reps) -> float {
         hipEventRecord(e0, stream);
-        for (int r = 0; r < kTimedReps; ++r)
-          hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, sc ? sc : sd, ld, sd, ld, &res[i].algo,
-                          c.workspace.data_ptr(), kWorkspace, stream);
+        for (int r = 0; r < reps; ++r) launch(i);
         hipEventRecord(e1, stream);
         hipEventSynchronize(e1);
         float ms = 0.f;
         hipEventElapsedTime(&ms, e0, e1);
+        return ms / reps;
+      };
+      std::vector<std::pair<float, int>> t1;
+      bool warmed = false;
+      for (int i = 0; i < nres; ++i) {
+        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > kWorkspace) continue;
+        if (!launch(i)) continue;
+        if (!warmed) {
+          for (int r = 0; r < 20; ++r) launch(i);
+          warmed = true;
+        }
+        t1.push_back({time(i, 2), i});
+      }
+      std::sort(t1.begin(), t1.end());
+      for (size_t j = 0; j < t1.size() && j < 4; ++j) {
+        const int i = t1[j].second;
+        const float ms = time(i, kTimedReps);
         if (lt_debug())
-          fprintf(stderr, "[gemm_lt]   candidate %d (index %d, %s) %.3f ms\n", i,
-                  hipblaslt_ext::getIndexFromAlgo(res[i].algo), from_table[i] ? "table" : "heuristic",
-                  ms / kTimedReps);
+          fprintf(stderr, "[gemm_lt]   finalist %d (%s) %.3f ms (first pass %.3f)\n", i,
+                  from_table[i] ? "table" : "heuristic", ms, t1[j].first);
         if (ms < best_ms) {
           best_ms = ms;
           best = i;
@@ -233,7 +276,7 @@ void run(const Gemm& g, int device, hipStream_t stream) {
       hipEventDestroy(e1);
     }
     it = cache.emplace(key, Algo{res[best].algo, res[best].workspaceSize, hipblaslt_ext::getIndexFromAlgo(res[best].algo),
-                                 nres > 1 ? best_ms / kTimedReps : -1.f, nres, from_table[best] != 0}).first;
+                                 nres > 1 ? best_ms : -1.f, nres, from_table[best] != 0}).first;
   }
   LT_CHECK(hipblasLtMatmul(c.handle, op, &alpha, g.A, la, g.B, lb, &beta, g.C ? g.C : g.D, ld, g.D, ld,
                            &it->second.algo, c.workspace.data_ptr(), kWorkspace, stream));
@@ -380,15 +423,16 @@ int64_t lt_algo_count(int64_t m, int64_t n, int64_t k, int64_t epi, bool with_au
   return st == HIPBLAS_STATUS_SUCCESS ? nres : -(int64_t)st;
 }
 
-// Candidate solution indices for one column-major problem (bf16 operands; d_bf16 false -> fp32 D).
+// Candidate solutions (by hipBLASLt solution name) for one column-major problem (bf16 operands;
+// d_bf16 false -> fp32 D).
 void lt_register(bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t epi, bool beta, bool d_bf16,
-                 std::vector<int64_t> idx) {
+                 std::vector<std::string> names) {
   std::lock_guard<std::mutex> lock(cache_mu());
   const RegKey rk{(int)(ta ? HIPBLAS_OP_T : HIPBLAS_OP_N), (int)(tb ? HIPBLAS_OP_T : HIPBLAS_OP_N), m, n, k, (int)epi,
                   beta, (int)HIP_R_16BF, (int)(d_bf16 ? HIP_R_16BF : HIP_R_32F)};
   auto& v = registry()[rk];
-  for (int64_t i : idx)
-    if (std::find(v.begin(), v.end(), (int)i) == v.end()) v.push_back((int)i);
+  for (auto& nm : names)
+    if (std::find(v.begin(), v.end(), nm) == v.end()) v.push_back(nm);
 }
 
 // The tuned choices so far: (ta, tb, m, n, k, epi, has_C, solution index, ms per call, candidates

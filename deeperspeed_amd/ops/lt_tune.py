@@ -8,8 +8,9 @@ transposes "TN") and `scripts/make_lt_table.py` keeps the fastest few per proble
 `ops/lt_table.json` (source data: `profiles/r4i_lt_sweep*.jsonl`).
 
 At run time (`ops/csrc/gemm_lt.cpp`):
-- the table's solution indices join the heuristic candidates that the wrapper times on the first
-  call of each problem (a stale index is checked with matmulIsAlgoSupported and can only lose);
+- the table's solutions (by hipBLASLt solution name; indices differ between processes) join the
+  heuristic candidates that the wrapper times on the first call of each problem (a stale name is
+  checked with matmulIsAlgoSupported and can only lose the timing);
 - `ops/linear.py` routes a linear's forward, input gradient and weight gradient through the
   wrapper for the problems the table covers, and picks per shape between the untransposed
   weight gradient (NT) and the transposed-operand one (TN + two HIP transposes) from the measured
@@ -67,7 +68,7 @@ def key(kind: str, M: int, N: int, K: int, bias: bool = False) -> Key:
 
 
 def load_table(path: Optional[str] = None) -> Dict[Key, dict]:
-    """{column-major key: {"idx": [solution indices], "tflops": best measured, ...}}."""
+    """{column-major key: {"names": [solution names], "tflops": best measured, ...}}."""
     global _table
     if path is None and _table is not None:
         return _table
@@ -94,8 +95,9 @@ def register(hip_ops) -> int:
         _registered = True
         n = 0
         for (ta, tb, m, n_, k, epi, beta), e in load_table().items():
-            hip_ops.lt_register(bool(ta), bool(tb), m, n_, k, epi, bool(beta), True, [int(i) for i in e["idx"]])
-            n += 1
+            if e.get("names"):
+                hip_ops.lt_register(bool(ta), bool(tb), m, n_, k, epi, bool(beta), True, list(e["names"]))
+                n += 1
         return n
 
 

@@ -160,6 +160,7 @@ static int sweep(hipblasLtHandle_t h, const std::string& spec, void* ws, size_t 
     float ms;
     int idx;
     std::string name;
+    std::string sol;
   };
   std::vector<R> res;
   const double flops = 2.0 * M * N * K;
@@ -185,7 +186,8 @@ static int sweep(hipblasLtHandle_t h, const std::string& spec, void* ws, size_t 
     hipEventSynchronize(e1);
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
-    res.push_back({ms / reps, hipblaslt_ext::getIndexFromAlgo(r.algo), hipblaslt_ext::getKernelNameFromAlgo(h, r.algo)});
+    res.push_back({ms / reps, hipblaslt_ext::getIndexFromAlgo(r.algo), hipblaslt_ext::getKernelNameFromAlgo(h, r.algo),
+                   hipblaslt_ext::getSolutionNameFromAlgo(h, r.algo)});
   }
   std::sort(res.begin(), res.end(), [](const R& a, const R& b) { return a.ms < b.ms; });
   float heur_ms = -1;
@@ -198,8 +200,8 @@ static int sweep(hipblasLtHandle_t h, const std::string& spec, void* ws, size_t 
          heur_ms > 0 ? flops / heur_ms / 1e9 : -1.0, ta == HIPBLAS_OP_T, tb == HIPBLAS_OP_T, (long)m, (long)n, (long)k,
          bias ? (int)HIPBLASLT_EPILOGUE_BIAS : (int)HIPBLASLT_EPILOGUE_DEFAULT, beta != 0.f);
   for (int i = 0; i < top && i < (int)res.size(); ++i)
-    printf("%s{\"idx\": %d, \"tflops\": %.1f, \"kernel\": \"%s\"}", i ? ", " : "", res[i].idx,
-           flops / res[i].ms / 1e9, res[i].name.substr(0, 120).c_str());
+    printf("%s{\"idx\": %d, \"tflops\": %.1f, \"kernel\": \"%s\", \"sol\": \"%s\"}", i ? ", " : "", res[i].idx,
+           flops / res[i].ms / 1e9, res[i].name.substr(0, 120).c_str(), res[i].sol.c_str());
   printf("]}\n");
   fflush(stdout);
   hipFree(A);

@@ -2,7 +2,7 @@
 
     python scripts/make_lt_table.py profiles/r4i_lt_sweep*.jsonl
 
-Each entry keeps the column-major problem, the fastest solution indices (they join the
+Each entry keeps the column-major problem, the fastest solutions by hipBLASLt solution name (they join the
 heuristic candidates that ops/csrc/gemm_lt.cpp times on first use) and the best / heuristic
 rates measured by the sweep (ops/lt_tune.py's NT-vs-TN weight-gradient choice reads them).
 """
@@ -36,12 +36,12 @@ def main(paths):
                 c = r.get("col") or col_of(r["layout"], r["M"], r["N"], r["K"])
                 k = (c["ta"], c["tb"], c["m"], c["n"], c["k"], c["epi"], c["beta"])
                 e = {"layout": r["layout"], "M": r["M"], "N": r["N"], "K": r["K"], "col": c,
-                     "idx": [t["idx"] for t in r["top"]], "tflops": r["top"][0]["tflops"],
+                     "names": [t["sol"] for t in r["top"] if t.get("sol")], "tflops": r["top"][0]["tflops"],
                      "heuristic_tflops": r["heuristic_tflops"], "kernel": r["top"][0]["kernel"], "source": p}
                 old = entries.get(k)
                 if old is None or e["tflops"] > old["tflops"]:
                     if old is not None:
-                        e["idx"] += [i for i in old["idx"] if i not in e["idx"]]
+                        e["names"] += [n for n in old["names"] if n not in e["names"]]
                     entries[k] = e
     data = {"about": "fastest hipBLASLt solutions per GEMM problem on MI355X (gfx950), from scripts/lt_sweep.cpp; "
                      "read by deeperspeed_amd/ops/lt_tune.py",

@@ -37,7 +37,7 @@ def _table(tmp_path, rows):
     ents = []
     for kind, M, N, K, tf in rows:
         k = lt_tune.key(kind, M, N, K)
-        ents.append({"col": dict(zip(("ta", "tb", "m", "n", "k", "epi", "beta"), k)), "idx": [1], "tflops": tf})
+        ents.append({"col": dict(zip(("ta", "tb", "m", "n", "k", "epi", "beta"), k)), "names": ["s"], "tflops": tf})
     p.write_text(json.dumps({"entries": ents}))
     return str(p)
 
@@ -67,4 +67,4 @@ def test_shipped_table_parses():
     t = lt_tune.load_table(lt_tune.TABLE_PATH)
     assert t, "ops/lt_table.json missing or empty"
     for k, e in t.items():
-        assert len(k) == 7 and e["idx"] and e["tflops"] > 0
+        assert len(k) == 7 and e["names"] and e["tflops"] > 0
