@@ -29,6 +29,8 @@
 #include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -452,7 +454,136 @@ std::vector<pybind11::tuple> lt_choices() {
   return out;
 }
 
+// Exhaustive sweep of one problem with THIS process's hipBLASLt (torch bundles its own build, which
+// the extension binds to: solution sets and names differ from /opt/rocm's).  Times every solution
+// getAllAlgos lists that supports the problem (1 warm-up + 3 timed launches on random bf16
+// operands; macro tiles under 128 skipped when both output dims are >= 2048) and returns
+// (heuristic first choice ms, [(ms, solution name, kernel name), ...] fastest first).
+// kind: 0 fwd (TN), 1 dgrad (NN), 2 wgrad (NT, beta 1), 3 wgradT (TN, beta 1); row-major M, N, K.
+pybind11::tuple lt_sweep(int64_t kind, int64_t M, int64_t N, int64_t K, bool bias, int64_t top) {
+  const int device = at::cuda::current_device();
+  Ctx& c = ctx_for(device);
+  hipblasOperation_t ta, tb;
+  int64_t m, n, k, lda, ldb, ldd, ar, ac, br, bc;
+  float beta = 0.f;
+  if (kind == 0) {
+    ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N, m = N, n = M, k = K, ar = K, ac = N, lda = K, br = K, bc = M, ldb = K, ldd = N;
+  } else if (kind == 1) {
+    ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_N, m = K, n = M, k = N, ar = K, ac = N, lda = K, br = N, bc = M, ldb = N, ldd = K;
+  } else if (kind == 2) {
+    ta = HIPBLAS_OP_N, tb = HIPBLAS_OP_T, m = K, n = N, k = M, beta = 1.f;
+    ar = K, ac = M, lda = K, br = N, bc = M, ldb = N, ldd = K;
+  } else {
+    ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N, m = K, n = N, k = M, beta = 1.f;
+    ar = M, ac = K, lda = M, br = M, bc = N, ldb = M, ldd = K;
+  }
+  TORCH_CHECK(!bias || kind == 0, "lt_sweep: bias only for the forward");
+  auto opts = at::TensorOptions().dtype(at::kBFloat16).device(at::kCUDA, device);
+  at::Tensor A = at::rand({ar * ac}, opts).mul_(2).sub_(1), B = at::rand({br * bc}, opts).mul_(2).sub_(1);
+  at::Tensor D = at::rand({m * n}, opts), bv = at::rand({m}, opts);
+  hipStream_t stream = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+  hipblasLtMatmulDesc_t op;
+  LT_CHECK(hipblasLtMatmulDescCreate(&op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
+  if (bias) {
+    const hipblasLtEpilogue_t e = HIPBLASLT_EPILOGUE_BIAS;
+    const hipDataType bt = HIP_R_16BF;
+    void* bp = bv.data_ptr();
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e)));
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(void*)));
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  }
+  hipblasLtMatrixLayout_t la, lb, ld;
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, ar, ac, lda));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, br, bc, ldb));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&ld, HIP_R_16BF, m, n, ldd));
+  const float alpha = 1.f;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  auto time = [&](hipblasLtMatmulAlgo_t& algo, int reps) -> float {
+    if (hipblasLtMatmul(c.handle, op, &alpha, A.data_ptr(), la, B.data_ptr(), lb, &beta, D.data_ptr(), ld, D.data_ptr(),
+                        ld, &algo, c.workspace.data_ptr(), kWorkspace, stream) != HIPBLAS_STATUS_SUCCESS)
+      return -1.f;
+    hipEventRecord(e0, stream);
+    for (int r = 0; r < reps; ++r)
+      hipblasLtMatmul(c.handle, op, &alpha, A.data_ptr(), la, B.data_ptr(), lb, &beta, D.data_ptr(), ld, D.data_ptr(),
+                      ld, &algo, c.workspace.data_ptr(), kWorkspace, stream);
+    hipEventRecord(e1, stream);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    return ms / reps;
+  };
+  // heuristic first choice
+  hipblasLtMatmulPreference_t pref;
+  LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+  uint64_t wsz = kWorkspace;
+  LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz)));
+  hipblasLtMatmulHeuristicResult_t heur[1];
+  int nh = 0;
+  hipblasLtMatmulAlgoGetHeuristic(c.handle, op, la, lb, ld, ld, pref, 1, heur, &nh);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  for (int r = 0; r < 20 && nh > 0; ++r) time(heur[0].algo, 1);  // clocks up before any timing
+  const float heur_ms = nh > 0 ? time(heur[0].algo, 5) : -1.f;
+  std::vector<hipblasLtMatmulHeuristicResult_t> all;
+  hipblaslt_ext::getAllAlgos(c.handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, ta, tb, HIP_R_16BF, HIP_R_16BF,
+                             HIP_R_16BF, HIP_R_16BF, HIPBLAS_COMPUTE_32F, all);
+  const bool big = m >= 2048 && n >= 2048;
+  struct Cand {
+    float ms;
+    std::string sol, kname;
+    hipblasLtMatmulAlgo_t algo;
+  };
+  std::vector<Cand> res;
+  for (auto& r : all) {
+    std::string kname = hipblaslt_ext::getKernelNameFromAlgo(c.handle, r.algo);
+    if (big) {
+      const size_t p = kname.find("_MT");
+      if (p != std::string::npos) {
+        const int a = atoi(kname.c_str() + p + 3);
+        const size_t x = kname.find('x', p + 3);
+        const int b = x == std::string::npos ? 0 : atoi(kname.c_str() + x + 1);
+        if (a < 128 || b < 128) continue;
+      }
+    }
+    size_t need = 0;
+    if (hipblaslt_ext::matmulIsAlgoSupported(c.handle, op, &alpha, la, lb, &beta, ld, ld, r.algo, need) !=
+            HIPBLAS_STATUS_SUCCESS || need > kWorkspace)
+      continue;
+    const float ms = time(r.algo, 3);
+    if (ms > 0) res.push_back({ms, hipblaslt_ext::getSolutionNameFromAlgo(c.handle, r.algo), kname, r.algo});
+  }
+  auto by_ms = [](const Cand& a, const Cand& b) { return a.ms < b.ms; };
+  std::sort(res.begin(), res.end(), by_ms);
+  // re-time the leaders over more launches (the single pass is noisy)
+  const size_t nre = std::min<size_t>(res.size(), (size_t)std::max<int64_t>(top * 2, 8));
+  std::vector<Cand> lead(res.begin(), res.begin() + nre);
+  for (auto& cnd : lead) cnd.ms = time(cnd.algo, 10);
+  std::sort(lead.begin(), lead.end(), by_ms);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipblasLtMatrixLayoutDestroy(la);
+  hipblasLtMatrixLayoutDestroy(lb);
+  hipblasLtMatrixLayoutDestroy(ld);
+  hipblasLtMatmulDescDestroy(op);
+  std::vector<pybind11::tuple> out;
+  for (size_t i = 0; i < lead.size() && (int64_t)i < top; ++i)
+    out.push_back(pybind11::make_tuple(lead[i].ms, lead[i].sol, lead[i].kname));
+  return pybind11::make_tuple(heur_ms, (int64_t)all.size(), (int64_t)res.size(), out);
+}
+
+// Which hipBLASLt shared library this extension's calls bind to (diagnostics: torch bundles its own).
+std::string lt_library() {
+  Dl_info info;
+  if (dladdr(reinterpret_cast<void*>(&hipblasLtMatmul), &info) && info.dli_fname) return info.dli_fname;
+  return "";
+}
+
 void register_gemm_lt(pybind11::module& m) {
+  m.def("lt_library", &lt_library);
+  m.def("lt_sweep", &lt_sweep);
   m.def("lt_register", &lt_register);
   m.def("lt_choices", &lt_choices);
   m.def("lt_algo_count", &lt_algo_count);
