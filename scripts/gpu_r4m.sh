@@ -25,5 +25,11 @@ print(sys.argv[2], r["value"], r["ms_per_step"], "attn", c["stashed_attention_la
 PY
   grep "warmup 2" gpurun_out/r4m_bench_$tag.log
 }
-run lt DSA_LT=1 && run nolt DSA_LT=0
+run lt DSA_LT=1 && run nolt DSA_LT=0 || exit 1
+# timed kernel + memory-copy trace of the default 20B N=1 step (3 timed steps)
+R=$GRAFT_REPO_ROOT
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace -d $R/gpurun_out/r4m_prof -o k --output-format csv -- python3 $R/bench.py --steps 3 --warmup 3 > $R/gpurun_out/r4m_prof.json 2> $R/gpurun_out/r4m_prof.log || { echo "rocprof failed"; tail -20 $R/gpurun_out/r4m_prof.log; exit 1; }
+cd $R
+grep -o '"value": [0-9.]*' gpurun_out/r4m_prof.json
 echo done
