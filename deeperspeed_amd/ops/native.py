@@ -434,6 +434,13 @@ def adam_compact_(hi, res, g, m, v, lr, beta1, beta2, eps, weight_decay, step, b
     res.copy_(r)
 
 
+def copy_nocu_(dst: torch.Tensor, src: torch.Tensor):
+    """dst <- src (same bytes; device or pinned host tensors) on the current stream through a DMA
+    engine (hipMemcpyDeviceToDeviceNoCU) instead of a copy kernel."""
+    hip_ops().copy_nocu(dst, src)
+    return dst
+
+
 def scale_copy_(x: torch.Tensor, y: torch.Tensor, scale: float = 1.0, scale_tensor: Optional[torch.Tensor] = None,
                 accumulate: bool = False):
     """y = x * scale (accumulate: y += x * scale), one pass for any dtype pair."""

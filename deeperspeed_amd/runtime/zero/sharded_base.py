@@ -24,6 +24,7 @@ MI355X design:
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -37,6 +38,11 @@ from ..fp16.loss_scaler import DynamicLossScaler, LossScaler
 from . import compact_master as cm
 from .layout import FlatGroup, layout_signature, params_to_shard, shards_to_params
 from .ref_layout import LAYOUT_VERSION, is_reference_layout, merge_reference_shards
+
+# Host-moments groups: write the updated m / v back to pinned host memory with DMA-engine copies
+# (DSA_HOST_D2H_NOCU=0: torch copy_, which ROCclr ran as copyBuffer kernels on every CU,
+# profiles/r4m_notes.md)
+HOST_D2H_NOCU = os.environ.get("DSA_HOST_D2H_NOCU", "1") != "0"
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
 CPU_STEP_PIECE = int(16 * 1024 * 1024)  # elements per CPU-Adam piece of the pipelined offload step
@@ -548,8 +554,12 @@ class ShardedOptimizerBase:
                         ev_done.record(hs)
                     with torch.cuda.stream(d2h):
                         d2h.wait_event(ev_done)
-                        st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
-                        st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
+                        if HOST_D2H_NOCU:  # DMA engine, not a copy kernel on every CU
+                            native.copy_nocu_(st["exp_avg"][lo:hi], m_dev)
+                            native.copy_nocu_(st["exp_avg_sq"][lo:hi], v_dev)
+                        else:
+                            st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
+                            st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
                         ev_free = torch.cuda.Event()
                         ev_free.record(d2h)
                     free_ev[i] = ev_free
@@ -683,8 +693,12 @@ class ShardedOptimizerBase:
                     ev_done.record(cur)
                     with torch.cuda.stream(d2h):
                         d2h.wait_event(ev_done)
-                        st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
-                        st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
+                        if HOST_D2H_NOCU:  # DMA engine, not a copy kernel on every CU
+                            native.copy_nocu_(st["exp_avg"][lo:hi], m_dev)
+                            native.copy_nocu_(st["exp_avg_sq"][lo:hi], v_dev)
+                        else:
+                            st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
+                            st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
                         ev_free = torch.cuda.Event()
                         ev_free.record(d2h)
                     free_ev[i] = ev_free

@@ -68,3 +68,19 @@ def test_host_moments_match_hbm_moments(overlap, compact):
         assert torch.equal(a, b)
     for a, b in zip(ref_m, m):
         assert torch.equal(a, b)
+
+
+def test_copy_nocu_pinned_roundtrip():
+    """DMA-engine copies (hipMemcpyDeviceToDeviceNoCU) between HBM and pinned host memory."""
+    from deeperspeed_amd.ops import native
+    x = torch.randn(3 * 1024 * 1024 + 7, device="cuda")
+    h = torch.empty(x.numel(), dtype=torch.float32, pin_memory=True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        native.copy_nocu_(h, x)
+        y = torch.empty_like(x)
+        native.copy_nocu_(y, h)
+    s.synchronize()
+    assert torch.equal(h, x.cpu())
+    assert torch.equal(y, x)
