@@ -1091,14 +1091,15 @@ Tensor embedding_bwd(Tensor sorted_ids, Tensor perm, Tensor dy, Tensor dw, int64
 // optimizer groups otherwise run (D2H) as ROCclr copyBuffer kernels with one workgroup on every CU,
 // next to the forward's GEMMs (profiles/r4m_notes.md).  Pinned host memory is device-addressable,
 // so the "device to device" DMA copy reaches it directly.
-void copy_nocu(at::Tensor dst, at::Tensor src) {
+void copy_nocu(at::Tensor dst, at::Tensor src, int64_t kind) {
   TORCH_CHECK(dst.is_contiguous() && src.is_contiguous(), "copy_nocu: contiguous tensors");
   const size_t n = (size_t)src.numel() * src.element_size();
   TORCH_CHECK((size_t)dst.numel() * dst.element_size() == n, "copy_nocu: byte counts differ");
   TORCH_CHECK(dst.is_cuda() || dst.is_pinned(), "copy_nocu: dst must be device or pinned host memory");
   TORCH_CHECK(src.is_cuda() || src.is_pinned(), "copy_nocu: src must be device or pinned host memory");
   if (n == 0) return;
-  const hipError_t e = hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), n, hipMemcpyDeviceToDeviceNoCU, cur_stream());
+  const hipError_t e = hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), n,
+                                      kind < 0 ? hipMemcpyDeviceToDeviceNoCU : (hipMemcpyKind)kind, cur_stream());
   TORCH_CHECK(e == hipSuccess, "copy_nocu: hipMemcpyAsync failed: ", hipGetErrorString(e));
 }
 
@@ -1145,7 +1146,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam_compact", &adam_compact);
   m.def("adam_multi", &adam_multi);
   m.def("sumsq_accum", &sumsq_accum);
-  m.def("copy_nocu", &copy_nocu);
+  m.def("copy_nocu", &copy_nocu, py::arg("dst"), py::arg("src"), py::arg("kind") = -1);
   m.def("scale_copy", &scale_copy, pybind11::arg("x"), pybind11::arg("y"), pybind11::arg("scale_t"),
         pybind11::arg("scale"), pybind11::arg("accumulate") = false);
   m.def("lamb", &lamb);

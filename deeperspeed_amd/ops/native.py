@@ -434,10 +434,11 @@ def adam_compact_(hi, res, g, m, v, lr, beta1, beta2, eps, weight_decay, step, b
     res.copy_(r)
 
 
-def copy_nocu_(dst: torch.Tensor, src: torch.Tensor):
-    """dst <- src (same bytes; device or pinned host tensors) on the current stream through a DMA
-    engine (hipMemcpyDeviceToDeviceNoCU) instead of a copy kernel."""
-    hip_ops().copy_nocu(dst, src)
+def copy_nocu_(dst: torch.Tensor, src: torch.Tensor, kind: int = -1):
+    """dst <- src (same bytes; device or pinned host tensors) on the current stream with one
+    hipMemcpyAsync of the given hipMemcpyKind (default -1: hipMemcpyDeviceToDeviceNoCU, a DMA
+    engine instead of a copy kernel)."""
+    hip_ops().copy_nocu(dst, src, kind)
     return dst
 
 
