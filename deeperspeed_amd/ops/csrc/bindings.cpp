@@ -1103,6 +1103,18 @@ void copy_nocu(at::Tensor dst, at::Tensor src, int64_t kind) {
   TORCH_CHECK(e == hipSuccess, "copy_nocu: hipMemcpyAsync failed: ", hipGetErrorString(e));
 }
 
+// dst <- src (byte copy) by copy_narrow_kernel on `wgs` workgroups (HBM -> pinned host memory).
+void copy_narrow(at::Tensor dst, at::Tensor src, int64_t wgs) {
+  TORCH_CHECK(dst.is_contiguous() && src.is_contiguous(), "copy_narrow: contiguous tensors");
+  const int64_t n = src.numel() * src.element_size();
+  TORCH_CHECK(dst.numel() * dst.element_size() == n, "copy_narrow: byte counts differ");
+  TORCH_CHECK(src.is_cuda() && (dst.is_cuda() || dst.is_pinned()), "copy_narrow: device src, device / pinned dst");
+  TORCH_CHECK(wgs >= 1 && wgs <= 1024, "copy_narrow: 1..1024 workgroups");
+  TORCH_CHECK(((uintptr_t)dst.data_ptr() & 15) == 0 && ((uintptr_t)src.data_ptr() & 15) == 0,
+              "copy_narrow: 16-byte aligned pointers");
+  dsa::launch_copy_narrow(src.data_ptr(), dst.data_ptr(), n, (int)wgs, cur_stream());
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("profile_marker", &profile_marker);
   m.def("embedding_bwd", &embedding_bwd);
@@ -1146,6 +1158,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam_compact", &adam_compact);
   m.def("adam_multi", &adam_multi);
   m.def("sumsq_accum", &sumsq_accum);
+  m.def("copy_narrow", &copy_narrow);
   m.def("copy_nocu", &copy_nocu, py::arg("dst"), py::arg("src"), py::arg("kind") = -1);
   m.def("scale_copy", &scale_copy, pybind11::arg("x"), pybind11::arg("y"), pybind11::arg("scale_t"),
         pybind11::arg("scale"), pybind11::arg("accumulate") = false);

@@ -185,6 +185,40 @@ __global__ void __launch_bounds__(256) sum_finish_kernel(const float* __restrict
   if (threadIdx.x == 0) out[0] += acc;
 }
 
+// Byte copy on a few workgroups, for HBM -> pinned host memory: ROCclr runs such copies as a blit
+// kernel with a workgroup on EVERY CU (profiles/r4p_*), whichever hipMemcpyKind is given, and the
+// PCIe link (~50 GB/s) is the bound either way.  Each thread keeps 4 16-byte loads in flight before
+// its stores so 16-32 workgroups reach the link rate; the rest of the chip stays with the compute.
+__global__ void __launch_bounds__(256) copy_narrow_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                          int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+__global__ void copy_tail_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
+void launch_copy_narrow(const void* src, void* dst, int64_t bytes, int wgs, hipStream_t s) {
+  if (bytes <= 0) return;
+  const int64_t n16 = bytes / 16;
+  if (n16 > 0)
+    hipLaunchKernelGGL(copy_narrow_kernel, dim3(wgs), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, n16);
+  const int64_t tail = bytes - n16 * 16;
+  if (tail > 0)
+    hipLaunchKernelGGL(copy_tail_kernel, dim3(1), dim3(64), 0, s, (const uint8_t*)src + n16 * 16,
+                       (uint8_t*)dst + n16 * 16, tail);
+}
+
 // y = x * scale, or y += x * scale (ACC: e.g. a bf16 micro-batch gradient accumulated into an
 // fp32 shard in one pass instead of a cast kernel plus an add kernel); mixed dtypes
 template <typename TI, typename TO, bool ACC>

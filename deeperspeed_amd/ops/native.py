@@ -434,6 +434,15 @@ def adam_compact_(hi, res, g, m, v, lr, beta1, beta2, eps, weight_decay, step, b
     res.copy_(r)
 
 
+def copy_narrow_(dst: torch.Tensor, src: torch.Tensor, wgs: int = 16):
+    """dst <- src on `wgs` workgroups (HBM -> pinned host at the PCIe rate without a workgroup on
+    every CU); falls back to copy_ for unaligned tensors."""
+    if (dst.data_ptr() | src.data_ptr()) & 15:
+        return dst.copy_(src, non_blocking=True)
+    hip_ops().copy_narrow(dst, src, wgs)
+    return dst
+
+
 def copy_nocu_(dst: torch.Tensor, src: torch.Tensor, kind: int = -1):
     """dst <- src (same bytes; device or pinned host tensors) on the current stream with one
     hipMemcpyAsync of the given hipMemcpyKind (default -1: hipMemcpyDeviceToDeviceNoCU, a DMA

@@ -39,10 +39,17 @@ from . import compact_master as cm
 from .layout import FlatGroup, layout_signature, params_to_shard, shards_to_params
 from .ref_layout import LAYOUT_VERSION, is_reference_layout, merge_reference_shards
 
-# Host-moments groups: write the updated m / v back to pinned host memory with DMA-engine copies
-# (DSA_HOST_D2H_NOCU=0: torch copy_, which ROCclr ran as copyBuffer kernels on every CU,
-# profiles/r4m_notes.md)
-HOST_D2H_NOCU = os.environ.get("DSA_HOST_D2H_NOCU", "1") != "0"
+# Host-moments groups ("stream" mode): DSA_HOST_D2H_NOCU=1 writes m / v back with
+# hipMemcpyDeviceToDeviceNoCU -- measured to take the same blit-kernel path as torch copy_
+# (profiles/r4p_*), kept for the record
+HOST_D2H_NOCU = os.environ.get("DSA_HOST_D2H_NOCU", "0") == "1"
+# "side": the host-moments Adam runs on the step's own stream after the HBM groups (no fifth
+# stream sharing a hardware queue with the compute stream); "stream": on a stream of its own,
+# beside the HBM groups (round-4 first version)
+HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "side")
+# workgroups of the HBM -> pinned-host moment write-back kernel (0: torch copy_, a blit kernel with a
+# workgroup on every CU)
+HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "16"))
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
 CPU_STEP_PIECE = int(16 * 1024 * 1024)  # elements per CPU-Adam piece of the pipelined offload step
@@ -462,8 +469,12 @@ class ShardedOptimizerBase:
                     self.optimizer.state[g.master]
                 st["step"] = st.get("step", 0) + 1
             host_groups = [g for g in self.groups if self._host_moment_group(g)]
-            if host_groups:  # their copy pipeline starts first and runs beside the HBM groups
+            pipe = None
+            if host_groups and HOST_STEP_MODE == "stream":  # copy pipeline + kernels beside the HBM groups
                 self._host_moments_step(host_groups, grad_scale)
+            elif host_groups:  # H2D of the first pieces starts now; their Adam follows the HBM groups
+                pipe = self._host_moments_pipeline(host_groups, grad_scale)
+                next(pipe)
             for g in self.groups:
                 if self._host_moment_group(g):
                     continue
@@ -475,7 +486,10 @@ class ShardedOptimizerBase:
                         self.optimizer.update_flat(grp, g.master, g.master, g.shard_grad, out=o,
                                                    grad_scale=grad_scale, lo=lo, hi=hi)
                     self._after_bucket_update(g, b)
-            if host_groups:  # the step's end (and the gradient zeroing after it) follows their kernels
+            if pipe is not None:
+                for _ in pipe:
+                    pass
+            elif host_groups:  # the step's end (and the gradient zeroing after it) follows their kernels
                 torch.cuda.current_stream().wait_stream(self._host_stream)
             return
         # generic torch optimizer over the fp32 master shards
@@ -565,6 +579,91 @@ class ShardedOptimizerBase:
                     free_ev[i] = ev_free
                 self._after_host_bucket_update(g, b, hs)
         self._host_free_ev = free_ev
+        done = torch.cuda.Event()
+        done.record(d2h)
+        self._host_d2h_done = done
+
+    def _host_moments_pipeline(self, groups, grad_scale):
+        """Adam for the host-moments groups on the CURRENT stream (the overlapped step's side
+        stream), after the HBM groups: a generator whose first next() issues the H2D of the first
+        pieces (copy stream, DMA engine) and whose remaining iterations issue, per piece, the fused
+        Adam on the current stream (waiting for that piece's H2D), the D2H of m / v on the second
+        copy stream (copy_narrow_kernel on HOST_D2H_WGS workgroups, not a blit kernel on every CU),
+        and the H2D of the piece three ahead into the slot it frees.  No extra compute stream: with
+        HIP's 4 hardware queues a fifth stream shares a queue with the compute stream, whose next
+        forward then waited for the whole copy pipeline (profiles/r4n_notes.md)."""
+        h2d, d2h = self._streams()
+        cur = torch.cuda.current_stream()
+        piece = min(self.HOST_PIECE, max(b.chunk for g in groups for b in g.buckets))
+        if self._host_staging is None or self._host_staging[0][0].numel() < piece:
+            self._host_staging = [(torch.empty(piece, dtype=torch.float32, device=self.device),
+                                   torch.empty(piece, dtype=torch.float32, device=self.device)) for _ in range(3)]
+        stages = self._host_staging
+        work = []  # (group, bucket, lo, hi, n, s, e, state, is_last_piece_of_bucket)
+        for g in groups:
+            st = self.optimizer.state_for(g.master) if isinstance(self.optimizer, FusedAdam) else \
+                self.optimizer.state[g.master]
+            for b in g.buckets:
+                starts = list(range(0, b.chunk, piece))
+                for j, s0 in enumerate(starts):
+                    e0 = min(s0 + piece, b.chunk)
+                    work.append((g, b, b.shard_offset + s0, b.shard_offset + e0, e0 - s0, s0, e0, st,
+                                 j == len(starts) - 1))
+        free_ev = [None] * 3
+        ev_in = [None] * len(work)
+        if self._host_d2h_done is not None:  # the previous step's moments are home
+            h2d.wait_event(self._host_d2h_done)
+
+        def issue_h2d(k):
+            g, b, lo, hi, n, _, _, st, _ = work[k]
+            i = k % 3
+            with torch.cuda.stream(h2d):
+                if free_ev[i] is not None:
+                    h2d.wait_event(free_ev[i])
+                stages[i][0][:n].copy_(st["exp_avg"][lo:hi], non_blocking=True)
+                stages[i][1][:n].copy_(st["exp_avg_sq"][lo:hi], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(h2d)
+            ev_in[k] = ev
+
+        for k in range(min(3, len(work))):
+            issue_h2d(k)
+        yield
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+        for k, (g, b, lo, hi, n, s0, e0, st, last) in enumerate(work):
+            i = k % 3
+            m_dev, v_dev = stages[i][0][:n], stages[i][1][:n]
+            grp = self._inner_group(g)
+            b1, b2 = grp["betas"]
+            cur.wait_event(ev_in[k])
+            out_full = self._bucket_out(g, b)
+            o = None if out_full is None else out_full[s0:e0]
+            if self.compact_master:
+                native.adam_compact_(o, g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, grp["lr"], b1, b2,
+                                     grp["eps"], grp["weight_decay"], st["step"], grp.get("bias_correction", True),
+                                     grad_scale, adamw)
+            else:
+                native.adam_flat_(g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, o, grp["lr"], b1, b2,
+                                  grp["eps"], grp["weight_decay"], st["step"], grp.get("bias_correction", True),
+                                  grad_scale, adamw)
+            ev_done = torch.cuda.Event()
+            ev_done.record(cur)
+            with torch.cuda.stream(d2h):
+                d2h.wait_event(ev_done)
+                if HOST_D2H_WGS > 0:
+                    native.copy_narrow_(st["exp_avg"][lo:hi], m_dev, HOST_D2H_WGS)
+                    native.copy_narrow_(st["exp_avg_sq"][lo:hi], v_dev, HOST_D2H_WGS)
+                else:
+                    st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
+                    st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
+                ev_free = torch.cuda.Event()
+                ev_free.record(d2h)
+            free_ev[i] = ev_free
+            if k + 3 < len(work):
+                issue_h2d(k + 3)
+            if last:
+                self._after_host_bucket_update(g, b, cur)
+            yield
         done = torch.cuda.Event()
         done.record(d2h)
         self._host_d2h_done = done

@@ -16,7 +16,11 @@ s = torch.cuda.Stream()
 variants = {"torch_copy": lambda: h.copy_(x, non_blocking=True),
             "nocu": lambda: native.copy_nocu_(h, x),
             "kind_d2h": lambda: native.copy_nocu_(h, x, 2),
-            "kind_default": lambda: native.copy_nocu_(h, x, 4)}
+            "kind_default": lambda: native.copy_nocu_(h, x, 4),
+            "narrow8": lambda: native.copy_narrow_(h, x, 8),
+            "narrow16": lambda: native.copy_narrow_(h, x, 16),
+            "narrow32": lambda: native.copy_narrow_(h, x, 32),
+            "narrow64": lambda: native.copy_narrow_(h, x, 64)}
 for name, fn in variants.items():
     with torch.cuda.stream(s):
         fn()
@@ -29,5 +33,6 @@ for name, fn in variants.items():
     s.synchronize()
     dt = (time.time() - t0) / 10
     assert torch.equal(h, x.cpu()), name
+    h.zero_()
     print(f"{name}: {dt * 1e3:.2f} ms per 64 MB copy ({64 / 1024 / dt:.1f} GB/s)", flush=True)
     time.sleep(0.05)

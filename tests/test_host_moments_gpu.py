@@ -58,8 +58,13 @@ def _run(host, overlap, compact, steps=3, ga=2, piece=None):
     return losses, [p.detach().float().cpu() for p in engine.module.parameters()], mom, on_host
 
 
-@pytest.mark.parametrize("overlap,compact", [(True, True), (False, True), (True, False)])
-def test_host_moments_match_hbm_moments(overlap, compact):
+@pytest.mark.parametrize("overlap,compact,mode,wgs", [(True, True, "side", 16), (False, True, "side", 16),
+                                                      (True, False, "side", 16), (True, True, "side", 0),
+                                                      (True, True, "stream", 16)])
+def test_host_moments_match_hbm_moments(overlap, compact, mode, wgs, monkeypatch):
+    from deeperspeed_amd.runtime.zero import sharded_base
+    monkeypatch.setattr(sharded_base, "HOST_STEP_MODE", mode)
+    monkeypatch.setattr(sharded_base, "HOST_D2H_WGS", wgs)
     ref_l, ref_w, ref_m, ref_host = _run(False, overlap, compact)
     l, w, m, host = _run(True, overlap, compact, piece=300_000)  # several pieces per bucket: ring reuse
     assert ref_host == [False, False] and host == [False, True]
@@ -84,3 +89,15 @@ def test_copy_nocu_pinned_roundtrip():
     s.synchronize()
     assert torch.equal(h, x.cpu())
     assert torch.equal(y, x)
+
+
+@pytest.mark.parametrize("wgs", [1, 16, 64])
+def test_copy_narrow_to_pinned(wgs):
+    """copy_narrow_kernel: HBM -> pinned host on a few workgroups, odd byte tails included."""
+    from deeperspeed_amd.ops import native
+    for n in (1, 17, 4 * 1024 * 1024 + 3):
+        x = torch.randint(0, 255, (n,), device="cuda", dtype=torch.uint8)
+        h = torch.zeros(n, dtype=torch.uint8, pin_memory=True)
+        native.copy_narrow_(h, x, wgs)
+        torch.cuda.synchronize()
+        assert torch.equal(h, x.cpu())
