@@ -43,10 +43,10 @@ from .ref_layout import LAYOUT_VERSION, is_reference_layout, merge_reference_sha
 # hipMemcpyDeviceToDeviceNoCU -- measured to take the same blit-kernel path as torch copy_
 # (profiles/r4p_*), kept for the record
 HOST_D2H_NOCU = os.environ.get("DSA_HOST_D2H_NOCU", "0") == "1"
-# "side": the host-moments Adam runs on the step's own stream after the HBM groups (no fifth
-# stream sharing a hardware queue with the compute stream); "stream": on a stream of its own,
-# beside the HBM groups (round-4 first version)
-HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "side")
+# "serial": the host-moments copies and Adam run on the step's own stream after the HBM groups (no
+# other stream, no cross-stream waits); "side": Adam on the step stream, copies on two copy
+# streams; "stream": Adam on a stream of its own beside the HBM groups (round-4 first version)
+HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "serial")
 # workgroups of the HBM -> pinned-host moment write-back kernel (0: torch copy_, a blit kernel with a
 # workgroup on every CU)
 HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "16"))
@@ -472,6 +472,8 @@ class ShardedOptimizerBase:
             pipe = None
             if host_groups and HOST_STEP_MODE == "stream":  # copy pipeline + kernels beside the HBM groups
                 self._host_moments_step(host_groups, grad_scale)
+            elif host_groups and HOST_STEP_MODE == "serial":  # after the HBM groups, on this stream only
+                pipe = self._host_moments_serial(host_groups, grad_scale)
             elif host_groups:  # H2D of the first pieces starts now; their Adam follows the HBM groups
                 pipe = self._host_moments_pipeline(host_groups, grad_scale)
                 next(pipe)
@@ -581,6 +583,57 @@ class ShardedOptimizerBase:
         self._host_free_ev = free_ev
         done = torch.cuda.Event()
         done.record(d2h)
+        self._host_d2h_done = done
+
+    def _host_moments_serial(self, groups, grad_scale):
+        """Adam for the host-moments groups entirely on the CURRENT stream (the overlapped step's
+        side stream), after the HBM groups: per piece, H2D of m / v (DMA engine), the fused Adam,
+        D2H of m / v (copy_narrow_kernel on HOST_D2H_WGS workgroups).  One stream and no cross-stream
+        waits: HIP maps streams onto 4 hardware queues by default, and a copy stream that waits on
+        another stream's events blocks whatever shares its queue -- the compute stream's next
+        forward waited for the whole copy pipeline that way (profiles/r4q_notes.md).  The PCIe
+        phase is serial (~0.4 s for 1.2 B parameters) but runs beside the next forward, whose
+        modules wait only for their own buckets (the host groups hold the LAST layers)."""
+        cur = torch.cuda.current_stream()
+        piece = min(self.HOST_PIECE, max(b.chunk for g in groups for b in g.buckets))
+        if self._host_staging is None or self._host_staging[0][0].numel() < piece:
+            self._host_staging = [(torch.empty(piece, dtype=torch.float32, device=self.device),
+                                   torch.empty(piece, dtype=torch.float32, device=self.device)) for _ in range(3)]
+        m_buf, v_buf = self._host_staging[0]
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+        yield
+        for g in groups:
+            grp = self._inner_group(g)
+            b1, b2 = grp["betas"]
+            st = self.optimizer.state_for(g.master) if isinstance(self.optimizer, FusedAdam) else \
+                self.optimizer.state[g.master]
+            for b in g.buckets:
+                out_full = self._bucket_out(g, b)
+                for s0 in range(0, b.chunk, piece):
+                    e0 = min(s0 + piece, b.chunk)
+                    lo, hi, n = b.shard_offset + s0, b.shard_offset + e0, e0 - s0
+                    m_dev, v_dev = m_buf[:n], v_buf[:n]
+                    m_dev.copy_(st["exp_avg"][lo:hi], non_blocking=True)
+                    v_dev.copy_(st["exp_avg_sq"][lo:hi], non_blocking=True)
+                    o = None if out_full is None else out_full[s0:e0]
+                    if self.compact_master:
+                        native.adam_compact_(o, g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, grp["lr"], b1,
+                                             b2, grp["eps"], grp["weight_decay"], st["step"],
+                                             grp.get("bias_correction", True), grad_scale, adamw)
+                    else:
+                        native.adam_flat_(g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, o, grp["lr"], b1, b2,
+                                          grp["eps"], grp["weight_decay"], st["step"],
+                                          grp.get("bias_correction", True), grad_scale, adamw)
+                    if HOST_D2H_WGS > 0:
+                        native.copy_narrow_(st["exp_avg"][lo:hi], m_dev, HOST_D2H_WGS)
+                        native.copy_narrow_(st["exp_avg_sq"][lo:hi], v_dev, HOST_D2H_WGS)
+                    else:
+                        st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
+                        st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
+                    yield
+                self._after_host_bucket_update(g, b, cur)
+        done = torch.cuda.Event()
+        done.record(cur)
         self._host_d2h_done = done
 
     def _host_moments_pipeline(self, groups, grad_scale):
