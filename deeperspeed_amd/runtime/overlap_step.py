@@ -46,6 +46,15 @@ def side_stream(device, num_cus: int = 0) -> torch.cuda.Stream:
     return torch.cuda.ExternalStream(hip.cu_masked_stream(words), device=device)
 
 
+def dedicated_stream(device) -> torch.cuda.Stream:
+    """A stream on a hardware queue of its own.  HIP spreads ordinary streams over
+    GPU_MAX_HW_QUEUES (4) pooled queues, so a copy or optimizer stream can share the compute
+    stream's queue, and its cross-stream waits (barrier packets) then stall the compute stream's
+    kernels (profiles/r4q_notes.md).  A CU-masked stream gets a queue of its own; the mask here
+    enables every CU, so only the queue differs."""
+    return side_stream(device, 1 << 30)
+
+
 def _in_backward() -> bool:
     return torch._C._current_graph_task_id() != -1
 

@@ -46,7 +46,9 @@ HOST_D2H_NOCU = os.environ.get("DSA_HOST_D2H_NOCU", "0") == "1"
 # "serial": the host-moments copies and Adam run on the step's own stream after the HBM groups (no
 # other stream, no cross-stream waits); "side": Adam on the step stream, copies on two copy
 # streams; "stream": Adam on a stream of its own beside the HBM groups (round-4 first version)
-HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "serial")
+HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "stream")
+# copy / host-moments streams on hardware queues of their own (overlap_step.dedicated_stream)
+DEDICATED_STREAMS = os.environ.get("DSA_DEDICATED_STREAMS", "1") != "0"
 # workgroups of the HBM -> pinned-host moment write-back kernel (0: torch copy_, a blit kernel with a
 # workgroup on every CU)
 HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "16"))
@@ -519,7 +521,7 @@ class ShardedOptimizerBase:
         Each bucket's update event is recorded for the forward pre-hooks (overlap_step)."""
         h2d, d2h = self._streams()
         if self._host_stream is None:
-            self._host_stream = torch.cuda.Stream(device=self.device)
+            self._host_stream = self._new_stream()
         hs, cur = self._host_stream, torch.cuda.current_stream()
         piece = min(self.HOST_PIECE, max(b.chunk for g in groups for b in g.buckets))
         if self._host_staging is None or self._host_staging[0][0].numel() < piece:
@@ -570,9 +572,12 @@ class ShardedOptimizerBase:
                         ev_done.record(hs)
                     with torch.cuda.stream(d2h):
                         d2h.wait_event(ev_done)
-                        if HOST_D2H_NOCU:  # DMA engine, not a copy kernel on every CU
+                        if HOST_D2H_NOCU:
                             native.copy_nocu_(st["exp_avg"][lo:hi], m_dev)
                             native.copy_nocu_(st["exp_avg_sq"][lo:hi], v_dev)
+                        elif HOST_D2H_WGS > 0:
+                            native.copy_narrow_(st["exp_avg"][lo:hi], m_dev, HOST_D2H_WGS)
+                            native.copy_narrow_(st["exp_avg_sq"][lo:hi], v_dev, HOST_D2H_WGS)
                         else:
                             st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
                             st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
@@ -733,8 +738,14 @@ class ShardedOptimizerBase:
     # ------------------------------------------------------------------ offload step
     def _streams(self):
         if self._copy_streams is None and torch.cuda.is_available():
-            self._copy_streams = (torch.cuda.Stream(), torch.cuda.Stream())
+            self._copy_streams = (self._new_stream(), self._new_stream())
         return self._copy_streams
+
+    def _new_stream(self):
+        if DEDICATED_STREAMS:
+            from ..overlap_step import dedicated_stream
+            return dedicated_stream(self.device)
+        return torch.cuda.Stream(device=self.device)
 
     def _offload_step(self, grad_scale: float):
         grp_steps = {}
