@@ -251,7 +251,8 @@ class WeightTPrefetch:
             self.bufs[slot] = buf = torch.empty(max(n, buf.numel() if buf is not None else 0), dtype=w.dtype,
                                                 device=w.device)
         if self.stream is None:
-            self.stream = torch.cuda.Stream(device=w.device)
+            from ..runtime.overlap_step import new_stream
+            self.stream = new_stream(w.device)
         cur = torch.cuda.current_stream(w.device)
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
@@ -430,7 +431,8 @@ def _linear_backward(ctx, g):
         dev = g2.device
         side = _par_streams.get(dev)
         if side is None:
-            side = _par_streams[dev] = torch.cuda.Stream(device=dev)
+            from ..runtime.overlap_step import new_stream
+            side = _par_streams[dev] = new_stream(dev)
         cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
         dx = input_grad(g2, weight).view(x.shape)

@@ -60,8 +60,9 @@ class HostStash:
 
     def _streams(self, device):
         if self._d2h is None:
-            self._d2h = torch.cuda.Stream(device=device)
-            self._h2d = torch.cuda.Stream(device=device)
+            from ..overlap_step import new_stream
+            self._d2h = new_stream(device)
+            self._h2d = new_stream(device)
         return self._d2h, self._h2d
 
     def _take_buffers(self, owner: int, tensors: Sequence[torch.Tensor]):

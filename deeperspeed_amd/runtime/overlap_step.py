@@ -29,11 +29,16 @@ import torch
 OVERLAP_CUS = int(os.environ.get("DSA_OVERLAP_CUS", "0"))
 
 
+# side / copy streams on hardware queues of their own (dedicated_stream); DSA_DEDICATED_STREAMS=0:
+# plain torch streams, which HIP spreads over its pooled queues
+DEDICATED_STREAMS = os.environ.get("DSA_DEDICATED_STREAMS", "1") != "0"
+
+
 def side_stream(device, num_cus: int = 0) -> torch.cuda.Stream:
     """A side stream; with num_cus > 0 one restricted to that many CUs (ops/csrc/bindings.cpp
-    cu_masked_stream)."""
+    cu_masked_stream), else a stream on a hardware queue of its own (new_stream)."""
     if num_cus <= 0:
-        return torch.cuda.Stream(device=device)
+        return new_stream(device)
     from ..ops import native
     hip = native.hip_ops()
     total = int(hip.device_cu_count())
@@ -53,6 +58,13 @@ def dedicated_stream(device) -> torch.cuda.Stream:
     kernels (profiles/r4q_notes.md).  A CU-masked stream gets a queue of its own; the mask here
     enables every CU, so only the queue differs."""
     return side_stream(device, 1 << 30)
+
+
+def new_stream(device) -> torch.cuda.Stream:
+    """The framework's side / copy streams: dedicated_stream unless DSA_DEDICATED_STREAMS=0."""
+    if DEDICATED_STREAMS and torch.cuda.is_available():
+        return dedicated_stream(device)
+    return torch.cuda.Stream(device=device)
 
 
 def _in_backward() -> bool:

@@ -47,8 +47,7 @@ HOST_D2H_NOCU = os.environ.get("DSA_HOST_D2H_NOCU", "0") == "1"
 # other stream, no cross-stream waits); "side": Adam on the step stream, copies on two copy
 # streams; "stream": Adam on a stream of its own beside the HBM groups (round-4 first version)
 HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "stream")
-# copy / host-moments streams on hardware queues of their own (overlap_step.dedicated_stream)
-DEDICATED_STREAMS = os.environ.get("DSA_DEDICATED_STREAMS", "1") != "0"
+
 # workgroups of the HBM -> pinned-host moment write-back kernel (0: torch copy_, a blit kernel with a
 # workgroup on every CU)
 HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "16"))
@@ -742,10 +741,8 @@ class ShardedOptimizerBase:
         return self._copy_streams
 
     def _new_stream(self):
-        if DEDICATED_STREAMS:
-            from ..overlap_step import dedicated_stream
-            return dedicated_stream(self.device)
-        return torch.cuda.Stream(device=self.device)
+        from ..overlap_step import new_stream
+        return new_stream(self.device)
 
     def _offload_step(self, grad_scale: float):
         grp_steps = {}

@@ -512,13 +512,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         if not self._overlap_step:
             return
         from ..overlap_step import OVERLAP_CUS, side_stream
-        # DSA_OVERLAP_CUS: CU-masked; otherwise a queue of its own (overlap_step.dedicated_stream)
-        from .sharded_base import DEDICATED_STREAMS
-        if OVERLAP_CUS <= 0 and DEDICATED_STREAMS:
-            from ..overlap_step import dedicated_stream
-            self._step_stream = dedicated_stream(self.device)
-        else:
-            self._step_stream = side_stream(self.device, OVERLAP_CUS)
+        # DSA_OVERLAP_CUS: CU-masked; otherwise a hardware queue of its own (overlap_step.new_stream)
+        self._step_stream = side_stream(self.device, OVERLAP_CUS)
         self._bucket_key = {}
         owner = {}
         for gi, g in enumerate(self.groups):
