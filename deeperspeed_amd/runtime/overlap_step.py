@@ -29,9 +29,11 @@ import torch
 OVERLAP_CUS = int(os.environ.get("DSA_OVERLAP_CUS", "0"))
 
 
-# side / copy streams on hardware queues of their own (dedicated_stream); DSA_DEDICATED_STREAMS=0:
-# plain torch streams, which HIP spreads over its pooled queues
-DEDICATED_STREAMS = os.environ.get("DSA_DEDICATED_STREAMS", "1") != "0"
+# DSA_DEDICATED_STREAMS=1: side / copy streams on hardware queues of their own (dedicated_stream).
+# Off by default: on the 20B N=1 step the optimizer step then runs concurrently with the next
+# forward and costs more than the queue sharing it removes (8,720 vs 8,868 tok/s, same box,
+# profiles/r4s_notes.md)
+DEDICATED_STREAMS = os.environ.get("DSA_DEDICATED_STREAMS", "0") == "1"
 
 
 def side_stream(device, num_cus: int = 0) -> torch.cuda.Stream:
@@ -61,7 +63,8 @@ def dedicated_stream(device) -> torch.cuda.Stream:
 
 
 def new_stream(device) -> torch.cuda.Stream:
-    """The framework's side / copy streams: dedicated_stream unless DSA_DEDICATED_STREAMS=0."""
+    """The framework's side / copy streams: plain torch streams, dedicated_stream with
+    DSA_DEDICATED_STREAMS=1."""
     if DEDICATED_STREAMS and torch.cuda.is_available():
         return dedicated_stream(device)
     return torch.cuda.Stream(device=device)

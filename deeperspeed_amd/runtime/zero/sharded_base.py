@@ -43,14 +43,16 @@ from .ref_layout import LAYOUT_VERSION, is_reference_layout, merge_reference_sha
 # hipMemcpyDeviceToDeviceNoCU -- measured to take the same blit-kernel path as torch copy_
 # (profiles/r4p_*), kept for the record
 HOST_D2H_NOCU = os.environ.get("DSA_HOST_D2H_NOCU", "0") == "1"
-# "serial": the host-moments copies and Adam run on the step's own stream after the HBM groups (no
-# other stream, no cross-stream waits); "side": Adam on the step stream, copies on two copy
-# streams; "stream": Adam on a stream of its own beside the HBM groups (round-4 first version)
+# "stream" (default): the host-moments Adam on a stream of its own, copies on two copy streams,
+# beside the HBM groups; "side": Adam on the step stream after the HBM groups; "serial": copies and
+# Adam all on the step stream.  Measured on the 20B N=1 step (profiles/r4q_notes.md,
+# profiles/r4s_notes.md): stream 8,868-8,972, side 8,557-8,670, serial 8,540-8,559 tok/s.
 HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "stream")
 
-# workgroups of the HBM -> pinned-host moment write-back kernel (0: torch copy_, a blit kernel with a
-# workgroup on every CU)
-HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "16"))
+# workgroups of the HBM -> pinned-host moment write-back kernel (copy_narrow_kernel); 0 (default):
+# torch copy_, a ROCclr blit kernel with a workgroup on every CU, which measured faster in the step
+# (8,787 vs 8,720 tok/s with dedicated queues, profiles/r4s_notes.md)
+HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "0"))
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
 CPU_STEP_PIECE = int(16 * 1024 * 1024)  # elements per CPU-Adam piece of the pipelined offload step
