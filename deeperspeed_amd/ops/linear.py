@@ -154,7 +154,8 @@ def nt_wgrad_planned(M: int, out_features: int, in_features: int, elem_size: int
     if lt_tune.wgrad_nt(M, out_features, in_features, elem_size):
         return False  # the measured NT GEMM reads the token-major operands directly
     if (WGRAD_SPLIT > 1 and M >= WGRAD_SPLIT_MIN_TOKENS and M % WGRAD_SPLIT == 0
-            and -(-out_features // 256) * -(-in_features // 256) <= WGRAD_SPLIT_MAX_TILES):
+            and -(-out_features // 256) * -(-in_features // 256) <= WGRAD_SPLIT_MAX_TILES
+            and not lt_tune.use_wgrad_t(M, out_features, in_features)):
         return False  # split-K path (_split_k)
     copies = (0 if g_ready else M * out_features) + (0 if x_ready else M * in_features)
     return copies * elem_size <= WGRAD_NT_MAX_BYTES
@@ -190,6 +191,8 @@ def _split_k(g2, x2):
             or not g2.is_contiguous() or not x2.is_contiguous()):
         return 1
     tiles = -(-out // 256) * -(-inp // 256)
+    if tiles <= WGRAD_SPLIT_MAX_TILES and lt_tune.use_wgrad_t(M, out, inp):
+        return 1  # a measured TN solution fills the chip without splitting (ops/lt_tune.py)
     return WGRAD_SPLIT if tiles <= WGRAD_SPLIT_MAX_TILES else 1
 
 
@@ -350,7 +353,10 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     if gw is not None and gw.is_contiguous():
         nt = _nt_operands(g2, x2, bias.grad if has_b else None, offer_gt)
         if nt is not None:
-            gw.addmm_(nt[0], nt[1].t())
+            if lt_tune.WGRAD and gw.dtype == torch.bfloat16 and lt_tune.use_wgrad_t(g2.size(0), g2.size(1), x2.size(1)):
+                _lt_ops().gemm_lt(nt[0], nt[1], trans_b=True, out=gw, accumulate=True)  # measured solution
+            else:
+                gw.addmm_(nt[0], nt[1].t())
         else:
             gw.addmm_(g2.t(), x2)
             if has_b:

@@ -36,6 +36,9 @@ ENABLED = os.environ.get("DSA_LT", "0") == "1"  # default off until the in-step 
 FWD = ENABLED and os.environ.get("DSA_LT_FWD", "1") != "0"
 DGRAD = ENABLED and os.environ.get("DSA_LT_DGRAD", "1") != "0"
 WGRAD = ENABLED and os.environ.get("DSA_LT_WGRAD", "1") != "0"
+# the untransposed layouts (NN input gradient, NT weight gradient): opt-in, slower on torch's build
+NN = os.environ.get("DSA_LT_NN", "0") == "1"
+NT = os.environ.get("DSA_LT_NT", "0") == "1"
 TABLE_PATH = os.environ.get("DSA_LT_TABLE", os.path.join(os.path.dirname(__file__), "lt_table.json"))
 # effective HBM rate of the HIP transpose kernel (read + write), bytes/s: profiles/aux transposes
 # stream at 4-4.5 TB/s on MI355X
@@ -107,12 +110,33 @@ def entry(kind: str, M: int, N: int, K: int, bias: bool = False) -> Optional[dic
     return load_table().get(key(kind, M, N, K, bias))
 
 
+# a measured solution is routed only when it beats the heuristic's first choice by this factor
+# (the sweep times each solution over few launches; smaller gains are within its noise)
+MIN_GAIN = float(os.environ.get("DSA_LT_MIN_GAIN", "1.05"))
+
+
+def gain(kind: str, M: int, N: int, K: int, bias: bool = False) -> float:
+    """Best measured rate over the heuristic's (0.0 when the table has no record)."""
+    e = entry(kind, M, N, K, bias)
+    if e is None or not e.get("heuristic_tflops"):
+        return 0.0
+    return float(e["tflops"]) / float(e["heuristic_tflops"])
+
+
 def use_fwd(M: int, N: int, K: int, bias: bool) -> bool:
-    return FWD and entry("fwd", M, N, K, bias) is not None
+    return FWD and gain("fwd", M, N, K, bias) >= MIN_GAIN
 
 
 def use_dgrad(M: int, N: int, K: int) -> bool:
-    return DGRAD and entry("dgrad", M, N, K) is not None
+    """Untransposed (NN) input gradient instead of W^T + TN: only on request (DSA_LT_NN=1) -- on
+    torch's hipBLASLt the NN solutions are slower than the transposed formulation at every
+    GPT-NeoX shape measured (profiles/r4m_notes.md)."""
+    return DGRAD and NN and entry("dgrad", M, N, K) is not None
+
+
+def use_wgrad_t(M: int, N: int, K: int) -> bool:
+    """Transposed-operand weight gradient (TN) through the wrapper's measured solution."""
+    return WGRAD and gain("wgradT", M, N, K) >= MIN_GAIN
 
 
 _nt_cache: Dict[Tuple[int, int, int, int], bool] = {}
@@ -122,7 +146,7 @@ def wgrad_nt(M: int, N: int, K: int, elem_size: int = 2) -> bool:
     """True when the weight gradient of an [N, K] linear over M tokens is cheaper as one NT GEMM
     on the token-major operands than as transposes of both operands plus the TN GEMM, by the
     table's measured rates."""
-    if not WGRAD:
+    if not (WGRAD and NT):
         return False
     ck = (M, N, K, elem_size)
     r = _nt_cache.get(ck)
