@@ -20,9 +20,9 @@ Reference counterpart: the reference calls cuBLAS with the default heuristic
 (`csrc/includes/cublas_wrappers.h`, `cublasGemmEx(..., CUBLAS_GEMM_DEFAULT_TENSOR_OP)`); the
 per-shape algorithm choice is an MI355X addition.
 
-DSA_LT=1 enables the routes (default off until they win in the step: profiles/r4j_notes.md);
-DSA_LT_FWD, DSA_LT_DGRAD and
-DSA_LT_WGRAD=0 disable one route each; DSA_LT_TABLE names another table file.
+DSA_LT=0 disables every route; DSA_LT_FWD=0 the forward route (on by default), DSA_LT_WGRAD=1 /
+DSA_LT_NN=1 / DSA_LT_NT=1 enable the weight-gradient / untransposed routes (off: they measured
+slower in the step); DSA_LT_TABLE names another table file.
 """
 
 from __future__ import annotations
@@ -32,10 +32,14 @@ import os
 import threading
 from typing import Dict, Optional, Tuple
 
-ENABLED = os.environ.get("DSA_LT", "0") == "1"  # default off until the in-step A/B wins
+ENABLED = os.environ.get("DSA_LT", "1") != "0"
+# forward GEMMs with a measured solution >= MIN_GAIN over the heuristic: on by default (BERT-Large
+# QKV projection +22 %, the seq-128 step +1.2 %, profiles/r4u_notes.md)
 FWD = ENABLED and os.environ.get("DSA_LT_FWD", "1") != "0"
 DGRAD = ENABLED and os.environ.get("DSA_LT_DGRAD", "1") != "0"
-WGRAD = ENABLED and os.environ.get("DSA_LT_WGRAD", "1") != "0"
+# weight gradients through the measured TN solutions: opt-in -- isolated gains of 5-50 % did not
+# survive in the step (20B N=1 -0.8 %, 1.3B ZeRO-2 -0.2 %, same boxes, profiles/r4u_notes.md)
+WGRAD = ENABLED and os.environ.get("DSA_LT_WGRAD", "0") == "1"
 # the untransposed layouts (NN input gradient, NT weight gradient): opt-in, slower on torch's build
 NN = os.environ.get("DSA_LT_NN", "0") == "1"
 NT = os.environ.get("DSA_LT_NT", "0") == "1"

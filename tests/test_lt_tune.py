@@ -48,6 +48,7 @@ def test_nt_choice_counts_transpose_traffic(tmp_path, monkeypatch):
     path = _table(tmp_path, [("wgrad", M, N, K, 1400.0), ("wgradT", M, N, K, 1540.0)])
     monkeypatch.setattr(lt_tune, "_table", lt_tune.load_table(path))
     monkeypatch.setattr(lt_tune, "WGRAD", True)
+    monkeypatch.setattr(lt_tune, "NT", True)
     monkeypatch.setattr(lt_tune, "ENABLED", True)
     lt_tune._nt_cache.clear()
     assert lt_tune.wgrad_nt(M, N, K)
@@ -68,3 +69,20 @@ def test_shipped_table_parses():
     assert t, "ops/lt_table.json missing or empty"
     for k, e in t.items():
         assert len(k) == 7 and e["names"] and e["tflops"] > 0
+
+
+def test_routes_gated_by_measured_gain(tmp_path, monkeypatch):
+    p = tmp_path / "g.json"
+    ents = []
+    for kind, bias, tf, h in (("fwd", True, 1100.0, 900.0), ("wgradT", False, 1000.0, 990.0)):
+        k = lt_tune.key(kind, 8192, 3072, 1024, bias)
+        ents.append({"col": dict(zip(("ta", "tb", "m", "n", "k", "epi", "beta"), k)), "names": ["s"], "tflops": tf,
+                     "heuristic_tflops": h})
+    p.write_text(json.dumps({"entries": ents}))
+    monkeypatch.setattr(lt_tune, "_table", lt_tune.load_table(str(p)))
+    monkeypatch.setattr(lt_tune, "ENABLED", True)
+    monkeypatch.setattr(lt_tune, "FWD", True)
+    monkeypatch.setattr(lt_tune, "WGRAD", True)
+    assert lt_tune.use_fwd(8192, 3072, 1024, True)  # +22 %
+    assert not lt_tune.use_wgrad_t(8192, 3072, 1024)  # +1 %: noise
+    assert not lt_tune.use_fwd(8192, 1024, 1024, True)  # no record
