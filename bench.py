@@ -86,7 +86,8 @@ def parse():
     p.add_argument("--host-moments-layers", type=str, default="auto",
                    help="Adam moments of the LM head and the last K transformer layers in pinned host memory, "
                         "streamed through HBM during the step (frees 8 B/param of HBM for the activation stash); "
-                        "auto: 2 for the 20B single-GPU bound ZeRO-3 run, else 0")
+                        "auto: 1 for the 20B single-GPU bound ZeRO-3 run (1 / 2 / 3 measured 8,936 / 8,895 / 8,647 "
+                        "tok/s, profiles/r4w_notes.md), else 0")
     p.add_argument("--fp32-reduce", type=str, default="off", choices=["on", "off"],
                    help="reduce bf16 gradients in fp32 (DeeperSpeed's bf16 default fp32_allreduce; "
                         "tests/test_zero_reduce_precision.py measures what bf16 reduction costs)")
@@ -467,7 +468,7 @@ def main():
     # forward): their Adam moments live in pinned host memory and stream through HBM on the copy
     # engines during the overlapped step, and the 8 B/param freed goes to the attention stash.
     hm = os.environ.get("DSA_BENCH_HOST_MOMENTS", args.host_moments_layers)
-    k_host = (2 if (world == 1 and args.zero == 3 and offload == "compact" and ckpt == "on" and big and on_gpu
+    k_host = (1 if (world == 1 and args.zero == 3 and offload == "compact" and ckpt == "on" and big and on_gpu
                     and not args.force_sharded and args.pipe == 1) else 0) if hm == "auto" else int(hm)
     params = model.parameters()
     host_numel = 0
