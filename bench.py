@@ -86,7 +86,8 @@ def parse():
     p.add_argument("--host-moments-layers", type=str, default="auto",
                    help="Adam moments of the LM head and the last K transformer layers in pinned host memory, "
                         "streamed through HBM during the step (frees 8 B/param of HBM for the activation stash); "
-                        "auto: 1 for the 20B single-GPU bound ZeRO-3 run (1 / 2 / 3 measured 8,936 / 8,895 / 8,647 "
+                        "head: the LM head only; auto: 1 for the 20B single-GPU bound ZeRO-3 run (1 / 2 / 3 measured "
+                        "8,936 / 8,895 / 8,647 "
                         "tok/s, profiles/r4w_notes.md), else 0")
     p.add_argument("--fp32-reduce", type=str, default="off", choices=["on", "off"],
                    help="reduce bf16 gradients in fp32 (DeeperSpeed's bf16 default fp32_allreduce; "
@@ -469,15 +470,17 @@ def main():
     # engines during the overlapped step, and the 8 B/param freed goes to the attention stash.
     hm = os.environ.get("DSA_BENCH_HOST_MOMENTS", args.host_moments_layers)
     k_host = (1 if (world == 1 and args.zero == 3 and offload == "compact" and ckpt == "on" and big and on_gpu
-                    and not args.force_sharded and args.pipe == 1) else 0) if hm == "auto" else int(hm)
+                    and not args.force_sharded and args.pipe == 1) else 0) if hm == "auto" else \
+        (0.5 if hm == "head" else int(hm))  # "head": the LM head only
     params = model.parameters()
     host_numel = 0
     if k_host > 0:
-        tail = {id(p) for m in [model.embed_out] + list(model.layers[-k_host:]) for p in m.parameters()}
+        host_mods = [model.embed_out] + (list(model.layers[-int(k_host):]) if k_host >= 1 else [])
+        tail = {id(p) for m in host_mods for p in m.parameters()}
         host_numel = sum(p.numel() for p in model.parameters() if id(p) in tail)
         params = [{"params": [p for p in model.parameters() if id(p) not in tail]},
                   {"params": [p for p in model.parameters() if id(p) in tail], "host_moments": True}]
-        log(f"host moments: LM head + last {k_host} layers = {host_numel / 1e9:.2f}B params "
+        log(f"host moments: LM head + last {int(k_host)} layers = {host_numel / 1e9:.2f}B params "
             f"({8 * host_numel / 2**30:.1f} GiB of Adam moments in pinned host memory)")
     engine, _, _, _ = ds.initialize(model=model, model_parameters=params, config_params=conf)
     del model
