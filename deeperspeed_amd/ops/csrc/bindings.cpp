@@ -96,6 +96,19 @@ void adam_multi(Tensor meta, int64_t T, int64_t total_chunks, int64_t chunk, int
 }
 
 // out[0] += sum(x^2) in fp32. workspace >= 1024 floats.
+// out[0] += sum of squares of every tensor listed in meta (see launch_sumsq_multi); partial holds
+// total_chunks floats.
+void sumsq_multi(Tensor meta, int64_t nt, int64_t total_chunks, int64_t chunk, int64_t xt, Tensor partial,
+                 Tensor out) {
+  TORCH_CHECK(meta.is_cuda() && meta.scalar_type() == at::kLong && meta.numel() == 3 * nt + 1, "sumsq_multi: meta");
+  TORCH_CHECK(partial.is_cuda() && partial.scalar_type() == at::kFloat && partial.numel() >= total_chunks,
+              "sumsq_multi: partial");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() >= 1, "sumsq_multi: out");
+  TORCH_CHECK(xt >= 0 && xt <= 2, "sumsq_multi: dtype code");
+  dsa::launch_sumsq_multi(meta.data_ptr<int64_t>(), (int)nt, total_chunks, chunk, (int)xt, partial.data_ptr<float>(),
+                          out.data_ptr<float>(), cur_stream());
+}
+
 void sumsq_accum(Tensor x, Tensor workspace, Tensor out) {
   check_dev(x, "x");
   TORCH_CHECK(workspace.numel() >= 1024 && workspace.scalar_type() == at::kFloat, "sumsq: workspace");
@@ -1158,6 +1171,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam_compact", &adam_compact);
   m.def("adam_multi", &adam_multi);
   m.def("sumsq_accum", &sumsq_accum);
+  m.def("sumsq_multi", &sumsq_multi);
   m.def("copy_narrow", &copy_narrow);
   m.def("copy_nocu", &copy_nocu, py::arg("dst"), py::arg("src"), py::arg("kind") = -1);
   m.def("scale_copy", &scale_copy, pybind11::arg("x"), pybind11::arg("y"), pybind11::arg("scale_t"),

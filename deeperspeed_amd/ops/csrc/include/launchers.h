@@ -33,6 +33,8 @@ void launch_adam_compact(void* hi, void* res, const void* g, int gt, float* m, f
 void launch_adam_multi(const int64_t* meta, int T, int64_t total_chunks, int64_t chunk, int wt, int gt, int ot,
                        AdamArgs a, hipStream_t s);
 void launch_sumsq_accum(const void* x, int xt, int64_t n, float* workspace, float* out, hipStream_t s);
+void launch_sumsq_multi(const int64_t* meta, int nt, int64_t total_chunks, int64_t chunk, int xt, float* partial,
+                        float* out, hipStream_t s);
 void launch_copy_narrow(const void* src, void* dst, int64_t bytes, int wgs, hipStream_t s);
 void launch_scale_copy(const void* x, int xt, void* y, int yt, int64_t n, const float* scale_ptr, float scale,
                        hipStream_t s, int accumulate = 0);

@@ -185,6 +185,55 @@ __global__ void __launch_bounds__(256) sum_finish_kernel(const float* __restrict
   if (threadIdx.x == 0) out[0] += acc;
 }
 
+// Multi-tensor sum of squares (the global gradient norm of a per-tensor optimizer): one block per
+// `chunk` elements of one tensor (meta = [T pointers | T numels | T+1 chunk prefix], the layout of
+// the multi-tensor LAMB), fp32 partial per block, reduced by sum_finish_kernel.  Replaces torch's
+// _foreach_norm (one multi_tensor_apply launch per ~100 tensors plus stack / square / sum kernels).
+template <typename T>
+__global__ void __launch_bounds__(256) sumsq_multi_kernel(const int64_t* __restrict__ meta, int nt, int64_t chunk,
+                                                          float* __restrict__ partial) {
+  __shared__ float red[32];
+  const int64_t* pref = meta + 2 * nt;
+  const int64_t c = blockIdx.x;
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pref[mid] <= c) lo = mid; else hi = mid - 1;
+  }
+  const T* x = reinterpret_cast<const T*>(meta[lo]);
+  const int64_t n = meta[nt + lo];
+  const int64_t start = (c - pref[lo]) * chunk;
+  const int64_t end = start + chunk < n ? start + chunk : n;
+  float acc = 0.f;
+  constexpr int N = Vec16<T>::N;
+  int64_t e0 = start;
+  if ((reinterpret_cast<uintptr_t>(x + start) & 15) == 0) {
+    const int64_t vend = start + ((end - start) / N) * N;
+    for (int64_t e = start + (int64_t)N * threadIdx.x; e < vend; e += (int64_t)N * blockDim.x) {
+      float f[N];
+      Vec16<T>::load(x + e, f);
+#pragma unroll
+      for (int k = 0; k < N; ++k) acc = fmaf(f[k], f[k], acc);
+    }
+    e0 = vend;
+  }
+  for (int64_t e = e0 + threadIdx.x; e < end; e += blockDim.x) {
+    const float f = Conv<T>::load(x, e);
+    acc = fmaf(f, f, acc);
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[c] = acc;
+}
+
+void launch_sumsq_multi(const int64_t* meta, int nt, int64_t total_chunks, int64_t chunk, int xt, float* partial,
+                        float* out, hipStream_t s) {
+  if (total_chunks <= 0) return;
+  DSA_DISPATCH_T(xt, T,
+    hipLaunchKernelGGL((sumsq_multi_kernel<T>), dim3((unsigned)total_chunks), dim3(256), 0, s, meta, nt, chunk,
+                       partial));
+  hipLaunchKernelGGL(sum_finish_kernel, dim3(1), dim3(256), 0, s, partial, (int)total_chunks, out);
+}
+
 // Byte copy on a few workgroups, for HBM -> pinned host memory: ROCclr runs such copies as a blit
 // kernel with a workgroup on EVERY CU (profiles/r4p_*), whichever hipMemcpyKind is given, and the
 // PCIe link (~50 GB/s) is the bound either way.  Each thread keeps 4 16-byte loads in flight before

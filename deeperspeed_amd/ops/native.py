@@ -343,6 +343,41 @@ def _workspace(device, n=2048):
     return ws
 
 
+_SUMSQ_CHUNK = 65536
+_sumsq_meta = {}
+
+
+def sumsq_multi_(tensors, out: torch.Tensor):
+    """out[0] += sum of squares of every tensor (one dtype, one device, contiguous) in two HIP
+    launches (multi-tensor partials + finish); CPU tensors fall back to torch."""
+    tensors = [t for t in tensors if t.numel() > 0]
+    if not tensors:
+        return out
+    t0 = tensors[0]
+    if not t0.is_cuda:
+        for t in tensors:
+            out += t.float().square().sum()
+        return out
+    code = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[t0.dtype]
+    key = tuple(t.data_ptr() for t in tensors) + tuple(t.numel() for t in tensors)
+    hit = _sumsq_meta.get(key)
+    if hit is None:
+        numels = [t.numel() for t in tensors]
+        pref = [0]
+        for n in numels:
+            pref.append(pref[-1] + (n + _SUMSQ_CHUNK - 1) // _SUMSQ_CHUNK)
+        rows = [t.data_ptr() for t in tensors] + numels + pref
+        # pinned staging + async copy (a pageable H2D copy would wait for the stream)
+        meta = torch.tensor(rows, dtype=torch.int64).pin_memory().to(t0.device, non_blocking=True)
+        hit = (meta, len(tensors), pref[-1], torch.empty(pref[-1], dtype=torch.float32, device=t0.device))
+        if len(_sumsq_meta) > 64:
+            _sumsq_meta.clear()
+        _sumsq_meta[key] = hit
+    meta, nt, total, partial = hit
+    hip_ops().sumsq_multi(meta, nt, total, _SUMSQ_CHUNK, code, partial, out)
+    return out
+
+
 def sumsq_accumulate(x: torch.Tensor, out: torch.Tensor):
     """out[0] += sum(x.float()**2) without a host sync (HIP on GPU)."""
     if x.numel() == 0:

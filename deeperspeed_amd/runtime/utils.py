@@ -125,9 +125,10 @@ def _dev():
 
 
 def grad_norm_sq_tensor(parameters, mpu=None) -> torch.Tensor:
-    """Sum of squared gradient entries as a 1-element fp32 tensor, without a host sync:
-    multi-tensor `_foreach_norm` (fp32 accumulation) over the gradients, model-parallel
-    duplicates counted once, summed over the model-parallel group."""
+    """Sum of squared gradient entries as a 1-element fp32 tensor, without a host sync: one
+    multi-tensor HIP reduction per (device, dtype) on the GPU (native.sumsq_multi_, fp32
+    accumulation; torch's `_foreach_norm` elsewhere), model-parallel duplicates counted once,
+    summed over the model-parallel group."""
     mp_rank = mpu.get_model_parallel_rank() if mpu is not None else 0
     grads = [p.grad.data for p in parameters if p.grad is not None and (mp_rank == 0 or is_model_parallel_parameter(p))]
     dev = grads[0].device if grads else _dev()
@@ -135,9 +136,13 @@ def grad_norm_sq_tensor(parameters, mpu=None) -> torch.Tensor:
     by_dev = {}
     for g in grads:
         by_dev.setdefault((g.device, g.dtype), []).append(g)
-    for (d, _), gs in by_dev.items():
-        norms = torch._foreach_norm(gs, 2, dtype=torch.float32)
-        acc += torch.stack(norms).square().sum().to(dev)
+    for (d, dt), gs in by_dev.items():
+        if d.type == "cuda" and d == acc.device and dt in (torch.float32, torch.bfloat16, torch.float16):
+            from ..ops import native
+            native.sumsq_multi_([g.contiguous() for g in gs], acc)  # two HIP launches
+        else:
+            norms = torch._foreach_norm(gs, 2, dtype=torch.float32)
+            acc += torch.stack(norms).square().sum().to(dev)
     if mpu is not None:
         dist.all_reduce(acc, group=mpu.get_model_parallel_group())
     return acc
