@@ -124,6 +124,9 @@ def _dev():
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
 
+_SUMSQ_MULTI = os.environ.get("DSA_SUMSQ_MULTI", "1") != "0"  # 0: torch _foreach_norm
+
+
 def grad_norm_sq_tensor(parameters, mpu=None) -> torch.Tensor:
     """Sum of squared gradient entries as a 1-element fp32 tensor, without a host sync: one
     multi-tensor HIP reduction per (device, dtype) on the GPU (native.sumsq_multi_, fp32
@@ -137,7 +140,8 @@ def grad_norm_sq_tensor(parameters, mpu=None) -> torch.Tensor:
     for g in grads:
         by_dev.setdefault((g.device, g.dtype), []).append(g)
     for (d, dt), gs in by_dev.items():
-        if d.type == "cuda" and d == acc.device and dt in (torch.float32, torch.bfloat16, torch.float16):
+        if (_SUMSQ_MULTI and d.type == "cuda" and d == acc.device
+                and dt in (torch.float32, torch.bfloat16, torch.float16)):
             from ..ops import native
             native.sumsq_multi_([g.contiguous() for g in gs], acc)  # two HIP launches
         else:
