@@ -35,6 +35,14 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 constexpr int BM = 64;  // rows per workgroup (16 per wave)
 constexpr int BN = 64;  // columns (keys or queries) per inner iteration
 
+// LDS row stride (elements) of the [rows][D] Q / K / V / dO tiles.  D + 8 keeps the ds_read_b128 row
+// reads conflict-free for every D; the 32x32x16 transposed reads (ds_read_b64_tr_b16, 4 rows x 4
+// lanes x 2 column halves per 32-lane half) are 2-way at D = 64 / 96 with +8 but 4-way at D = 128
+// (stride 272 B puts rows 4 banks apart); +24 (304 B) brings D = 128 to 2-way with the row reads
+// still conflict-free (rocprofv3 SQ_LDS_BANK_CONFLICT: 3.2-3.4 cycles per LDS instruction at D = 128
+// vs 1.2 at D = 96 before, profiles/r4z_notes.md).
+template <int D> constexpr int LDP = D + (D == 128 ? 24 : 8);
+
 template <typename T> struct Mfma;
 template <> struct Mfma<bf16_t> {
   __device__ __forceinline__ static f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
@@ -75,7 +83,7 @@ __device__ __forceinline__ void stage_rows(uint16_t* lds, const uint16_t* __rest
     const int r = c / CH, ch = c - r * CH;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (r0 + r < S) v = *reinterpret_cast<const uint4*>(g + (int64_t)(r0 + r) * D + ch * 8);
-    *reinterpret_cast<uint4*>(lds + r * (D + 8) + ch * 8) = v;
+    *reinterpret_cast<uint4*>(lds + r * LDP<D> + ch * 8) = v;
   }
 }
 
@@ -101,9 +109,9 @@ __global__ void __launch_bounds__(256) fwd_kernel(const uint16_t* __restrict__ Q
                                                   float* __restrict__ LSE, int S, float scale) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ks = smem;                       // [BN][D+8]
-  uint16_t* Vs = Ks + BN * (D + 8);          // [BN][D+8]
+  uint16_t* Vs = Ks + BN * LDP<D>;          // [BN][D+8]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint16_t* Ps = Vs + BN * (D + 8) + w * 16 * (BN + 8);  // per wave [16][BN+8]
+  uint16_t* Ps = Vs + BN * LDP<D> + w * 16 * (BN + 8);  // per wave [16][BN+8]
   const int g = lane >> 4, i = lane & 15;
   const int64_t bh = blockIdx.y;
   const int qb = blockIdx.x * BM;
@@ -138,7 +146,7 @@ __global__ void __launch_bounds__(256) fwd_kernel(const uint16_t* __restrict__ Q
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < D / 32; ++kk)
-        s[t] = Mfma<T>::run(qf[kk], lds_row8(Ks + (16 * t + i) * (D + 8) + 32 * kk + 8 * g), s[t]);
+        s[t] = Mfma<T>::run(qf[kk], lds_row8(Ks + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), s[t]);
     }
     // mask + online softmax (rows 4g+r of this wave, keys j0+16t+i)
     float mx[4];
@@ -243,8 +251,8 @@ __global__ void __launch_bounds__(256) bwd_dkdv_kernel(const uint16_t* __restric
                                                        float scale) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Qs = smem;                   // [BN queries][D+8]
-  uint16_t* dOs = Qs + BN * (D + 8);     // [BN][D+8]
-  float* lse_s = reinterpret_cast<float*>(dOs + BN * (D + 8));  // [BN]
+  uint16_t* dOs = Qs + BN * LDP<D>;     // [BN][D+8]
+  float* lse_s = reinterpret_cast<float*>(dOs + BN * LDP<D>);  // [BN]
   float* del_s = lse_s + BN;                                     // [BN]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint16_t* Pt = reinterpret_cast<uint16_t*>(del_s + BN) + w * 2 * 16 * (BN + 8);  // per wave P^T [16][BN+8]
@@ -286,8 +294,8 @@ __global__ void __launch_bounds__(256) bwd_dkdv_kernel(const uint16_t* __restric
       dp[t] = s[t];
 #pragma unroll
       for (int kk = 0; kk < D / 32; ++kk) {
-        s[t] = Mfma<T>::run(kf[kk], lds_row8(Qs + (16 * t + i) * (D + 8) + 32 * kk + 8 * g), s[t]);
-        dp[t] = Mfma<T>::run(vf[kk], lds_row8(dOs + (16 * t + i) * (D + 8) + 32 * kk + 8 * g), dp[t]);
+        s[t] = Mfma<T>::run(kf[kk], lds_row8(Qs + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), s[t]);
+        dp[t] = Mfma<T>::run(vf[kk], lds_row8(dOs + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), dp[t]);
       }
     }
 #pragma unroll
@@ -342,9 +350,9 @@ __global__ void __launch_bounds__(256) bwd_dq_kernel(const uint16_t* __restrict_
                                                      uint16_t* __restrict__ dQ, int S, float scale) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ks = smem;                 // [BN keys][D+8]
-  uint16_t* Vs = Ks + BN * (D + 8);    // [BN][D+8]
+  uint16_t* Vs = Ks + BN * LDP<D>;    // [BN][D+8]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint16_t* dSs = Vs + BN * (D + 8) + w * 16 * (BN + 8);  // per wave dS [16][BN+8]
+  uint16_t* dSs = Vs + BN * LDP<D> + w * 16 * (BN + 8);  // per wave dS [16][BN+8]
   const int g = lane >> 4, i = lane & 15;
   const int64_t bh = blockIdx.y;
   const int qb = blockIdx.x * BM;
@@ -383,8 +391,8 @@ __global__ void __launch_bounds__(256) bwd_dq_kernel(const uint16_t* __restrict_
       dp[t] = s[t];
 #pragma unroll
       for (int kk = 0; kk < D / 32; ++kk) {
-        s[t] = Mfma<T>::run(qf[kk], lds_row8(Ks + (16 * t + i) * (D + 8) + 32 * kk + 8 * g), s[t]);
-        dp[t] = Mfma<T>::run(of[kk], lds_row8(Vs + (16 * t + i) * (D + 8) + 32 * kk + 8 * g), dp[t]);
+        s[t] = Mfma<T>::run(qf[kk], lds_row8(Ks + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), s[t]);
+        dp[t] = Mfma<T>::run(of[kk], lds_row8(Vs + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), dp[t]);
       }
     }
 #pragma unroll
@@ -513,7 +521,7 @@ __device__ __forceinline__ void tile_store(uint16_t* lds, const uint4 (&r)[D / 3
   for (int k = 0; k < D / 32; ++k) {
     const int c = threadIdx.x + 256 * k;
     const int row = c / CH, ch = c - row * CH;
-    *reinterpret_cast<uint4*>(lds + row * (D + 8) + ch * 8) = r[k];
+    *reinterpret_cast<uint4*>(lds + row * LDP<D> + ch * 8) = r[k];
   }
 }
 
@@ -596,7 +604,7 @@ __device__ __forceinline__ uint32_t drop_pair(uint32_t hb, int q, int half_s, in
 // vector-memory instructions of the encoder kernels (fwd 31 -> 51 us at B16 H16 S512 D64)
 template <int D>
 __device__ __forceinline__ float* stage_kbias(uint16_t* smem, const float* __restrict__ kbrow, int S) {
-  float* kbs = reinterpret_cast<float*>(smem + 4 * BN2 * (D + 8));
+  float* kbs = reinterpret_cast<float*>(smem + 4 * BN2 * LDP<D>);
   for (int i = threadIdx.x; i < S / 4; i += blockDim.x)
     reinterpret_cast<float4*>(kbs)[i] = reinterpret_cast<const float4*>(kbrow)[i];
   return kbs;  // visible after the caller's first __syncthreads()
@@ -608,7 +616,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
                                                         float* __restrict__ LSE, int S, float scale, int onh,
                                                         Extra ex = Extra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int TS = BN2 * (D + 8);
+  constexpr int TS = BN2 * LDP<D>;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
@@ -683,7 +691,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks)
-        acc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), qf[ks], acc);
+        acc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), qf[ks], acc);
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[16 * t + r] = acc[r];
     }
@@ -758,9 +766,9 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
       const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
-        const uint16_t* a0 = Vs + row1 * (D + 8) + 32 * dt + 16 * (g16 & 1) + 4 * pc;
+        const uint16_t* a0 = Vs + row1 * LDP<D> + 32 * dt + 16 * (g16 & 1) + 4 * pc;
         const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * (D + 8)));
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * LDP<D>));
         o[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, pf, o[dt]);
       }
     }
@@ -809,7 +817,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
                                              uint16_t* __restrict__ dV, int S, float scale, int onh, const Extra& ex,
                                              uint16_t* __restrict__ dQ = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int TS = BN2 * (D + 8);
+  constexpr int TS = BN2 * LDP<D>;
   float* stats = reinterpret_cast<float*>(smem + 4 * TS);  // [2 stages][LSE 64 | DELTA 64]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
@@ -831,13 +839,13 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   // FQ (S <= BM2: this workgroup owns every key of the head): K [BM2][D+8] and the tile's dS
   // [BN2 queries][BM2 + 8 keys] also live in LDS, and dQ = dS K is formed per query tile here
   uint16_t* const Ks = smem + 4 * TS + 4 * BN2 * 2;
-  uint16_t* const dSs = Ks + BM2 * (D + 8);
+  uint16_t* const dSs = Ks + BM2 * LDP<D>;
   if constexpr (FQ) {
     uint4 kr2[D / 32];
     tile_load<D>(kr2, K + base, 0, S, ldi);
     tile_store<D>(Ks, kr2);
     tile_load<D>(kr2, K + base, BN2, S, ldi);
-    tile_store<D>(Ks + BN2 * (D + 8), kr2);
+    tile_store<D>(Ks + BN2 * LDP<D>, kr2);
   }
 
   s16x8 kf[D / 16], vf[D / 16];
@@ -936,8 +944,8 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
       }
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), kf[ks], sacc);
-        pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), vf[ks], pacc);
+        sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), kf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), vf[ks], pacc);
       }
       float pv[16], dsv[16];
       if constexpr (INIT) {
@@ -1002,11 +1010,11 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt) {
           const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
-          const s16x4 ox = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + row1 * (D + 8) + col));
-          const s16x4 oy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (row1 + 8) * (D + 8) + col));
+          const s16x4 ox = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + row1 * LDP<D> + col));
+          const s16x4 oy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (row1 + 8) * LDP<D> + col));
           dv[dt] = Mfma32<T>::run(s16x8{ox[0], ox[1], ox[2], ox[3], oy[0], oy[1], oy[2], oy[3]}, pf, dv[dt]);
-          const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + row1 * (D + 8) + col));
-          const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * (D + 8) + col));
+          const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + row1 * LDP<D> + col));
+          const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * LDP<D> + col));
           dk[dt] = Mfma32<T>::run(s16x8{qx[0], qx[1], qx[2], qx[3], qy[0], qy[1], qy[2], qy[3]}, sf, dk[dt]);
         }
         if constexpr (V3) __builtin_amdgcn_sched_barrier(0);  // bounds the tr-read hoisting: 0 spills vs 12
@@ -1031,8 +1039,8 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
           const s16x4 hi = *reinterpret_cast<const s16x4*>(srow + 8);
           const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
           const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
-          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * (D + 8) + col));
-          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * (D + 8) + col));
+          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * LDP<D> + col));
+          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * LDP<D> + col));
           dq = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]},
                               s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}, dq);
         }
@@ -1089,7 +1097,7 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
                                            float scale, int onh, const Extra& ex,
                                            const uint16_t* __restrict__ O = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int TS = BN2 * (D + 8);
+  constexpr int TS = BN2 * LDP<D>;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
   const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
@@ -1185,8 +1193,8 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
       for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        sacc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), qf[ks], sacc);
-        pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), of[ks], pacc);
+        sacc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), qf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), of[ks], pacc);
       }
       float dsv[16];
       if constexpr (BIAS) {
@@ -1231,8 +1239,8 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt) {
           const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
-          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * (D + 8) + col));
-          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * (D + 8) + col));
+          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * LDP<D> + col));
+          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * LDP<D> + col));
           dq[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, sf, dq[dt]);
         }
       }
@@ -1313,9 +1321,9 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_both_v2_kernel(
                                  ex);
 }
 
-template <int D> constexpr int dkdv_v2_lds() { return 2 * 2 * BN2 * (D + 8) * 2 + 2 * 2 * BN2 * 4; }
+template <int D> constexpr int dkdv_v2_lds() { return 2 * 2 * BN2 * LDP<D> * 2 + 2 * 2 * BN2 * 4; }
 // + K [BM2][D+8] and one tile's dS [BN2][BM2+8] for the fused short-sequence backward
-template <int D> constexpr int bwd_short_lds() { return dkdv_v2_lds<D>() + BM2 * (D + 8) * 2 + BN2 * (BM2 + 8) * 2; }
+template <int D> constexpr int bwd_short_lds() { return dkdv_v2_lds<D>() + BM2 * LDP<D> * 2 + BN2 * (BM2 + 8) * 2; }
 
 // Whole backward of one head in one workgroup for S <= BM2 (= 128, BERT's sequence): dK / dV
 // as in the dK/dV kernel, and dQ from the same dS tiles through LDS -- Q, K, V and dO are read
@@ -1329,11 +1337,11 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_short_kernel(
   dkdv_v2_body<T, D, false, EX, true>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh, ex, dQ);
 }
 
-template <int D> constexpr int fwd_v2_lds() { return 2 * 2 * BN2 * (D + 8) * 2; }
+template <int D> constexpr int fwd_v2_lds() { return 2 * 2 * BN2 * LDP<D> * 2; }
 
-template <int D> constexpr int fwd_lds() { return (2 * BN * (D + 8) + 4 * 16 * (BN + 8)) * 2; }
-template <int D> constexpr int dkdv_lds() { return (2 * BN * (D + 8)) * 2 + 2 * BN * 4 + 4 * 2 * 16 * (BN + 8) * 2; }
-template <int D> constexpr int dq_lds() { return (2 * BN * (D + 8) + 4 * 16 * (BN + 8)) * 2; }
+template <int D> constexpr int fwd_lds() { return (2 * BN * LDP<D> + 4 * 16 * (BN + 8)) * 2; }
+template <int D> constexpr int dkdv_lds() { return (2 * BN * LDP<D>) * 2 + 2 * BN * 4 + 4 * 2 * 16 * (BN + 8) * 2; }
+template <int D> constexpr int dq_lds() { return (2 * BN * LDP<D> + 4 * 16 * (BN + 8)) * 2; }
 
 // ======================================================================== block-sparse (LUT-driven)
 // Flash attention restricted to the active blocks of a block-sparse layout (reference:
@@ -1375,7 +1383,7 @@ __device__ __forceinline__ void stile_store(uint16_t* lds, const uint4 (&r)[8 * 
   for (int k = 0; k < 8 * D / NT; ++k) {
     const int c = threadIdx.x + NT * k;
     const int row = c / CH, ch = c - row * CH;
-    *reinterpret_cast<uint4*>(lds + row * (D + 8) + ch * 8) = r[k];
+    *reinterpret_cast<uint4*>(lds + row * LDP<D> + ch * 8) = r[k];
   }
 }
 
@@ -1455,7 +1463,7 @@ __global__ void __launch_bounds__(128, RP ? ((SX == 3 || (SX && D >= 128)) ? 1 :
                                                       int S, float scale, int onh, int H, int Hl, int shift,
                                                       SExtra sx = SExtra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int TS = STILE * (D + 8);
+  constexpr int TS = STILE * LDP<D>;
   constexpr int NT = 128;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
@@ -1519,7 +1527,7 @@ __global__ void __launch_bounds__(128, RP ? ((SX == 3 || (SX && D >= 128)) ? 1 :
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks)
-        acc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), qf[ks], acc);
+        acc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), qf[ks], acc);
 #pragma unroll
       for (int r = 0; r < 16; ++r) sv[16 * t + r] = acc[r];
     }
@@ -1581,9 +1589,9 @@ __global__ void __launch_bounds__(128, RP ? ((SX == 3 || (SX && D >= 128)) ? 1 :
       const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
-        const uint16_t* a0 = Vs + row1 * (D + 8) + 32 * dt + 16 * (g16 & 1) + 4 * pc;
+        const uint16_t* a0 = Vs + row1 * LDP<D> + 32 * dt + 16 * (g16 & 1) + 4 * pc;
         const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * (D + 8)));
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * LDP<D>));
         o[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, pf, o[dt]);
       }
     }
@@ -1628,7 +1636,7 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
                                                        float* __restrict__ ws, int nslot, int S, float scale, int onh,
                                                        int H, int Hl, int shift, SExtra sx = SExtra()) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int TS = STILE * (D + 8);
+  constexpr int TS = STILE * LDP<D>;
   constexpr int NT = 128;
   float* stats = reinterpret_cast<float*>(smem + (RP ? 4 : 2) * TS);  // [stages][LSE 64 | DELTA 64]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1724,8 +1732,8 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
       }
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), kf[ks], sacc);
-        pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), vf[ks], pacc);
+        sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), kf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), vf[ks], pacc);
       }
       float pv[16], dsv[16];
       if constexpr (SX != 0) {
@@ -1760,11 +1768,11 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdkdv_kernel(const uint16_t* 
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt) {
           const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
-          const s16x4 ox = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + row1 * (D + 8) + col));
-          const s16x4 oy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (row1 + 8) * (D + 8) + col));
+          const s16x4 ox = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + row1 * LDP<D> + col));
+          const s16x4 oy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (row1 + 8) * LDP<D> + col));
           dv[dt] = Mfma32<T>::run(s16x8{ox[0], ox[1], ox[2], ox[3], oy[0], oy[1], oy[2], oy[3]}, pf, dv[dt]);
-          const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + row1 * (D + 8) + col));
-          const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * (D + 8) + col));
+          const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + row1 * LDP<D> + col));
+          const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * LDP<D> + col));
           dk[dt] = Mfma32<T>::run(s16x8{qx[0], qx[1], qx[2], qx[3], qy[0], qy[1], qy[2], qy[3]}, sf, dk[dt]);
         }
       }
@@ -1855,7 +1863,7 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
                                                      int S, float scale, int onh, int H, int Hl, int shift,
                                                      SExtra sx = SExtra(), const uint16_t* __restrict__ O = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int TS = STILE * (D + 8);
+  constexpr int TS = STILE * LDP<D>;
   constexpr int NT = 128;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, c32 = lane & 31;
@@ -1936,8 +1944,8 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
       for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        sacc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), qf[ks], sacc);
-        pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * (D + 8) + 16 * ks + 8 * h), of[ks], pacc);
+        sacc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), qf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), of[ks], pacc);
       }
       float dsv[16];
       if constexpr (SX != 0) {
@@ -1972,8 +1980,8 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt) {
           const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
-          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * (D + 8) + col));
-          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * (D + 8) + col));
+          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * LDP<D> + col));
+          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * LDP<D> + col));
           dq[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, sf, dq[dt]);
         }
       }
@@ -1999,8 +2007,8 @@ __global__ void __launch_bounds__(128, RP ? 1 : 3) sdq_kernel(const uint16_t* __
     }
 }
 
-template <int D> constexpr int sfwd_lds(bool rp) { return (rp ? 2 : 1) * 2 * STILE * (D + 8) * 2; }
-template <int D> constexpr int sdkdv_lds(bool rp) { return (rp ? 2 : 1) * (2 * STILE * (D + 8) * 2 + 2 * STILE * 4); }
+template <int D> constexpr int sfwd_lds(bool rp) { return (rp ? 2 : 1) * 2 * STILE * LDP<D> * 2; }
+template <int D> constexpr int sdkdv_lds(bool rp) { return (rp ? 2 : 1) * (2 * STILE * LDP<D> * 2 + 2 * STILE * 4); }
 
 }  // namespace fa
 
