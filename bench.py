@@ -469,8 +469,11 @@ def main():
     # forward): their Adam moments live in pinned host memory and stream through HBM on the copy
     # engines during the overlapped step, and the 8 B/param freed goes to the attention stash.
     hm = os.environ.get("DSA_BENCH_HOST_MOMENTS", args.host_moments_layers)
+    # (only where the freed HBM buys stash: not with block-sparse attention, which the stash planner skips --
+    # there host moments only add the PCIe phase to the step, 8,565 vs 8,726 tok/s at BigBird seq 8192)
     k_host = (1 if (world == 1 and args.zero == 3 and offload == "compact" and ckpt == "on" and big and on_gpu
-                    and not args.force_sharded and args.pipe == 1) else 0) if hm == "auto" else \
+                    and not args.force_sharded and args.pipe == 1 and not args.sparse
+                    and os.environ.get("DSA_STASH", "1") != "0") else 0) if hm == "auto" else \
         (0.5 if hm == "head" else int(hm))  # "head": the LM head only
     params = model.parameters()
     host_numel = 0
