@@ -469,10 +469,10 @@ def main():
     # forward): their Adam moments live in pinned host memory and stream through HBM on the copy
     # engines during the overlapped step, and the 8 B/param freed goes to the attention stash.
     hm = os.environ.get("DSA_BENCH_HOST_MOMENTS", args.host_moments_layers)
-    # (only where the freed HBM buys stash: not with block-sparse attention, which the stash planner skips --
-    # there host moments only add the PCIe phase to the step, 8,565 vs 8,726 tok/s at BigBird seq 8192)
+    # (only where the freed HBM buys attention stash: with DSA_STASH=0 host moments only add the PCIe
+    # phase to the step)
     k_host = (1 if (world == 1 and args.zero == 3 and offload == "compact" and ckpt == "on" and big and on_gpu
-                    and not args.force_sharded and args.pipe == 1 and not args.sparse
+                    and not args.force_sharded and args.pipe == 1
                     and os.environ.get("DSA_STASH", "1") != "0") else 0) if hm == "auto" else \
         (0.5 if hm == "head" else int(hm))  # "head": the LM head only
     params = model.parameters()
@@ -554,7 +554,7 @@ def main():
         HBM left above the allocator's reserved peak (minus a margin) keeps the attention
         q, k, v, output and LSE of as many layers as fit (NeoXAttention.stash_outputs), so their
         recompute skips the QKV GEMM, rotary split and flash forward."""
-        if not cfg.checkpoint_activations or args.sparse or not on_gpu or os.environ.get("DSA_STASH", "1") == "0":
+        if not cfg.checkpoint_activations or not on_gpu or os.environ.get("DSA_STASH", "1") == "0":
             return 0
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4

@@ -300,12 +300,17 @@ class NeoXAttention(nn.Module):
             qkv = self.query_key_value(x)
             q, k, v = rotary_split(qkv, cfg.num_heads, cfg.head_dim, cfg.rotary_dim, cfg.rotary_base, qscale=qs,
                                    stash=stash[:3])
-            ctx = native.flash_attention(q, k, v, True, 1.0, out_layout="bshd", stash=stash[3:])
+            if self._sparsity is not None:
+                from ..ops.sparse_attention import flash as sflash
+                ctx = sflash.sparse_flash_attention(q, k, v, self._sparse_ops(S)[3], 1.0, out_bshd=True,
+                                                    stash=stash[3:])
+            else:
+                ctx = native.flash_attention(q, k, v, True, 1.0, out_layout="bshd", stash=stash[3:])
             return self.dense(ctx.reshape(B, S, H))
         qkv = self.query_key_value(x)
         q, k, v = rotary_split(qkv, cfg.num_heads, cfg.head_dim, cfg.rotary_dim, cfg.rotary_base, qscale=qs)
         if self._sparsity is not None:
-            ctx = self._sparse_attention(q, k, v)
+            ctx = self._sparse_attention(q, k, v, key)
             if ctx.shape[1] == S:  # fused kernel wrote the token-major [B, S, H, D] layout
                 return self.dense(ctx.reshape(B, S, H))
         else:
@@ -347,13 +352,25 @@ class NeoXAttention(nn.Module):
                                Softmax(layout, blk), lut)
         return self._sp_ops[S]
 
-    def _sparse_attention(self, q, k, v):
+    def _sparse_attention(self, q, k, v, key=None):
         """Block-sparse causal attention (q is pre-scaled).  On the GPU one fused kernel walks the
         layout's active tiles and returns [B, S, H, D]; otherwise SDD -> causal sparse softmax ->
-        DSD returns [B, H, S, D]."""
+        DSD returns [B, H, S, D].  With stash_outputs, the checkpointed first forward keeps q, k,
+        v, the output and the LSE for the recompute (as the dense path does)."""
         sdd, dsd, softmax, lut = self._sparse_ops(q.shape[2])
         from ..ops.sparse_attention import flash as sflash
         if self.cfg.attention_dropout == 0.0 and sflash.supported(q, lut):
+            if self.stash_outputs and ds_ckpt.is_checkpoint_forward() and key is not None:
+                ctx, lse = sflash.sparse_flash_fwd_lse(q, k, v, lut, 1.0, out_bshd=True)
+                if key in self._stash or len(self._stash) >= self._STASH_LIMIT:
+                    raise RuntimeError(f"layer {self.layer_number}: selective-recompute stash for this input "
+                                       f"was never consumed (forward without backward?)")
+                if self.stash_offload:
+                    from ..runtime.activation_checkpointing.host_stash import host_stash
+                    self._stash[key] = host_stash().park(id(self), (q, k, v, ctx, lse))
+                else:
+                    self._stash[key] = (q, k, v, ctx, lse)
+                return ctx
             return sflash.sparse_flash_attention(q, k, v, lut, 1.0, out_bshd=True)
         w = softmax(sdd(q, k), scale=1.0, causal=True)
         return dsd(w, v)

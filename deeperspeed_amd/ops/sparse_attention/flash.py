@@ -281,9 +281,39 @@ class _SparseFlash(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None
 
 
+class _StashedSparseFlash(_SparseFlash):
+    """Recompute-time stand-in (selective recompute): (o, lse) kept from the checkpointed first
+    forward (`sparse_flash_fwd_lse`); the backward is _SparseFlash's."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, lut, scale, out_bshd, kbias, ebias, stash):
+        o, lse = stash
+        ctx.save_for_backward(q.contiguous(), k.contiguous(), v.contiguous(), o, lse)
+        ctx.lut, ctx.scale, ctx.out_bshd = lut, float(scale), bool(out_bshd)
+        ctx.kbias, ctx.ebias = kbias, ebias
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        return _SparseFlash.backward(ctx, do) + (None,)
+
+
+def sparse_flash_fwd_lse(q, k, v, lut: SparseFlashLUT, scale: float = 1.0, out_bshd: bool = False,
+                         kbias: Optional[torch.Tensor] = None, ebias: Optional[torch.Tensor] = None):
+    """Forward only (no autograd): (o, lse) for a later stashed backward (selective recompute)."""
+    from .. import native
+    rp, cols, masks = lut.device_tensors(q.device)[:3]
+    return native.hip_ops().sparse_flash_fwd(q.contiguous(), k.contiguous(), v.contiguous(), rp, cols, masks,
+                                             lut.heads, lut.causal, float(scale), lut.shift, bool(out_bshd), kbias,
+                                             ebias)
+
+
 def sparse_flash_attention(q, k, v, lut: SparseFlashLUT, scale: float = 1.0, out_bshd: bool = False,
-                           kbias: Optional[torch.Tensor] = None, ebias: Optional[torch.Tensor] = None):
+                           kbias: Optional[torch.Tensor] = None, ebias: Optional[torch.Tensor] = None, stash=None):
     """softmax(scale * Q K^T [+ kbias[b, key] + ebias[b, h, q, key]] restricted to the layout
     [+ causal]) V for q, k, v [B, H, S, D]; returns [B, H, S, D], or [B, S, H, D] with out_bshd.
-    kbias / ebias: see `score_biases` (rows with no unmasked key give 0)."""
+    kbias / ebias: see `score_biases` (rows with no unmasked key give 0).
+    stash: (o, lse) from sparse_flash_fwd_lse of the same inputs (selective recompute)."""
+    if stash is not None:
+        return _StashedSparseFlash.apply(q, k, v, lut, scale, out_bshd, kbias, ebias, tuple(stash))
     return _SparseFlash.apply(q, k, v, lut, scale, out_bshd, kbias, ebias)

@@ -8,11 +8,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _grads(stash_layers, offload=False):
+def _grads(stash_layers, offload=False, sparse=None):
     from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
     torch.manual_seed(0)
+    extra = {"sparse_attention": {"mode": sparse, "block": 16}} if sparse else {}
     cfg = get_config("tiny", hidden_size=384, num_heads=4, num_layers=3, max_seq_len=128,
-                     checkpoint_activations=True)
+                     checkpoint_activations=True, **extra)
     model = GPTNeoX(cfg, device="cuda", dtype=torch.bfloat16).train()
     layers = [m for m in model.modules() if type(m).__name__ == "NeoXTransformerLayer"]
     for m in layers[:stash_layers]:
@@ -34,6 +35,18 @@ def test_stash_matches_full_recompute(offload):
     back by the recompute of the layer above) give the full-recompute gradients."""
     l0, g0 = _grads(0)
     l1, g1 = _grads(3 if offload else 2, offload)
+    assert l0 == l1
+    assert g0.keys() == g1.keys()
+    for n in g0:
+        torch.testing.assert_close(g1[n], g0[n], atol=1e-3, rtol=1e-3, msg=n)
+
+
+@pytest.mark.parametrize("sparse", ["bigbird", "fixed"])
+def test_sparse_stash_matches_full_recompute(sparse):
+    """Block-sparse attention (fused LUT kernels): the stashed (o, lse) of the first forward
+    give the full-recompute gradients."""
+    l0, g0 = _grads(0, sparse=sparse)
+    l1, g1 = _grads(2, sparse=sparse)
     assert l0 == l1
     assert g0.keys() == g1.keys()
     for n in g0:
