@@ -53,6 +53,8 @@ HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "stream")
 # torch copy_, a ROCclr blit kernel with a workgroup on every CU, which measured faster in the step
 # (8,787 vs 8,720 tok/s with dedicated queues, profiles/r4s_notes.md)
 HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "0"))
+# optimizer offload (states all / master / moments, NVMe): copy streams on dedicated hardware queues
+OFFLOAD_DEDICATED_STREAMS = os.environ.get("DSA_OFFLOAD_DEDICATED_STREAMS", "1") != "0"
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
 CPU_STEP_PIECE = int(16 * 1024 * 1024)  # elements per CPU-Adam piece of the pipelined offload step
@@ -743,7 +745,12 @@ class ShardedOptimizerBase:
         return self._copy_streams
 
     def _new_stream(self):
-        from ..overlap_step import new_stream
+        from ..overlap_step import dedicated_stream, new_stream
+        if self.offload is not None and OFFLOAD_DEDICATED_STREAMS:
+            # an offloaded step IS the critical path (nothing computes beside it): its copy
+            # streams get hardware queues of their own, or a copy stream's waits can stall the
+            # compute stream's Adam kernels behind them in a shared queue (profiles/r4ag_notes.md)
+            return dedicated_stream(self.device)
         return new_stream(self.device)
 
     def _offload_step(self, grad_scale: float):
