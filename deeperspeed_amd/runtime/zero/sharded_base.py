@@ -57,6 +57,8 @@ HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "0"))
 OFFLOAD_DEDICATED_STREAMS = os.environ.get("DSA_OFFLOAD_DEDICATED_STREAMS", "1") != "0"
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
+# device staging slots of the states="moments" step (each holds one piece of m and v)
+OFFLOAD_NBUF = int(os.environ.get("DSA_OFFLOAD_NBUF", "3"))
 CPU_STEP_PIECE = int(16 * 1024 * 1024)  # elements per CPU-Adam piece of the pipelined offload step
 
 
@@ -819,7 +821,7 @@ class ShardedOptimizerBase:
         (stream B); three device staging slots keep both copy engines and the kernel busy."""
         h2d, d2h = self._streams()
         cur = torch.cuda.current_stream()
-        nbuf = 3
+        nbuf = OFFLOAD_NBUF
         piece = min(OFFLOAD_SUBCHUNK // 2, max(b.chunk for g in self.groups for b in g.buckets))
         stages = [(torch.empty(piece, dtype=torch.float32, device=self.device),
                    torch.empty(piece, dtype=torch.float32, device=self.device)) for _ in range(nbuf)]
