@@ -58,7 +58,7 @@ OFFLOAD_DEDICATED_STREAMS = os.environ.get("DSA_OFFLOAD_DEDICATED_STREAMS", "1")
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
 # device staging slots of the states="moments" step (each holds one piece of m and v)
-OFFLOAD_NBUF = int(os.environ.get("DSA_OFFLOAD_NBUF", "3"))
+OFFLOAD_NBUF = int(os.environ.get("DSA_OFFLOAD_NBUF", "6"))  # 6 vs 3: +4 % at 30.3B (profiles/r4ag_notes.md)
 CPU_STEP_PIECE = int(16 * 1024 * 1024)  # elements per CPU-Adam piece of the pipelined offload step
 
 
