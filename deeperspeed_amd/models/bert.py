@@ -9,6 +9,14 @@ Encoder layers are `ops.transformer.DeepSpeedTransformerLayer` (HIP LayerNorm, b
 masked softmax, Philox dropout, bias+dropout+residual kernels, hipBLASLt GEMMs).  The MLM decoder
 is tied to the word embedding and evaluated only on the gathered masked positions; its
 cross-entropy is the fused HIP kernel.
+
+Progressive layer dropping (PLD, reference: deepspeed/runtime/progressive_layer_drop.py and the
+engine's forward kwargs, deepspeed/runtime/engine.py `progressive_layer_drop` / `pld_theta`): the
+engine passes `progressive_layer_drop=True, pld_theta=theta(t)`; in training, encoder layer i
+(1-based) of L runs with keep probability 1 - i / L * (1 - theta) and is an identity otherwise
+(pre-LN layers are residual blocks, so a dropped layer passes its input through).  The draws come
+from a host generator seeded by the config, so every data-parallel rank skips the same layers
+(their gradient buckets stay aligned) without a collective.
 """
 
 from __future__ import annotations
@@ -97,8 +105,17 @@ class BertForPreTraining(nn.Module):
             nn.init.normal_(m.weight, 0.0, cfg.init_range)
             nn.init.zeros_(m.bias)
         self.to(device=device, dtype=dtype)
+        self._pld_gen = torch.Generator().manual_seed(cfg.seed)
+        self.pld_kept = []  # layers run by the last PLD forward (tests / diagnostics)
 
-    def encode(self, input_ids, token_type_ids=None, attention_mask=None):
+    def _pld_keep(self, theta: float):
+        """Bernoulli keep mask over the encoder layers for one PLD forward."""
+        L = len(self.layers)
+        u = torch.rand(L, generator=self._pld_gen).tolist()
+        return [u[i] < 1.0 - (i + 1) / L * (1.0 - theta) for i in range(L)]
+
+    def encode(self, input_ids, token_type_ids=None, attention_mask=None, progressive_layer_drop=False,
+               pld_theta=1.0):
         B, S = input_ids.shape
         pos = torch.arange(S, device=input_ids.device)
         x = self.word_embeddings(input_ids) + self.position_embeddings(pos)[None]
@@ -109,15 +126,19 @@ class BertForPreTraining(nn.Module):
         ext = None
         if attention_mask is not None:
             ext = ((1.0 - attention_mask.to(x.dtype)) * -10000.0)[:, None, None, :]
-        for layer in self.layers:
-            x = layer(x, ext)
+        keep = self._pld_keep(pld_theta) if progressive_layer_drop and self.training else None
+        if keep is not None:
+            self.pld_kept = [i for i, k in enumerate(keep) if k]
+        for i, layer in enumerate(self.layers):
+            if keep is None or keep[i]:
+                x = layer(x, ext)
         if self.final_ln is not None:
             x = self.final_ln(x)
         return x
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, masked_positions=None, masked_labels=None,
-                next_sentence_labels=None):
-        x = self.encode(input_ids, token_type_ids, attention_mask)
+                next_sentence_labels=None, progressive_layer_drop=False, pld_theta=1.0):
+        x = self.encode(input_ids, token_type_ids, attention_mask, progressive_layer_drop, pld_theta)
         B, S, H = x.shape
         if masked_positions is None:
             masked_positions = torch.arange(S, device=x.device)[None].expand(B, S)

@@ -25,10 +25,27 @@ class BertSparseSelfAttention(nn.Module):
         x = x.view(*x.size()[:-1], self.num_attention_heads, self.attention_head_size)
         return x.permute(0, 2, 1, 3)
 
-    def forward(self, hidden_states, attention_mask):
+    def forward(self, hidden_states, attention_mask=None, *args, **kwargs):
+        """attention_mask: additive key-padding mask ([B, S] or HF's extended [B, 1, 1, S]).
+
+        Called the way current HuggingFace BertAttention calls its self-attention (keyword
+        arguments such as encoder_hidden_states / past_key_values, an (output, weights) pair
+        expected back) it returns (context, None); called as the reference's
+        layer(hidden_states, attention_mask) it returns the context tensor."""
+        if kwargs.get("encoder_hidden_states") is not None:
+            raise NotImplementedError("block-sparse attention is self-attention only")
         q = self.transpose_for_scores(self.query(hidden_states))
         k = self.transpose_for_scores(self.key(hidden_states))
         v = self.transpose_for_scores(self.value(hidden_states))
+        if attention_mask is not None and attention_mask.dim() == 4 and attention_mask.size(-2) > 1:
+            # current HF passes the padding mask expanded over the query rows ([B, 1, S, S]); for
+            # an encoder every row is the same key-padding row
+            attention_mask = attention_mask[:, :, :1, :]
+        if attention_mask is not None and attention_mask.is_floating_point():
+            # HF fills masked keys with the dtype's minimum; the reference convention is -10000
+            # (finite after the log2(e) scaling inside the kernels)
+            attention_mask = attention_mask.clamp(min=-10000.0)
         ctx = self.sparse_self_attention(q, k, v, key_padding_mask=attention_mask)
         ctx = ctx.permute(0, 2, 1, 3).contiguous()
-        return ctx.view(*ctx.size()[:-2], self.all_head_size)
+        ctx = ctx.view(*ctx.size()[:-2], self.all_head_size)
+        return (ctx, None) if (args or kwargs) else ctx

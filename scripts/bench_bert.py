@@ -38,7 +38,14 @@ def main():
     ap.add_argument("--overlap-step", choices=["on", "off"], default="off",
                     help="run the LAMB step on a side stream overlapped with the next forward "
                          "(zero_optimization.overlap_step; identical math)")
+    ap.add_argument("--pld", type=float, default=0.0,
+                    help="progressive layer dropping with this theta (BASELINE.md row 20; 0 = off)")
+    ap.add_argument("--pld-gamma", type=float, default=1.0,
+                    help="PLD decay rate; the default reaches theta within the warmup steps, so the timed "
+                         "steps measure the steady state (the reference's default 0.001 gets there after ~5k steps)")
     args = ap.parse_args()
+    if args.pld and (args.hip_graphs == "on" or args.overlap_step == "on"):
+        raise SystemExit("--pld runs the eager encoder (graphs / overlapped-step hooks assume every layer runs)")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29541")
     os.environ.setdefault("RANK", "0")
@@ -59,6 +66,8 @@ def main():
             # the reference's BERT configs clip at 1.0 (tests/model/BingBertSquad/*_config.json)
             "gradient_clipping": 1.0,
             "zero_optimization": {"stage": 0, "overlap_step": args.overlap_step == "on"}}
+    if args.pld:
+        conf["progressive_layer_drop"] = {"enabled": True, "theta": args.pld, "gamma": args.pld_gamma}
     B, S = args.batch, args.seq
     if args.hip_graphs == "on" and dev.type == "cuda":
         # captured before initialize: overlap_step registers forward pre-hooks, which
@@ -81,8 +90,11 @@ def main():
     lab = torch.randint(0, cfg.vocab_size, (B, npred), device=dev, generator=g)
     nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
 
+    kept = []
+
     def step():
         loss = engine(ids, tt, am, pos, lab, nsp)
+        kept.append(len(model.pld_kept) if args.pld else cfg.num_layers)
         engine.backward(loss)
         engine.step()
         return loss
@@ -93,6 +105,7 @@ def main():
         torch.cuda.synchronize()
         from deeperspeed_amd.ops import native
         native.hip_ops().profile_marker(1)  # timed-region trace markers (scripts/prof_summary.py --timed)
+    kept.clear()
     t0 = time.time()
     for _ in range(args.steps):
         loss = step()
@@ -122,13 +135,18 @@ def main():
                     for fr in e.stack:
                         f.write(f"    {fr}\n")
     sps = B / dt
-    tflops = sps * cfg.flops_per_sample(S, npred) / 1e12
+    run = sum(kept[:args.steps]) / max(1, min(len(kept), args.steps))
+    import dataclasses
+    # FLOPs of the layers that ran (PLD skips some); linear in the layer count
+    tflops = sps * dataclasses.replace(cfg, num_layers=run).flops_per_sample(S, npred) / 1e12
     ref = REF.get(S)
     print(json.dumps({"metric": f"BERT pre-training samples/s ({args.model}, seq {S})", "value": round(sps, 1),
                       "unit": "samples/s", "ms_per_step": round(dt * 1e3, 2), "batch": B, "seq": S,
                       "masked_per_seq": npred, "model_tflops": round(tflops, 1), "dtype": "bf16",
                       "optimizer": "FusedLamb", "overlap_step": args.overlap_step == "on",
                       "hip_graphs": args.hip_graphs == "on",
+                      "pld_theta": args.pld or None,
+                      "mean_layers_run": round(run, 2),
                       "gradient_clipping": 1.0, "data": "synthetic", "final_loss": round(float(loss.detach()), 4),
                       "ref_v100_samples_per_s": ref[0] if ref else None,
                       "vs_ref_v100": round(sps / ref[0], 2) if ref else None}), flush=True)

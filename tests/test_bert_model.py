@@ -46,3 +46,47 @@ def _train(out_dir):
 
 def test_bert_pretraining_trains_with_lamb(tmp_path):
     run_distributed(_train, 1, str(tmp_path))
+
+
+def _train_pld(out_dir):
+    import torch.distributed as dist
+
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.bert import BertForPreTraining, get_config
+    torch.manual_seed(0)
+    cfg = get_config("tiny", num_layers=6, hidden_dropout=0.0, attn_dropout=0.0)
+    model = BertForPreTraining(cfg)
+    conf = {"train_micro_batch_size_per_gpu": 2, "optimizer": {"type": "Lamb", "params": {"lr": 1e-2}},
+            "progressive_layer_drop": {"enabled": True, "theta": 0.5, "gamma": 0.5}}
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    rank = dist.get_rank()
+    g = torch.Generator().manual_seed(1 + rank)  # different data per rank, same layer draws
+    kept, thetas = [], []
+    for _ in range(12):
+        ids = torch.randint(0, cfg.vocab_size, (2, 32), generator=g)
+        pos = torch.stack([torch.randperm(32, generator=g)[:5].sort().values for _ in range(2)])
+        lab = torch.randint(0, cfg.vocab_size, (2, 5), generator=g)
+        nsp = torch.randint(0, 2, (2,), generator=g)
+        thetas.append(engine.progressive_layer_drop.get_theta())
+        loss = engine(ids, None, torch.ones(2, 32, dtype=torch.long), pos, lab, nsp)
+        kept.append(list(model.pld_kept))
+        engine.backward(loss)
+        engine.step()
+        assert torch.isfinite(loss)
+    assert thetas[0] == 1.0 and thetas[-1] < 0.51, thetas
+    assert kept[0] == list(range(6))  # theta 1: every layer runs
+    assert any(len(k) < 6 for k in kept), kept
+    everyone = [None] * dist.get_world_size()
+    dist.all_gather_object(everyone, kept)
+    assert all(k == everyone[0] for k in everyone)  # every rank skipped the same layers
+    for p in model.parameters():  # and the replicas stayed identical
+        ps = [torch.empty_like(p.data) for _ in range(dist.get_world_size())]
+        dist.all_gather(ps, p.data.contiguous())
+        assert all(torch.equal(ps[0], q) for q in ps)
+    model.eval()
+    model(ids, progressive_layer_drop=True, pld_theta=0.0)  # eval: PLD never applies
+    assert model.pld_kept == kept[-1]
+
+
+def test_progressive_layer_drop_skips_same_layers_on_every_rank(tmp_path):
+    run_distributed(_train_pld, 2, str(tmp_path))

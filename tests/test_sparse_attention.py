@@ -224,3 +224,24 @@ def test_dsd_row_segments_cover_every_block_once():
         lens = (seg[:, 2] - seg[:, 1]).tolist()
         assert lens == sorted(lens, reverse=True)
     assert L.segments(True)[2] > 0  # the global key columns are split when walked transposed
+
+
+def test_hf_bert_with_sparse_self_attention_matches_dense():
+    """SparseAttentionUtils on the installed HuggingFace BertModel (its current attention call:
+    keyword arguments, an (output, weights) pair back, a [B, 1, S, S] dtype-min padding mask):
+    a layout that covers every block must equal HF's own eager attention, padding included."""
+    transformers = pytest.importorskip("transformers")
+    cfg = transformers.BertConfig(hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=128,
+                                  max_position_embeddings=128, vocab_size=100, attn_implementation="eager")
+    torch.manual_seed(0)
+    m = transformers.BertModel(cfg).eval()
+    ids = torch.randint(0, 100, (2, 128))
+    am = torch.ones(2, 128, dtype=torch.long)
+    am[0, 96:] = 0
+    ref = m(ids, attention_mask=am).last_hidden_state
+    holder = type("Holder", (), {})()
+    holder.bert, holder.config = m, cfg
+    sa.SparseAttentionUtils.replace_model_self_attention_with_sparse_self_attention(
+        holder, 128, sa.FixedSparsityConfig(num_heads=4, block=16, num_local_blocks=8, attention="bidirectional"))
+    assert isinstance(m.encoder.layer[0].attention.self, sa.BertSparseSelfAttention)
+    torch.testing.assert_close(m(ids, attention_mask=am).last_hidden_state, ref, atol=1e-5, rtol=1e-5)
