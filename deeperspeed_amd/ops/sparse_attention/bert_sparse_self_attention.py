@@ -19,7 +19,10 @@ class BertSparseSelfAttention(nn.Module):
         self.query = nn.Linear(config.hidden_size, self.all_head_size)
         self.key = nn.Linear(config.hidden_size, self.all_head_size)
         self.value = nn.Linear(config.hidden_size, self.all_head_size)
-        self.sparse_self_attention = SparseSelfAttention(sparsity_config)
+        # layouts sized for the model's positions (the reference keeps SparseSelfAttention's
+        # 2048 default here, which caps BERT at 2048 tokens)
+        self.sparse_self_attention = SparseSelfAttention(
+            sparsity_config, max_seq_length=max(2048, int(getattr(config, "max_position_embeddings", 2048) or 2048)))
 
     def transpose_for_scores(self, x):
         x = x.view(*x.size()[:-1], self.num_attention_heads, self.attention_head_size)

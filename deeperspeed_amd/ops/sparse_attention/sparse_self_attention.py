@@ -43,6 +43,9 @@ class SparseSelfAttention(nn.Module):
         if L % block != 0:
             raise ValueError(f"Sequence Length, {L}, needs to be dividable by Block size {block}!")
         nb = L // block
+        if nb > self.master_layout.shape[-1]:
+            raise RuntimeError(f"sequence length {L} exceeds this SparseSelfAttention's max_seq_length "
+                               f"({self.master_layout.shape[-1] * block}); build it with a larger max_seq_length")
         return self.master_layout[..., :nb, :nb].cpu()
 
     def get_ops(self, H, L):

@@ -30,8 +30,8 @@ PRESETS = {"bert-large": dict(hidden_size=1024, num_hidden_layers=24, num_attent
            "bert-base": dict(hidden_size=768, num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072)}
 SEQS = {"dense": [2048, 4096, 6144, 8192, 10240, 12288, 16384, 20480, 24576, 32768],
         "sparse": [8192, 16384, 32768, 65536, 98304, 131072, 163840, 196608, 229376, 262144, 327680, 393216],
-        # dense flash attention is O(S^2) work: stop at 256k (a pass there takes ~1 min)
-        "flash": [8192, 16384, 32768, 65536, 131072, 196608, 262144]}
+        # dense flash attention is O(S^2) work: stop at 320k (a pass there takes ~70 s)
+        "flash": [8192, 16384, 32768, 65536, 131072, 196608, 262144, 327680]}
 
 
 def attempt(variant, model_name, S, block):
@@ -49,15 +49,17 @@ def attempt(variant, model_name, S, block):
                                       **shape)
         m = transformers.BertModel(cfg, add_pooling_layer=False).to(dev, torch.bfloat16).train()
         if variant == "sparse":
-            from deeperspeed_amd.ops.sparse_attention import BigBirdSparsityConfig, SparseAttentionUtils
+            from deeperspeed_amd.ops.sparse_attention import (BigBirdSparsityConfig, SparseAttentionUtils,
+                                                              SparseSelfAttention)
             holder = type("Holder", (), {})()
             holder.bert, holder.config = m, cfg
-            SparseAttentionUtils.replace_model_self_attention_with_sparse_self_attention(
-                holder, S, BigBirdSparsityConfig(num_heads=shape["num_attention_heads"], block=block,
-                                                 num_random_blocks=1, num_sliding_window_blocks=3,
-                                                 num_global_blocks=1, attention="bidirectional"))
-            # one layout / LUT for all layers (each layer would otherwise draw and walk its own)
-            shared = m.encoder.layer[0].attention.self.sparse_self_attention
+            sc = BigBirdSparsityConfig(num_heads=shape["num_attention_heads"], block=block, num_random_blocks=1,
+                                       num_sliding_window_blocks=3, num_global_blocks=1, attention="bidirectional")
+            # the utils swap HF's self-attention modules (their layouts sized for 2048 positions),
+            # then one SparseSelfAttention sized for S serves every layer: one [H, S/64, S/64] layout
+            # and one LUT instead of 24 (host memory / build time at S ~ 300k)
+            SparseAttentionUtils.replace_model_self_attention_with_sparse_self_attention(holder, 2048, sc)
+            shared = SparseSelfAttention(sc, max_seq_length=S)
             for lyr in m.encoder.layer:
                 lyr.attention.self.sparse_self_attention = shared
         run = lambda ids: m(ids).last_hidden_state  # noqa: E731
