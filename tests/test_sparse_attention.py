@@ -245,3 +245,15 @@ def test_hf_bert_with_sparse_self_attention_matches_dense():
         holder, 128, sa.FixedSparsityConfig(num_heads=4, block=16, num_local_blocks=8, attention="bidirectional"))
     assert isinstance(m.encoder.layer[0].attention.self, sa.BertSparseSelfAttention)
     torch.testing.assert_close(m(ids, attention_mask=am).last_hidden_state, ref, atol=1e-5, rtol=1e-5)
+
+
+def test_sparse_self_attention_rejects_sequences_past_its_layout():
+    """A sequence longer than max_seq_length raises instead of silently using a truncated layout;
+    BertSparseSelfAttention sizes its layout from the model's max_position_embeddings."""
+    from types import SimpleNamespace
+    attn = sa.SparseSelfAttention(sa.FixedSparsityConfig(num_heads=2, block=16), max_seq_length=64)
+    with pytest.raises(RuntimeError, match="max_seq_length"):
+        attn.get_layout(128)
+    cfg = SimpleNamespace(hidden_size=32, num_attention_heads=2, max_position_embeddings=4096)
+    layer = sa.BertSparseSelfAttention(cfg, sa.FixedSparsityConfig(num_heads=2, block=64))
+    assert layer.sparse_self_attention.get_layout(4096).shape[-1] == 64
