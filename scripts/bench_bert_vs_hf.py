@@ -36,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="384x32,128x64", help="seqxbatch list")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     args = ap.parse_args()
     import transformers
 
@@ -55,7 +56,7 @@ def main():
         def step_ours():
             ours.encode(ids, tt, am).float().sum().backward()
 
-        res["dsa_ms"] = round(time_it(step_ours, args.iters), 2)
+        res["dsa_ms"] = round(time_it(step_ours, args.iters, args.warmup), 2)
         del ours
         torch.cuda.empty_cache()
         for impl in ("sdpa", "eager"):
@@ -67,7 +68,7 @@ def main():
             def step_hf():
                 hf(input_ids=ids, token_type_ids=tt, attention_mask=am).last_hidden_state.float().sum().backward()
 
-            res[f"hf_{impl}_ms"] = round(time_it(step_hf, args.iters), 2)
+            res[f"hf_{impl}_ms"] = round(time_it(step_hf, args.iters, args.warmup), 2)
             res[f"speedup_vs_hf_{impl}"] = round(res[f"hf_{impl}_ms"] / res["dsa_ms"], 2)
             del hf
             torch.cuda.empty_cache()
