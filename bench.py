@@ -129,8 +129,10 @@ def log(msg):
 # timed step (one stderr line + a file the spawning parent watches) and a watchdog thread ends
 # the rank -- after printing its last heartbeat and every thread's Python stack -- when no beat
 # came for DSA_BENCH_WATCHDOG_S seconds.  Its non-zero exit makes torchrun, or spawn_ranks
-# below, stop the whole job.
-WATCHDOG_S = float(os.environ.get("DSA_BENCH_WATCHDOG_S", "480"))
+# below, stop the whole job.  Warmup steps beat once per micro-batch phase (forward / backward /
+# step), so the default limit stays below a 180 s silence guard of the job's supervisor and a
+# stall leaves every rank's stacks behind, not a killed job without evidence.
+WATCHDOG_S = float(os.environ.get("DSA_BENCH_WATCHDOG_S", "150"))
 PG_TIMEOUT_S = float(os.environ.get("DSA_BENCH_PG_TIMEOUT_S", "600"))
 
 
@@ -156,10 +158,11 @@ class Heartbeat:
                 f.write(f"{self.t:.3f} {self.last}\n")
             os.replace(tmp, self.path)
 
-    def beat(self, what, **info):
+    def beat(self, what, quiet=False, **info):
         self.last = what + "".join(f" {k}={v}" for k, v in info.items())
         self.t = time.time()
-        print(f"[hb] rank={self.rank} {self.last}", file=sys.stderr, flush=True)
+        if not quiet:
+            print(f"[hb] rank={self.rank} {self.last}", file=sys.stderr, flush=True)
         self._write()
 
     def _watch(self):
@@ -171,6 +174,11 @@ class Heartbeat:
                 print(f"[bench] WATCHDOG rank {self.rank}: no progress for {idle:.0f}s "
                       f"(limit {self.limit:.0f}s, DSA_BENCH_WATCHDOG_S); last heartbeat: {self.last}; "
                       f"Python stacks follow", file=sys.stderr, flush=True)
+                try:
+                    from deeperspeed_amd.utils import comm
+                    print(f"[bench] WATCHDOG rank {self.rank}: {comm.progress()}", file=sys.stderr, flush=True)
+                except Exception:  # noqa: BLE001 - diagnostics only
+                    pass
                 faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
                 sys.stderr.flush()
                 os._exit(124)
@@ -523,6 +531,7 @@ def main():
                 r = fn()
                 sync()
                 ph[name] += time.time() - t
+                hb.beat(f"warmup micro {i} {name} done", s=round(time.time() - t, 2), quiet=not verbose_hb)
                 if name == "fwd":
                     loss = r
                 if memtrace:
@@ -531,6 +540,7 @@ def main():
         return loss, ph
 
     memtrace = os.environ.get("DSA_MEMTRACE", "0") == "1" and on_gpu
+    verbose_hb = world > 1 or os.environ.get("DSA_BENCH_VERBOSE_HB", "0") == "1"
     if memtrace:  # per-layer activation footprint of the first forward (planner calibration)
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         marks = []

@@ -374,6 +374,11 @@ def sumsq_multi_(tensors, out: torch.Tensor):
             _sumsq_meta.clear()
         _sumsq_meta[key] = hit
     meta, nt, total, partial = hit
+    # the cache may drop these on a later call while this stream still reads them: tie their
+    # reuse to the stream that consumes them (the norm can run on an overlap / side stream)
+    cur = torch.cuda.current_stream(t0.device)
+    meta.record_stream(cur)
+    partial.record_stream(cur)
     hip_ops().sumsq_multi(meta, nt, total, _SUMSQ_CHUNK, code, partial, out)
     return out
 

@@ -52,14 +52,16 @@ class AmpState:
         self.enabled = self.opt_level != "O0"
         self.device_type = "cuda" if device.type == "cuda" else "cpu"
         self.scaler = None
+        self.static_scale = None
         if self.enabled and self.dtype == torch.float16:
             ls = params.get("loss_scale", "dynamic")
             dynamic = ls in (None, "dynamic", 0, 0.0)
             init = float(params.get("init_scale", 2.0 ** 16)) if dynamic else float(ls)
+            # a fixed loss_scale uses the scaler's default factors (torch asserts growth > 1 and
+            # backoff < 1) and pins the scale back after every update
+            self.static_scale = None if dynamic else init
             self.scaler = torch.amp.GradScaler(self.device_type, init_scale=init,
-                                               growth_interval=int(params.get("growth_interval", 2000)),
-                                               growth_factor=2.0 if dynamic else 1.0,
-                                               backoff_factor=0.5 if dynamic else 1.0)
+                                               growth_interval=int(params.get("growth_interval", 2000)))
         self.overflow = False
         self._unscaled = False
 
@@ -89,11 +91,16 @@ class AmpState:
             self.overflow = False
             return True
         self.unscale(optimizer)
-        before = self.scaler.get_scale()
-        self.scaler.step(optimizer)
-        self.scaler.update()
+        # overflow = the unscale's found-inf flags (a static scale never backs off, so comparing
+        # scales before / after the update would miss its skipped steps)
+        found = self.scaler._found_inf_per_device(optimizer)
+        self.overflow = bool(sum(float(v.item()) for v in found.values()) > 0)
+        self.scaler.step(optimizer)  # skips the update when a found-inf flag is set
+        if self.static_scale is not None:
+            self.scaler.update(new_scale=self.static_scale)
+        else:
+            self.scaler.update()
         self._unscaled = False
-        self.overflow = self.scaler.get_scale() < before
         return not self.overflow
 
     def state_dict(self):

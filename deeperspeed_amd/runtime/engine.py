@@ -875,9 +875,12 @@ class DeepSpeedEngine(Module):
             self.skipped_steps += 1
         elif self.lr_scheduler is not None:
             self.lr_scheduler.step(**(lr_kwargs or {}))
-        if report_progress and (self.global_steps + 1) % self.steps_per_print() == 0:
+        if (self.global_steps + 1) % self.steps_per_print() == 0:
+            # every rank reconciles at the same boundary: the roll-back of the optimizer's step
+            # counters must stay identical across data-parallel replicas
             self._reconcile_device_skips()
-            self._report_progress(self.global_steps + 1)
+            if report_progress:
+                self._report_progress(self.global_steps + 1)
         self.global_steps += 1
         self.global_samples += self.train_batch_size()
 
@@ -1074,6 +1077,7 @@ class DeepSpeedEngine(Module):
             tag = f"global_step{self.global_steps}"
         tag = str(tag)
         self._checkpoint_tag_validation(tag)
+        self._reconcile_device_skips()  # on every rank, not only the ones that write the model file
         if self.save_non_zero_checkpoint:
             self._create_checkpoint_file(save_dir, tag, False)
             self._save_checkpoint(save_dir, tag, client_state=client_state)

@@ -205,8 +205,13 @@ class FP16_UnfusedOptimizer:
         if keep:
             torch._foreach_zero_(keep)
 
+    def mark_new_gradients(self):
+        """A backward that did not go through backward() (the pipeline engine's autograd calls)
+        accumulated into the persistent buffers: the next zero_grad must zero them again."""
+        self._persistent_zeroed = False
+
     def backward(self, loss, retain_graph=False):
-        self._persistent_zeroed = False  # new gradients accumulate into the persistent buffers
+        self.mark_new_gradients()
         (loss.float() * self.loss_scale).backward(retain_graph=retain_graph)
 
     def step(self, closure=None):

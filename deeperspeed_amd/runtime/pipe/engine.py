@@ -425,6 +425,8 @@ class PipelineEngine(DeepSpeedEngine):
                 torch.autograd.backward(tensors=out_t, grad_tensors=grads)
             else:
                 torch.autograd.backward(tensors=(outputs,), grad_tensors=(grads[0],))
+            if hasattr(self.optimizer, "mark_new_gradients"):
+                self.optimizer.mark_new_gradients()  # persistent buffers hold fresh gradients again
         _linear_ops.end_backward_pass()  # pre-transposed operands never outlive their backward
         self.pipe_buffers["output_tensors"][buffer_id] = None
         self.pipe_buffers["outputs"][buffer_id] = None

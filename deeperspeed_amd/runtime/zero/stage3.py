@@ -227,7 +227,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         for m in module.modules():
             for p in m.__dict__.get("_external_params", []):
                 self.register_external_parameter(m, p)
-        if verbose or True:
+        if verbose:
             n = sum(u.numel for u in self._units)
             logger.info(f"ZeRO-3: {len(self._units)} units, {n / 1e9:.3f}B params, dp_world={self.dp_world}, "
                         f"persistent units={sum(u.persistent for u in self._units)}")

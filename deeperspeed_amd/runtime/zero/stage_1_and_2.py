@@ -261,17 +261,17 @@ class DeepSpeedZeroOptimizer(ShardedOptimizerBase):
             return
         out_slice = dst_full[b.shard_offset: b.shard_offset + b.chunk]
         accumulate = self._bucketed() and self.gradient_accumulation_steps > 1
-        if accumulate or out_slice.dtype != src.dtype or not self.use_reduce_scatter:
-            out = torch.empty(b.chunk, dtype=src.dtype, device=src.device)
-        else:
-            out = out_slice
+        staged = accumulate or out_slice.dtype != src.dtype or not self.use_reduce_scatter
+        out = out_slice
         if _dist_ready() and world > 1 and self.use_reduce_scatter:
+            if staged:  # reduce-scatter into a staging buffer only where finish() must convert / add
+                out = torch.empty(b.chunk, dtype=src.dtype, device=src.device)
             work = comm.reduce_scatter_tensor(out, src, group=self.dp_group, async_op=True, tag="zero.reduce")
         elif _dist_ready() and world > 1:
             work = comm.all_reduce(src, group=self.dp_group, async_op=True, tag="zero.allreduce")
             out = src[self.dp_rank * b.chunk: (self.dp_rank + 1) * b.chunk]
         else:
-            if out is out_slice:
+            if not staged:
                 out.copy_(src[: b.chunk])
             else:  # one rank: finish() reads the bucket itself (no staging copy)
                 out = src[: b.chunk]

@@ -29,6 +29,11 @@ DEBUG = os.environ.get("DSA_DEBUG_COLLECTIVES", "0") == "1"
 
 _log: List[Tuple[int, str, int, str]] = []
 _seq = 0
+# always on (an int and a tuple per call): how many collectives this rank has issued and the last
+# one, which a watchdog prints when a rank stalls -- equal counts on every rank point at a slow or
+# hung collective, different counts at a rank that took another path (order divergence)
+_issued = 0
+_last: Tuple[str, int, str] = ("none", 0, "")
 
 
 def set_debug(enabled: bool):
@@ -49,7 +54,9 @@ def trace_range(name: str):
 
 
 def _record(op: str, t: torch.Tensor):
-    global _seq
+    global _seq, _issued, _last
+    _issued += 1
+    _last = (op, int(t.numel()), str(t.dtype))
     if DEBUG:
         _log.append((_seq, op, int(t.numel()), str(t.dtype)))
         _seq += 1
@@ -71,6 +78,11 @@ def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False, tag="all_red
     _record(tag, t)
     with trace_range(f"rccl.{tag}[{t.numel()}]"):
         return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+
+
+def progress() -> str:
+    """One line: collectives issued by this rank so far and the last one."""
+    return f"collectives issued={_issued} last={_last[0]}[{_last[1]} {_last[2]}]"
 
 
 def collective_log():

@@ -83,6 +83,25 @@ def test_amp_fp16_dynamic_scaler_skips_overflow():
     assert eng.amp.loss_scale < 2.0 ** 10
 
 
+def test_amp_fp16_static_scale_counts_overflow():
+    """a fixed loss_scale builds (no GradScaler factor assert), keeps its scale, and a
+    non-finite gradient still skips and counts the step."""
+    eng, net = _engine(_conf(dtype="float16", loss_scale=128))
+    assert eng.amp.loss_scale == 128.0
+    x, y = torch.randn(4, 16), torch.randint(0, 4, (4,))
+    eng.backward(eng(x, y))
+    w0 = net.a.weight.detach().clone()
+    eng.step()
+    assert not torch.equal(w0, net.a.weight) and eng.skipped_steps == 0
+    eng.backward(eng(x, y))
+    net.a.weight.grad[0, 0] = float("nan")
+    w1 = net.a.weight.detach().clone()
+    eng.step()
+    assert torch.equal(w1, net.a.weight)
+    assert eng.skipped_steps == 1
+    assert eng.amp.loss_scale == 128.0
+
+
 def test_amp_o0_is_plain_fp32():
     eng, net = _engine(_conf(opt_level="O0"))
     eng(torch.randn(4, 16), torch.randint(0, 4, (4,)))

@@ -7,7 +7,9 @@ import math
 import pytest
 import torch
 
-from common import run_distributed
+from common import distributed_test, run_distributed
+
+import deeperspeed_amd as ds
 
 
 def _ref_lamb(w, g, m, v, lr, b1, b2, eps, wd, step, maxc, minc):
@@ -65,3 +67,34 @@ def _engine_body(dtype):
 @pytest.mark.parametrize("dtype", ["bfloat16"])
 def test_engine_lamb_unfused(dtype):
     run_distributed(_engine_body, 2, dtype)
+
+
+@distributed_test(world_size=2)
+def _reconcile_every_rank_body(tmpdir):
+    """the sync-free LAMB step's device-side skip count is reconciled -- and the
+    optimizer's step counters rolled back -- on EVERY rank at the print / checkpoint boundary, not
+    only on the reporting rank, so replicated parameters keep identical bias corrections."""
+    import torch.distributed as dist
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.Linear(8, 2)).to(torch.bfloat16)
+    conf = {"train_micro_batch_size_per_gpu": 2, "steps_per_print": 2,
+            "optimizer": {"type": "Lamb", "params": {"lr": 1e-3}}, "fp16": {"enabled": True, "type": "bfloat16"}}
+    eng, opt, _, _ = ds.initialize(model=net, model_parameters=net.parameters(), config_params=conf)
+    assert hasattr(opt, "reconcile_skipped_steps")
+    x = torch.randn(2, 8, dtype=torch.bfloat16)
+    for i in range(4):
+        eng.backward(eng(x).float().pow(2).mean())
+        if i == 0:  # the kernels skipped one step on the device (emulated: CPU has no sync-free path)
+            opt._dev_skipped = torch.ones(1, dtype=torch.int32)
+        eng.step()
+    steps = [st["step"] for st in opt.state.values() if "step" in st]
+    mine = torch.tensor([eng.skipped_steps, min(steps), max(steps)], dtype=torch.float64)
+    both = [torch.empty_like(mine) for _ in range(2)]
+    dist.all_gather(both, mine)
+    assert torch.equal(both[0], both[1]), both
+    assert int(mine[0]) == 1
+    eng.save_checkpoint(tmpdir, tag="t")  # the checkpoint boundary reconciles on every rank as well
+
+
+def test_reconcile_device_skips_on_every_rank(tmp_path):
+    _reconcile_every_rank_body(str(tmp_path))

@@ -134,3 +134,68 @@ def test_engine_bf16_reduction_error_world8(tmp_path):
     assert errs["fp32_reduce"] < 1e-5, errs
     assert errs["per_micro_bf16"] < 1e-2, errs
     assert errs["resident_bf16"] < 1e-2, errs
+
+
+def _single_rank_accum_body(out_dir):
+    """The headline N = 1 path (bound single-rank ZeRO-3): 4 micro-batch gradients accumulate
+    in bf16 in place in the bound shard.  Compared here with a float64 sum of the same bf16
+    per-micro-batch gradients, next to an fp32 accumulation of them (`grad_accum_dtype` fp32
+    on the forced-sharded path)."""
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
+    cfg = get_config("tiny", num_layers=2, checkpoint_activations=False)
+    ga, mb, seq = 4, 2, 32
+    gen = torch.Generator().manual_seed(7)
+    data = [torch.randint(0, cfg.vocab_size, (mb, seq), generator=gen) for _ in range(ga)]
+    torch.manual_seed(0)
+    ref = GPTNeoX(cfg, dtype=torch.bfloat16)
+    exact = {n: torch.zeros(p.shape, dtype=torch.float64) for n, p in ref.named_parameters()}
+    for ids in data:
+        ref.zero_grad()
+        (ref(ids, labels=ids) / ga).backward()
+        for n, p in ref.named_parameters():
+            exact[n] += p.grad.double()
+    modes = {"bound_bf16": dict(), "sharded_fp32": dict(stage3_force_sharded=True, grad_accum_dtype="fp32"),
+             "sharded_bf16": dict(stage3_force_sharded=True, grad_accum_dtype="param")}
+    errs = {}
+    for tag, z in modes.items():
+        torch.manual_seed(0)
+        model = GPTNeoX(cfg, dtype=torch.bfloat16)
+        names = {id(p): n for n, p in model.named_parameters()}
+        conf = {"train_micro_batch_size_per_gpu": mb, "gradient_accumulation_steps": ga,
+                "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "fp16": {"enabled": True, "type": "bfloat16"},
+                "fp32_allreduce": False,  # as bench.py (DeeperSpeed's bf16 default would reduce in fp32)
+                "zero_optimization": dict(stage=3, stage3_unit_max_numel=20000, stage3_param_persistence_threshold=0,
+                                          reduce_bucket_size=4096, **z)}
+        engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+        for m, ids in enumerate(data):
+            engine.backward(engine(ids, labels=ids))
+            if m < ga - 1:
+                engine.step()
+        num = den = 0.0
+        for g in engine.optimizer.groups:
+            for b in g.buckets:
+                for i, p in enumerate(b.params):
+                    ov = b.chunk_overlap(0, i)
+                    if ov is None:
+                        continue
+                    p0, c0, ln = ov
+                    got = g.shard_grad[b.shard_offset + c0: b.shard_offset + c0 + ln].double()
+                    want = exact[names[id(p)]].reshape(-1)[p0: p0 + ln]
+                    num += float((got - want).pow(2).sum())
+                    den += float(want.pow(2).sum())
+        errs[tag] = (num / den) ** 0.5
+        engine.step()
+    torch.save(errs, os.path.join(out_dir, "errs1.pt"))
+
+
+def test_single_rank_bf16_accumulation_error(tmp_path):
+    """the N = 1 bf16 accumulation costs about one bf16 rounding, the same
+    order as the N > 1 resident-bf16 path above, and fp32 accumulation removes it."""
+    run_distributed(_single_rank_accum_body, 1, str(tmp_path))
+    errs = torch.load(os.path.join(tmp_path, "errs1.pt"), weights_only=True)
+    print("N=1, 4 micro-batches, relative L2 error of the accumulated gradient vs float64:",
+          {k: f"{v:.2e}" for k, v in errs.items()})
+    assert errs["sharded_fp32"] < 1e-5, errs
+    assert errs["bound_bf16"] < 1e-2, errs
+    assert errs["sharded_bf16"] < 1e-2, errs
