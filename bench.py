@@ -89,6 +89,11 @@ def parse():
                         "head: the LM head only; auto: 1 for the 20B single-GPU bound ZeRO-3 run (1 / 2 / 3 measured "
                         "8,936 / 8,895 / 8,647 "
                         "tok/s, profiles/r4w_notes.md), else 0")
+    p.add_argument("--moments-tiers", type=str, default="auto",
+                   help="--offload moments: where the Adam moments live, per layer, in the order HBM -> pinned host "
+                        "-> NVMe file (--nvme-path).  auto: HBM headroom, then the host budget "
+                        "(DSA_HOST_MOMENTS_GIB, default min(available - 24 GiB, 215 GiB)), then the free disk; "
+                        "host: everything in pinned host memory")
     p.add_argument("--fp32-reduce", type=str, default="off", choices=["on", "off"],
                    help="reduce bf16 gradients in fp32 (DeeperSpeed's bf16 default fp32_allreduce; "
                         "tests/test_zero_reduce_precision.py measures what bf16 reduction costs)")
@@ -117,6 +122,45 @@ def plan_memory(cfg, mb, seq, world, offload, ckpt, ga=1):
     logits = seq * mb * cfg.vocab_size * 4  # bf16 logits + bf16 grad (fused HIP cross-entropy)
     transient = 2 * 2 * 2e8 * 2 + logits + 2 * 2**30
     return states + acts + transient
+
+
+def plan_moment_tiers(model, P, hbm_free, nvme_path):
+    """Peak-parameter layout (--offload moments): the Adam moments (8 B/param) of consecutive
+    blocks of the model go to HBM while its headroom lasts, then to pinned host memory up to the
+    host budget, then to an NVMe file, so a model whose moments exceed any one tier still trains.
+    Returns the param groups ("moments_device" per group) and a record of the split; raises,
+    naming the tier that ran out and by how much, when the three together are too small."""
+    import shutil
+    margin = float(os.environ.get("DSA_TIER_HBM_MARGIN_GIB", "6")) * 2**30
+    hbm = max(0.0, hbm_free - margin)
+    try:
+        import psutil
+        avail = psutil.virtual_memory().available
+    except Exception:  # noqa: BLE001
+        avail = 1 << 50
+    host = float(os.environ.get("DSA_HOST_MOMENTS_GIB", "0")) * 2**30 or min(avail - 24 * 2**30, 215 * 2**30)
+    os.makedirs(nvme_path, exist_ok=True)
+    disk = max(0.0, shutil.disk_usage(nvme_path).free - float(os.environ.get("DSA_DISK_MARGIN_GIB", "6")) * 2**30)
+    blocks = [[model.embed_in]] + [[l] for l in model.layers] + [[model.final_layer_norm, model.embed_out]]
+    left = {"gpu": hbm, "cpu": host, "nvme": disk}
+    groups = {"gpu": [], "cpu": [], "nvme": []}
+    for mods in blocks:
+        ps = [p for m in mods for p in m.parameters()]
+        need = 8.0 * sum(p.numel() for p in ps)
+        tier = next((t for t in ("gpu", "cpu", "nvme") if left[t] >= need), None)
+        if tier is None:
+            short = need - max(left.values())
+            raise SystemExit(f"[bench] moments do not fit: HBM {hbm / 2**30:.1f} + host {host / 2**30:.1f} + "
+                             f"disk {disk / 2**30:.1f} GiB for {8 * P / 2**30:.1f} GiB of moments; the next block "
+                             f"needs {need / 2**30:.2f} GiB, {short / 2**30:.2f} GiB more than any tier has left")
+        left[tier] -= need
+        groups[tier] += ps
+    rec = {t: {"params": sum(p.numel() for p in groups[t]),
+               "gib": round(8 * sum(p.numel() for p in groups[t]) / 2**30, 1)} for t in groups}
+    rec["budget_gib"] = {"hbm": round(hbm / 2**30, 1), "host": round(host / 2**30, 1), "disk": round(disk / 2**30, 1)}
+    log(f"moment tiers: HBM {rec['gpu']['gib']} GiB, pinned host {rec['cpu']['gib']} GiB, NVMe "
+        f"{rec['nvme']['gib']} GiB ({nvme_path}); budgets {rec['budget_gib']}")
+    return [{"params": groups[t], "moments_device": t} for t in ("gpu", "cpu", "nvme") if groups[t]], rec
 
 
 def log(msg):
@@ -422,7 +466,11 @@ def main():
         fit.live, fit.resident = live, resident
     floor = float(os.environ.get("DSA_MEM_FLOOR_GIB", "3")) * 2**30
     limit = hbm / share - floor
-    zcfg = {"stage": args.zero, "overlap_comm": True, "reduce_scatter": True, "reduce_bucket_size": int(2e8),
+    # gloo rehearsal of an N-GPU job on one GPU: gloo's asynchronous collectives on device tensors
+    # stalled for ~50 s when several ZeRO reductions were in flight (profiles/r5a_notes.md), so the
+    # rehearsal waits for each collective as it is issued (RCCL runs keep the overlap)
+    gloo_gpu = on_gpu and args.dist_backend == "gloo"
+    zcfg = {"stage": args.zero, "overlap_comm": not gloo_gpu, "reduce_scatter": True, "reduce_bucket_size": int(2e8),
             "stage3_prefetch_bucket_size": int(5e8), "stage3_param_persistence_threshold": int(1e6),
             "stage3_unit_max_numel": int(2e8), "stage3_max_live_parameters": live,
             "stage3_max_reuse_distance": int(2 * P)}
@@ -441,7 +489,8 @@ def main():
         zcfg["compact_master"] = True
     elif offload == "moments":
         zcfg["compact_master"] = True
-        zcfg["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": "moments"}
+        zcfg["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": "moments",
+                                     "nvme_path": args.nvme_path}
     elif offload == "nvme":
         zcfg["offload_optimizer"] = {"device": "nvme", "nvme_path": args.nvme_path, "pin_memory": True,
                                      "states": "all"}
@@ -485,6 +534,9 @@ def main():
         (0.5 if hm == "head" else int(hm))  # "head": the LM head only
     params = model.parameters()
     host_numel = 0
+    tiers = None
+    if offload == "moments" and on_gpu and args.moments_tiers != "host":
+        params, tiers = plan_moment_tiers(model, P, budget - planned, args.nvme_path)
     if k_host > 0:
         host_mods = [model.embed_out] + (list(model.layers[-int(k_host):]) if k_host >= 1 else [])
         tail = {id(p) for m in host_mods for p in m.parameters()}
@@ -781,6 +833,7 @@ def main():
                    "dist_backend": dist.get_backend(),
                    "overlap_step": bool(zcfg.get("overlap_step", False)),
                    "host_moments_params": host_numel,
+                   "moment_tiers": tiers,
                    "lt_gemm": _lt_summary() if on_gpu else None,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N): BASELINE.md's derived target "
                                     "(reference's best published ZeRO-3 49 TFLOPS/GPU on V100 at 6N FLOPs/token); "

@@ -1069,6 +1069,23 @@ int64_t cu_masked_stream(std::vector<int64_t> mask_words) {
   return reinterpret_cast<int64_t>(st);
 }
 
+// A non-blocking stream at a given HIP priority.  HIP keeps one pool of hardware queues per
+// priority level, so a stream of another priority never shares the compute stream's queue (a
+// shared queue serialises: a side stream's cross-stream wait then stalls the compute stream).
+int64_t priority_stream(int64_t priority) {
+  hipStream_t st = nullptr;
+  TORCH_CHECK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, (int)priority) == hipSuccess,
+              "hipStreamCreateWithPriority failed");
+  return reinterpret_cast<int64_t>(st);
+}
+
+std::vector<int64_t> stream_priority_range() {
+  int least = 0, greatest = 0;
+  TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess,
+              "hipDeviceGetStreamPriorityRange failed");
+  return {least, greatest};
+}
+
 int64_t device_cu_count() {
   int dev = 0, n = 0;
   (void)hipGetDevice(&dev);
@@ -1133,6 +1150,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("cu_masked_stream", &cu_masked_stream);
   m.def("device_cu_count", &device_cu_count);
+  m.def("priority_stream", &priority_stream);
+  m.def("stream_priority_range", &stream_priority_range);
   register_gemm_lt(m);
   m.def("sum_slices", &sum_slices);
   m.def("dropout_bwd_db", &dropout_bwd_db);

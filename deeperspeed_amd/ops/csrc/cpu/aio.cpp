@@ -254,8 +254,26 @@ class Worker {
     }
     if (fd < 0) return false;
     bool ok = uring_ ? run_uring(fd, s) : run_psync(fd, s, block_);
+    if (ok && !direct && drop_cache()) {
+      // buffered fallback (overlay / tmpfs refuse O_DIRECT): keep the page cache from holding
+      // the swapped bytes -- written ranges are flushed, then both kinds are dropped
+      if (!s.req->read)
+        sync_file_range(fd, s.off, s.len, SYNC_FILE_RANGE_WAIT_BEFORE | SYNC_FILE_RANGE_WRITE |
+                                              SYNC_FILE_RANGE_WAIT_AFTER);
+      posix_fadvise(fd, s.off, s.len, POSIX_FADV_DONTNEED);
+    }
     close(fd);
     return ok;
+  }
+
+  // DSA_AIO_DROP_CACHE=1: buffered I/O does not leave the swapped data in the page cache (a
+  // memory-capped job counts the cache; a real NVMe device is then read at its own rate)
+  static bool drop_cache() {
+    static const bool on = [] {
+      const char* e = std::getenv("DSA_AIO_DROP_CACHE");
+      return e && e[0] == '1';
+    }();
+    return on;
   }
 
   // io_uring_enter, retrying transient failures: EINTR (inside Ring::enter), EAGAIN (no kernel

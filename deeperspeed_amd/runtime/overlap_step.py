@@ -62,11 +62,34 @@ def dedicated_stream(device) -> torch.cuda.Stream:
     return side_stream(device, 1 << 30)
 
 
-def new_stream(device) -> torch.cuda.Stream:
-    """The framework's side / copy streams: plain torch streams, dedicated_stream with
-    DSA_DEDICATED_STREAMS=1."""
+# DSA_STREAM_KIND: what new_stream() creates for the framework's side / copy streams
+#   torch - a stream from torch's pool;
+#   hip   - hipStreamCreateWithPriority(normal) through the extension;
+#   low   - the same at HIP's lowest priority (a queue pool of its own: never the compute
+#           stream's hardware queue, and the dispatcher favours the compute queue's waves).
+STREAM_KIND = os.environ.get("DSA_STREAM_KIND", "torch")
+_keep = []  # external streams live for the process (torch does not own them)
+
+
+def priority_stream(device, priority: int) -> torch.cuda.Stream:
+    from ..ops import native
+    hip = native.hip_ops()
+    least, greatest = hip.stream_priority_range()
+    priority = max(min(int(priority), least), greatest)
+    with torch.cuda.device(device):
+        s = torch.cuda.ExternalStream(hip.priority_stream(priority), device=device)
+    _keep.append(s)
+    return s
+
+
+def new_stream(device, kind: str = None) -> torch.cuda.Stream:
+    """The framework's side / copy streams: plain torch streams by default, dedicated_stream
+    with DSA_DEDICATED_STREAMS=1, HIP priority streams with DSA_STREAM_KIND=hip|low."""
+    kind = kind or STREAM_KIND
     if DEDICATED_STREAMS and torch.cuda.is_available():
         return dedicated_stream(device)
+    if kind in ("hip", "low") and torch.cuda.is_available():
+        return priority_stream(device, 0 if kind == "hip" else 1 << 20)
     return torch.cuda.Stream(device=device)
 
 

@@ -62,9 +62,10 @@ class OptimizerSwapper:
                 for n in self.names:
                     b[n] = _pinned(an, torch.float32)
 
-    def register(self, key, tensors: Dict[str, torch.Tensor]):
-        """Create the swap files of `key` from initial values (missing names start at 0)."""
-        n = next(iter(tensors.values())).numel()
+    def register(self, key, tensors: Dict[str, torch.Tensor], numel: int = None):
+        """Create the swap files of `key` from initial values (missing names start at 0; with
+        `numel` and no tensors, every name starts at 0)."""
+        n = int(numel) if numel is not None else next(iter(tensors.values())).numel()
         self.numel[key] = n
         self.max_numel = max(self.max_numel, n)
         self._ensure_buffers(1)

@@ -162,6 +162,8 @@ class ShardedOptimizerBase:
         self.offload_states = (offload_optimizer or {}).get("states", "all") if offload_optimizer else None
         self.nvme = bool(offload_optimizer) and offload_optimizer.get("device") == "nvme"
         self._swapper = None
+        self._mswap = None  # NVMe tier of offload states='moments' (_moment_tier)
+        self._mswap_keys = {}
         self.fused = isinstance(init_optimizer, FusedAdam) or getattr(init_optimizer, "supports_flat_update", False)
         self.groups: List[FlatGroup] = []
         self.is_gradient_accumulation_boundary = True
@@ -211,6 +213,18 @@ class ShardedOptimizerBase:
         pieces on copy engines (_host_moments_step)."""
         return bool(self.optimizer.param_groups[g.group_index].get("host_moments", False)) and self.fused \
             and torch.cuda.is_available() and self.offload is None
+
+    def _moment_tier(self, g) -> str:
+        """Where group g's Adam moments live under offload_optimizer states='moments': the param
+        group's "moments_device" ("cpu" = pinned host, "nvme" = an aio-swapped file, "gpu" = HBM),
+        default "cpu".  Three tiers let a single GPU train a model whose moments exceed any one of
+        HBM headroom, the host-memory budget and the disk (bench.py --offload moments sizes them)."""
+        if not (self.offload is not None and self.offload_states == "moments"):
+            return "gpu"
+        t = str(self.optimizer.param_groups[g.group_index].get("moments_device", "cpu")).lower()
+        if t not in ("cpu", "nvme", "gpu", "hbm"):
+            raise ValueError(f"moments_device must be cpu, nvme or gpu, got {t!r}")
+        return "gpu" if t == "hbm" else t
 
     def _split_groups(self):
         """Split each inner param group into (dtype, model-parallel) flat groups."""
@@ -263,7 +277,14 @@ class ShardedOptimizerBase:
             for g in self.groups:
                 st = self.optimizer.state[g.master]
                 st["step"] = 0
-                on_host = (host and self.offload_states == "all") or moments_only or self._host_moment_group(g)
+                tier = self._moment_tier(g) if moments_only else None
+                if tier == "nvme":
+                    self._register_nvme_moments(g)
+                    st["exp_avg"] = torch.zeros(0, dtype=torch.float32)
+                    st["exp_avg_sq"] = torch.zeros(0, dtype=torch.float32)
+                    continue
+                on_host = (host and self.offload_states == "all") or (moments_only and tier == "cpu") or \
+                    self._host_moment_group(g)
                 kw = dict(dtype=torch.float32, pin_memory=on_host and (pin or moments_only or
                                                                        self._host_moment_group(g)))
                 if on_host:
@@ -272,6 +293,35 @@ class ShardedOptimizerBase:
                 else:
                     st["exp_avg"] = torch.zeros(g.shard_numel, dtype=torch.float32, device=self.device)
                     st["exp_avg_sq"] = torch.zeros(g.shard_numel, dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------------ NVMe tier of the moments
+    def _register_nvme_moments(self, g):
+        """Zero-initialised exp_avg / exp_avg_sq files for every bucket of group g."""
+        import os
+        from ..swap_tensor.optimizer_utils import PipelinedOptimizerSwapper
+        if self._mswap is None:
+            path = self.offload.get("nvme_path") or "/tmp/deeperspeed_amd_nvme"
+            folder = os.path.join(path, f"zero_stage_{self._zero_stage()}_moments",
+                                  f"rank{self.dp_rank}_mp{self.mp_rank}")
+            self._mswap = PipelinedOptimizerSwapper(folder, names=("exp_avg", "exp_avg_sq"),
+                                                    aio_config=self.offload.get("aio") or {})
+        gi = self.groups.index(g)
+        for bi, b in enumerate(g.buckets):
+            if b.chunk > 0:
+                self._mswap.register((gi, bi), {}, numel=b.chunk)
+                self._mswap_keys[(gi, bi)] = b
+
+    def _nvme_moments_group(self, gi, name) -> torch.Tensor:
+        g = self.groups[gi]
+        parts = [self._mswap.read((gi, bi), name) for bi, b in enumerate(g.buckets) if b.chunk > 0]
+        return torch.cat(parts) if parts else torch.zeros(0)
+
+    def _nvme_moments_write(self, gi, name, value: torch.Tensor):
+        g = self.groups[gi]
+        value = value.reshape(-1).float().cpu()
+        for bi, b in enumerate(g.buckets):
+            if b.chunk > 0:
+                self._mswap.write((gi, bi), name, value[b.shard_offset: b.shard_offset + b.chunk])
 
     # ------------------------------------------------------------------ NVMe (ZeRO-Infinity)
     def _setup_nvme(self, init_shard_fn):
@@ -815,22 +865,51 @@ class ShardedOptimizerBase:
         d2h.synchronize()
         del stages
 
+    def _moments_kernel(self, g, grp, o, lo, hi, m, v, step, grad_scale, adamw):
+        b1, b2 = grp["betas"]
+        if self.compact_master:
+            native.adam_compact_(o, g.master[lo:hi], g.shard_grad[lo:hi], m, v, grp["lr"], b1, b2, grp["eps"],
+                                 grp["weight_decay"], step, grp.get("bias_correction", True), grad_scale, adamw)
+        else:
+            native.adam_flat_(g.master[lo:hi], g.shard_grad[lo:hi], m, v, o, grp["lr"], b1, b2, grp["eps"],
+                              grp["weight_decay"], step, grp.get("bias_correction", True), grad_scale, adamw)
+
     def _offload_moments_step(self, grad_scale, grp_steps):
-        """Adam moments in pinned host memory, master (compact or fp32) and gradients in HBM.
-        Per piece: H2D of m, v (stream A) -> fused Adam on the compute stream -> D2H of m, v
-        (stream B); three device staging slots keep both copy engines and the kernel busy."""
+        """Adam moments off-HBM, master (compact or fp32) and gradients in HBM.  Three tiers, per
+        param group (_moment_tier): HBM-resident moments update in place; pinned-host moments
+        stream per piece: H2D of m, v (stream A) -> fused Adam on the compute stream -> D2H of m, v
+        (stream B), three device staging slots keeping both copy engines and the kernel busy;
+        NVMe moments (_nvme_moments_step) are read / written by the aio engine on the host while
+        their H2D / Adam / D2H run on a stream of their own, beside the host tier."""
         h2d, d2h = self._streams()
         cur = torch.cuda.current_stream()
+        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
+        tiers = {id(g): self._moment_tier(g) for g in self.groups}
+        for g in self.groups:  # HBM tier: no copies
+            if tiers[id(g)] != "gpu":
+                continue
+            grp, st = self._inner_group(g), self.optimizer.state[g.master]
+            for b in g.buckets:
+                out_full = self._bucket_out(g, b)
+                lo, hi = b.shard_offset, b.shard_offset + b.chunk
+                self._moments_kernel(g, grp, out_full, lo, hi, st["exp_avg"][lo:hi], st["exp_avg_sq"][lo:hi],
+                                     grp_steps[id(g)], grad_scale, adamw)
+                self._after_bucket_update(g, b)
+        host_groups = [g for g in self.groups if tiers[id(g)] == "cpu"]
+        nvme_groups = [g for g in self.groups if tiers[id(g)] == "nvme"]
+        if not host_groups:
+            if nvme_groups:
+                self._nvme_moments_step(nvme_groups, grad_scale, grp_steps, adamw)
+            return
         nbuf = OFFLOAD_NBUF
-        piece = min(OFFLOAD_SUBCHUNK // 2, max(b.chunk for g in self.groups for b in g.buckets))
+        piece = min(OFFLOAD_SUBCHUNK // 2, max(b.chunk for g in host_groups for b in g.buckets))
         stages = [(torch.empty(piece, dtype=torch.float32, device=self.device),
                    torch.empty(piece, dtype=torch.float32, device=self.device)) for _ in range(nbuf)]
         free_ev = [None] * nbuf
         start = torch.cuda.Event()
         start.record(cur)  # gradients are final
-        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
         k = 0
-        for g in self.groups:
+        for g in host_groups:
             grp = self._inner_group(g)
             b1, b2 = grp["betas"]
             st = self.optimizer.state[g.master]
@@ -874,11 +953,57 @@ class ShardedOptimizerBase:
                         ev_free.record(d2h)
                     free_ev[i] = ev_free
                 self._after_bucket_update(g, b)
+        if nvme_groups:  # its host loop runs while the GPU works through the host tier above
+            self._nvme_moments_step(nvme_groups, grad_scale, grp_steps, adamw)
         # host moments final before a checkpoint or the next step reads them; staging buffers
         # are released only after the copies that use them
         cur.wait_stream(d2h)
         d2h.synchronize()
         del stages
+
+    NVME_PIECE = int(32 * 1024 * 1024)  # elements of m / v per H2D / Adam / D2H piece of the NVMe tier
+
+    def _nvme_moments_step(self, groups, grad_scale, grp_steps, adamw):
+        """NVMe tier of the moments.  The aio engine reads bucket k+1's m / v files into pinned
+        buffers and writes bucket k-1's back while bucket k runs H2D -> fused Adam -> D2H on a
+        stream of its own (PipelinedOptimizerSwapper); the host waits for that stream once per
+        bucket before its buffers are written back."""
+        cur = torch.cuda.current_stream()
+        if getattr(self, "_nvme_stream", None) is None:
+            self._nvme_stream = self._new_stream()
+        ns = self._nvme_stream
+        start = torch.cuda.Event()
+        start.record(cur)  # gradients are final
+        ns.wait_event(start)
+        keys = [k for k, b in self._mswap_keys.items() if self.groups[k[0]] in groups]
+        piece = min(self.NVME_PIECE, max(self._mswap_keys[k].chunk for k in keys))
+        m_dev = torch.empty(piece, dtype=torch.float32, device=self.device)
+        v_dev = torch.empty(piece, dtype=torch.float32, device=self.device)
+
+        def update(key, t):
+            gi, bi = key
+            g, b = self.groups[gi], self._mswap_keys[key]
+            grp = self._inner_group(g)
+            out_full = self._bucket_out(g, b)
+            with torch.cuda.stream(ns):
+                for s0 in range(0, b.chunk, piece):
+                    e0 = min(s0 + piece, b.chunk)
+                    n, lo, hi = e0 - s0, b.shard_offset + s0, b.shard_offset + e0
+                    m, v = m_dev[:n], v_dev[:n]
+                    m.copy_(t["exp_avg"][s0:e0], non_blocking=True)
+                    v.copy_(t["exp_avg_sq"][s0:e0], non_blocking=True)
+                    self._moments_kernel(g, grp, None if out_full is None else out_full[s0:e0], lo, hi, m, v,
+                                         grp_steps[id(g)], grad_scale, adamw)
+                    t["exp_avg"][s0:e0].copy_(m, non_blocking=True)
+                    t["exp_avg_sq"][s0:e0].copy_(v, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(ns)
+            done.synchronize()  # m / v are home in the pinned buffers: the swapper writes them next
+            self._after_bucket_update(g, b)
+
+        self._mswap.update(keys, update)
+        cur.wait_stream(ns)
+        del m_dev, v_dev
 
     def _offload_all_step(self, grad_scale, grp_steps):
         """Reference ZeRO-Offload: master + moments on host, native CPU Adam.  Pipelined over
@@ -928,6 +1053,12 @@ class ShardedOptimizerBase:
                 if st is not None:
                     st["exp_avg"] = self._nvme_read_group(gi, "exp_avg")
                     st["exp_avg_sq"] = self._nvme_read_group(gi, "exp_avg_sq")
+        if self._mswap is not None:  # NVMe tier of offload states='moments'
+            for gi, g in enumerate(self.groups):
+                st = base.get("state", {}).get(gi)
+                if st is not None and self._moment_tier(g) == "nvme":
+                    st["exp_avg"] = self._nvme_moments_group(gi, "exp_avg")
+                    st["exp_avg_sq"] = self._nvme_moments_group(gi, "exp_avg_sq")
         # move state tensors to cpu (checkpoint files are host tensors)
         for k, v in base.get("state", {}).items():
             for kk, vv in list(v.items()):
@@ -1060,6 +1191,9 @@ class ShardedOptimizerBase:
             for k, v in s.items():
                 if self.nvme and torch.is_tensor(v) and k in ("exp_avg", "exp_avg_sq"):
                     self._nvme_write_group(gi, k, v)
+                elif (self._mswap is not None and torch.is_tensor(v) and k in ("exp_avg", "exp_avg_sq")
+                      and self._moment_tier(g) == "nvme"):
+                    self._nvme_moments_write(gi, k, v)
                 elif torch.is_tensor(v) and k in st and torch.is_tensor(st[k]) and st[k].numel() == v.numel():
                     st[k].copy_(v.to(st[k].device))
                 elif torch.is_tensor(v):

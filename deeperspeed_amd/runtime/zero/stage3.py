@@ -24,6 +24,7 @@ MI355X design:
 from __future__ import annotations
 
 import functools
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -33,6 +34,8 @@ from ...utils.logging import logger
 from ...utils import comm
 from .layout import ALIGN, FlatGroup, build_unit_buckets
 from .sharded_base import ShardedOptimizerBase, _dist_ready
+
+OVERLAP_TRACE = os.environ.get("DSA_OVERLAP_TRACE", "0") == "1"
 
 
 class ZeroParamStatus:
@@ -539,18 +542,30 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self._uncovered = None  # bucket keys the root waits for; None = not calibrated yet
         self._handles.append(self.module.register_forward_pre_hook(self._root_wait_uncovered))
 
+    def _trace_wait(self, what, key):
+        """DSA_OVERLAP_TRACE=1: log each bucket wait of the first forward after a step, with the
+        position of that bucket's update in the step (how much of the step the forward waits for)."""
+        if not OVERLAP_TRACE:
+            return
+        order = list(self._bucket_events)
+        pos = order.index(key) if key in order else -1
+        logger.info(f"overlap_step wait: {what} bucket {key} = update {pos + 1} of {len(order)}")
+
     def _root_wait_uncovered(self, module, inputs):
         if not self._bucket_events or _in_backward():
             return
         cur = torch.cuda.current_stream()
         if self._uncovered is None:
             cur.wait_event(self._step_done_event)  # calibration pass: the whole step
+            if OVERLAP_TRACE:
+                logger.info("overlap_step wait: calibration pass waits for the whole step")
             self._calibrating = True
             self._fired = set()
             return
         for key in self._uncovered:
             ev = self._bucket_events.get(key)
             if ev is not None:
+                self._trace_wait("root (uncovered)", key)
                 cur.wait_event(ev)
 
     def _wait_bucket_updates(self, module, inputs):
@@ -562,6 +577,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         for key in self._module_buckets.get(module, ()):
             ev = self._bucket_events.get(key)
             if ev is not None:
+                self._trace_wait(type(module).__name__, key)
                 cur.wait_event(ev)
 
     def _finish_calibration(self):
@@ -569,6 +585,9 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             self._calibrating = False
             self._uncovered = sorted({k for m, keys in self._module_buckets.items() if m not in self._fired
                                       for k in keys})
+            if OVERLAP_TRACE:
+                logger.info(f"overlap_step calibrated: {len(self._fired)} modules fired, root waits for "
+                            f"{len(self._uncovered)} uncovered bucket(s) {self._uncovered[:8]}")
 
     def synchronize_step(self):
         """Order the compute stream after an overlapped optimizer step (no host wait)."""

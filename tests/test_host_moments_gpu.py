@@ -101,3 +101,69 @@ def test_copy_narrow_to_pinned(wgs):
         native.copy_narrow_(h, x, wgs)
         torch.cuda.synchronize()
         assert torch.equal(h, x.cpu())
+
+
+def _run_tiers(tiers, tmpdir, steps=3, ga=2):
+    """offload_optimizer states='moments' with one param group per entry of `tiers`
+    ("gpu" / "cpu" / "nvme" moments); None = no offload (all moments in HBM)."""
+    _env()
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.gpt_neox import GPTNeoX, get_config
+    from deeperspeed_amd.runtime.zero import sharded_base
+    sharded_base.ShardedOptimizerBase.NVME_PIECE = 200_000  # several pieces per bucket
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = get_config("gpt-neox-125m", num_layers=3, max_seq_len=128)
+    model = GPTNeoX(cfg, device=dev, dtype=torch.bfloat16)
+    mods = [[model.embed_in, model.layers[0]], [model.layers[1]], [model.layers[2], model.final_layer_norm,
+                                                                   model.embed_out]]
+    groups = []
+    for i, ms in enumerate(mods):
+        pg = {"params": [p for m in ms for p in m.parameters()]}
+        if tiers is not None:
+            pg["moments_device"] = tiers[i]
+        groups.append(pg)
+    z = {"stage": 3, "reduce_bucket_size": int(5e6), "compact_master": True}
+    if tiers is not None:
+        z["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "states": "moments",
+                                  "nvme_path": str(tmpdir)}
+    conf = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": ga,
+            "optimizer": {"type": "Adam", "params": {"lr": 3e-4}}, "fp16": {"enabled": True, "type": "bfloat16"},
+            "gradient_clipping": 1.0, "zero_optimization": z}
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=groups, config_params=conf)
+    g = torch.Generator(device=dev).manual_seed(7)
+    losses = []
+    for _ in range(steps):
+        for _ in range(ga):
+            ids = torch.randint(0, cfg.vocab_size, (2, 128), device=dev, generator=g)
+            loss = engine(ids, labels=ids)
+            engine.backward(loss)
+            engine.step()
+        losses.append(float(loss))
+    torch.cuda.synchronize()
+    sd = engine.optimizer.state_dict()
+    mom = [v["exp_avg_sq"].clone() for v in sd["base_optimizer_state"]["state"].values()]
+    sharded_base.ShardedOptimizerBase.NVME_PIECE = int(32 * 1024 * 1024)
+    return losses, [p.detach().float().cpu() for p in engine.module.parameters()], mom, engine
+
+
+def test_three_tier_moments_match_hbm(tmp_path):
+    """HBM / pinned-host / NVMe moment tiers (peak-params layout) equal the all-HBM step bit for
+    bit, and a checkpoint written from the tiered optimizer restores into it exactly."""
+    ref_l, ref_w, ref_m, _ = _run_tiers(None, tmp_path / "a")
+    l, w, m, eng = _run_tiers(["gpu", "nvme", "cpu"], tmp_path / "b")
+    assert eng.optimizer._mswap is not None and eng.optimizer._mswap.bytes_read > 0
+    assert l == ref_l
+    for a, b in zip(ref_w, w):
+        assert torch.equal(a, b)
+    for a, b in zip(ref_m, m):
+        assert torch.equal(a, b)
+    # round trip of the NVMe tier through state_dict / load_state_dict
+    sd = eng.optimizer.state_dict()
+    for gi in sd["base_optimizer_state"]["state"]:
+        sd["base_optimizer_state"]["state"][gi]["exp_avg"] = sd["base_optimizer_state"]["state"][gi]["exp_avg"] + 1
+    eng.optimizer.load_state_dict(sd)
+    sd2 = eng.optimizer.state_dict()
+    for gi in sd["base_optimizer_state"]["state"]:
+        assert torch.equal(sd2["base_optimizer_state"]["state"][gi]["exp_avg"],
+                           sd["base_optimizer_state"]["state"][gi]["exp_avg"])
