@@ -125,12 +125,11 @@ def plan_memory(cfg, mb, seq, world, offload, ckpt, ga=1):
 
 
 def plan_moment_tiers(model, P, hbm_free, nvme_path):
-    """Peak-parameter layout (--offload moments): the Adam moments (8 B/param) of consecutive
-    blocks of the model go to HBM while its headroom lasts, then to pinned host memory up to the
-    host budget, then to an NVMe file, so a model whose moments exceed any one tier still trains.
-    Returns the param groups ("moments_device" per group) and a record of the split; raises,
-    naming the tier that ran out and by how much, when the three together are too small."""
+    """Peak-parameter layout (--offload moments): budgets of the three moment tiers from what this
+    box measures (HBM headroom under the plan, host memory, free disk at --nvme-path), then
+    runtime/memory_fit.split_moment_tiers assigns the model's blocks to them in order."""
     import shutil
+    from deeperspeed_amd.runtime import memory_fit
     margin = float(os.environ.get("DSA_TIER_HBM_MARGIN_GIB", "6")) * 2**30
     hbm = max(0.0, hbm_free - margin)
     try:
@@ -142,25 +141,14 @@ def plan_moment_tiers(model, P, hbm_free, nvme_path):
     os.makedirs(nvme_path, exist_ok=True)
     disk = max(0.0, shutil.disk_usage(nvme_path).free - float(os.environ.get("DSA_DISK_MARGIN_GIB", "6")) * 2**30)
     blocks = [[model.embed_in]] + [[l] for l in model.layers] + [[model.final_layer_norm, model.embed_out]]
-    left = {"gpu": hbm, "cpu": host, "nvme": disk}
-    groups = {"gpu": [], "cpu": [], "nvme": []}
-    for mods in blocks:
-        ps = [p for m in mods for p in m.parameters()]
-        need = 8.0 * sum(p.numel() for p in ps)
-        tier = next((t for t in ("gpu", "cpu", "nvme") if left[t] >= need), None)
-        if tier is None:
-            short = need - max(left.values())
-            raise SystemExit(f"[bench] moments do not fit: HBM {hbm / 2**30:.1f} + host {host / 2**30:.1f} + "
-                             f"disk {disk / 2**30:.1f} GiB for {8 * P / 2**30:.1f} GiB of moments; the next block "
-                             f"needs {need / 2**30:.2f} GiB, {short / 2**30:.2f} GiB more than any tier has left")
-        left[tier] -= need
-        groups[tier] += ps
-    rec = {t: {"params": sum(p.numel() for p in groups[t]),
-               "gib": round(8 * sum(p.numel() for p in groups[t]) / 2**30, 1)} for t in groups}
-    rec["budget_gib"] = {"hbm": round(hbm / 2**30, 1), "host": round(host / 2**30, 1), "disk": round(disk / 2**30, 1)}
+    blocks = [[p for m in mods for p in m.parameters()] for mods in blocks]
+    try:
+        groups, rec = memory_fit.split_moment_tiers(blocks, {"gpu": hbm, "cpu": host, "nvme": disk})
+    except memory_fit.TierShortfall as e:
+        raise SystemExit(f"[bench] {e}")
     log(f"moment tiers: HBM {rec['gpu']['gib']} GiB, pinned host {rec['cpu']['gib']} GiB, NVMe "
         f"{rec['nvme']['gib']} GiB ({nvme_path}); budgets {rec['budget_gib']}")
-    return [{"params": groups[t], "moments_device": t} for t in ("gpu", "cpu", "nvme") if groups[t]], rec
+    return groups, rec
 
 
 def log(msg):
@@ -569,6 +557,8 @@ def main():
             loss = engine(batches[i], labels=batches[i])
             engine.backward(loss)
             engine.step()
+            if gloo_gpu:
+                sync()  # gloo rehearsal: bounded work in flight per rank (see zcfg above)
         return loss
 
     def timed_step():
@@ -780,7 +770,8 @@ def main():
                 if stacks:  # where the fills / copies come from (python call sites)
                     f.write("\n\nfill / zero / copy call sites\n")
                     for e in prof.key_averages(group_by_stack_n=6):
-                        if any(k in e.key for k in ("fill_", "zero_", "copy_", "aten::zeros", "aten::cat")):
+                        if any(k in e.key for k in ("fill_", "zero_", "copy_", "aten::zeros", "aten::cat", "aten::add",
+                                                    "aten::add_")):
                             f.write(f"{e.key} count={e.count} device_us={e.device_time_total:.0f}\n")
                             for fr in e.stack:
                                 f.write(f"    {fr}\n")

@@ -99,3 +99,37 @@ def apply(engine, acts) -> bool:
             engine.set_batch_shape(*val)
             reshaped = True
     return reshaped
+
+
+class TierShortfall(RuntimeError):
+    """The three moment tiers together cannot hold the model's Adam moments."""
+
+
+def split_moment_tiers(blocks, budgets, bytes_per_param: int = 8):
+    """Peak-parameter placement of Adam moments (offload_optimizer states='moments'): consecutive
+    blocks of parameters (embedding, each layer, head) go to the first tier of ("gpu", "cpu",
+    "nvme") -- HBM, pinned host memory, an aio-swapped file -- that still has room, so the
+    fastest tiers fill first and a model whose moments exceed any one tier still trains.
+
+    blocks: list of parameter lists; budgets: bytes per tier.  Returns (param groups with
+    "moments_device", record); raises TierShortfall naming the shortfall when nothing fits."""
+    order = ("gpu", "cpu", "nvme")
+    left = {t: float(budgets.get(t, 0.0)) for t in order}
+    groups = {t: [] for t in order}
+    total = sum(p.numel() for ps in blocks for p in ps) * bytes_per_param
+    for ps in blocks:
+        need = float(bytes_per_param * sum(p.numel() for p in ps))
+        tier = next((t for t in order if left[t] >= need), None)
+        if tier is None:
+            raise TierShortfall(
+                f"moments do not fit: HBM {budgets.get('gpu', 0) / 2**30:.1f} + host {budgets.get('cpu', 0) / 2**30:.1f}"
+                f" + disk {budgets.get('nvme', 0) / 2**30:.1f} GiB for {total / 2**30:.1f} GiB of moments; the next "
+                f"block needs {need / 2**30:.2f} GiB, {(need - max(left.values())) / 2**30:.2f} GiB more than any "
+                f"tier has left")
+        left[tier] -= need
+        groups[tier] += list(ps)
+    rec = {t: {"params": sum(p.numel() for p in groups[t]),
+               "gib": round(bytes_per_param * sum(p.numel() for p in groups[t]) / 2**30, 1)} for t in order}
+    rec["budget_gib"] = {k: round(float(budgets.get(t, 0)) / 2**30, 1)
+                         for k, t in (("hbm", "gpu"), ("host", "cpu"), ("disk", "nvme"))}
+    return [{"params": groups[t], "moments_device": t} for t in order if groups[t]], rec

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One parameterised runner for every GPU-box job (run through gpurun; chain steps with &&).
 #
-#   scripts/gpu.sh tests  [TIMEOUT] [pytest args...]       GPU test suite -> gpurun_out/tests.log
+#   scripts/gpu.sh tests  [TIMEOUT] [paths / pytest args]  GPU tests (default: all of tests/) -> gpurun_out/tests.log
 #   scripts/gpu.sh smoke                                   __graft_entry__.smoke()
 #   scripts/gpu.sh bench  TAG TIMEOUT [bench.py args...]   1-rank bench -> gpurun_out/TAG.{json,log}
 #   scripts/gpu.sh torchrun TAG TIMEOUT N [bench args...]  N ranks under torch.distributed.run (N ranks
@@ -32,7 +32,8 @@ case "$task" in
   tests)
     t=${1:-900}
     shift || true
-    timeout -k 10 "$t" python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread "$@" \
+    [ $# -eq 0 ] && set -- tests
+    timeout -k 10 "$t" python -u -m pytest -m gpu -x -v --timeout 200 --timeout-method thread "$@" \
       > "$O/tests.log" 2>&1 || fail $? "$O/tests.log"
     tail -3 "$O/tests.log"
     ;;

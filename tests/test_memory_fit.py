@@ -99,3 +99,17 @@ def test_runtime_knobs_keep_trajectory(tmp_path):
     # fp32 everywhere: the knobs only change where gradients are summed (micro-batch split
     # 4x2 -> 2x4 changes the summation order), so the masters agree to fp32 rounding
     torch.testing.assert_close(d["b"], d["a"], rtol=0, atol=2e-6)
+
+
+def test_split_moment_tiers_fills_fastest_first():
+    import torch
+    from deeperspeed_amd.runtime.memory_fit import split_moment_tiers, TierShortfall
+    blocks = [[torch.zeros(100)], [torch.zeros(100)], [torch.zeros(100), torch.zeros(50)], [torch.zeros(100)]]
+    groups, rec = split_moment_tiers(blocks, {"gpu": 900, "cpu": 2100, "nvme": 10_000})
+    assert [g["moments_device"] for g in groups] == ["gpu", "cpu", "nvme"]
+    assert rec["gpu"]["params"] == 100 and rec["cpu"]["params"] == 250 and rec["nvme"]["params"] == 100
+    try:
+        split_moment_tiers(blocks, {"gpu": 900, "cpu": 900, "nvme": 900})
+        raise AssertionError("expected a shortfall")
+    except TierShortfall as e:
+        assert "more than any tier has left" in str(e)
