@@ -825,6 +825,7 @@ def main():
                    "overlap_step": bool(zcfg.get("overlap_step", False)),
                    "host_moments_params": host_numel,
                    "moment_tiers": tiers,
+                   "peak_host_rss_gib": round(_peak_rss() / 2**30, 1),
                    "lt_gemm": _lt_summary() if on_gpu else None,
                    "baseline_note": "vs_baseline = value / (410 tok/s/GPU * N): BASELINE.md's derived target "
                                     "(reference's best published ZeRO-3 49 TFLOPS/GPU on V100 at 6N FLOPs/token); "
@@ -834,6 +835,12 @@ def main():
         emit_result(out)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _peak_rss():
+    """Peak resident host memory of this process (bytes): pinned moments, staging, the runtime."""
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
 
 
 def _lt_summary():

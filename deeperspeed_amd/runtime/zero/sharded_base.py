@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 from typing import Dict, List, Optional
 
 import torch
@@ -53,6 +54,8 @@ HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "stream")
 # torch copy_, a ROCclr blit kernel with a workgroup on every CU, which measured faster in the step
 # (8,787 vs 8,720 tok/s with dedicated queues, profiles/r4s_notes.md)
 HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "0"))
+# DSA_NVME_PROGRESS=1: the NVMe moments tier logs its progress every 8 buckets (long steps)
+NVME_PROGRESS = os.environ.get("DSA_NVME_PROGRESS", "0") == "1"
 # optimizer offload (states all / master / moments, NVMe): copy streams on dedicated hardware queues
 OFFLOAD_DEDICATED_STREAMS = os.environ.get("DSA_OFFLOAD_DEDICATED_STREAMS", "1") != "0"
 
@@ -980,9 +983,15 @@ class ShardedOptimizerBase:
         m_dev = torch.empty(piece, dtype=torch.float32, device=self.device)
         v_dev = torch.empty(piece, dtype=torch.float32, device=self.device)
 
+        t0, done_n = time.time(), [0]
+
         def update(key, t):
             gi, bi = key
             g, b = self.groups[gi], self._mswap_keys[key]
+            done_n[0] += 1
+            if NVME_PROGRESS and done_n[0] % 8 == 0:
+                logger.info(f"NVMe moments tier: {done_n[0]}/{len(keys)} buckets, {time.time() - t0:.1f}s, "
+                            f"{self._mswap.bytes_read / 2**30:.1f} GiB read")
             grp = self._inner_group(g)
             out_full = self._bucket_out(g, b)
             with torch.cuda.stream(ns):
