@@ -7,6 +7,9 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include <ATen/Parallel.h>
+
+#include <cstring>
 #include <optional>
 #include <vector>
 
@@ -1086,6 +1089,28 @@ std::vector<int64_t> stream_priority_range() {
   return {least, greatest};
 }
 
+// Page-locked host memory of exactly `numel` elements (hipHostMalloc), zero-filled, freed with
+// the tensor.  torch's caching host allocator rounds every pinned allocation up to a power of two:
+// 111 GB of Adam moments then pin 128 GiB, which is what put the 41B peak-parameter run over its
+// host-memory budget (profiles/r5c_notes.md).
+Tensor pinned_zeros(int64_t numel, int64_t dtype_code) {
+  const auto dt = dtype_code == 0 ? at::kFloat : (dtype_code == 1 ? at::kBFloat16 : (dtype_code == 2 ? at::kHalf
+                                                                                     : (dtype_code == 3 ? at::kShort : at::kLong)));
+  const size_t bytes = (size_t)std::max<int64_t>(numel, 1) * c10::elementSize(dt);
+  void* p = nullptr;
+  TORCH_CHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess, "hipHostMalloc of ", bytes, " bytes failed");
+  // parallel first touch + zero (one thread would take tens of seconds for 100 GB)
+  const int64_t chunk = 1LL << 26;
+  const int64_t nchunks = ((int64_t)bytes + chunk - 1) / chunk;
+  at::parallel_for(0, nchunks, 1, [&](int64_t b, int64_t e) {
+    for (int64_t c = b; c < e; ++c) {
+      const int64_t off = c * chunk;
+      std::memset((char*)p + off, 0, (size_t)std::min<int64_t>(chunk, (int64_t)bytes - off));
+    }
+  });
+  return at::from_blob(p, {numel}, [](void* q) { (void)hipHostFree(q); }, at::TensorOptions().dtype(dt));
+}
+
 int64_t device_cu_count() {
   int dev = 0, n = 0;
   (void)hipGetDevice(&dev);
@@ -1151,6 +1176,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cu_masked_stream", &cu_masked_stream);
   m.def("device_cu_count", &device_cu_count);
   m.def("priority_stream", &priority_stream);
+  m.def("pinned_zeros", &pinned_zeros);
   m.def("stream_priority_range", &stream_priority_range);
   register_gemm_lt(m);
   m.def("sum_slices", &sum_slices);

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "../include/dsa_common.h"
 #include "../include/launchers.h"
@@ -795,6 +796,177 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
       }
     if (h == 0)
       // a row with every key masked out stores +inf so the backward recomputes P = 0 for it
+      LSE[bh * (int64_t)S + myq] = (m == -INFINITY) ? INFINITY : (m + log2f(l)) * 0.6931471805599453f;
+  }
+}
+
+// ======================================================================== forward v3
+// (opt-in, DSA_FA_FWD=3; measured no faster than v2, which keeps 3 waves per SIMD at D=96)
+// v2's tile math with the key loop software-pipelined inside each wave: the S^T = K Q^T MFMAs of
+// tile j+1 are issued before the softmax and the O^T += V^T P^T MFMAs of tile j, so the matrix
+// pipe works on the next tile while the VALU forms this tile's probabilities (one wave per SIMD
+// no longer idles its matrix pipe through its own softmax; v2 relied on a second wave for that).
+// The K tiles run one stage ahead of the V tiles in LDS: during iteration j the waves read
+// K(j+1) and V(j) and write K(j+2) and V(j+1) into the slots nobody reads in iteration j.
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) fwd_v3_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+                                                        const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
+                                                        float* __restrict__ LSE, int S, float scale, int onh) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int TS = BN2 * LDP<D>;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, c32 = lane & 31;
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  const int nqb = (S + BM2 - 1) / BM2;
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int64_t bh = task / nqb;
+  const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
+  const int myq = qb + 32 * w + c32;
+  const int64_t ib = bh * (int64_t)S * D;
+  const uint16_t* Qb = Q + ib;
+  auto Kslot = [&](int i) { return smem + i * TS; };
+  auto Vslot = [&](int i) { return smem + (2 + i) * TS; };
+
+  s16x8 qf[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks)
+    qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Qb + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const float sl2 = scale * 1.4426950408889634f;
+
+  const int kend = CAUSAL ? min(S, qb + BM2) : S;
+  const int ntiles = (kend + BN2 - 1) / BN2;
+  uint4 kr[D / 32], vr[D / 32];
+  const __amdgpu_buffer_rsrc_t k_rs = head_rsrc(K + ib, S, D), v_rs = head_rsrc(V + ib, S, D);
+  tile_load_buf<D>(kr, k_rs, 0, D);
+  tile_load_buf<D>(vr, v_rs, 0, D);
+  tile_store<D>(Kslot(0), kr);
+  tile_store<D>(Vslot(0), vr);
+  if (ntiles > 1) {
+    tile_load_buf<D>(kr, k_rs, BN2, D);
+    tile_store<D>(Kslot(1), kr);
+  }
+  __syncthreads();
+
+  f32x16 sa[2];
+  // S^T of one tile: the two 32-key halves' MFMA chains interleaved (independent accumulators)
+  auto qk_mfma = [&](const uint16_t* Ks, f32x16 (&acc)[2], int k) {
+    const int t = k & 1, ks = k >> 1;
+    acc[t] = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), qf[ks], acc[t]);
+  };
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sa[t][r] = 0.f;
+#pragma unroll
+  for (int k = 0; k < D / 8; ++k) qk_mfma(Kslot(0), sa, k);
+  __syncthreads();  // every wave has read K(0) before iteration 0 overwrites its slot with K(2)
+
+  // one key tile; NEXT: issue the next tile's S^T MFMAs between this tile's softmax instructions
+  auto tile = [&](int it, auto next_tag) {
+    constexpr bool NEXT = decltype(next_tag)::value;
+    const int j0 = it * BN2;
+    const bool has_next2 = it + 2 < ntiles;
+    if (NEXT) tile_load_buf<D>(vr, v_rs, j0 + BN2, D);
+    if (has_next2) tile_load_buf<D>(kr, k_rs, j0 + 2 * BN2, D);
+    const uint16_t* Vs = Vslot(it & 1);
+    const uint16_t* Kn = Kslot((it + 1) & 1);
+    if ((j0 + BN2 > S) || (CAUSAL && j0 + BN2 - 1 > qb + 32 * w)) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          if (key >= S || (CAUSAL && key > myq)) sa[t][r] = -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[t][r]);
+    mx = xhalf_max(mx);
+    const float mt = mx * sl2;
+    if (__any(mt > m + LAZY_TH)) {  // wave-uniform lazy rescale (v2's LAZY)
+      const float mn = fmaxf(m, mt);
+      const float alpha = fast_exp2(m - ((mn == -INFINITY) ? 0.f : mn));
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    }
+    const float mu = (m == -INFINITY) ? 0.f : m;
+    f32x16 sn[2];
+    if constexpr (NEXT) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sn[t][r] = 0.f;
+    }
+    float pv[32];
+    float ps = 0.f, ps1 = 0.f;
+    // 16 element pairs of exp2 / sums; the next tile's D/8 MFMAs are spread over them
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      if constexpr (NEXT) {
+        if (e < D / 8) qk_mfma(Kn, sn, e);
+      }
+      const int t = e >> 3, r = 2 * (e & 7);
+      pv[16 * t + r] = fast_exp2(fmaf(sa[t][r], sl2, -mu));
+      pv[16 * t + r + 1] = fast_exp2(fmaf(sa[t][r + 1], sl2, -mu));
+      ps += pv[16 * t + r];
+      ps1 += pv[16 * t + r + 1];
+    }
+    if constexpr (NEXT) {
+#pragma unroll
+      for (int k = 16; k < D / 8; ++k) qk_mfma(Kn, sn, k);
+    }
+    ps = xhalf_sum(ps + ps1);
+    l += ps;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const s16x8 pf = __is_same(T, bf16_t) ? pack8(pv, 8 * ks) : pack8_h(pv, 8 * ks);
+      const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const uint16_t* a0 = Vs + row1 * LDP<D> + 32 * dt + 16 * (g16 & 1) + 4 * pc;
+        const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * LDP<D>));
+        o[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, pf, o[dt]);
+      }
+    }
+    if (NEXT) tile_store<D>(Vslot((it + 1) & 1), vr);
+    if (has_next2) tile_store<D>(Kslot(it & 1), kr);
+    __syncthreads();
+    if constexpr (NEXT) {
+      sa[0] = sn[0];
+      sa[1] = sn[1];
+    }
+  };
+  for (int it = 0; it + 1 < ntiles; ++it) tile(it, std::true_type{});
+  if (ntiles > 0) tile(ntiles - 1, std::false_type{});
+  if (myq < S) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh);
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        ushort4 v4;
+        v4.x = to16<T>(o[dt][4 * rb + 0] * inv);
+        v4.y = to16<T>(o[dt][4 * rb + 1] * inv);
+        v4.z = to16<T>(o[dt][4 * rb + 2] * inv);
+        v4.w = to16<T>(o[dt][4 * rb + 3] * inv);
+        *reinterpret_cast<ushort4*>(orow + 32 * dt + 8 * rb + 4 * h) = v4;
+      }
+    if (h == 0)
       LSE[bh * (int64_t)S + myq] = (m == -INFINITY) ? INFINITY : (m + log2f(l)) * 0.6931471805599453f;
   }
 }
@@ -2041,10 +2213,17 @@ void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, floa
   // K / V tiles are addressed per head with 32-bit buffer offsets
   if ((int64_t)S * D * 2 >= (1LL << 31))
     throw std::runtime_error("flash fwd: S * head dim too large for 32-bit buffer offsets");
+  // DSA_FA_FWD=3: the software-pipelined v3 forward (opt-in: 0.357 vs 0.339 ms at B4 H64 S2048 D96
+  // causal, equal at D=64/128 -- it needs 2 waves/SIMD where v2 runs 3, profiles/r5c_notes.md)
+  static const int fwdv = getenv("DSA_FA_FWD") ? atoi(getenv("DSA_FA_FWD")) : 2;
   if (!v1 || onh) {
     dim3 grid2((S + fa::BM2 - 1) / fa::BM2, BH);
     FA_DISPATCH(dt, D, causal,
-      if (eager)
+      if (fwdv == 3 && !eager && bufload)
+        hipLaunchKernelGGL((fa::fwd_v3_kernel<T, DD, CC>), dim3(grid2.x * grid2.y), dim3(256),
+                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                           (uint16_t*)o, lse, S, scale, onh);
+      else if (eager)
         hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, false>), dim3(grid2.x * grid2.y), dim3(256),
                            fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                            (uint16_t*)o, lse, S, scale, onh);

@@ -33,6 +33,20 @@ def hip_ops():
     return _hip
 
 
+_PIN_CODES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int16: 3, torch.int64: 4}
+
+
+def pinned_zeros(numel: int, dtype=torch.float32) -> torch.Tensor:
+    """Zero-filled page-locked host tensor of exactly `numel` elements (hipHostMalloc through the
+    extension; torch's caching host allocator would round a 111 GB request up to 128 GiB).  A
+    plain CPU tensor when no GPU is visible."""
+    if not torch.cuda.is_available():
+        return torch.zeros(numel, dtype=dtype)
+    if numel * torch.empty(0, dtype=dtype).element_size() < (64 << 20) or dtype not in _PIN_CODES:
+        return torch.zeros(numel, dtype=dtype, pin_memory=True)  # small: the caching allocator is fine
+    return hip_ops().pinned_zeros(int(numel), _PIN_CODES[dtype])
+
+
 def on_gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 

@@ -31,8 +31,8 @@ def aligned_numel(numel, element_size):
 
 
 def _pinned(numel, dtype):
-    t = torch.zeros(numel, dtype=dtype)
-    return t.pin_memory() if torch.cuda.is_available() else t
+    from ...ops import native
+    return native.pinned_zeros(numel, dtype)
 
 
 class SwapBuffer:

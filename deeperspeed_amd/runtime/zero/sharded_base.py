@@ -266,7 +266,8 @@ class ShardedOptimizerBase:
                 continue
             m = init_shard_fn(g).float()
             if host:
-                hm = torch.empty(g.shard_numel, dtype=torch.float32, pin_memory=pin)
+                hm = native.pinned_zeros(g.shard_numel, torch.float32) if pin else \
+                    torch.empty(g.shard_numel, dtype=torch.float32)
                 hm.copy_(m)
                 m = hm
             g.master = m
@@ -291,8 +292,12 @@ class ShardedOptimizerBase:
                 kw = dict(dtype=torch.float32, pin_memory=on_host and (pin or moments_only or
                                                                        self._host_moment_group(g)))
                 if on_host:
-                    st["exp_avg"] = torch.zeros(g.shard_numel, **kw)
-                    st["exp_avg_sq"] = torch.zeros(g.shard_numel, **kw)
+                    if kw["pin_memory"]:  # exact-size page-locked memory (native.pinned_zeros)
+                        st["exp_avg"] = native.pinned_zeros(g.shard_numel, torch.float32)
+                        st["exp_avg_sq"] = native.pinned_zeros(g.shard_numel, torch.float32)
+                    else:
+                        st["exp_avg"] = torch.zeros(g.shard_numel, **kw)
+                        st["exp_avg_sq"] = torch.zeros(g.shard_numel, **kw)
                 else:
                     st["exp_avg"] = torch.zeros(g.shard_numel, dtype=torch.float32, device=self.device)
                     st["exp_avg_sq"] = torch.zeros(g.shard_numel, dtype=torch.float32, device=self.device)

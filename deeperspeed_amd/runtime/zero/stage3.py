@@ -362,7 +362,10 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
             t.zero_()
             return t
         pin = bool(self.offload_param.get("pin_memory", True)) and torch.cuda.is_available()
-        return torch.zeros(g.shard_numel, dtype=g.dtype, pin_memory=pin)
+        if pin:
+            from ...ops import native
+            return native.pinned_zeros(g.shard_numel, g.dtype)  # exact size, not a power of two
+        return torch.zeros(g.shard_numel, dtype=g.dtype)
 
     def _grad_dtype(self, g):
         """dtype of the reduced gradient shard (where micro-batch reductions accumulate)."""
