@@ -515,15 +515,73 @@ __device__ __forceinline__ void tile_load(uint4 (&r)[D / 32], const uint16_t* __
   }
 }
 
-template <int D>
+template <int D, int LD = LDP<D>>
 __device__ __forceinline__ void tile_store(uint16_t* lds, const uint4 (&r)[D / 32]) {
   constexpr int CH = D / 8;
 #pragma unroll
   for (int k = 0; k < D / 32; ++k) {
     const int c = threadIdx.x + 256 * k;
     const int row = c / CH, ch = c - row * CH;
-    *reinterpret_cast<uint4*>(lds + row * LDP<D> + ch * 8) = r[k];
+    *reinterpret_cast<uint4*>(lds + row * LD + ch * 8) = r[k];
   }
+}
+
+// Row stride of a tile that is ONLY read transposed (ds_read_b64_tr_b16, 32 lanes = 4 rows x 64 B):
+// the 4 rows must start 16 banks apart.  At D = 96 the unpadded 192-byte row (48 banks) does that;
+// the padded 208-byte row (52 banks) puts rows 0 and 1 of the two column halves on banks 0-3 (2-way).
+// Tiles also read row-wise keep LDP (whose padding makes the ds_read_b128 row reads conflict-free).
+template <int D> constexpr int LDPT = D == 96 ? 96 : LDP<D>;
+
+// Dual-use LDS image for a [64][D] tile read BOTH row-wise (ds_read_b128 A fragments) and
+// transposed (ds_read_b64_tr_b16): 8-row x 32-column subtiles of 512 B with the 16-byte chunks of
+// each row XOR-permuted by bits 2-3 of the row (cdna_hip_programming.md T10, image (a)).  Both
+// read kinds are conflict-free; on the padded 208-byte rows (D = 96) the transposed reads are 2-way
+// for half the lanes.  Element offset of 16-byte chunk `ch` of row `r`:
+template <int D>
+__device__ __forceinline__ int swz_el(int r, int ch) {
+  return (D * 8) * (r >> 3) + 256 * (ch >> 2) + 32 * (r & 7) + 8 * ((ch & 3) ^ ((r >> 2) & 3));
+}
+template <int D>
+__device__ __forceinline__ void tile_store_sw(uint16_t* lds, const uint4 (&r)[D / 32]) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int k = 0; k < D / 32; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    const int row = c / CH, ch = c - row * CH;
+    *reinterpret_cast<uint4*>(lds + swz_el<D>(row, ch)) = r[k];
+  }
+}
+// The kernels' two read patterns on a swizzled image, split into a lane constant (two per pattern,
+// computed once) and a compile-time offset per unrolled step, so every read is one base VGPR plus
+// an immediate offset, as on the padded image:
+//   row read of the 32x32x16 A fragment: row 32t + c32, chunk 2ks + h
+//     = swz_row_lane(ks & 1) + 32*D*t + 256*(ks >> 1)
+//   transposed read: rows 16kb + 4(g16 >> 1) + qd (+ 8 e8), chunk 4dt + 2(g16 & 1) + (pc >> 1)
+//     = swz_tr_lane(e8) + 16*D*kb + 256*dt
+template <int D>
+__device__ __forceinline__ int swz_row_lane(int lane, int odd) {
+  const int c32 = lane & 31, h = lane >> 5;
+  return D * 8 * (c32 >> 3) + 32 * (c32 & 7) + 8 * ((2 * odd + h) ^ ((c32 >> 2) & 3));
+}
+template <int D>
+__device__ __forceinline__ int swz_tr_lane(int lane, int e8) {
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  return D * 8 * e8 + 32 * (4 * (g16 >> 1) + qd) + 8 * ((2 * (g16 & 1) + (pc >> 1)) ^ ((g16 >> 1) + 2 * e8)) +
+         4 * (pc & 1);
+}
+template <int D>
+struct SwzLanes {
+  int r0, r1, t0, t1;
+  __device__ __forceinline__ explicit SwzLanes(int lane)
+      : r0(swz_row_lane<D>(lane, 0)), r1(swz_row_lane<D>(lane, 1)), t0(swz_tr_lane<D>(lane, 0)),
+        t1(swz_tr_lane<D>(lane, 1)) {}
+  __device__ __forceinline__ int row(int t, int ks) const { return ((ks & 1) ? r1 : r0) + 32 * D * t + 256 * (ks >> 1); }
+  __device__ __forceinline__ int tr(int kb, int e8, int dt) const { return (e8 ? t1 : t0) + 16 * D * kb + 256 * dt; }
+};
+template <int D, bool SW>
+__device__ __forceinline__ void tile_put(uint16_t* lds, const uint4 (&r)[D / 32]) {
+  if constexpr (SW) tile_store_sw<D>(lds, r);
+  else tile_store<D>(lds, r);
 }
 
 __device__ __forceinline__ s16x8 pack8(const float* v, int base) {
@@ -611,8 +669,8 @@ __device__ __forceinline__ float* stage_kbias(uint16_t* smem, const float* __res
   return kbs;  // visible after the caller's first __syncthreads()
 }
 
-template <typename T, int D, bool CAUSAL, bool LAZY = true, int EX = 0, bool BUF = true>
-__global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
+template <typename T, int D, bool CAUSAL, bool LAZY = true, int EX = 0, bool BUF = true, bool NL = true>
+__global__ void __launch_bounds__(256, (D >= 128 ? 2 : 3)) fwd_v2_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
                                                         const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
                                                         float* __restrict__ LSE, int S, float scale, int onh,
                                                         Extra ex = Extra()) {
@@ -660,7 +718,7 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
     tile_load<D>(vr, Vb, 0, S, ldi);
   }
   tile_store<D>(smem, kr);
-  tile_store<D>(smem + TS, vr);
+  tile_store<D, (NL ? LDPT<D> : LDP<D>)>(smem + TS, vr);
   __syncthreads();
   for (int it = 0; it < ntiles; ++it) {
     const int j0 = it * BN2;
@@ -767,16 +825,16 @@ __global__ void __launch_bounds__(256, 2) fwd_v2_kernel(const uint16_t* __restri
       const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
-        const uint16_t* a0 = Vs + row1 * LDP<D> + 32 * dt + 16 * (g16 & 1) + 4 * pc;
+        const uint16_t* a0 = Vs + row1 * (NL ? LDPT<D> : LDP<D>) + 32 * dt + 16 * (g16 & 1) + 4 * pc;
         const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * LDP<D>));
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * (NL ? LDPT<D> : LDP<D>)));
         o[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, pf, o[dt]);
       }
     }
     if (has_next) {
       uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
       tile_store<D>(nxt, kr);
-      tile_store<D>(nxt + TS, vr);
+      tile_store<D, (NL ? LDPT<D> : LDP<D>)>(nxt + TS, vr);
     }
     __syncthreads();
   }
@@ -1004,6 +1062,12 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   const float sl2 = scale * 1.4426950408889634f;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
   constexpr bool INIT = V3 && !DROP;
+  // Q, dO: swizzled dual-use images -- off: at D = 96 this kernel is at 256 VGPRs and the image's
+  // extra lane bases cost 48 spilled registers (kSwzDkdv = true builds it for A/B runs)
+  constexpr int kSwzDkdv = 0;  // bit 0: Q image, bit 1: dO image
+  constexpr bool SWQ = (kSwzDkdv & 1) && D == 96 && EX == 0 && !FQ;
+  constexpr bool SWO = (kSwzDkdv & 2) && D == 96 && EX == 0 && !FQ;
+  const SwzLanes<D> sz(lane);
   // this lane's key bias (log2 units) and which 16-bit half of a pair draw is its key's
   const float kb2 = (BIAS && mykey < S) ? ex.kbias[(bh / ex.hdiv) * (int64_t)S + mykey] * LOG2E : 0.f;
   const uint32_t hb = DROP ? drop_head(ex_seed(ex), bh) : 0u;
@@ -1054,8 +1118,8 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   };
   auto store_tile = [&](int stage) {
     uint16_t* b = smem + stage * 2 * TS;
-    tile_store<D>(b, qr);
-    tile_store<D>(b + TS, orr);
+    tile_put<D, SWQ>(b, qr);
+    tile_put<D, SWO>(b + TS, orr);
     if (threadIdx.x < BN2) {
       stats[stage * 2 * BN2 + threadIdx.x] = st_l;
       stats[stage * 2 * BN2 + BN2 + threadIdx.x] = st_d;
@@ -1093,7 +1157,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
       if constexpr (V3) {
         if (t == 1 && has_next) {
           const int nx = (it + 1) & 1;
-          tile_store<D>(smem + nx * 2 * TS, qr);
+          tile_put<D, SWQ>(smem + nx * 2 * TS, qr);
           if (threadIdx.x < BN2) {
             stats[nx * 2 * BN2 + threadIdx.x] = st_l;
             stats[nx * 2 * BN2 + BN2 + threadIdx.x] = st_d;
@@ -1116,8 +1180,9 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
       }
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        sacc = Mfma32<T>::run(lds_row8(Qs + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), kf[ks], sacc);
-        pacc = Mfma32<T>::run(lds_row8(Os + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), vf[ks], pacc);
+        const int rp = (32 * t + c32) * LDP<D> + 16 * ks + 8 * h;
+        sacc = Mfma32<T>::run(lds_row8(Qs + (SWQ ? sz.row(t, ks) : rp)), kf[ks], sacc);
+        pacc = Mfma32<T>::run(lds_row8(Os + (SWO ? sz.row(t, ks) : rp)), vf[ks], pacc);
       }
       float pv[16], dsv[16];
       if constexpr (INIT) {
@@ -1182,11 +1247,12 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt) {
           const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
-          const s16x4 ox = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + row1 * LDP<D> + col));
-          const s16x4 oy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (row1 + 8) * LDP<D> + col));
+          const int px = row1 * LDP<D> + col, py = (row1 + 8) * LDP<D> + col;
+          const s16x4 ox = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (SWO ? sz.tr(ks, 0, dt) : px)));
+          const s16x4 oy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Os + (SWO ? sz.tr(ks, 1, dt) : py)));
           dv[dt] = Mfma32<T>::run(s16x8{ox[0], ox[1], ox[2], ox[3], oy[0], oy[1], oy[2], oy[3]}, pf, dv[dt]);
-          const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + row1 * LDP<D> + col));
-          const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (row1 + 8) * LDP<D> + col));
+          const s16x4 qx = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (SWQ ? sz.tr(ks, 0, dt) : px)));
+          const s16x4 qy = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qs + (SWQ ? sz.tr(ks, 1, dt) : py)));
           dk[dt] = Mfma32<T>::run(s16x8{qx[0], qx[1], qx[2], qx[3], qy[0], qy[1], qy[2], qy[3]}, sf, dk[dt]);
         }
         if constexpr (V3) __builtin_amdgcn_sched_barrier(0);  // bounds the tr-read hoisting: 0 spills vs 12
@@ -1231,7 +1297,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
     }
     if (has_next) {
       if constexpr (V3)
-        tile_store<D>(smem + ((it + 1) & 1) * 2 * TS + TS, orr);
+        tile_put<D, SWO>(smem + ((it + 1) & 1) * 2 * TS + TS, orr);
       else
         store_tile((it + 1) & 1);
     }
@@ -1261,7 +1327,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
 // FD (fused delta): the workgroup that owns a query row also forms its Delta = rowsum(dO * O)
 // from the dO fragments it holds anyway plus the matching O fragments, uses it, and stores it
 // for the dK/dV kernel that runs after it -- no separate Delta pass over dO and O.
-template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true, bool FD = false>
+template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true, bool FD = false, bool NL = true>
 __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_t* __restrict__ Q,
                                            const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
                                            const uint16_t* __restrict__ dO, const float* __restrict__ LSE,
@@ -1281,6 +1347,8 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
   const int64_t base = in_base<D, EX>(ex, bh, S), ldi = in_ld<D, EX>(ex);
   const float sl2 = scale * 1.4426950408889634f;
   constexpr bool BIAS = (EX & EX_BIAS) != 0, DROP = (EX & EX_DROP) != 0;
+  constexpr bool SW = NL && D == 96 && EX == 0;  // K: swizzled dual-use image (row + transposed reads)
+  const SwzLanes<D> sz(lane);
   const float* kbrow = BIAS ? ex.kbias + (bh / ex.hdiv) * (int64_t)S : nullptr;
   const uint32_t hb = DROP ? drop_head(ex_seed(ex), bh) : 0u;
   const float* kbs = BIAS ? stage_kbias<D>(smem, kbrow, S) : nullptr;
@@ -1333,7 +1401,7 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
     tile_load<D>(kr, K + base, 0, S, ldi);
     tile_load<D>(vr, V + base, 0, S, ldi);
   }
-  tile_store<D>(smem, kr);
+  tile_put<D, SW>(smem, kr);
   tile_store<D>(smem + TS, vr);
   __syncthreads();
   for (int it = 0; it < ntiles; ++it) {
@@ -1365,7 +1433,8 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
       for (int r = 0; r < 16; ++r) { sacc[r] = 0.f; pacc[r] = 0.f; }
 #pragma unroll
       for (int ks = 0; ks < D / 16; ++ks) {
-        sacc = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), qf[ks], sacc);
+        sacc = Mfma32<T>::run(lds_row8(SW ? Ks + sz.row(t, ks) : Ks + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h),
+                              qf[ks], sacc);
         pacc = Mfma32<T>::run(lds_row8(Vs + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), of[ks], pacc);
       }
       float dsv[16];
@@ -1411,15 +1480,17 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
 #pragma unroll
         for (int dt = 0; dt < D / 32; ++dt) {
           const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
-          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + row1 * LDP<D> + col));
-          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Ks + (row1 + 8) * LDP<D> + col));
+          const uint16_t* kx = SW ? Ks + sz.tr(ks, 0, dt) : Ks + row1 * LDP<D> + col;
+          const uint16_t* ky = SW ? Ks + sz.tr(ks, 1, dt) : Ks + (row1 + 8) * LDP<D> + col;
+          const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(kx));
+          const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ky));
           dq[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, sf, dq[dt]);
         }
       }
     }
     if (has_next) {
       uint16_t* nxt = smem + ((it + 1) & 1) * 2 * TS;
-      tile_store<D>(nxt, kr);
+      tile_put<D, SW>(nxt, kr);
       tile_store<D>(nxt + TS, vr);
     }
     __syncthreads();
@@ -1452,12 +1523,12 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_dkdv_v2_kernel(
 }
 
 // dQ that also forms and stores Delta (runs before the dK/dV kernel, which reads it)
-template <typename T, int D, bool CAUSAL>
+template <typename T, int D, bool CAUSAL, bool NL = true>
 __global__ void __launch_bounds__(256, 2) bwd_dq_v3_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const uint16_t* __restrict__ O, const float* __restrict__ LSE,
     float* __restrict__ DELTA, uint16_t* __restrict__ dQ, int S, float scale, int onh) {
-  dq_v2_body<T, D, CAUSAL, 0, true, true>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh, Extra(),
+  dq_v2_body<T, D, CAUSAL, 0, true, true, NL>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh, Extra(),
                                           O);
 }
 
@@ -2216,6 +2287,9 @@ void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, floa
   // DSA_FA_FWD=3: the software-pipelined v3 forward (opt-in: 0.357 vs 0.339 ms at B4 H64 S2048 D96
   // causal, equal at D=64/128 -- it needs 2 waves/SIMD where v2 runs 3, profiles/r5c_notes.md)
   static const int fwdv = getenv("DSA_FA_FWD") ? atoi(getenv("DSA_FA_FWD")) : 2;
+  // DSA_FA_LAYOUT=0: padded V rows in the forward and the padded K image in dQ (round 4), for A/B
+  // against the transposed-read layouts (unpadded V at D = 96, swizzled dual-use K image)
+  static const bool old_layout = getenv("DSA_FA_LAYOUT") && getenv("DSA_FA_LAYOUT")[0] == '0';
   if (!v1 || onh) {
     dim3 grid2((S + fa::BM2 - 1) / fa::BM2, BH);
     FA_DISPATCH(dt, D, causal,
@@ -2227,8 +2301,12 @@ void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, floa
         hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, false>), dim3(grid2.x * grid2.y), dim3(256),
                            fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                            (uint16_t*)o, lse, S, scale, onh);
-      else if (bufload)
+      else if (bufload && !old_layout)
         hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true>), dim3(grid2.x * grid2.y), dim3(256),
+                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
+                           (uint16_t*)o, lse, S, scale, onh);
+      else if (bufload)  // DSA_FA_LAYOUT=0: the round-4 LDS layout (A/B)
+        hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true, 0, true, false>), dim3(grid2.x * grid2.y), dim3(256),
                            fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
                            (uint16_t*)o, lse, S, scale, onh);
       else  // DSA_FA_BUFLOAD=0: pointer-form K / V tile loads (A/B only)
@@ -2260,10 +2338,16 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
   if (!v1 && !merge && bufload && fdelta && (dkdv == 3 || dkdv == 31)) {
     // dQ (+ Delta) first, then dK/dV reading that Delta: two launches, no Delta pass
     const unsigned g = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
+    static const bool old_layout = getenv("DSA_FA_LAYOUT") && getenv("DSA_FA_LAYOUT")[0] == '0';
     FA_DISPATCH(dt, D, causal,
-      hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
-                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
-                         (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
+      if (old_layout)
+        hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC, false>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
+                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
+                           (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
+      else
+        hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
+                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
+                           (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
       // D = 128 at two waves per SIMD spills ~160 VGPRs to scratch (hipcc resource usage): one
       // wave per SIMD keeps the whole working set in VGPR + AGPR (4.7x -> see profiles/r4b_*)
       if (dkdv == 3 && DD < 128)
