@@ -31,6 +31,7 @@ import torch.nn.functional as F
 from ..ops import native
 from ..ops.linear import Linear
 from ..ops.transformer import DeepSpeedTransformerConfig, DeepSpeedTransformerLayer
+from ..ops.transformer.transformer import chain_layer_norms, take_chained_norm
 
 
 @dataclass
@@ -106,6 +107,8 @@ class BertForPreTraining(nn.Module):
             nn.init.zeros_(m.bias)
         self.to(device=device, dtype=dtype)
         self._pld_gen = torch.Generator().manual_seed(cfg.seed)
+        # each encoder layer's output pass applies the next LayerNorm (ops/transformer chain_layer_norms)
+        self.chain_norms = True
         self.pld_kept = []  # layers run by the last PLD forward (tests / diagnostics)
 
     def _pld_keep(self, theta: float):
@@ -129,11 +132,14 @@ class BertForPreTraining(nn.Module):
         keep = self._pld_keep(pld_theta) if progressive_layer_drop and self.training else None
         if keep is not None:
             self.pld_kept = [i for i, k in enumerate(keep) if k]
-        for i, layer in enumerate(self.layers):
-            if keep is None or keep[i]:
-                x = layer(x, ext)
+        run = [layer for i, layer in enumerate(self.layers) if keep is None or keep[i]]
+        # each layer's output pass also applies the LayerNorm that reads it next
+        chain_layer_norms(run, self.final_ln, enabled=self.chain_norms)
+        for layer in run:
+            x = layer(x, ext)
         if self.final_ln is not None:
-            x = self.final_ln(x)
+            y = take_chained_norm(x, self.final_ln)
+            x = self.final_ln(x) if y is None else y
         return x
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, masked_positions=None, masked_labels=None,

@@ -704,6 +704,81 @@ std::vector<Tensor> bias_dropout_residual(Tensor x, Tensor bias, Tensor res, dou
   return {y, mask};
 }
 
+// (y, out, mask, mean, rstd): out = res + dropout(x + bias), y = LayerNorm(out) in one pass
+std::vector<Tensor> bdr_ln_fwd(Tensor x, Tensor bias, Tensor res, Tensor gamma, OptT beta, double p, double eps,
+                               int64_t seed, int64_t offset, OptT rng) {
+  check_dev(x, "x"); check_dev(bias, "bias"); check_dev(res, "res"); check_dev(gamma, "gamma");
+  const int64_t H = x.size(-1), rows = x.numel() / H;
+  const int dt = dcode(x);
+  TORCH_CHECK(dsa::bdr_ln_supported((int)H, dt), "bdr_ln_fwd: 16-bit rows of <= 1024 elements (multiple of 8)");
+  TORCH_CHECK(x.is_contiguous() && res.is_contiguous() && res.sizes() == x.sizes() &&
+                  res.scalar_type() == x.scalar_type(), "bdr_ln_fwd: contiguous x / res of one shape and dtype");
+  TORCH_CHECK(bias.numel() == H && bias.is_contiguous() && bias.scalar_type() == x.scalar_type(), "bdr_ln_fwd: bias");
+  TORCH_CHECK(gamma.numel() == H && gamma.is_contiguous() && gamma.scalar_type() == x.scalar_type(),
+              "bdr_ln_fwd: gamma");
+  if (beta.has_value())
+    TORCH_CHECK(beta->numel() == H && beta->is_contiguous() && beta->scalar_type() == x.scalar_type(),
+                "bdr_ln_fwd: beta");
+  for (const Tensor* t : {&x, &res, &bias, &gamma})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "bdr_ln_fwd: 16-byte aligned tensors");
+  if (beta.has_value()) TORCH_CHECK(reinterpret_cast<uintptr_t>(beta->data_ptr()) % 16 == 0, "bdr_ln_fwd: beta align");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  Tensor out = at::empty_like(x), y = at::empty_like(x);
+  Tensor mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({rows}, f32), rstd = at::empty({rows}, f32);
+  dsa::launch_bdr_ln_fwd(x.data_ptr(), bias.data_ptr(), res.data_ptr(), out.data_ptr(), mask.data_ptr<uint8_t>(),
+                         gamma.data_ptr(), beta.has_value() ? beta->data_ptr() : nullptr, y.data_ptr(),
+                         mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)H, (float)p, (float)eps,
+                         (uint64_t)seed, (uint64_t)offset, dt, cur_stream(), rng_ptr(rng, x));
+  return {y, out, mask, mean, rstd};
+}
+
+// (dtot, dxb, dgamma, dbeta, dbias) of bdr_ln_fwd: dtot = d(out) (the residual input's gradient),
+// dxb = the branch input's.  *_acc: bound gradient buffers accumulated into (returned as is).
+std::vector<Tensor> bdr_ln_bwd(Tensor dy, Tensor out, Tensor gamma, Tensor mean, Tensor rstd, bool has_beta,
+                               OptT dres, Tensor mask, double p, OptT dgamma_acc, OptT dbeta_acc, OptT dbias_acc) {
+  check_dev(dy, "dy"); check_dev(out, "out"); check_dev(mask, "mask");
+  const int64_t H = out.size(-1), rows = out.numel() / H;
+  const int dt = dcode(out);
+  TORCH_CHECK(dsa::bdr_ln_supported((int)H, dt), "bdr_ln_bwd: 16-bit rows of <= 1024 elements");
+  TORCH_CHECK(dy.is_contiguous() && dy.sizes() == out.sizes() && dy.scalar_type() == out.scalar_type() &&
+                  out.is_contiguous(), "bdr_ln_bwd: contiguous dy / out of one shape");
+  TORCH_CHECK(mask.is_contiguous() && mask.numel() == out.numel() && mask.scalar_type() == at::kByte,
+              "bdr_ln_bwd: uint8 mask of out's size");
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "bdr_ln_bwd: stats size");
+  if (dres.has_value())
+    TORCH_CHECK(dres->sizes() == out.sizes() && dres->is_contiguous() && dres->scalar_type() == out.scalar_type(),
+                "bdr_ln_bwd: dres");
+  auto like_gamma = [&](const OptT& t, const char* what) {
+    TORCH_CHECK(t->numel() == H && t->is_contiguous() && t->scalar_type() == gamma.scalar_type(), what);
+  };
+  const bool acc = dgamma_acc.has_value();
+  if (acc) {
+    like_gamma(dgamma_acc, "bdr_ln_bwd: dgamma_acc");
+    TORCH_CHECK(!has_beta || dbeta_acc.has_value(), "bdr_ln_bwd: dbeta_acc");
+    if (has_beta) like_gamma(dbeta_acc, "bdr_ln_bwd: dbeta_acc");
+  }
+  if (dbias_acc.has_value()) like_gamma(dbias_acc, "bdr_ln_bwd: dbias_acc");
+  for (const Tensor* t : {&dy, &out, &gamma})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "bdr_ln_bwd: 16-byte aligned tensors");
+  if (dres.has_value()) TORCH_CHECK(reinterpret_cast<uintptr_t>(dres->data_ptr()) % 16 == 0, "bdr_ln_bwd: dres align");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(mask.data_ptr()) % 8 == 0, "bdr_ln_bwd: mask align");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
+  Tensor dtot = at::empty_like(out), dxb = at::empty_like(out);
+  Tensor dgamma = acc ? *dgamma_acc : at::empty_like(gamma);
+  Tensor dbeta = has_beta ? (acc ? *dbeta_acc : at::empty_like(gamma)) : Tensor();
+  Tensor dbias = dbias_acc.has_value() ? *dbias_acc : at::empty_like(gamma);
+  const int grid = dsa::bdr_ln_bwd_grid(rows);
+  Tensor partial = at::empty({3 * (int64_t)grid * H}, out.options().dtype(at::kFloat));
+  dsa::launch_bdr_ln_bwd(dy.data_ptr(), out.data_ptr(), gamma.data_ptr(), mean.data_ptr<float>(),
+                         rstd.data_ptr<float>(), dres.has_value() ? dres->data_ptr() : nullptr,
+                         mask.data_ptr<uint8_t>(), dtot.data_ptr(), dxb.data_ptr(), dgamma.data_ptr(),
+                         has_beta ? dbeta.data_ptr() : nullptr, dbias.data_ptr(), partial.data_ptr<float>(), rows,
+                         (int)H, (float)p, acc ? 1 : 0, dbias_acc.has_value() ? 1 : 0, dt, cur_stream());
+  return {dtot, dxb, dgamma, dbeta, dbias};
+}
+
 // (dx, db) for a bias + dropout + residual block: dx = dy * mask / (1 - p), db = column sums of dx
 std::vector<Tensor> dropout_bwd_db(Tensor dy, Tensor mask, double p) {
   check_dev(dy, "dropout_bwd_db"); check_dev(mask, "dropout_bwd_db");
@@ -1199,6 +1274,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sparse_softmax_bwd", &sparse_softmax_bwd);
   m.def("dropout_fwd", &dropout_fwd, py::arg("x"), py::arg("p"), py::arg("seed"), py::arg("offset"),
         py::arg("rng") = py::none());
+  m.def("bdr_ln_fwd", &bdr_ln_fwd, py::arg("x"), py::arg("bias"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
+        py::arg("p"), py::arg("eps"), py::arg("seed"), py::arg("offset") = 0, py::arg("rng") = py::none());
+  m.def("bdr_ln_bwd", &bdr_ln_bwd, py::arg("dy"), py::arg("out"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("has_beta"), py::arg("dres"), py::arg("mask"), py::arg("p"), py::arg("dgamma_acc") = py::none(),
+        py::arg("dbeta_acc") = py::none(), py::arg("dbias_acc") = py::none());
+  m.def("bdr_ln_supported", [](int64_t H, int64_t code) { return dsa::bdr_ln_supported((int)H, (int)code); });
   m.def("bias_dropout_residual", &bias_dropout_residual, py::arg("x"), py::arg("bias"), py::arg("res"), py::arg("p"),
         py::arg("seed"), py::arg("offset"), py::arg("rng") = py::none());
   m.def("dropout_bwd", &dropout_bwd);

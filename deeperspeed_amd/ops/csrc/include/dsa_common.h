@@ -94,6 +94,10 @@ template <> struct Vec16<float> {
   __device__ __forceinline__ static void store(float* p, const float (&o)[4]) {
     *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
   }
+  // the raw 16-byte vector of o (pack + unpack = the values a store / load round trip yields)
+  __device__ __forceinline__ static uint4 pack(const float (&o)[4]) {
+    return make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
+  }
   // the elements of a raw 16-byte vector already in registers (software-pipelined loads)
   __device__ __forceinline__ static void unpack(const uint4& v, float (&o)[4]) {
     o[0] = __uint_as_float(v.x); o[1] = __uint_as_float(v.y); o[2] = __uint_as_float(v.z); o[3] = __uint_as_float(v.w);
@@ -114,12 +118,15 @@ struct Vec16Half {
       o[2 * i + 1] = TO((uint16_t)(w[i] >> 16));
     }
   }
-  __device__ __forceinline__ static void store(T16* p, const float (&o)[8]) {
+  __device__ __forceinline__ static uint4 pack(const float (&o)[8]) {
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       w[i] = (uint32_t)FROM(o[2 * i]) | ((uint32_t)FROM(o[2 * i + 1]) << 16);
-    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __device__ __forceinline__ static void store(T16* p, const float (&o)[8]) {
+    *reinterpret_cast<uint4*>(p) = pack(o);
   }
 };
 template <> struct Vec16<bf16_t> : Vec16Half<bf16_t, bf16_to_f32, f32_to_bf16> {};

@@ -69,6 +69,10 @@ void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C
                    hipStream_t s);
 // out[c] (+)= sum_r partial[r][c] (fp32 partials, out in dtype dt)
 void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s);
+// three consecutive [R, C] partial blocks into out1, out2 (accum12) and out3 (accum3) in one launch;
+// a null out skips its block
+void launch_colsum3(const float* partial, int R, int C, void* out1, void* out2, void* out3, int accum12, int accum3,
+                    int dt, hipStream_t s);
 // embedding.hip: sync-free deterministic embedding backward over sorted ids (H % 8 == 0)
 int64_t embedding_bwd_chunks(int64_t n);
 void launch_embedding_bwd_sorted(const int64_t* sorted_ids, const int64_t* perm, const void* dy, void* dw,
@@ -143,6 +147,19 @@ void launch_bias_dropout_residual(const void* x, const void* bias, const void* r
                                   int64_t rows, int C, float p, uint64_t seed, uint64_t offset, int dt, hipStream_t s,
                                   const int64_t* rng = nullptr);
 void launch_dropout_bwd(const void* dy, const uint8_t* mask, void* dx, int64_t n, float p, int dt, hipStream_t s);
+// out = res + dropout(x + bias) and y = LayerNorm(out) in one pass (16-bit, H % 8 == 0, H <= 1024)
+bool bdr_ln_supported(int H, int dt);
+int bdr_ln_bwd_grid(int64_t rows);
+void launch_bdr_ln_fwd(const void* x, const void* bias, const void* res, void* out, uint8_t* mask, const void* gamma,
+                       const void* beta, void* y, float* mean, float* rstd, int64_t rows, int H, float p, float eps,
+                       uint64_t seed, uint64_t offset, int dt, hipStream_t s, const int64_t* rng = nullptr);
+// its backward: dtot = LN-backward(dy) + dres, dxb = dtot * mask / (1 - p); gamma / beta / bias
+// gradients from one set of partials (3 * bdr_ln_bwd_grid(rows) * H floats); accum: dgamma / dbeta
+// +=, accum_bias: dbias +=
+void launch_bdr_ln_bwd(const void* dy, const void* xo, const void* gamma, const float* mean, const float* rstd,
+                       const void* dres, const uint8_t* mask, void* dtot, void* dxb, void* dgamma, void* dbeta,
+                       void* dbias, float* partial, int64_t rows, int H, float p, int accum, int accum_bias, int dt,
+                       hipStream_t s);
 
 // flash_attn.hip: q,k,v,o [BH, S, D] (D in 64/96/128), lse/delta [BH, S] fp32
 bool flash_supported(int D);

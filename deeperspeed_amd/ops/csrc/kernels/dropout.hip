@@ -266,6 +266,230 @@ void launch_dropout_bwd_colsum(const void* dy, const uint8_t* mask, void* dx, vo
   launch_colsum_partials(partial, pr, C, db, 0, dt, s);
 }
 
+// ---------------------------------------------------------------------------
+// bias + dropout + residual fused with the LayerNorm that reads its output (pre-LN blocks:
+// out = res + dropout(x + b) is the next sub-layer's LayerNorm input and its residual).  One wave
+// per row (H <= 64 lanes x WV vectors): the row stays in registers between the residual sum and
+// the statistics, so `out` is not read back by a separate LayerNorm launch.  Masks use the same
+// element -> Philox counter map as bias_dropout_residual_vec_kernel and the statistics are taken
+// over the ROUNDED out (what a LayerNorm kernel reading it would see): y, out and the mask are
+// bit-identical to the two-kernel path.
+// ---------------------------------------------------------------------------
+template <typename T, int WV>
+__global__ void __launch_bounds__(256) bdr_ln_fwd_wave_kernel(
+    const T* __restrict__ x, const T* __restrict__ b, const T* __restrict__ res, T* __restrict__ out,
+    uint8_t* __restrict__ mask, const T* __restrict__ gamma, const T* __restrict__ beta, T* __restrict__ y,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int64_t rows, int H, float p, float eps,
+    uint64_t seed, uint64_t offset, const int64_t* __restrict__ rng) {
+  rng_apply(rng, seed, offset);
+  constexpr int VN = Vec16<T>::N;
+  const float scale = 1.f / (1.f - p);
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;  // whole wave
+  const int nvec = H / VN;
+  float vals[WV][VN];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < WV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nvec) {
+      const int64_t v = row * nvec + vi;  // flat vector index = the unfused kernel's Philox group
+      float u[VN], a[VN], bb[VN], r[VN];
+      bool keep[VN];
+      draws<VN>(seed, offset, v, u);
+      Vec16<T>::load(x + v * VN, a);
+      Vec16<T>::load(b + vi * VN, bb);
+      Vec16<T>::load(res + v * VN, r);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) {
+        keep[j] = u[j] >= p;
+        a[j] = r[j] + (keep[j] ? (a[j] + bb[j]) * scale : 0.f);
+      }
+      const uint4 pk = Vec16<T>::pack(a);
+      *reinterpret_cast<uint4*>(out + v * VN) = pk;
+      store_mask<VN>(mask + v * VN, keep);
+      Vec16<T>::unpack(pk, vals[k]);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) s += vals[k][j];
+    }
+  }
+  const float mean = wave_sum(s) / H;
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < WV; ++k)
+    if (lane + 64 * k < nvec) {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) { const float d = vals[k][j] - mean; ss = fmaf(d, d, ss); }
+    }
+  const float rstd = rsqrtf(wave_sum(ss) / H + eps);
+#pragma unroll
+  for (int k = 0; k < WV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nvec) {
+      float gm[VN], bt[VN], o[VN];
+      Vec16<T>::load(gamma + vi * VN, gm);
+      if (beta) Vec16<T>::load(beta + vi * VN, bt);
+#pragma unroll
+      for (int j = 0; j < VN; ++j) o[j] = (vals[k][j] - mean) * rstd * gm[j] + (beta ? bt[j] : 0.f);
+      Vec16<T>::store(y + row * H + vi * VN, o);
+    }
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// Backward of bdr_ln_fwd: the LayerNorm backward (dy, with the residual-path gradient dres added)
+// gives dtot = d(out), which is also the residual input's gradient; the same pass applies the
+// dropout mask (dxb = dtot * mask / (1 - p), the branch gradient) and gathers three column
+// partials per block -- gamma, beta and the bias (sum of dxb) -- folded by one colsum launch.
+// Replaces ln_bwd_wave + colsum + dropout_bwd_colsum + colsum (dtot is not re-read).
+template <typename T, int WV>
+__global__ void __launch_bounds__(256) bdr_ln_bwd_wave_kernel(
+    const T* __restrict__ dy, const T* __restrict__ xo, const T* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const T* __restrict__ dres, const uint8_t* __restrict__ mask,
+    T* __restrict__ dtot, T* __restrict__ dxb, float* __restrict__ partial, int64_t rows, int H, float scale) {
+  extern __shared__ float fold[];  // [4 waves][3][H]
+  constexpr int VN = Vec16<T>::N;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nvec = H / VN;
+  float dg[WV][VN], dbt[WV][VN], dbi[WV][VN], gm[WV][VN];
+#pragma unroll
+  for (int k = 0; k < WV; ++k) {
+    const int vi = lane + 64 * k;
+#pragma unroll
+    for (int j = 0; j < VN; ++j) { dg[k][j] = 0.f; dbt[k][j] = 0.f; dbi[k][j] = 0.f; gm[k][j] = 0.f; }
+    if (vi < nvec) Vec16<T>::load(gamma + vi * VN, gm[k]);
+  }
+  // software-pipelined like ln_bwd_wave_kernel: the next row's loads are in flight during this
+  // row's reductions
+  const int64_t rstep = (int64_t)gridDim.x * 4;
+  int64_t row = (int64_t)blockIdx.x * 4 + w;
+  uint4 nx[WV], ng[WV], nr[WV];
+  uint2 nk[WV];  // raw mask bytes (one per element; VN == 4 uses .x only)
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int64_t r) {
+    if (r >= rows) return;
+    nmu = mean[r];
+    nrs = rstd[r];
+#pragma unroll
+    for (int k = 0; k < WV; ++k) {
+      const int vi = lane + 64 * k;
+      if (vi < nvec) {
+        nx[k] = *reinterpret_cast<const uint4*>(xo + r * H + vi * VN);
+        ng[k] = *reinterpret_cast<const uint4*>(dy + r * H + vi * VN);
+        if (dres) nr[k] = *reinterpret_cast<const uint4*>(dres + r * H + vi * VN);
+        if constexpr (VN == 8) nk[k] = *reinterpret_cast<const uint2*>(mask + r * H + vi * VN);
+        else nk[k] = make_uint2(*reinterpret_cast<const uint32_t*>(mask + r * H + vi * VN), 0u);
+      }
+    }
+  };
+  fetch(row);
+  for (; row < rows; row += rstep) {
+    const float mu = nmu, rs = nrs;
+    float xh[WV][VN], g[WV][VN], rr[WV][VN];
+    uint2 keep[WV];
+#pragma unroll
+    for (int k = 0; k < WV; ++k) {
+      Vec16<T>::unpack(nx[k], xh[k]);
+      Vec16<T>::unpack(ng[k], g[k]);
+      if (dres) Vec16<T>::unpack(nr[k], rr[k]);
+      keep[k] = nk[k];
+    }
+    fetch(row + rstep);
+    float a = 0.f, bsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < WV; ++k) {
+      const int vi = lane + 64 * k;
+      if (vi < nvec) {
+#pragma unroll
+        for (int j = 0; j < VN; ++j) {
+          xh[k][j] = (xh[k][j] - mu) * rs;
+          dg[k][j] = fmaf(g[k][j], xh[k][j], dg[k][j]);
+          dbt[k][j] += g[k][j];
+          const float dxh = g[k][j] * gm[k][j];
+          a += dxh;
+          bsum = fmaf(dxh, xh[k][j], bsum);
+        }
+      }
+    }
+    a = wave_sum(a) / H;
+    bsum = wave_sum(bsum) / H;
+#pragma unroll
+    for (int k = 0; k < WV; ++k) {
+      const int vi = lane + 64 * k;
+      if (vi < nvec) {
+        float o[VN];
+#pragma unroll
+        for (int j = 0; j < VN; ++j) o[j] = rs * (g[k][j] * gm[k][j] - a - xh[k][j] * bsum);
+        if (dres) {
+#pragma unroll
+          for (int j = 0; j < VN; ++j) o[j] += rr[k][j];
+        }
+        const uint4 pk = Vec16<T>::pack(o);
+        *reinterpret_cast<uint4*>(dtot + row * H + vi * VN) = pk;
+        Vec16<T>::unpack(pk, o);  // the rounded dtot, as the unfused dropout backward reads it
+#pragma unroll
+        for (int j = 0; j < VN; ++j) {
+          const uint32_t wd = j < 4 ? keep[k].x : keep[k].y;
+          o[j] = ((wd >> (8 * (j & 3))) & 0xffu) ? o[j] * scale : 0.f;
+          dbi[k][j] += o[j];
+        }
+        Vec16<T>::store(dxb + row * H + vi * VN, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < WV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nvec) {
+#pragma unroll
+      for (int j = 0; j < VN; ++j) {
+        fold[(w * 3) * H + vi * VN + j] = dg[k][j];
+        fold[(w * 3 + 1) * H + vi * VN + j] = dbt[k][j];
+        fold[(w * 3 + 2) * H + vi * VN + j] = dbi[k][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 3 * H; c += 256) {
+    const int which = c / H, col = c - which * H;
+    const float v = fold[(0 * 3 + which) * H + col] + fold[(1 * 3 + which) * H + col] +
+                    fold[(2 * 3 + which) * H + col] + fold[(3 * 3 + which) * H + col];
+    partial[(int64_t)(which * gridDim.x + blockIdx.x) * H + col] = v;
+  }
+}
+
+bool bdr_ln_supported(int H, int dt) { return dt != kF32 && H % 8 == 0 && H <= 64 * 2 * 8; }
+
+int bdr_ln_bwd_grid(int64_t rows) {
+  const int64_t g = (rows + 3) / 4;
+  return (int)(g < 512 ? (g < 1 ? 1 : g) : 512);
+}
+
+void launch_bdr_ln_fwd(const void* x, const void* bias, const void* res, void* out, uint8_t* mask, const void* gamma,
+                       const void* beta, void* y, float* mean, float* rstd, int64_t rows, int H, float p, float eps,
+                       uint64_t seed, uint64_t offset, int dt, hipStream_t s, const int64_t* rng) {
+  if (rows <= 0) return;
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((bdr_ln_fwd_wave_kernel<T, 2>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s,
+                       (const T*)x, (const T*)bias, (const T*)res, (T*)out, mask, (const T*)gamma, (const T*)beta,
+                       (T*)y, mean, rstd, rows, H, p, eps, seed, offset, rng));
+}
+
+// partial workspace: 3 * bdr_ln_bwd_grid(rows) * H floats
+void launch_bdr_ln_bwd(const void* dy, const void* xo, const void* gamma, const float* mean, const float* rstd,
+                       const void* dres, const uint8_t* mask, void* dtot, void* dxb, void* dgamma, void* dbeta,
+                       void* dbias, float* partial, int64_t rows, int H, float p, int accum, int accum_bias, int dt,
+                       hipStream_t s) {
+  if (rows <= 0) return;
+  const int grid = bdr_ln_bwd_grid(rows);
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((bdr_ln_bwd_wave_kernel<T, 2>), dim3(grid), dim3(256), 12 * H * sizeof(float), s,
+                       (const T*)dy, (const T*)xo, (const T*)gamma, mean, rstd, (const T*)dres, mask, (T*)dtot,
+                       (T*)dxb, partial, rows, H, 1.f / (1.f - p)));
+  launch_colsum3(partial, grid, H, dgamma, dbeta, dbias, accum, accum_bias, dt, s);
+}
+
 static inline bool vec_ok(int64_t n, int vn, std::initializer_list<const void*> ptrs) {
   if (n % vn) return false;
   for (const void* q : ptrs)

@@ -368,14 +368,22 @@ __global__ void __launch_bounds__(256) ln_bwd_wave_kernel(const T* __restrict__ 
 // (optionally accumulated into existing out when `accum`).
 // blockIdx.y == 1 sums a second partial block (partial + second_off) into out2 in the same launch
 // (LayerNorm's gamma and beta gradients).
+// blockIdx.y == 2: a third block (partial + 2 * second_off) into out3 with its own accumulate flag
+// (the bias gradient of the fused dropout + LayerNorm backward).
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ partial, int R, int C,
                                                      T* __restrict__ out, int accum, int64_t second_off = 0,
-                                                     T* __restrict__ out2 = nullptr) {
+                                                     T* __restrict__ out2 = nullptr, T* __restrict__ out3 = nullptr,
+                                                     int accum3 = 0) {
   if (blockIdx.y == 1) {
     partial += second_off;
     out = out2;
+  } else if (blockIdx.y == 2) {
+    partial += 2 * second_off;
+    out = out3;
+    accum = accum3;
   }
+  if (out == nullptr) return;
   // 16 columns x 64 row-groups per block: a lane reads 4 columns (float4) of every 64th row
   // (loads issued 4 at a time, all independent), and C / 16 blocks spread the fold over the chip
   // (C % 4 == 0).  The partials are usually L2-resident (written by the previous kernel).
@@ -748,6 +756,13 @@ void launch_sum_slices_f32(const float* part, int S, int64_t n, void* out, int a
 void launch_colsum_partials(const float* partial, int R, int C, void* out, int accum, int dt, hipStream_t s) {
   DSA_DISPATCH_T(dt, T,
     hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 15) / 16), dim3(256), 0, s, partial, R, C, (T*)out, accum));
+}
+
+void launch_colsum3(const float* partial, int R, int C, void* out1, void* out2, void* out3, int accum12, int accum3,
+                    int dt, hipStream_t s) {
+  DSA_DISPATCH_T(dt, T,
+    hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 15) / 16, 3), dim3(256), 0, s, partial, R, C, (T*)out1, accum12,
+                       (int64_t)R * C, (T*)out2, (T*)out3, accum3));
 }
 
 void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C, int accum, int dt,

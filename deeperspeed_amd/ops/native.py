@@ -631,6 +631,27 @@ class _FlashAttnQkvFn(torch.autograd.Function):
         return dqkv, None, None, None, None, None
 
 
+_KB_CACHE = []  # [(source tensor, its key, fp32 [B, S] copy)]: the last conversion
+
+
+def _fp32_key_bias(key_bias, B, S):
+    """key_bias as a contiguous fp32 [B, S]: the conversion of the mask every layer of a forward
+    passes is made once and reused while the same (unmodified) tensor comes back -- one launch per
+    forward instead of one per layer.  Holding the source keeps its storage from being recycled."""
+    if key_bias.dtype == torch.float32 and key_bias.is_contiguous():
+        return key_bias.reshape(B, S)
+    if key_bias.is_cuda and torch.cuda.is_current_stream_capturing():
+        return key_bias.reshape(B, S).float().contiguous()  # a graph may only bake in its own buffers
+    # every layer passes a fresh view of the same mask: match on storage, layout and version
+    key = (key_bias.data_ptr(), key_bias.dtype, key_bias.device, tuple(key_bias.shape), key_bias.stride(),
+           key_bias._version, B, S)
+    if _KB_CACHE and _KB_CACHE[0][1] == key:
+        return _KB_CACHE[0][2]
+    out = key_bias.reshape(B, S).float().contiguous()
+    _KB_CACHE[:] = [(key_bias, key, out)]
+    return out
+
+
 def flash_attention_qkv(qkv, num_heads, key_bias=None, scale=1.0, dropout_p=0.0, training=True, generator=None,
                         rng=None, site=0):
     """Encoder attention straight from the fused QKV projection: qkv [B, S, 3*H*D] (q | k | v,
@@ -641,7 +662,7 @@ def flash_attention_qkv(qkv, num_heads, key_bias=None, scale=1.0, dropout_p=0.0,
     D = C // (3 * num_heads)
     p = float(dropout_p) if training else 0.0
     if key_bias is not None:
-        key_bias = key_bias.reshape(B, S).float().contiguous()
+        key_bias = _fp32_key_bias(key_bias, B, S)
     if rng is not None:  # device [seed, step] (graph-replayable): the host value only names the call site
         seed = site
     else:
@@ -944,6 +965,79 @@ def bias_dropout_residual(x, bias, residual, p, training=True, generator=None, r
     if rng is not None and x.is_cuda:
         return _BiasDropoutResidualFn.apply(x, bias, residual, float(p), int(site) << 20, rng)
     return _BiasDropoutResidualFn.apply(x, bias, residual, float(p), _draw_seed(generator))
+
+
+class _BiasDropoutResidualLNFn(torch.autograd.Function):
+    """(LayerNorm(out), out) with out = res + dropout(x + bias): the residual sum and the LayerNorm
+    of a pre-LN block in one HIP pass (ops/csrc/kernels/dropout.hip bdr_ln_*), and in backward the
+    LayerNorm backward, the residual-gradient add, the dropout backward and the gamma / beta /
+    bias column sums in one pass plus one fold.  `out` is returned for the residual path, like
+    layer_norm_residual.  Reference: the fused bias-residual-LayerNorm of
+    csrc/transformer/normalize_kernels.cu (fused_bias_residual_layer_norm) fed by
+    dropout_kernels.cu ForwardWithBias, ds_transformer_cuda.cpp:224-240."""
+
+    @staticmethod
+    def forward(ctx, x, bias, res, gamma, beta, p, eps, seed, rng):
+        y, out, mask, mean, rstd = hip_ops().bdr_ln_fwd(x, bias, res, gamma, beta, p, eps, seed, 0, rng)
+        _macs(7 * x.numel())
+        ctx.save_for_backward(out, gamma, mean, rstd, mask)
+        ctx.p = p
+        ctx.has_beta = beta is not None
+        ctx.ln_params = (gamma, beta)
+        ctx.bias = bias
+        return y, out
+
+    @staticmethod
+    def backward(ctx, dy, dout):
+        out, gamma, mean, rstd, mask = ctx.saved_tensors
+        if dy is None:  # the LayerNorm output went unused: plain dropout backward of dout
+            dx, db = hip_ops().dropout_bwd_db(dout.contiguous(), mask, ctx.p)
+            return dx, db, dout, None, None, None, None, None, None
+        from .linear import FUSE_WGRAD, _bound_grad
+        g, b = ctx.ln_params
+        acc = None
+        if FUSE_WGRAD and ctx.needs_input_grad[3] and (b is None or ctx.needs_input_grad[4]):
+            gg, gb = _bound_grad(g), (_bound_grad(b) if b is not None else None)
+            if gg is not None and gg.is_contiguous() and (b is None or (gb is not None and gb.is_contiguous())):
+                acc = (gg, gb)
+        bacc = _bound_grad(ctx.bias) if (FUSE_WGRAD and ctx.needs_input_grad[1]) else None
+        if bacc is not None and not bacc.is_contiguous():
+            bacc = None
+        dtot, dxb, dg, dbt, dbias = hip_ops().bdr_ln_bwd(
+            dy.contiguous(), out, gamma, mean, rstd, ctx.has_beta, None if dout is None else dout.contiguous(), mask,
+            ctx.p, None if acc is None else acc[0], None if acc is None else acc[1], bacc)
+        return (dxb, None if bacc is not None else dbias, dtot, None if acc is not None else dg,
+                None if (acc is not None or not ctx.has_beta) else dbt, None, None, None, None)
+
+
+# DSA_BDR_LN=0: the residual sum and the LayerNorm stay two kernels (A/B)
+BDR_LN = os.environ.get("DSA_BDR_LN", "1") != "0"
+
+
+def bdr_ln_supported(x: torch.Tensor, res: torch.Tensor, bias, gamma, beta) -> bool:
+    if not BDR_LN:
+        return False
+    H = x.shape[-1]
+    ts = [x, res, bias, gamma] + ([beta] if beta is not None else [])
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and H % 8 == 0 and H <= 1024
+            and res.shape == x.shape and all(t.dtype == x.dtype and t.is_contiguous() and t.data_ptr() % 16 == 0
+                                             for t in ts))
+
+
+def bias_dropout_residual_ln(x, bias, residual, gamma, beta, eps, p, training=True, generator=None, rng=None,
+                             site=0):
+    """(LayerNorm(out), out) for out = residual + dropout(x + bias) -- the attention / MLP output
+    of a pre-LN block feeding the next sub-layer's LayerNorm.  One fused HIP pass when supported
+    (training with dropout, 16-bit rows of <= 1024), else bias_dropout_residual followed by
+    layer_norm_residual (identical values and masks)."""
+    if training and p > 0 and bdr_ln_supported(x, residual, bias, gamma, beta):
+        if rng is not None:
+            return _BiasDropoutResidualLNFn.apply(x, bias, residual, gamma, beta, float(p), float(eps),
+                                                  int(site) << 20, rng)
+        return _BiasDropoutResidualLNFn.apply(x, bias, residual, gamma, beta, float(p), float(eps),
+                                              _draw_seed(generator), None)
+    out = bias_dropout_residual(x, bias, residual, p, training, generator, rng=rng, site=site)
+    return layer_norm_residual(out, gamma, beta, eps)
 
 
 # --------------------------------------------------------------------------- embedding

@@ -142,7 +142,10 @@ class DeepSpeedTransformerFunction:
         # pre-LN: the block input feeds both the LayerNorm and the residual add; the fused form
         # returns it as a second output so the LN backward adds the residual gradient in-kernel
         fuse_res = cfg.pre_layer_norm and not invertible
-        if fuse_res:
+        pre = getattr(x, "_dsa_next_ln", None)
+        if fuse_res and pre is not None and pre[0] is layer:
+            inp = pre[1]  # the previous layer's output pass already normalised x with this layer's LN
+        elif fuse_res:
             inp, x = native.layer_norm_residual(x, norm_w, norm_b, eps)
         else:
             inp = ln(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
@@ -178,15 +181,25 @@ class DeepSpeedTransformerFunction:
                 ctx = torch.matmul(probs, v)
             ctx = _MergeHeads.apply(ctx) if fast else ctx.transpose(1, 2).reshape(B, S, Hd)
         attn_out = _linear(ctx, attn_ow)
-        add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen, rng=rng,
-                                               site=2)
         if fuse_res:
-            ff1_inp, add_res = native.layer_norm_residual(add_res, attn_nw, attn_nb, eps)
+            # residual sum + the MLP's LayerNorm in one pass (native.bias_dropout_residual_ln)
+            ff1_inp, add_res = native.bias_dropout_residual_ln(attn_out, attn_ob, x, attn_nw, attn_nb, eps,
+                                                               cfg.hidden_dropout_ratio, training, gen, rng=rng, site=2)
         else:
+            add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen,
+                                                   rng=rng, site=2)
             ff1_inp = ln(add_res, attn_nw, attn_nb, eps)
         inter = _gelu_tanh(_linear(ff1_inp, inter_w), inter_b)
         out = _linear(inter, output_w)
-        if cfg.pre_layer_norm:
+        nxt = getattr(layer, "_dsa_next_norm", None) if layer is not None else None
+        if cfg.pre_layer_norm and fuse_res and nxt is not None:
+            # the block output is the next layer's (or the final) LayerNorm input: normalise it in
+            # the same pass and hand the result over on the output tensor (consumed by that owner)
+            owner, nw, nb, neps = nxt
+            y_next, out = native.bias_dropout_residual_ln(out, output_b, add_res, nw, nb, neps,
+                                                          cfg.hidden_dropout_ratio, training, gen, rng=rng, site=3)
+            out._dsa_next_ln = (owner, y_next)
+        elif cfg.pre_layer_norm:
             out = native.bias_dropout_residual(out, output_b, add_res, cfg.hidden_dropout_ratio, training, gen, rng=rng,
                                                site=3)
         else:
@@ -296,6 +309,41 @@ class DeepSpeedTransformerLayer(nn.Module):
         return (out,) if self.config.huggingface else out
 
 
+def chain_layer_norms(layers, final_norm=None, enabled: bool = True):
+    """Let each pre-LN layer of `layers` (the ones that run, in order) normalise its output with
+    the LayerNorm that reads it next -- the following layer's input LayerNorm, or `final_norm`
+    (a FusedLayerNorm / nn.LayerNorm) after the last layer -- in the pass that forms the output
+    (native.bias_dropout_residual_ln), so that LayerNorm is not a separate launch that re-reads the
+    residual stream.  The result travels on the output tensor and is taken only by that owner; any
+    other consumer recomputes the LayerNorm (same values).  Call before every forward whose set of
+    layers can change (progressive layer drop); layers captured as HIP graphs are left unchained,
+    and enabled=False unchains every layer."""
+    def ln_of(mod):
+        if isinstance(mod, DeepSpeedTransformerLayer):
+            c = mod.config
+            if c.pre_layer_norm and not getattr(c, "normalize_invertible", False) and not getattr(mod, "_dsa_graphed", False):
+                return (mod, mod.norm_w, mod.norm_b, c.layer_norm_eps)
+            return None
+        if mod is not None and getattr(mod, "weight", None) is not None and hasattr(mod, "eps"):
+            return (mod, mod.weight, getattr(mod, "bias", None), mod.eps)
+        return None
+
+    layers = list(layers)
+    for i, layer in enumerate(layers):
+        if not isinstance(layer, DeepSpeedTransformerLayer):
+            continue
+        nxt = None
+        if enabled and native.BDR_LN and not getattr(layer, "_dsa_graphed", False):
+            nxt = ln_of(layers[i + 1] if i + 1 < len(layers) else final_norm)
+        object.__setattr__(layer, "_dsa_next_norm", nxt)
+
+
+def take_chained_norm(x, owner):
+    """The LayerNorm output chain_layer_norms' previous layer left on x for `owner`, or None."""
+    pre = getattr(x, "_dsa_next_ln", None)
+    return pre[1] if pre is not None and pre[0] is owner else None
+
+
 def make_graphed_encoder(layers, sample_hidden, sample_mask=None, seed: int = 1234, warmup: int = 3,
                          persistent_grads: bool = True):
     """Capture every DeepSpeedTransformerLayer of `layers` (an nn.ModuleList, replaced in place)
@@ -311,6 +359,9 @@ def make_graphed_encoder(layers, sample_hidden, sample_mask=None, seed: int = 12
     for i, layer in enumerate(layers):
         if not isinstance(layer, DeepSpeedTransformerLayer):
             raise TypeError("make_graphed_encoder: every layer must be a DeepSpeedTransformerLayer")
+        # a graph replays its captured outputs only: no LayerNorm hand-over between layers
+        object.__setattr__(layer, "_dsa_graphed", True)
+        object.__setattr__(layer, "_dsa_next_norm", None)
         layer.enable_device_rng(seed + 7919 * i)
         if persistent_grads:
             # the backward graphs accumulate weight / bias / LayerNorm gradients straight into these

@@ -48,6 +48,9 @@ def _train(graphs, steps=4):
         for layer in engine.module.layers:
             layer._rng[1] = 0
     else:  # eager reference with the same device RNG and the same persistent, in-place-accumulated grads
+        # graphed layers keep their own input LayerNorm (no hand-over between graphs): so does the
+        # reference, or the two would differ in the fp32 summation order of some bias gradients
+        engine.module.chain_norms = False
         for i, layer in enumerate(engine.module.layers):
             layer.enable_device_rng(77 + 7919 * i)
             for p in layer.parameters():
