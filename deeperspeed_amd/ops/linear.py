@@ -297,6 +297,110 @@ class WeightTPrefetch:
 _wt_prefetch = WeightTPrefetch()
 
 
+# Weight transposes made once per optimizer step, off the critical path.  The reduction-contiguous
+# input gradient needs W^T for every linear in every backward; the weights only change at the
+# optimizer step.  With an engine that keeps whole weights resident (ZeRO stage < 3) the first
+# FORWARD use of a weight after a step launches its transpose into a persistent buffer on a
+# low-priority HIP stream of its own hardware queue -- beside the forward GEMMs, which leave CUs
+# idle at BERT-Large's shapes -- and the backward (of every micro-batch until the next step) waits
+# on that event instead of transposing just in time.  A cached transpose is used only while the
+# weight's storage, its autograd version counter and the engine's step epoch (bumped after every
+# optimizer step and checkpoint load: the fused optimizers write weights through raw pointers)
+# all match the ones it was made from.  Opt-in (DSA_WT_CACHE=1): on BERT-Large it measured 3-4 %
+# SLOWER than just-in-time transposes (2,318-2,353 vs 2,415 samples/s at seq 128, 536 vs 554 at
+# seq 512, same box, profiles/r5e_bert_wt_cache_ab.jsonl) -- the concurrent transposes delay the
+# forward's dependency chain by more than they take off the backward's.  It pays only where a
+# step runs several micro-batches (one transpose per weight per step instead of per micro-batch).
+# DSA_WT_CACHE_MAX_GB caps the buffers (default 8 GiB).
+WT_CACHE = os.environ.get("DSA_WT_CACHE", "0") == "1"
+WT_CACHE_MAX_BYTES = float(os.environ.get("DSA_WT_CACHE_MAX_GB", "8")) * 2**30
+
+
+class WeightTCache:
+    def __init__(self):
+        self.enabled = False
+        self.epoch = 0
+        self.ent = {}  # id(weight) -> [weakref(weight), W^T buffer, key, event]
+        self.bytes = 0
+        self.stream = None
+        self.hits = 0  # transposes served from the cache (tests / diagnostics)
+        self.made = 0  # transposes launched by prepare()
+
+    def enable(self, on: bool = True):
+        self.enabled = bool(on) and WT_CACHE
+        if not self.enabled:
+            self.clear()
+
+    def clear(self):
+        if self.stream is not None and self.ent:
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+        self.ent.clear()
+        self.bytes = 0
+
+    def bump(self):
+        """The weights may have changed (optimizer step, checkpoint load): every entry is stale."""
+        self.epoch += 1
+        dead = [k for k, e in self.ent.items() if e[0]() is None]
+        for k in dead:
+            e = self.ent.pop(k)
+            self.bytes -= e[1].numel() * e[1].element_size()
+
+    def _key(self, w):
+        return (w.data_ptr(), w._version, self.epoch)
+
+    def prepare(self, w, tokens: int):
+        """Forward-time hook of a linear over `tokens` rows: make W^T for its backward."""
+        if not (self.enabled and w.is_cuda and w.dim() == 2 and w.dtype in (torch.bfloat16, torch.float16)
+                and DGRAD_NT and w.numel() >= DGRAD_NT_MIN_NUMEL and tokens >= 1024):
+            return
+        if torch.cuda.is_current_stream_capturing():
+            return
+        if lt_tune.DGRAD and lt_tune.use_dgrad(tokens, w.size(0), w.size(1)):
+            return  # that input gradient reads W untransposed
+        e = self.ent.get(id(w))
+        key = self._key(w)
+        if e is not None and e[0]() is w and e[2] == key:
+            return
+        from . import native
+        if not native.transpose_supported(w):
+            return
+        if e is None or e[0]() is not w:
+            n = w.numel() * w.element_size()
+            if e is not None:
+                self.bytes -= e[1].numel() * e[1].element_size()
+                del self.ent[id(w)]
+            if self.bytes + n > WT_CACHE_MAX_BYTES:
+                return
+            import weakref
+            e = self.ent[id(w)] = [weakref.ref(w), torch.empty(w.shape[1], w.shape[0], dtype=w.dtype,
+                                                               device=w.device), None, None]
+            self.bytes += n
+        if self.stream is None:
+            from ..runtime.overlap_step import priority_stream
+            self.stream = priority_stream(w.device, 1 << 20)  # lowest priority, own hardware queue
+        cur = torch.cuda.current_stream(w.device)
+        # after the optimizer step that wrote w and the backward GEMMs that last read the buffer
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            native.transpose2d(w.detach(), out=e[1])
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        e[2], e[3] = key, ev
+        self.made += 1
+
+    def get(self, w):
+        """W^T made by prepare() for this weight's current value, or None."""
+        e = self.ent.get(id(w)) if self.enabled else None
+        if e is None or e[0]() is not w or e[2] != self._key(w):
+            return None
+        torch.cuda.current_stream(w.device).wait_event(e[3])
+        self.hits += 1
+        return e[1]
+
+
+weight_t_cache = WeightTCache()
+
+
 def end_backward_pass():
     clear_transposed()
     _wt_prefetch.end_pass()
@@ -310,6 +414,9 @@ def input_grad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     if (DGRAD_NT and g2.is_cuda and g2.dtype == weight.dtype and weight.numel() >= DGRAD_NT_MIN_NUMEL
             and g2.size(0) >= 1024):
         from . import native
+        wt = weight_t_cache.get(weight)
+        if wt is not None:
+            return g2 @ wt.t()
         if native.transpose_supported(weight):
             if WT_PREFETCH and not torch.cuda.is_current_stream_capturing():
                 return g2 @ _wt_prefetch.get(weight).t()
@@ -461,7 +568,10 @@ class _AccumLinear(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.bias = bias
         ctx.share_gt = share_gt
-        return forward_gemm(x, weight, bias)
+        y = forward_gemm(x, weight, bias)
+        if weight_t_cache.enabled and ctx.needs_input_grad[0]:
+            weight_t_cache.prepare(weight, x.numel() // max(1, x.shape[-1]))
+        return y
 
     @staticmethod
     def backward(ctx, g):
