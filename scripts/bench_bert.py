@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--torch-profile", default="", help="write a torch.profiler op table of one step here")
+    ap.add_argument("--host-sleep-ms", type=float, default=0.0,
+                    help="diagnostic: sleep this long on the host after issuing each step (a GPU-bound "
+                         "step absorbs it up to its host slack; a host-bound one slows by it)")
     ap.add_argument("--hip-graphs", choices=["on", "off"], default="off",
                     help="capture every encoder layer's forward / backward as HIP graphs "
                          "(ops/transformer make_graphed_encoder; dropout from device RNG state)")
@@ -97,6 +100,8 @@ def main():
         kept.append(len(model.pld_kept) if args.pld else cfg.num_layers)
         engine.backward(loss)
         engine.step()
+        if args.host_sleep_ms > 0:
+            time.sleep(args.host_sleep_ms / 1e3)
         return loss
 
     for _ in range(args.warmup):
