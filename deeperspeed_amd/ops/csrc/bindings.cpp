@@ -177,9 +177,21 @@ void lamb_multi(Tensor meta, int64_t T, int64_t total_chunks, int64_t chunk, int
                          partial.data_ptr<float>(), coeff.data_ptr<float>(), cur_stream());
 }
 
+// A caller-provided output buffer (layer-stacked slabs, ops/wgrad_batch.py) or a fresh one like `like`.
+static Tensor out_or_new(const OptT& out, at::IntArrayRef sizes, const at::TensorOptions& opt, const char* what) {
+  if (!out.has_value()) return at::empty(sizes, opt);
+  TORCH_CHECK(out->sizes() == sizes && out->scalar_type() == opt.dtype().toScalarType() && out->is_contiguous() &&
+                  out->device() == opt.device() && reinterpret_cast<uintptr_t>(out->data_ptr()) % 16 == 0,
+              what, ": out must be a contiguous 16-byte aligned tensor of the result's shape and dtype");
+  return *out;
+}
+static Tensor out_or_empty(const OptT& out, const Tensor& like, const char* what) {
+  return out_or_new(out, like.sizes(), like.options(), what);
+}
+
 // ----------------------------------------------------------------------------- layer norm
 // Returns (y, mean, rstd, sum) where sum = x + res (+bias) when res is given (else undefined).
-std::vector<Tensor> ln_fwd(Tensor x, Tensor gamma, OptT beta, double eps, OptT res, OptT bias) {
+std::vector<Tensor> ln_fwd(Tensor x, Tensor gamma, OptT beta, double eps, OptT res, OptT bias, OptT y_out) {
   check_dev(x, "x"); check_dev(gamma, "gamma");
   const int64_t H = x.size(-1);
   const int64_t rows = x.numel() / H;
@@ -196,7 +208,7 @@ std::vector<Tensor> ln_fwd(Tensor x, Tensor gamma, OptT beta, double eps, OptT r
     if (bias.has_value()) TORCH_CHECK(bias->numel() == H && bias->scalar_type() == x.scalar_type());
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  Tensor y = at::empty_like(x);
+  Tensor y = out_or_empty(y_out, x, "ln_fwd");
   auto f32 = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({rows}, f32), rstd = at::empty({rows}, f32);
   dsa::launch_ln_fwd(x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr,
@@ -274,28 +286,28 @@ Tensor add3(Tensor a, Tensor b, OptT c) {
   return y;
 }
 
-Tensor bias_gelu_fwd(Tensor x, OptT b, bool approx) {
+Tensor bias_gelu_fwd(Tensor x, OptT b, bool approx, OptT out) {
   check_dev(x, "x");
   const int64_t C = x.size(-1);
   const int dt = dcode(x);
   TORCH_CHECK(C % (dt == dsa::kCodeF32 ? 4 : 8) == 0, "bias_gelu: last dim must be a multiple of 16 bytes");
   if (b.has_value()) TORCH_CHECK(b->numel() == C && b->scalar_type() == x.scalar_type(), "bias_gelu: bias");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  Tensor y = at::empty_like(x);
+  Tensor y = out_or_empty(out, x, "bias_gelu_fwd");
   dsa::launch_bias_gelu_fwd(x.data_ptr(), b.has_value() ? b->data_ptr() : nullptr, y.data_ptr(), x.numel() / C,
                             (int)C, approx ? 1 : 0, dt, cur_stream());
   return y;
 }
 
 // Returns (dx, dbias)
-std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, OptT b, bool approx) {
+std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, OptT b, bool approx, OptT dx_out) {
   check_dev(dy, "dy"); check_dev(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "bias_gelu_bwd: mismatch");
   const int64_t C = x.size(-1);
   const int64_t rows = x.numel() / C;
   const int dt = dcode(x);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  Tensor dx = at::empty_like(x);
+  Tensor dx = out_or_empty(dx_out, x, "bias_gelu_bwd");
   Tensor db, partial;
   if (b.has_value()) {
     db = at::empty_like(*b);
@@ -706,7 +718,7 @@ std::vector<Tensor> bias_dropout_residual(Tensor x, Tensor bias, Tensor res, dou
 
 // (y, out, mask, mean, rstd): out = res + dropout(x + bias), y = LayerNorm(out) in one pass
 std::vector<Tensor> bdr_ln_fwd(Tensor x, Tensor bias, Tensor res, Tensor gamma, OptT beta, double p, double eps,
-                               int64_t seed, int64_t offset, OptT rng) {
+                               int64_t seed, int64_t offset, OptT rng, OptT y_out) {
   check_dev(x, "x"); check_dev(bias, "bias"); check_dev(res, "res"); check_dev(gamma, "gamma");
   const int64_t H = x.size(-1), rows = x.numel() / H;
   const int dt = dcode(x);
@@ -723,7 +735,7 @@ std::vector<Tensor> bdr_ln_fwd(Tensor x, Tensor bias, Tensor res, Tensor gamma, 
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "bdr_ln_fwd: 16-byte aligned tensors");
   if (beta.has_value()) TORCH_CHECK(reinterpret_cast<uintptr_t>(beta->data_ptr()) % 16 == 0, "bdr_ln_fwd: beta align");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  Tensor out = at::empty_like(x), y = at::empty_like(x);
+  Tensor out = at::empty_like(x), y = out_or_empty(y_out, x, "bdr_ln_fwd");
   Tensor mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
   auto f32 = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({rows}, f32), rstd = at::empty({rows}, f32);
@@ -737,7 +749,8 @@ std::vector<Tensor> bdr_ln_fwd(Tensor x, Tensor bias, Tensor res, Tensor gamma, 
 // (dtot, dxb, dgamma, dbeta, dbias) of bdr_ln_fwd: dtot = d(out) (the residual input's gradient),
 // dxb = the branch input's.  *_acc: bound gradient buffers accumulated into (returned as is).
 std::vector<Tensor> bdr_ln_bwd(Tensor dy, Tensor out, Tensor gamma, Tensor mean, Tensor rstd, bool has_beta,
-                               OptT dres, Tensor mask, double p, OptT dgamma_acc, OptT dbeta_acc, OptT dbias_acc) {
+                               OptT dres, Tensor mask, double p, OptT dgamma_acc, OptT dbeta_acc, OptT dbias_acc,
+                               OptT dxb_out) {
   check_dev(dy, "dy"); check_dev(out, "out"); check_dev(mask, "mask");
   const int64_t H = out.size(-1), rows = out.numel() / H;
   const int dt = dcode(out);
@@ -765,7 +778,7 @@ std::vector<Tensor> bdr_ln_bwd(Tensor dy, Tensor out, Tensor gamma, Tensor mean,
   if (dres.has_value()) TORCH_CHECK(reinterpret_cast<uintptr_t>(dres->data_ptr()) % 16 == 0, "bdr_ln_bwd: dres align");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(mask.data_ptr()) % 8 == 0, "bdr_ln_bwd: mask align");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
-  Tensor dtot = at::empty_like(out), dxb = at::empty_like(out);
+  Tensor dtot = at::empty_like(out), dxb = out_or_empty(dxb_out, out, "bdr_ln_bwd");
   Tensor dgamma = acc ? *dgamma_acc : at::empty_like(gamma);
   Tensor dbeta = has_beta ? (acc ? *dbeta_acc : at::empty_like(gamma)) : Tensor();
   Tensor dbias = dbias_acc.has_value() ? *dbias_acc : at::empty_like(gamma);
@@ -956,7 +969,7 @@ static void check_qkv(const Tensor& qkv, const char* what) {
 }
 
 std::vector<Tensor> flash_attn_qkv_fwd(Tensor qkv, c10::optional<Tensor> kbias, double scale, double p_drop,
-                                       int64_t seed, OptT rng) {
+                                       int64_t seed, OptT rng, OptT o_out) {
   check_qkv(qkv, "flash_attn_qkv_fwd");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
   TORCH_CHECK(S % 8 == 0 && (D == 64 || D == 128), "flash_attn_qkv_fwd: S % 8 == 0 and head dim 64 or 128");
@@ -967,7 +980,7 @@ std::vector<Tensor> flash_attn_qkv_fwd(Tensor qkv, c10::optional<Tensor> kbias, 
                 "flash_attn_qkv_fwd: kbias must be contiguous fp32 [B, S]");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
-  Tensor o = at::empty({B, S, H, D}, qkv.options());
+  Tensor o = out_or_new(o_out, {B, S, H, D}, qkv.options(), "flash_attn_qkv_fwd");
   Tensor lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
   const char* base = static_cast<const char*>(qkv.data_ptr());
   const int64_t hd = H * D * qkv.element_size();
@@ -978,7 +991,7 @@ std::vector<Tensor> flash_attn_qkv_fwd(Tensor qkv, c10::optional<Tensor> kbias, 
 }
 
 Tensor flash_attn_qkv_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, c10::optional<Tensor> kbias, double scale,
-                          double p_drop, int64_t seed, OptT rng) {
+                          double p_drop, int64_t seed, OptT rng, OptT dqkv_out) {
   check_qkv(qkv, "flash_attn_qkv_bwd");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
   for (auto* t : {&dout, &o}) {
@@ -994,7 +1007,7 @@ Tensor flash_attn_qkv_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, c10::op
                 "flash_attn_qkv_bwd: kbias");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
-  Tensor dqkv = at::empty_like(qkv);
+  Tensor dqkv = out_or_empty(dqkv_out, qkv, "flash_attn_qkv_bwd");
   Tensor delta = at::empty_like(lse);
   const char* base = static_cast<const char*>(qkv.data_ptr());
   char* dbase = static_cast<char*>(dqkv.data_ptr());
@@ -1261,9 +1274,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_fwd_ex", &flash_attn_fwd_ex);
   m.def("flash_attn_bwd_ex", &flash_attn_bwd_ex);
   m.def("flash_attn_qkv_fwd", &flash_attn_qkv_fwd, py::arg("qkv"), py::arg("kbias"), py::arg("scale"), py::arg("p_drop"),
-        py::arg("seed"), py::arg("rng") = py::none());
+        py::arg("seed"), py::arg("rng") = py::none(), py::arg("o_out") = py::none());
   m.def("flash_attn_qkv_bwd", &flash_attn_qkv_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"), py::arg("lse"),
-        py::arg("kbias"), py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("rng") = py::none());
+        py::arg("kbias"), py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("rng") = py::none(),
+        py::arg("dqkv_out") = py::none());
   m.def("sparse_flash_bwd", &sparse_flash_bwd);
   m.def("onebit_worker_compress", &onebit_worker_compress);
   m.def("onebit_server_compress", &onebit_server_compress);
@@ -1275,10 +1289,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_fwd", &dropout_fwd, py::arg("x"), py::arg("p"), py::arg("seed"), py::arg("offset"),
         py::arg("rng") = py::none());
   m.def("bdr_ln_fwd", &bdr_ln_fwd, py::arg("x"), py::arg("bias"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
-        py::arg("p"), py::arg("eps"), py::arg("seed"), py::arg("offset") = 0, py::arg("rng") = py::none());
+        py::arg("p"), py::arg("eps"), py::arg("seed"), py::arg("offset") = 0, py::arg("rng") = py::none(),
+        py::arg("y_out") = py::none());
   m.def("bdr_ln_bwd", &bdr_ln_bwd, py::arg("dy"), py::arg("out"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("has_beta"), py::arg("dres"), py::arg("mask"), py::arg("p"), py::arg("dgamma_acc") = py::none(),
-        py::arg("dbeta_acc") = py::none(), py::arg("dbias_acc") = py::none());
+        py::arg("dbeta_acc") = py::none(), py::arg("dbias_acc") = py::none(), py::arg("dxb_out") = py::none());
   m.def("bdr_ln_supported", [](int64_t H, int64_t code) { return dsa::bdr_ln_supported((int)H, (int)code); });
   m.def("bias_dropout_residual", &bias_dropout_residual, py::arg("x"), py::arg("bias"), py::arg("res"), py::arg("p"),
         py::arg("seed"), py::arg("offset"), py::arg("rng") = py::none());
@@ -1307,12 +1322,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("wt"), py::arg("gt"), py::arg("ot"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
         py::arg("wd"), py::arg("bc1"), py::arg("bc2"), py::arg("grad_scale"), py::arg("max_coeff"), py::arg("min_coeff"),
         py::arg("adamw"), py::arg("partial"), py::arg("coeff"), py::arg("scale") = py::none());
-  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("res"),
+        py::arg("bias"), py::arg("y_out") = py::none());
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("has_beta"), py::arg("dres") = py::none(), py::arg("dgamma_acc") = py::none(),
         py::arg("dbeta_acc") = py::none());
-  m.def("bias_gelu_fwd", &bias_gelu_fwd);
-  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("bias_gelu_fwd", &bias_gelu_fwd, py::arg("x"), py::arg("b"), py::arg("approx"), py::arg("out") = py::none());
+  m.def("bias_gelu_bwd", &bias_gelu_bwd, py::arg("dy"), py::arg("x"), py::arg("b"), py::arg("approx"),
+        py::arg("dx_out") = py::none());
   m.def("bias_gelu_fwd_t", &bias_gelu_fwd_t);
   m.def("bias_gelu_bwd_t", &bias_gelu_bwd_t);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);

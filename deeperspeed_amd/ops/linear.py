@@ -36,6 +36,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import lt_tune
+from . import wgrad_batch as _wb
 
 FUSE_WGRAD = os.environ.get("DSA_FUSE_WGRAD", "1") != "0"
 WGRAD_NT = os.environ.get("DSA_WGRAD_NT", "1") != "0"
@@ -436,6 +437,14 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     has_b = bias is not None and need_b
     fuse = FUSE_WGRAD and need_w and (not has_b or _bound_grad(bias) is not None)
     gw = _bound_grad(weight) if fuse else None
+    if gw is not None and _wb.state.defer and (not has_b or bias.grad.is_contiguous()) and _wb.deferrable(g2, x2, gw):
+        # run at the end of the backward, batched with the other layers' (ops/wgrad_batch.py)
+        _wb.record(g2, x2, gw)
+        if has_b:
+            from . import native
+            native.colsum(g2, bias.grad, accumulate=True)
+        _count[0] += 1
+        return None, None
     split = _split_k(g2, x2) if need_w else 1
     if split > 1:
         from . import native

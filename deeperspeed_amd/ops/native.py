@@ -115,6 +115,15 @@ class _LayerNormFn(torch.autograd.Function):
         return dx, dg, (db if ctx.has_beta else None), None
 
 
+def _slab(spec, like, backward=False):
+    """A layer slot of ops/wgrad_batch's stacked buffers for this output (spec = (kind, layer,
+    layers)), or None for ordinary memory."""
+    if spec is None or not like.is_cuda:
+        return None
+    from . import wgrad_batch
+    return wgrad_batch.view(spec[0], spec[1], spec[2], like, backward)
+
+
 def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float = 1e-5):
     return _LayerNormFn.apply(x, weight, bias, eps)
 
@@ -126,11 +135,11 @@ class _LayerNormResidualFn(torch.autograd.Function):
     normalize_kernels.cu:1350-1790) instead of autograd summing the two branches separately."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps):
+    def forward(ctx, x, gamma, beta, eps, y_slab=None):
         x = x.contiguous()
         _macs(5 * x.numel())
         if x.is_cuda:
-            y, mean, rstd, _ = hip_ops().ln_fwd(x, gamma, beta, eps, None, None)
+            y, mean, rstd, _ = hip_ops().ln_fwd(x, gamma, beta, eps, None, None, _slab(y_slab, x))
         else:
             y, mean, rstd = _ln_ref(x, gamma, beta, eps)
         ctx.save_for_backward(x, gamma, mean, rstd)
@@ -143,19 +152,21 @@ class _LayerNormResidualFn(torch.autograd.Function):
         x, gamma, mean, rstd = ctx.saved_tensors
         if not x.is_cuda:
             dx, dg, db, _ = _LayerNormFn.backward(ctx, dy)
-            return (dx if dres is None else dx + dres), dg, db, None
+            return (dx if dres is None else dx + dres), dg, db, None, None
         dres = None if dres is None else dres.contiguous()
         acc = _ln_param_acc(ctx)
         if acc is not None:
             dx, _, _ = hip_ops().ln_bwd(dy.contiguous(), x, gamma, mean, rstd, ctx.has_beta, dres, acc[0], acc[1])
-            return dx, None, None, None
+            return dx, None, None, None, None
         dx, dg, db = hip_ops().ln_bwd(dy.contiguous(), x, gamma, mean, rstd, ctx.has_beta, dres)
-        return dx, dg, (db if ctx.has_beta else None), None
+        return dx, dg, (db if ctx.has_beta else None), None, None
 
 
-def layer_norm_residual(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float = 1e-5):
-    """(LayerNorm(x), x): use the second output for the residual path (fused backward add)."""
-    return _LayerNormResidualFn.apply(x, weight, bias, eps)
+def layer_norm_residual(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], eps: float = 1e-5,
+                        y_slab=None):
+    """(LayerNorm(x), x): use the second output for the residual path (fused backward add).
+    y_slab: (kind, layer, layers) slot of ops/wgrad_batch for the normalised output."""
+    return _LayerNormResidualFn.apply(x, weight, bias, eps, y_slab)
 
 
 class _InvertibleLayerNormFn(torch.autograd.Function):
@@ -234,7 +245,7 @@ def _gelu_t_ok(x2: torch.Tensor) -> bool:
             and x2.size(0) % 128 == 0 and x2.size(1) % 64 == 0 and x2.size(0) > 0 and x2.data_ptr() % 16 == 0)
 
 
-def _gelu_bwd(dy, x, bias, approx, offer_t):
+def _gelu_bwd(dy, x, bias, approx, offer_t, dx_out=None):
     """(dx, db) of y = gelu(x + bias).  With offer_t, on the GPU one pass also writes dx^T and
     hands it to ops.linear as the pre-transposed output gradient of the linear that produced x
     (its weight gradient then skips the transpose of dx)."""
@@ -245,7 +256,7 @@ def _gelu_bwd(dy, x, bias, approx, offer_t):
         from . import linear as _linear
         _linear.offer_transposed(dx, dxt)
         return dx.view(x.shape), db
-    return hip_ops().bias_gelu_bwd(dy, x, bias, approx)
+    return hip_ops().bias_gelu_bwd(dy, x, bias, approx, dx_out)
 
 
 # DSA_DUAL_GELU_BWD=0: the bias+GeLU backward writes only dx (the linear transposes it itself)
@@ -254,17 +265,18 @@ DUAL_GELU_BWD = os.environ.get("DSA_DUAL_GELU_BWD", "1") != "0"
 
 class _BiasGeluFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias, approx, offer_t=False):
+    def forward(ctx, x, bias, approx, offer_t=False, slabs=None):
         x = x.contiguous()
         _macs(2 * x.numel())
         if x.is_cuda:
-            y = hip_ops().bias_gelu_fwd(x, bias, approx)
+            y = hip_ops().bias_gelu_fwd(x, bias, approx, _slab(slabs and slabs[0], x))
         else:
             y = _gelu_ref((x.float() + (bias.float() if bias is not None else 0)), approx).to(x.dtype)
         ctx.save_for_backward(x, bias)
         ctx.approx = approx
         ctx.offer_t = offer_t
         ctx.has_bias = bias is not None
+        ctx.dx_slab = slabs and slabs[1]
         return y
 
     @staticmethod
@@ -272,7 +284,7 @@ class _BiasGeluFn(torch.autograd.Function):
         x, bias = ctx.saved_tensors
         dy = dy.contiguous()
         if x.is_cuda:
-            dx, db = _gelu_bwd(dy, x, bias, ctx.approx, ctx.offer_t)
+            dx, db = _gelu_bwd(dy, x, bias, ctx.approx, ctx.offer_t, _slab(ctx.dx_slab, x, backward=True))
         else:
             with torch.enable_grad():
                 xi = (x.float() + (bias.float() if bias is not None else 0)).detach().requires_grad_(True)
@@ -280,13 +292,15 @@ class _BiasGeluFn(torch.autograd.Function):
                 (g,) = torch.autograd.grad(y, xi, dy.float())
             dx = g.to(x.dtype)
             db = g.reshape(-1, g.shape[-1]).sum(0).to(bias.dtype) if bias is not None else None
-        return dx, (db if ctx.has_bias else None), None, None
+        return dx, (db if ctx.has_bias else None), None, None, None
 
 
-def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False, offer_t: bool = False):
+def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor], approximate: bool = False, offer_t: bool = False,
+              slabs=None):
     """gelu(x + bias).  offer_t: x is the output of an ops.linear whose weight gradient takes
-    the reduction-contiguous path -- the backward then also forms dx^T for it in the same pass."""
-    return _BiasGeluFn.apply(x, bias, approximate, offer_t)
+    the reduction-contiguous path -- the backward then also forms dx^T for it in the same pass.
+    slabs: (y spec, dx spec) layer slots of ops/wgrad_batch for the output and its input gradient."""
+    return _BiasGeluFn.apply(x, bias, approximate, offer_t, slabs)
 
 
 class _BiasGeluTFn(torch.autograd.Function):
@@ -615,20 +629,22 @@ def flash_attention_encoder(q, k, v, key_bias=None, scale=1.0, dropout_p=0.0, tr
 
 class _FlashAttnQkvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv5, kbias, scale, p, seed, rng=None):
+    def forward(ctx, qkv5, kbias, scale, p, seed, rng=None, slabs=None):
         B, S, _, H, D = qkv5.shape
         _macs(2 * B * H * S * S * D)
-        o, lse = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed, rng)
+        o_out = _slab(slabs and slabs[0], qkv5[:, :, 0])
+        o, lse = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed, rng, o_out)
         ctx.save_for_backward(qkv5, o, lse, kbias)
         ctx.scale, ctx.p, ctx.seed, ctx.rng = scale, p, seed, rng
+        ctx.dqkv_slab = slabs and slabs[1]
         return o
 
     @staticmethod
     def backward(ctx, do):
         qkv5, o, lse, kbias = ctx.saved_tensors
         dqkv = hip_ops().flash_attn_qkv_bwd(do.contiguous(), qkv5, o, lse, kbias, ctx.scale, ctx.p, ctx.seed,
-                                            ctx.rng)
-        return dqkv, None, None, None, None, None
+                                            ctx.rng, _slab(ctx.dqkv_slab, qkv5, backward=True))
+        return dqkv, None, None, None, None, None, None
 
 
 _KB_CACHE = []  # [(source tensor, its key, fp32 [B, S] copy)]: the last conversion
@@ -653,7 +669,7 @@ def _fp32_key_bias(key_bias, B, S):
 
 
 def flash_attention_qkv(qkv, num_heads, key_bias=None, scale=1.0, dropout_p=0.0, training=True, generator=None,
-                        rng=None, site=0):
+                        rng=None, site=0, slabs=None):
     """Encoder attention straight from the fused QKV projection: qkv [B, S, 3*H*D] (q | k | v,
     heads contiguous inside each) -> context [B, S, H*D], same math as flash_attention_encoder
     (same keep mask for the same seed) without the head split / merge copies; the backward
@@ -668,7 +684,7 @@ def flash_attention_qkv(qkv, num_heads, key_bias=None, scale=1.0, dropout_p=0.0,
     else:
         seed = (_draw_seed(generator) if p > 0.0 else 0) & ((1 << 63) - 1)
     o = _FlashAttnQkvFn.apply(qkv.contiguous().view(B, S, 3, num_heads, D), key_bias, float(scale), p, int(seed),
-                              rng if p > 0.0 else None)
+                              rng if p > 0.0 else None, slabs)
     return o.view(B, S, num_heads * D)
 
 
@@ -977,8 +993,10 @@ class _BiasDropoutResidualLNFn(torch.autograd.Function):
     dropout_kernels.cu ForwardWithBias, ds_transformer_cuda.cpp:224-240."""
 
     @staticmethod
-    def forward(ctx, x, bias, res, gamma, beta, p, eps, seed, rng):
-        y, out, mask, mean, rstd = hip_ops().bdr_ln_fwd(x, bias, res, gamma, beta, p, eps, seed, 0, rng)
+    def forward(ctx, x, bias, res, gamma, beta, p, eps, seed, rng, slabs=None):
+        y, out, mask, mean, rstd = hip_ops().bdr_ln_fwd(x, bias, res, gamma, beta, p, eps, seed, 0, rng,
+                                                        _slab(slabs and slabs[0], x))
+        ctx.dxb_slab = slabs and slabs[1]
         _macs(7 * x.numel())
         ctx.save_for_backward(out, gamma, mean, rstd, mask)
         ctx.p = p
@@ -992,7 +1010,7 @@ class _BiasDropoutResidualLNFn(torch.autograd.Function):
         out, gamma, mean, rstd, mask = ctx.saved_tensors
         if dy is None:  # the LayerNorm output went unused: plain dropout backward of dout
             dx, db = hip_ops().dropout_bwd_db(dout.contiguous(), mask, ctx.p)
-            return dx, db, dout, None, None, None, None, None, None
+            return dx, db, dout, None, None, None, None, None, None, None
         from .linear import FUSE_WGRAD, _bound_grad
         g, b = ctx.ln_params
         acc = None
@@ -1005,9 +1023,10 @@ class _BiasDropoutResidualLNFn(torch.autograd.Function):
             bacc = None
         dtot, dxb, dg, dbt, dbias = hip_ops().bdr_ln_bwd(
             dy.contiguous(), out, gamma, mean, rstd, ctx.has_beta, None if dout is None else dout.contiguous(), mask,
-            ctx.p, None if acc is None else acc[0], None if acc is None else acc[1], bacc)
+            ctx.p, None if acc is None else acc[0], None if acc is None else acc[1], bacc,
+            _slab(ctx.dxb_slab, out, backward=True))
         return (dxb, None if bacc is not None else dbias, dtot, None if acc is not None else dg,
-                None if (acc is not None or not ctx.has_beta) else dbt, None, None, None, None)
+                None if (acc is not None or not ctx.has_beta) else dbt, None, None, None, None, None)
 
 
 # DSA_BDR_LN=0: the residual sum and the LayerNorm stay two kernels (A/B)
@@ -1025,19 +1044,20 @@ def bdr_ln_supported(x: torch.Tensor, res: torch.Tensor, bias, gamma, beta) -> b
 
 
 def bias_dropout_residual_ln(x, bias, residual, gamma, beta, eps, p, training=True, generator=None, rng=None,
-                             site=0):
+                             site=0, slabs=None):
     """(LayerNorm(out), out) for out = residual + dropout(x + bias) -- the attention / MLP output
     of a pre-LN block feeding the next sub-layer's LayerNorm.  One fused HIP pass when supported
     (training with dropout, 16-bit rows of <= 1024), else bias_dropout_residual followed by
-    layer_norm_residual (identical values and masks)."""
+    layer_norm_residual (identical values and masks).  slabs: (LayerNorm output spec, x-gradient
+    spec) layer slots of ops/wgrad_batch."""
     if training and p > 0 and bdr_ln_supported(x, residual, bias, gamma, beta):
         if rng is not None:
             return _BiasDropoutResidualLNFn.apply(x, bias, residual, gamma, beta, float(p), float(eps),
-                                                  int(site) << 20, rng)
+                                                  int(site) << 20, rng, slabs)
         return _BiasDropoutResidualLNFn.apply(x, bias, residual, gamma, beta, float(p), float(eps),
-                                              _draw_seed(generator), None)
+                                              _draw_seed(generator), None, slabs)
     out = bias_dropout_residual(x, bias, residual, p, training, generator, rng=rng, site=site)
-    return layer_norm_residual(out, gamma, beta, eps)
+    return layer_norm_residual(out, gamma, beta, eps, y_slab=slabs and slabs[0])
 
 
 # --------------------------------------------------------------------------- embedding

@@ -119,10 +119,6 @@ def _use_head_kernels(x, hd):
     return x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and hd % 8 == 0
 
 
-def _gelu_tanh(x, b):
-    return native.bias_gelu(x, b, approximate=True)
-
-
 class DeepSpeedTransformerFunction:
     """Functional form of the layer (reference exposes an autograd.Function with this name)."""
 
@@ -142,11 +138,19 @@ class DeepSpeedTransformerFunction:
         # pre-LN: the block input feeds both the LayerNorm and the residual add; the fused form
         # returns it as a second output so the LN backward adds the residual gradient in-kernel
         fuse_res = cfg.pre_layer_norm and not invertible
+        # layer slots of the stacked activation / gradient buffers of ops/wgrad_batch (the weight
+        # gradients of all layers then run as batched GEMMs); set by chain_layer_norms
+        si, sn = (getattr(layer, "_dsa_slab_index", None), getattr(layer, "_dsa_slab_count", 0)) \
+            if (layer is not None and torch.is_grad_enabled()) else (None, 0)
+
+        def slab(kind, idx=None):
+            return None if si is None else (kind, si if idx is None else idx, sn)
+
         pre = getattr(x, "_dsa_next_ln", None)
         if fuse_res and pre is not None and pre[0] is layer:
             inp = pre[1]  # the previous layer's output pass already normalised x with this layer's LN
         elif fuse_res:
-            inp, x = native.layer_norm_residual(x, norm_w, norm_b, eps)
+            inp, x = native.layer_norm_residual(x, norm_w, norm_b, eps, y_slab=slab("qkv_x"))
         else:
             inp = ln(x, norm_w, norm_b, eps) if cfg.pre_layer_norm else x
         qkv = _linear(inp, attn_qkvw, attn_qkvb)
@@ -164,7 +168,8 @@ class DeepSpeedTransformerFunction:
             # scores, key-padding bias, softmax, dropout and P V stay on chip, the context is
             # written token-major [B, S, nh * hd] for the output projection, dqkv in qkv's layout
             ctx = native.flash_attention_qkv(qkv, nh, None if mask is None else mask.reshape(B, S),
-                                             1.0 / math.sqrt(hd), cfg.attn_dropout_ratio, training, gen, rng=rng, site=1)
+                                             1.0 / math.sqrt(hd), cfg.attn_dropout_ratio, training, gen, rng=rng, site=1,
+                                             slabs=(slab("ao_x"), slab("qkv_dy")))
         else:
             if fast:
                 q, k, v = _SplitHeads.apply(qkv, nh)  # contiguous [B, nh, S, hd]: batched GEMMs without copies
@@ -184,20 +189,25 @@ class DeepSpeedTransformerFunction:
         if fuse_res:
             # residual sum + the MLP's LayerNorm in one pass (native.bias_dropout_residual_ln)
             ff1_inp, add_res = native.bias_dropout_residual_ln(attn_out, attn_ob, x, attn_nw, attn_nb, eps,
-                                                               cfg.hidden_dropout_ratio, training, gen, rng=rng, site=2)
+                                                               cfg.hidden_dropout_ratio, training, gen, rng=rng, site=2,
+                                                               slabs=(slab("fc1_x"), slab("ao_dy")))
         else:
             add_res = native.bias_dropout_residual(attn_out, attn_ob, x, cfg.hidden_dropout_ratio, training, gen,
                                                    rng=rng, site=2)
             ff1_inp = ln(add_res, attn_nw, attn_nb, eps)
-        inter = _gelu_tanh(_linear(ff1_inp, inter_w), inter_b)
+        inter = native.bias_gelu(_linear(ff1_inp, inter_w), inter_b, approximate=True,
+                                 slabs=(slab("fc2_x"), slab("fc1_dy")))
         out = _linear(inter, output_w)
         nxt = getattr(layer, "_dsa_next_norm", None) if layer is not None else None
         if cfg.pre_layer_norm and fuse_res and nxt is not None:
             # the block output is the next layer's (or the final) LayerNorm input: normalise it in
             # the same pass and hand the result over on the output tensor (consumed by that owner)
             owner, nw, nb, neps = nxt
+            nidx = getattr(owner, "_dsa_slab_index", None) if isinstance(owner, DeepSpeedTransformerLayer) else None
             y_next, out = native.bias_dropout_residual_ln(out, output_b, add_res, nw, nb, neps,
-                                                          cfg.hidden_dropout_ratio, training, gen, rng=rng, site=3)
+                                                          cfg.hidden_dropout_ratio, training, gen, rng=rng, site=3,
+                                                          slabs=(None if nidx is None else slab("qkv_x", nidx),
+                                                                 slab("fc2_dy")))
             out._dsa_next_ln = (owner, y_next)
         elif cfg.pre_layer_norm:
             out = native.bias_dropout_residual(out, output_b, add_res, cfg.hidden_dropout_ratio, training, gen, rng=rng,
@@ -329,6 +339,10 @@ def chain_layer_norms(layers, final_norm=None, enabled: bool = True):
         return None
 
     layers = list(layers)
+    ours = [l for l in layers if isinstance(l, DeepSpeedTransformerLayer) and not getattr(l, "_dsa_graphed", False)]
+    for i, layer in enumerate(ours):  # slots of the layer-stacked buffers (ops/wgrad_batch.py)
+        object.__setattr__(layer, "_dsa_slab_index", i if enabled else None)
+        object.__setattr__(layer, "_dsa_slab_count", len(ours))
     for i, layer in enumerate(layers):
         if not isinstance(layer, DeepSpeedTransformerLayer):
             continue

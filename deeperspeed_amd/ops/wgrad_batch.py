@@ -1,0 +1,219 @@
+"""Layer-batched weight gradients for deep stacks of equal layers.
+
+A BERT-Large encoder layer has four linears whose weight gradients dW = dY^T X (a reduction over
+the 8k tokens of a step) are each too small for 256 CUs: 16-64 output tiles of 256 x 256, so the
+per-layer path splits the token reduction four ways and folds fp32 partials (0.4-0.7 PF/s; ~6.5 ms
+of a 26.5 ms seq-128 step).  The same gradient of all 24 layers together is 384-1536 tiles -- one
+strided-batched hipBLASLt GEMM at 0.7-1.1 PF/s (profiles/r5f_wgrad_batched.jsonl).  hipBLASLt's
+grouped GEMM (per-problem pointers) rejects every solution on this build and rocBLAS's pointer-array
+batched GEMM runs at ~3 TF/s, so the operands must sit at a constant stride:
+
+* slabs -- the producers of every X and dY of these linears (LayerNorm, bias-GeLU, encoder flash
+  attention forward and backward, the fused dropout + LayerNorm backward) write into per-layer
+  slots of persistent [layers, ...] buffers (`view`); a slot is lent once per backward pass and
+  reclaimed when that backward ends (`release`), so a second forward before a backward, or an
+  activation-checkpoint recompute, simply gets ordinary memory;
+* gradient stacks -- the parameters of equal shape get their .grad bound to slots of one
+  [layers, out, in] buffer (`bind_grad_stacks`, persistent gradients zeroed in place by the
+  optimizer);
+* deferral -- inside an engine backward whose gradients nobody reads before it returns (no ZeRO
+  bucket hooks), ops/linear.py records (dY, X, dW) instead of running the GEMM (`record`), and the
+  end of the backward runs each shape's records as ONE batched GEMM when all three operands are
+  consecutive slots of their buffers (`flush`), else one GEMM per record.
+
+Bias gradients are still formed in place.  Same math as the per-layer path up to fp32 summation
+order.  DSA_BATCH_WGRAD=0 disables.  No reference counterpart: the reference computes each
+layer's weight gradients inside its layer backward (csrc/transformer/ds_transformer_cuda.cpp:370-540).
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+ENABLED = os.environ.get("DSA_BATCH_WGRAD", "1") != "0"
+MIN_TOKENS = 1024
+
+
+class _Slab:
+    def __init__(self, buf: torch.Tensor):
+        self.buf = buf
+        self.busy = [False] * buf.shape[0]
+        self.slot_bytes = buf[0].numel() * buf.element_size()
+        self.base = buf.data_ptr()
+
+    def slot_of(self, t: torch.Tensor) -> Optional[int]:
+        off = t.data_ptr() - self.base
+        if off < 0 or off % self.slot_bytes or off // self.slot_bytes >= len(self.busy):
+            return None
+        if t.numel() != self.buf[0].numel():
+            return None
+        return off // self.slot_bytes
+
+
+class _State:
+    def __init__(self):
+        self.slabs_on = False  # set by an engine whose backward may defer (no gradient hooks)
+        self.slabs: Dict[tuple, _Slab] = {}
+        self.stacks: List[_Slab] = []  # persistent gradient stacks
+        self.defer = False
+        self.pending: List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
+        self.batched = 0  # batched GEMMs launched (tests / diagnostics)
+        self.single = 0  # records run one by one
+        self.recorded = 0
+        self.last_miss = None  # why the last group could not be batched (diagnostics)
+
+
+state = _State()
+
+
+def enable(on: bool = True):
+    """An engine whose gradients are only read after its backward returns turns slabs on."""
+    state.slabs_on = bool(on) and ENABLED
+
+
+def view(kind: str, index: int, count: int, like: torch.Tensor, backward: bool = False) -> Optional[torch.Tensor]:
+    """Slot `index` of the [count, *like.shape] slab `kind`, or None (slabs off, or the slot already
+    lent in this pass).  Callers ask only for tensors of a forward that records a graph (inside an
+    autograd Function grad mode is off, so the caller decides that before entering it)."""
+    if not (state.slabs_on and like.is_cuda and 0 <= index < count) or count < 2:
+        return None
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    key = (kind, count, tuple(like.shape), like.dtype, like.device)
+    slab = state.slabs.get(key)
+    if slab is None:
+        slab = state.slabs[key] = _Slab(torch.empty((count,) + tuple(like.shape), dtype=like.dtype,
+                                                    device=like.device))
+    if slab.busy[index]:
+        return None
+    slab.busy[index] = True
+    return slab.buf[index]
+
+
+def release():
+    """End of a backward: every lent slot may be written again by the next forward."""
+    for slab in state.slabs.values():
+        slab.busy = [False] * len(slab.busy)
+
+
+def bind_grad_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> int:
+    """Bind the .grad of every group of >= min_count equal-shape parameters -- weights of >= min_numel
+    elements, and the 1-D biases / LayerNorm parameters whose in-place gradient sums let their
+    linear's weight gradient be deferred -- to consecutive slots of one zeroed [n, *shape] buffer
+    (persistent gradients: the fp16 optimizer zeroes them in place instead of dropping them).
+    Returns the number of parameters bound."""
+    groups: Dict[tuple, list] = {}
+    for p in params:
+        if p.requires_grad and p.is_cuda and (p.dim() == 1 or (p.dim() == 2 and p.numel() >= min_numel)):
+            groups.setdefault((tuple(p.shape), p.dtype, p.device), []).append(p)
+    n = 0
+    for (shape, dtype, dev), ps in groups.items():
+        if len(ps) < min_count:
+            continue
+        buf = torch.zeros((len(ps),) + shape, dtype=dtype, device=dev)
+        for i, p in enumerate(ps):
+            p.grad = buf[i]
+            p._dsa_persistent_grad = True
+        state.stacks.append(_Slab(buf))
+        n += len(ps)
+    return n
+
+
+class deferred:
+    """Context of one backward whose bound weight gradients are recorded and run at its end."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = bool(enabled) and ENABLED
+
+    def __enter__(self):
+        self.owner = self.enabled and not state.defer
+        if self.owner:
+            state.defer = True
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if not self.owner:
+            return False
+        state.defer = False
+        if exc_type is not None:
+            state.pending.clear()
+            release()
+            return False
+        flush()
+        release()
+        return False
+
+
+def deferrable(g2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor) -> bool:
+    return (state.defer and g2.is_cuda and g2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == g2.dtype
+            and gw.dtype == g2.dtype and g2.dim() == 2 and x2.dim() == 2 and g2.is_contiguous()
+            and x2.is_contiguous() and gw.is_contiguous() and g2.size(0) >= MIN_TOKENS
+            and not torch.cuda.is_current_stream_capturing())
+
+
+def record(g2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor):
+    if gw.requires_grad:
+        raise RuntimeError(f"wgrad_batch.record: gradient buffer requires grad: shape {tuple(gw.shape)} "
+                           f"leaf {gw.is_leaf} param {isinstance(gw, torch.nn.Parameter)} base "
+                           f"{None if gw._base is None else tuple(gw._base.shape)}")
+    state.pending.append((g2, x2, gw))
+    state.recorded += 1
+
+
+def _owner(t: torch.Tensor, pools) -> Optional[Tuple[_Slab, int]]:
+    for slab in pools:
+        i = slab.slot_of(t)
+        if i is not None:
+            return slab, i
+    return None
+
+
+def _batch(items):
+    """(dY [L, M, N], X [L, M, K], dW [L, N, K]) strided views over consecutive slots when every
+    record's operands sit in one slab each, in the same slot order; else None."""
+    slabs = list(state.slabs.values())
+    locs = []
+    for g2, x2, gw in items:
+        a, b, c = _owner(g2, slabs), _owner(x2, slabs), _owner(gw, state.stacks)
+        if a is None or b is None or c is None:
+            state.last_miss = ("operand outside the slabs", tuple(g2.shape), tuple(x2.shape), a is None, b is None,
+                               c is None)
+            return None
+        locs.append((a, b, c))
+    order = sorted(range(len(items)), key=lambda i: locs[i][1][1])
+    views = []
+    for k in range(3):
+        slab0 = locs[order[0]][k][0]
+        first = locs[order[0]][k][1]
+        for j, i in enumerate(order):
+            s, idx = locs[i][k]
+            if s is not slab0 or idx != first + j:
+                state.last_miss = ("slots not consecutive", k, [locs[i][k][1] for i in order])
+                return None
+        rows, cols = items[0][k].shape
+        views.append(slab0.buf[first:first + len(items)].view(len(items), rows, cols))
+    return views
+
+
+@torch.no_grad()
+def flush():
+    """Run every recorded weight gradient (see the module docstring).  Gradient accumulation is
+    not part of any graph: the GEMMs run outside autograd, as they would inside the backward."""
+    pend, state.pending = state.pending, []
+    groups: Dict[tuple, list] = {}
+    for g2, x2, gw in pend:
+        groups.setdefault((tuple(g2.shape), tuple(x2.shape), g2.dtype, g2.device), []).append((g2, x2, gw))
+    for items in groups.values():
+        if len(items) > 1 and len({gw.data_ptr() for _, _, gw in items}) == len(items):
+            v = _batch(items)
+            if v is not None:
+                dy, x, dw = v
+                dw.baddbmm_(dy.transpose(1, 2), x)
+                state.batched += 1
+                continue
+        for g2, x2, gw in items:  # a weight used twice accumulates in order
+            gw.addmm_(g2.t(), x2)
+            state.single += 1

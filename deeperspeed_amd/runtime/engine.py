@@ -25,6 +25,7 @@ import torch.distributed as dist
 from torch.nn.modules import Module
 
 from ..ops import linear as _linear_ops
+from ..ops import wgrad_batch as _wgrad_batch
 from ..ops.adam.fused_adam import FusedAdam
 from ..utils.distributed import init_distributed
 from ..utils import comm
@@ -132,6 +133,17 @@ class DeepSpeedEngine(Module):
         # releases weights per unit, and its HBM goes to retention instead
         _linear_ops.weight_t_cache.enable(self.optimizer is not None and self.zero_optimization_stage() < 3
                                           and self.device.type == "cuda")
+        # weight gradients may wait for the end of backward only where no gradient hook reads them
+        # during it: no ZeRO stage, no bucket hooks of a flat-arena optimizer, no overlapped step;
+        # then equal layers' weight gradients run as batched GEMMs (ops/wgrad_batch.py) with their
+        # .grad bound to persistent stacks the fp16 optimizer zeroes in place
+        from .fp16.unfused_optimizer import FP16_UnfusedOptimizer
+        self._defer_wgrad = (isinstance(self.optimizer, FP16_UnfusedOptimizer) and self.device.type == "cuda"
+                             and not self.zero_optimization() and getattr(self.optimizer, "_overlap", None) is None
+                             and _wgrad_batch.ENABLED)
+        _wgrad_batch.enable(self._defer_wgrad)
+        if self._defer_wgrad:
+            _wgrad_batch.bind_grad_stacks(self.module.parameters())
 
         self.csr_tensor_module_names = set()
         if self.sparse_gradients_enabled():
@@ -786,13 +798,16 @@ class DeepSpeedEngine(Module):
             self.timers("backward_inner").start()
         if hasattr(self.optimizer, "is_gradient_accumulation_boundary"):
             self.optimizer.is_gradient_accumulation_boundary = self.is_gradient_accumulation_boundary()
-        if hasattr(self.optimizer, "backward") and (self.zero_optimization() or self.fp16_enabled()):
-            self.optimizer.backward(loss)
-        elif self.amp is not None:
-            # the unscale is delayed to the accumulation boundary (apex delay_unscale)
-            self.amp.scale(loss).backward()
-        else:
-            loss.backward()
+        # weight gradients deferred to one batched GEMM per shape at the end of this backward,
+        # where nothing reads gradients before it returns (ops/linear.py deferred_wgrads)
+        with _wgrad_batch.deferred(self._defer_wgrad):
+            if hasattr(self.optimizer, "backward") and (self.zero_optimization() or self.fp16_enabled()):
+                self.optimizer.backward(loss)
+            elif self.amp is not None:
+                # the unscale is delayed to the accumulation boundary (apex delay_unscale)
+                self.amp.scale(loss).backward()
+            else:
+                loss.backward()
         _linear_ops.end_backward_pass()  # pre-transposed operands never outlive their backward
         if self.wall_clock_breakdown():
             self.timers("backward_inner").stop()

@@ -1,0 +1,118 @@
+"""Layer-batched weight gradients (ops/wgrad_batch.py): the slab / gradient-stack bookkeeping and
+the batched flush against per-record GEMMs, a weight used twice in one backward, and BERT training
+through the engine with and without batching."""
+
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_flush_batches_consecutive_slots():
+    from deeperspeed_amd.ops import wgrad_batch as wb
+    g = torch.Generator().manual_seed(0)
+    L, M, N, K = 4, 1024, 384, 256
+    wb.state.slabs.clear()
+    wb.state.stacks.clear()
+    wb.enable(True)
+    try:
+        xs = [wb.view("x", i, L, torch.empty(M, K, device="cuda", dtype=torch.bfloat16)) for i in range(L)]
+        dys = [wb.view("dy", i, L, torch.empty(M, N, device="cuda", dtype=torch.bfloat16), backward=True)
+               for i in range(L)]
+        assert all(t is not None for t in xs + dys)
+        assert wb.view("dy", 0, L, dys[0], backward=True) is None  # lent until release()
+        for t in xs + dys:
+            t.copy_(torch.randn(t.shape, generator=g).to(t.dtype))
+        ps = [torch.nn.Parameter(torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)) for _ in range(L)]
+        assert wb.bind_grad_stacks(ps, min_numel=1) == L
+        for p in ps:
+            p.grad.copy_(torch.randn(N, K, generator=g).to(torch.bfloat16))
+        ref = [p.grad.float() + d.float().t() @ x.float() for p, d, x in zip(ps, dys, xs)]
+        b0 = wb.state.batched
+        with wb.deferred(True):
+            for i in (2, 0, 3, 1):  # recorded out of order
+                wb.record(dys[i], xs[i], ps[i].grad)
+        assert wb.state.batched == b0 + 1 and not wb.state.pending
+        for p, r in zip(ps, ref):
+            assert (p.grad.float() - r).abs().max().item() <= 1e-2 * r.abs().max().item()
+        assert wb.view("dy", 0, L, dys[0], backward=True) is not None  # released at the end of the pass
+    finally:
+        wb.enable(False)
+        wb.release()
+
+
+def test_deferred_weight_used_twice():
+    from deeperspeed_amd.ops import linear as L
+    from deeperspeed_amd.ops import wgrad_batch as wb
+    torch.manual_seed(0)
+    lin = L.Linear(256, 256).cuda().bfloat16()
+    other = L.Linear(256, 256).cuda().bfloat16()
+    x = torch.randn(2048, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    grads = {}
+    for defer in (False, True):
+        for p in list(lin.parameters()) + list(other.parameters()):
+            p.grad = torch.zeros_like(p)  # bound gradients, as the engine binds them
+        r0 = wb.state.recorded
+        with wb.deferred(defer):
+            y = lin(other(lin(x)))  # lin's weight gradient recorded twice
+            y.float().pow(2).mean().backward()
+        assert (wb.state.recorded > r0) == defer and not wb.state.pending
+        grads[defer] = [p.grad.float().clone() for p in list(lin.parameters()) + list(other.parameters())]
+    for a, b in zip(grads[False], grads[True]):
+        assert (a - b).abs().max().item() <= 2e-2 * max(1e-3, a.abs().max().item())
+
+
+def _env():
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29573")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+
+
+def _train(batch, monkeypatch, steps=3):
+    _env()
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.bert import BertForPreTraining, get_config
+    from deeperspeed_amd.ops import wgrad_batch as wb
+    monkeypatch.setattr(wb, "ENABLED", batch)
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = get_config("bert-large", num_layers=4, vocab_size=4096, max_position=128)  # dropout 0.1
+    model = BertForPreTraining(cfg, device=dev, dtype=torch.bfloat16).train()
+    conf = {"train_micro_batch_size_per_gpu": 8, "optimizer": {"type": "Lamb", "params": {"lr": 2e-3}},
+            "fp16": {"enabled": True, "type": "bfloat16"}, "gradient_clipping": 1.0}
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    assert engine._defer_wgrad == batch
+    g = torch.Generator(device=dev).manual_seed(1)
+    B, S, npred = 8, 128, 20
+    ids = torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)
+    am = torch.ones(B, S, device=dev, dtype=torch.long)
+    am[:, 100:] = 0
+    pos = torch.stack([torch.randperm(100, device=dev, generator=g)[:npred].sort().values for _ in range(B)])
+    lab = torch.randint(0, cfg.vocab_size, (B, npred), device=dev, generator=g)
+    nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
+    b0, losses = wb.state.batched, []
+    for _ in range(steps):
+        loss = engine(ids, None, am, pos, lab, nsp)
+        engine.backward(loss)
+        engine.step()
+        losses.append(float(loss.detach()))
+    torch.cuda.synchronize()
+    out = losses, [p.detach().float().clone() for p in engine.module.parameters()], wb.state.batched - b0
+    print("last batching miss:", wb.state.last_miss, "slabs:", [(k[0], k[1], k[2]) for k in wb.state.slabs],
+          "recorded:", wb.state.recorded, "single:", wb.state.single)
+    wb.enable(False)
+    return out
+
+
+def test_bert_training_with_batched_wgrads(monkeypatch):
+    l0, w0, n0 = _train(False, monkeypatch)
+    l1, w1, n1 = _train(True, monkeypatch)
+    assert n0 == 0 and n1 == 4 * 3, (n0, n1)  # qkv / attn-out / fc1 / fc2, every step
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 2e-2 * abs(a)
+    for a, b in zip(w0, w1):
+        assert (a - b).abs().max().item() <= 1e-2 * max(1.0, a.abs().max().item())
