@@ -437,7 +437,8 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     has_b = bias is not None and need_b
     fuse = FUSE_WGRAD and need_w and (not has_b or _bound_grad(bias) is not None)
     gw = _bound_grad(weight) if fuse else None
-    if gw is not None and _wb.state.defer and (not has_b or bias.grad.is_contiguous()) and _wb.deferrable(g2, x2, gw):
+    if (gw is not None and _wb.state.defer and (not has_b or bias.grad.is_contiguous()) and _wb.deferrable(g2, x2, gw)
+            and _wb.in_slab(x2)):
         # run at the end of the backward, batched with the other layers' (ops/wgrad_batch.py)
         _wb.record(g2, x2, gw)
         if has_b:
@@ -490,6 +491,25 @@ def accumulate_param_grads(g2: torch.Tensor, x2: torch.Tensor, weight: torch.Ten
     if has_b:
         db = g2.sum(0)
     return dw, db
+
+
+def wgrad_into(g2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor):
+    """gw += g2^T x2 by the path accumulate_param_grads takes for a bound gradient without bias
+    (split-K, a measured NT solution, transposed operands or one GEMM)."""
+    split = _split_k(g2, x2)
+    if split > 1 and gw.is_contiguous():
+        _wgrad_split(g2, x2, split, out=gw)
+    elif (lt_tune.WGRAD and _lt_ok(g2, x2, gw)
+          and lt_tune.wgrad_nt(g2.size(0), g2.size(1), x2.size(1), g2.element_size())):
+        _lt_ops().gemm_lt(g2, x2, trans_a=True, out=gw, accumulate=True)
+    else:
+        nt = _nt_operands(g2, x2, None) if gw.is_contiguous() else None
+        if nt is None:
+            gw.addmm_(g2.t(), x2)
+        elif lt_tune.WGRAD and gw.dtype == torch.bfloat16 and lt_tune.use_wgrad_t(g2.size(0), g2.size(1), x2.size(1)):
+            _lt_ops().gemm_lt(nt[0], nt[1], trans_b=True, out=gw, accumulate=True)
+        else:
+            gw.addmm_(nt[0], nt[1].t())
 
 
 def _lt_ops():

@@ -154,6 +154,12 @@ def deferrable(g2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor) -> bool:
             and not torch.cuda.is_current_stream_capturing())
 
 
+def in_slab(t: torch.Tensor) -> bool:
+    """t is a slot of a slab: worth deferring (a record whose input is ordinary memory can never
+    join a batched GEMM, so it runs where autograd reaches it)."""
+    return any(slab.slot_of(t) is not None for slab in state.slabs.values())
+
+
 def record(g2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor):
     if gw.requires_grad:
         raise RuntimeError(f"wgrad_batch.record: gradient buffer requires grad: shape {tuple(gw.shape)} "
@@ -214,6 +220,7 @@ def flush():
                 dw.baddbmm_(dy.transpose(1, 2), x)
                 state.batched += 1
                 continue
-        for g2, x2, gw in items:  # a weight used twice accumulates in order
-            gw.addmm_(g2.t(), x2)
+        from .linear import wgrad_into
+        for g2, x2, gw in items:  # a weight used twice accumulates in order, by the per-layer path
+            wgrad_into(g2, x2, gw)
             state.single += 1

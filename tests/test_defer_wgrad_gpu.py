@@ -49,17 +49,25 @@ def test_deferred_weight_used_twice():
     torch.manual_seed(0)
     lin = L.Linear(256, 256).cuda().bfloat16()
     other = L.Linear(256, 256).cuda().bfloat16()
-    x = torch.randn(2048, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    x0 = torch.randn(2048, 256, device="cuda", dtype=torch.bfloat16)
     grads = {}
-    for defer in (False, True):
-        for p in list(lin.parameters()) + list(other.parameters()):
-            p.grad = torch.zeros_like(p)  # bound gradients, as the engine binds them
-        r0 = wb.state.recorded
-        with wb.deferred(defer):
-            y = lin(other(lin(x)))  # lin's weight gradient recorded twice
-            y.float().pow(2).mean().backward()
-        assert (wb.state.recorded > r0) == defer and not wb.state.pending
-        grads[defer] = [p.grad.float().clone() for p in list(lin.parameters()) + list(other.parameters())]
+    wb.enable(True)
+    try:
+        for defer in (False, True):
+            for p in list(lin.parameters()) + list(other.parameters()):
+                p.grad = torch.zeros_like(p)  # bound gradients, as the engine binds them
+            slot = wb.view("twice", 0, 2, x0)  # the input in a slab slot: its gradients may be deferred
+            slot.copy_(x0)
+            x = slot.detach().requires_grad_(True)
+            r0 = wb.state.recorded
+            with wb.deferred(defer):
+                y = lin(other(lin(x)))  # lin's weight gradient is recorded for its first use
+                y.float().pow(2).mean().backward()
+            wb.release()
+            assert (wb.state.recorded > r0) == defer and not wb.state.pending
+            grads[defer] = [p.grad.float().clone() for p in list(lin.parameters()) + list(other.parameters())]
+    finally:
+        wb.enable(False)
     for a, b in zip(grads[False], grads[True]):
         assert (a - b).abs().max().item() <= 2e-2 * max(1e-3, a.abs().max().item())
 
