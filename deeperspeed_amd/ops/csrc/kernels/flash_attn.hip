@@ -1045,7 +1045,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
                                              const uint16_t* __restrict__ dO, const float* __restrict__ LSE,
                                              const float* __restrict__ DELTA, uint16_t* __restrict__ dK,
                                              uint16_t* __restrict__ dV, int S, float scale, int onh, const Extra& ex,
-                                             uint16_t* __restrict__ dQ = nullptr) {
+                                             uint16_t* __restrict__ dQ = nullptr, const uint16_t* __restrict__ Ofw = nullptr) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   constexpr int TS = BN2 * LDP<D>;
   float* stats = reinterpret_cast<float*>(smem + 4 * TS);  // [2 stages][LSE 64 | DELTA 64]
@@ -1076,12 +1076,36 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
   // [BN2 queries][BM2 + 8 keys] also live in LDS, and dQ = dS K is formed per query tile here
   uint16_t* const Ks = smem + 4 * TS + 4 * BN2 * 2;
   uint16_t* const dSs = Ks + BM2 * LDP<D>;
+  // FQ with the forward output O: Delta = rowsum(dO * O) of the head's S <= BM2 queries is formed
+  // here into LDS (8 lanes per row, 16-byte loads) instead of by a separate pass over dO and O
+  float* const dls = reinterpret_cast<float*>(dSs + BN2 * (BM2 + 8));
   if constexpr (FQ) {
     uint4 kr2[D / 32];
     tile_load<D>(kr2, K + base, 0, S, ldi);
     tile_store<D>(Ks, kr2);
     tile_load<D>(kr2, K + base, BN2, S, ldi);
     tile_store<D>(Ks + BN2 * LDP<D>, kr2);
+    if (Ofw) {
+      const int sub = threadIdx.x & 7;
+      for (int q = threadIdx.x >> 3; q < BM2; q += 32) {  // uniform trip count: every lane shuffles
+        float acc = 0.f;
+        if (q < S) {
+          const int64_t off = obase + (int64_t)q * o_ld<D>(onh);
+          for (int c = sub; c < D / 8; c += 8) {
+            float a[8], b[8];
+            Vec16<T>::load(reinterpret_cast<const T*>(dO) + off + c * 8, a);
+            Vec16<T>::load(reinterpret_cast<const T*>(Ofw) + off + c * 8, b);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc = fmaf(a[j], b[j], acc);
+          }
+        }
+        acc += __shfl_xor(acc, 1, 64);
+        acc += __shfl_xor(acc, 2, 64);
+        acc += __shfl_xor(acc, 4, 64);
+        if (sub == 0) dls[q] = acc;
+      }
+      __syncthreads();
+    }
   }
 
   s16x8 kf[D / 16], vf[D / 16];
@@ -1112,8 +1136,9 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
     }
     if (threadIdx.x < BN2) {
       const int q = i0 + threadIdx.x;
+      const float dq_ = q < S ? ((FQ && Ofw) ? dls[q] : DELTA[bh * (int64_t)S + q]) : 0.f;
       st_l = q < S ? LSE[bh * (int64_t)S + q] * (INIT ? -1.f / scale : 1.4426950408889634f) : 0.f;
-      st_d = q < S ? (INIT ? -DELTA[bh * (int64_t)S + q] : DELTA[bh * (int64_t)S + q]) : 0.f;
+      st_d = INIT ? -dq_ : dq_;
     }
   };
   auto store_tile = [&](int stage) {
@@ -1566,7 +1591,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_both_v2_kernel(
 
 template <int D> constexpr int dkdv_v2_lds() { return 2 * 2 * BN2 * LDP<D> * 2 + 2 * 2 * BN2 * 4; }
 // + K [BM2][D+8] and one tile's dS [BN2][BM2+8] for the fused short-sequence backward
-template <int D> constexpr int bwd_short_lds() { return dkdv_v2_lds<D>() + BM2 * LDP<D> * 2 + BN2 * (BM2 + 8) * 2; }
+template <int D> constexpr int bwd_short_lds() { return dkdv_v2_lds<D>() + BM2 * LDP<D> * 2 + BN2 * (BM2 + 8) * 2 + BM2 * 4; }
 
 // Whole backward of one head in one workgroup for S <= BM2 (= 128, BERT's sequence): dK / dV
 // as in the dK/dV kernel, and dQ from the same dS tiles through LDS -- Q, K, V and dO are read
@@ -1576,8 +1601,8 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_short_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     uint16_t* __restrict__ dQ, uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh,
-    Extra ex = Extra()) {
-  dkdv_v2_body<T, D, false, EX, true>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh, ex, dQ);
+    Extra ex = Extra(), const uint16_t* __restrict__ O = nullptr) {
+  dkdv_v2_body<T, D, false, EX, true>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh, ex, dQ, O);
 }
 
 template <int D> constexpr int fwd_v2_lds() { return 2 * 2 * BN2 * LDP<D> * 2; }
@@ -2486,13 +2511,17 @@ void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const v
   // the buffer resources of the dK/dV tile loads address one head's rows with 32-bit offsets
   if ((int64_t)S * std::max<int64_t>(ild > 0 ? ild : D, onh ? (int64_t)onh * D : D) * 2 >= (1LL << 31))
     throw std::runtime_error("flash bwd: S * row stride too large for 32-bit buffer offsets");
+  // DSA_FA_SHORT_DELTA=0: the short backward reads Delta from a separate pass (A/B)
+  static const bool short_delta = !(getenv("DSA_FA_SHORT_DELTA") && getenv("DSA_FA_SHORT_DELTA")[0] == '0');
   FA_EX_DISPATCH(dt, D, kbias, pdrop,
-    hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
-                       (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
+    if (!(use_short && short_delta))
+      hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
+                         (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
     if (use_short)
       hipLaunchKernelGGL((fa::bwd_short_kernel<T, DD, EE>), dim3(grid), dim3(256), fa::bwd_short_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex);
+                         (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex,
+                         short_delta ? (const uint16_t*)o : nullptr);
     else if (merge)
       hipLaunchKernelGGL((fa::bwd_both_v2_kernel<T, DD, false, EE>), dim3(2 * grid), dim3(256),
                          std::max(fa::dkdv_v2_lds<DD>(), fa::fwd_v2_lds<DD>() + kb_lds), s, (int)grid, (const uint16_t*)q, (const uint16_t*)k,

@@ -35,6 +35,9 @@ import torch
 
 ENABLED = os.environ.get("DSA_BATCH_WGRAD", "1") != "0"
 MIN_TOKENS = 1024
+# DSA_WGRAD_EARLY=k: as soon as k layers' records of one linear are in, their batched GEMM starts on
+# a low-priority stream of its own hardware queue, beside the rest of the backward (0: all at the end)
+EARLY = int(os.environ.get("DSA_WGRAD_EARLY", "0"))
 
 
 class _Slab:
@@ -64,6 +67,9 @@ class _State:
         self.single = 0  # records run one by one
         self.recorded = 0
         self.last_miss = None  # why the last group could not be batched (diagnostics)
+        self.side = None  # stream of the early batched GEMMs
+        self.side_pending = False
+        self.early = 0  # early batched GEMMs launched (tests / diagnostics)
 
 
 state = _State()
@@ -122,6 +128,22 @@ def bind_grad_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> in
     return n
 
 
+def zero_stacks(grads):
+    """Zero persistent gradients in place: the gradient stacks among them as whole buffers (one
+    fill each instead of one per tensor); returns the gradients that are not stack slots."""
+    rest, hit = [], set()
+    for g in grads:
+        o = _owner(g, state.stacks) if state.stacks else None
+        if o is None:
+            rest.append(g)
+        else:
+            hit.add(id(o[0]))
+    for slab in state.stacks:
+        if id(slab) in hit:
+            slab.buf.zero_()
+    return rest
+
+
 class deferred:
     """Context of one backward whose bound weight gradients are recorded and run at its end."""
 
@@ -167,6 +189,38 @@ def record(g2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor):
                            f"{None if gw._base is None else tuple(gw._base.shape)}")
     state.pending.append((g2, x2, gw))
     state.recorded += 1
+    if EARLY > 1:
+        key = _key(g2, x2)
+        group = [it for it in state.pending if _key(it[0], it[1]) == key]
+        if len(group) >= EARLY:
+            _flush_early(key, group)
+
+
+def _key(g2, x2):
+    return (tuple(g2.shape), tuple(x2.shape), g2.dtype, g2.device)
+
+
+@torch.no_grad()
+def _flush_early(key, group):
+    if len({gw.data_ptr() for _, _, gw in group}) != len(group):
+        return
+    v = _batch(group)
+    if v is None:
+        return
+    dev = group[0][0].device
+    if state.side is None:
+        from ..runtime.overlap_step import priority_stream
+        state.side = priority_stream(dev, 1 << 20)
+    main = torch.cuda.current_stream(dev)
+    state.side.wait_stream(main)  # the records' dY / X are complete
+    with torch.cuda.stream(state.side):
+        dy, x, dw = v
+        dw.baddbmm_(dy.transpose(1, 2), x)
+    state.side_pending = True
+    state.early += 1
+    state.batched += 1
+    ids = {id(it) for it in group}
+    state.pending = [it for it in state.pending if id(it) not in ids]
 
 
 def _owner(t: torch.Tensor, pools) -> Optional[Tuple[_Slab, int]]:
@@ -211,7 +265,7 @@ def flush():
     pend, state.pending = state.pending, []
     groups: Dict[tuple, list] = {}
     for g2, x2, gw in pend:
-        groups.setdefault((tuple(g2.shape), tuple(x2.shape), g2.dtype, g2.device), []).append((g2, x2, gw))
+        groups.setdefault(_key(g2, x2), []).append((g2, x2, gw))
     for items in groups.values():
         if len(items) > 1 and len({gw.data_ptr() for _, _, gw in items}) == len(items):
             v = _batch(items)
@@ -224,3 +278,6 @@ def flush():
         for g2, x2, gw in items:  # a weight used twice accumulates in order, by the per-layer path
             wgrad_into(g2, x2, gw)
             state.single += 1
+    if state.side_pending:  # everything after the backward sees the early batches' gradients
+        torch.cuda.current_stream(state.side.device).wait_stream(state.side)
+        state.side_pending = False

@@ -203,7 +203,10 @@ class FP16_UnfusedOptimizer:
                     p.grad.detach_()
                     p.grad.zero_()
         if keep:
-            torch._foreach_zero_(keep)
+            from ...ops import wgrad_batch  # layer-stacked gradients: one fill per stack
+            keep = wgrad_batch.zero_stacks(keep)
+            if keep:
+                torch._foreach_zero_(keep)
 
     def mark_new_gradients(self):
         """A backward that did not go through backward() (the pipeline engine's autograd calls)

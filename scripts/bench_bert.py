@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--torch-profile", default="", help="write a torch.profiler op table of one step here")
+    ap.add_argument("--loss-trace", action="store_true",
+                    help="report every step's loss (read back once at the end) in the JSON line")
     ap.add_argument("--host-sleep-ms", type=float, default=0.0,
                     help="diagnostic: sleep this long on the host after issuing each step (a GPU-bound "
                          "step absorbs it up to its host slack; a host-bound one slows by it)")
@@ -94,9 +96,12 @@ def main():
     nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
 
     kept = []
+    trace = []
 
     def step():
         loss = engine(ids, tt, am, pos, lab, nsp)
+        if args.loss_trace:
+            trace.append(loss.detach().float())
         kept.append(len(model.pld_kept) if args.pld else cfg.num_layers)
         engine.backward(loss)
         engine.step()
@@ -153,6 +158,7 @@ def main():
                       "pld_theta": args.pld or None,
                       "mean_layers_run": round(run, 2),
                       "gradient_clipping": 1.0, "data": "synthetic", "final_loss": round(float(loss.detach()), 4),
+                      **({"loss_trace": [round(x, 5) for x in torch.stack(trace).tolist()]} if trace else {}),
                       "ref_v100_samples_per_s": ref[0] if ref else None,
                       "vs_ref_v100": round(sps / ref[0], 2) if ref else None}), flush=True)
 

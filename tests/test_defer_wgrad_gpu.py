@@ -119,7 +119,8 @@ def _train(batch, monkeypatch, steps=3):
 def test_bert_training_with_batched_wgrads(monkeypatch):
     l0, w0, n0 = _train(False, monkeypatch)
     l1, w1, n1 = _train(True, monkeypatch)
-    assert n0 == 0 and n1 == 4 * 3, (n0, n1)  # qkv / attn-out / fc1 / fc2, every step
+    # qkv / attn-out / fc1 / fc2 every step (more with DSA_WGRAD_EARLY: several batches per linear)
+    assert n0 == 0 and n1 >= 4 * 3, (n0, n1)
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 2e-2 * abs(a)
     for a, b in zip(w0, w1):
