@@ -300,7 +300,8 @@ Tensor bias_gelu_fwd(Tensor x, OptT b, bool approx, OptT out) {
 }
 
 // Returns (dx, dbias)
-std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, OptT b, bool approx, OptT dx_out) {
+// db_acc: a bound bias gradient the column sums are accumulated into (returned as db)
+std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, OptT b, bool approx, OptT dx_out, OptT db_acc) {
   check_dev(dy, "dy"); check_dev(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "bias_gelu_bwd: mismatch");
   const int64_t C = x.size(-1);
@@ -310,13 +311,16 @@ std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, OptT b, bool approx, OptT
   Tensor dx = out_or_empty(dx_out, x, "bias_gelu_bwd");
   Tensor db, partial;
   if (b.has_value()) {
-    db = at::empty_like(*b);
+    if (db_acc.has_value())
+      TORCH_CHECK(db_acc->sizes() == b->sizes() && db_acc->scalar_type() == b->scalar_type() && db_acc->is_contiguous(),
+                  "bias_gelu_bwd: db_acc must match the bias");
+    db = db_acc.has_value() ? *db_acc : at::empty_like(*b);
     partial = at::empty({(int64_t)dsa::bias_gelu_row_chunks(rows, (int)C, dt) * C}, x.options().dtype(at::kFloat));
   }
   dsa::launch_bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), b.has_value() ? b->data_ptr() : nullptr, dx.data_ptr(),
                             b.has_value() ? db.data_ptr() : nullptr,
                             b.has_value() ? partial.data_ptr<float>() : nullptr, rows, (int)C, approx ? 1 : 0, dt,
-                            cur_stream());
+                            cur_stream(), db_acc.has_value() ? 1 : 0);
   return {dx, db};
 }
 
@@ -1329,7 +1333,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dbeta_acc") = py::none());
   m.def("bias_gelu_fwd", &bias_gelu_fwd, py::arg("x"), py::arg("b"), py::arg("approx"), py::arg("out") = py::none());
   m.def("bias_gelu_bwd", &bias_gelu_bwd, py::arg("dy"), py::arg("x"), py::arg("b"), py::arg("approx"),
-        py::arg("dx_out") = py::none());
+        py::arg("dx_out") = py::none(), py::arg("db_acc") = py::none());
   m.def("bias_gelu_fwd_t", &bias_gelu_fwd_t);
   m.def("bias_gelu_bwd_t", &bias_gelu_bwd_t);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(), py::arg("accumulate") = false);

@@ -64,7 +64,7 @@ void launch_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, i
                           hipStream_t s);
 int bias_gelu_row_chunks(int64_t rows, int C, int dt);
 void launch_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, void* db, float* partial,
-                          int64_t rows, int C, int approx, int dt, hipStream_t s);
+                          int64_t rows, int C, int approx, int dt, hipStream_t s, int db_accum = 0);
 void launch_colsum(const void* x, void* out, float* partial, int64_t rows, int C, int accum, int dt,
                    hipStream_t s);
 // out[c] (+)= sum_r partial[r][c] (fp32 partials, out in dtype dt)

@@ -2511,8 +2511,11 @@ void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const v
   // the buffer resources of the dK/dV tile loads address one head's rows with 32-bit offsets
   if ((int64_t)S * std::max<int64_t>(ild > 0 ? ild : D, onh ? (int64_t)onh * D : D) * 2 >= (1LL << 31))
     throw std::runtime_error("flash bwd: S * row stride too large for 32-bit buffer offsets");
-  // DSA_FA_SHORT_DELTA=0: the short backward reads Delta from a separate pass (A/B)
-  static const bool short_delta = !(getenv("DSA_FA_SHORT_DELTA") && getenv("DSA_FA_SHORT_DELTA")[0] == '0');
+  // DSA_FA_SHORT_DELTA=1: the short backward forms Delta itself instead of reading a separate pass
+  // (opt-in: BERT-Large seq 128 measured 2,530 vs 2,551 samples/s with the separate pass, same box,
+  // profiles/r5f_bert_short_delta_ab2.jsonl -- the per-workgroup prologue serialises what the
+  // Delta kernel spreads over the whole chip)
+  static const bool short_delta = getenv("DSA_FA_SHORT_DELTA") && getenv("DSA_FA_SHORT_DELTA")[0] == '1';
   FA_EX_DISPATCH(dt, D, kbias, pdrop,
     if (!(use_short && short_delta))
       hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,

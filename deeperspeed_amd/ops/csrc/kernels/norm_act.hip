@@ -623,7 +623,7 @@ int bias_gelu_row_chunks(int64_t rows, int C, int dt) {
 
 // partial workspace: bias_gelu_row_chunks(rows, C) * C floats (when db != null)
 void launch_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, void* db, float* partial,
-                          int64_t rows, int C, int approx, int dt, hipStream_t s) {
+                          int64_t rows, int C, int approx, int dt, hipStream_t s, int db_accum) {
   if (rows <= 0) return;
   const int vn = dt == kF32 ? 4 : 8;
   const int cblocks = (C / vn + 255) / 256;
@@ -632,7 +632,7 @@ void launch_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx
     hipLaunchKernelGGL((bias_gelu_bwd_kernel<T>), dim3(cblocks, rc), dim3(256), 0, s,
                        (const T*)dy, (const T*)x, (const T*)b, (T*)dx, db ? partial : nullptr, rows, C, approx);
     if (db) hipLaunchKernelGGL((colsum_kernel<T>), dim3((C + 15) / 16), dim3(256), 0, s, partial, rc, C,
-                               (T*)db, 0));
+                               (T*)db, db_accum));
 }
 
 // Column sum of a [rows, C] tensor into out[C] (bias gradients of plain linears).

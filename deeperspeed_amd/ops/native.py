@@ -245,7 +245,7 @@ def _gelu_t_ok(x2: torch.Tensor) -> bool:
             and x2.size(0) % 128 == 0 and x2.size(1) % 64 == 0 and x2.size(0) > 0 and x2.data_ptr() % 16 == 0)
 
 
-def _gelu_bwd(dy, x, bias, approx, offer_t, dx_out=None):
+def _gelu_bwd(dy, x, bias, approx, offer_t, dx_out=None, db_acc=None):
     """(dx, db) of y = gelu(x + bias).  With offer_t, on the GPU one pass also writes dx^T and
     hands it to ops.linear as the pre-transposed output gradient of the linear that produced x
     (its weight gradient then skips the transpose of dx)."""
@@ -255,8 +255,10 @@ def _gelu_bwd(dy, x, bias, approx, offer_t, dx_out=None):
         dx, dxt, db = hip_ops().bias_gelu_bwd_t(dy.view(-1, C), x.view(-1, C), bias, approx)
         from . import linear as _linear
         _linear.offer_transposed(dx, dxt)
+        if db_acc is not None and db is not None:  # db_acc: the caller's bound bias gradient
+            db = db_acc.add_(db)
         return dx.view(x.shape), db
-    return hip_ops().bias_gelu_bwd(dy, x, bias, approx, dx_out)
+    return hip_ops().bias_gelu_bwd(dy, x, bias, approx, dx_out, db_acc)
 
 
 # DSA_DUAL_GELU_BWD=0: the bias+GeLU backward writes only dx (the linear transposes it itself)
@@ -284,7 +286,14 @@ class _BiasGeluFn(torch.autograd.Function):
         x, bias = ctx.saved_tensors
         dy = dy.contiguous()
         if x.is_cuda:
-            dx, db = _gelu_bwd(dy, x, bias, ctx.approx, ctx.offer_t, _slab(ctx.dx_slab, x, backward=True))
+            # a bound bias gradient (persistent, ops/wgrad_batch.py stacks) takes the column sums in place
+            from .linear import FUSE_WGRAD, _bound_grad
+            bacc = _bound_grad(bias) if (bias is not None and FUSE_WGRAD and ctx.needs_input_grad[1]) else None
+            if bacc is not None and not bacc.is_contiguous():
+                bacc = None
+            dx, db = _gelu_bwd(dy, x, bias, ctx.approx, ctx.offer_t, _slab(ctx.dx_slab, x, backward=True), bacc)
+            if bacc is not None:
+                db = None
         else:
             with torch.enable_grad():
                 xi = (x.float() + (bias.float() if bias is not None else 0)).detach().requires_grad_(True)
