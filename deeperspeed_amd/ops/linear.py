@@ -416,6 +416,9 @@ def input_grad(g2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
             and g2.size(0) >= 1024):
         from . import native
         wt = weight_t_cache.get(weight)
+        if wt is None and _wb.state.wstacks:
+            # a slot of a stacked weight: its W^T is a column block of one per-step stack transpose
+            wt = _wb.stacked_wt(weight, weight_t_cache.epoch)
         if wt is not None:
             return g2 @ wt.t()
         if native.transpose_supported(weight):

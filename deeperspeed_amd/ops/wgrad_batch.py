@@ -35,6 +35,12 @@ import torch
 
 ENABLED = os.environ.get("DSA_BATCH_WGRAD", "1") != "0"
 MIN_TOKENS = 1024
+# DSA_STACK_WEIGHTS=1: equal-shape weights share a buffer and one W^T transpose per step (stacked_wt)
+# instead of one transpose per weight per backward.  Opt-in: BERT-Large measured 2,528-2,580 vs
+# 2,570-2,576 samples/s at seq 128 and 576 vs 587 at seq 512 (same box,
+# profiles/r5f_bert_stacked_weights_ab.jsonl): the input-gradient GEMMs reading W^T at the stack's
+# row stride and the one large transpose on the critical path cost what the 96 small ones did.
+STACK_WEIGHTS = os.environ.get("DSA_STACK_WEIGHTS", "0") == "1"
 # DSA_WGRAD_EARLY=k: as soon as k layers' records of one linear are in, their batched GEMM starts on
 # a low-priority stream of its own hardware queue, beside the rest of the backward (0: all at the end)
 EARLY = int(os.environ.get("DSA_WGRAD_EARLY", "0"))
@@ -61,6 +67,7 @@ class _State:
         self.slabs_on = False  # set by an engine whose backward may defer (no gradient hooks)
         self.slabs: Dict[tuple, _Slab] = {}
         self.stacks: List[_Slab] = []  # persistent gradient stacks
+        self.wstacks: List[dict] = []  # stacked weights and their shared transposes
         self.defer = False
         self.pending: List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
         self.batched = 0  # batched GEMMs launched (tests / diagnostics)
@@ -142,6 +149,55 @@ def zero_stacks(grads):
         if id(slab) in hit:
             slab.buf.zero_()
     return rest
+
+
+def bind_weight_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> int:
+    """Move every group of >= min_count equal-shape 2-D weights into one [n, out, in] buffer (each
+    parameter's data becomes a slot view, values copied) so that the input-gradient GEMMs can take
+    all their W^T from ONE transpose per optimizer step (`stacked_wt`).  Call before anything caches
+    the parameters' addresses (the optimizer's pointer tables are built at its first step)."""
+    groups: Dict[tuple, list] = {}
+    for p in params:
+        if p.dim() == 2 and p.numel() >= min_numel and p.is_cuda and p.dtype in (torch.bfloat16, torch.float16):
+            groups.setdefault((tuple(p.shape), p.dtype, p.device), []).append(p)
+    n = 0
+    for (shape, dtype, dev), ps in groups.items():
+        if len(ps) < min_count:
+            continue
+        buf = torch.empty((len(ps),) + shape, dtype=dtype, device=dev)
+        with torch.no_grad():
+            for i, p in enumerate(ps):
+                buf[i].copy_(p.data)
+                p.data = buf[i]
+        state.wstacks.append({"slab": _Slab(buf), "wt": None, "epoch": None, "params": list(ps), "vers": None})
+        n += len(ps)
+    return n
+
+
+def stacked_wt(weight: torch.Tensor, epoch: int) -> Optional[torch.Tensor]:
+    """W^T [in, out] of a stacked weight: a column block of the whole stack's transpose
+    [in, n * out], made by one HIP transpose the first time a weight of the stack asks after an
+    optimizer step (`epoch`) or after an in-place write to that weight (its version counter, checked
+    per weight when it asks).  Not inside a HIP graph capture: a replay would not refresh the shared
+    buffer for the other layers' graphs."""
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    for ws in state.wstacks:
+        slab = ws["slab"]
+        i = slab.slot_of(weight)
+        if i is None:
+            continue
+        L, N, K = slab.buf.shape
+        if ws["epoch"] != epoch or ws["vers"][i] != weight._version:
+            from . import native
+            if not native.transpose_supported(slab.buf.view(L * N, K)):
+                return None
+            if ws["wt"] is None:
+                ws["wt"] = torch.empty(K, L * N, dtype=slab.buf.dtype, device=slab.buf.device)
+            native.transpose2d(slab.buf.view(L * N, K), out=ws["wt"])
+            ws["epoch"], ws["vers"] = epoch, [p._version for p in ws["params"]]
+        return ws["wt"][:, i * N:(i + 1) * N]
+    return None
 
 
 class deferred:

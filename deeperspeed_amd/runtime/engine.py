@@ -144,6 +144,8 @@ class DeepSpeedEngine(Module):
         _wgrad_batch.enable(self._defer_wgrad)
         if self._defer_wgrad:
             _wgrad_batch.bind_grad_stacks(self.module.parameters())
+            if _wgrad_batch.STACK_WEIGHTS:  # one dgrad weight transpose per stack and step
+                _wgrad_batch.bind_weight_stacks(self.module.parameters())
 
         self.csr_tensor_module_names = set()
         if self.sparse_gradients_enabled():
