@@ -610,6 +610,7 @@ constexpr float LAZY_TH = 8.0f;
 //            one 32-bit hash yields the 16-bit draws of keys 2j and 2j+1 of a query row.
 //            The normaliser l / LSE stays the undropped one; O = (P * Z) V / (1 - p).
 constexpr int EX_BIAS = 1, EX_DROP = 2, EX_QKV = 4;  // EX_QKV: token-major q/k/v (Extra::inh/ild)
+constexpr int EX_DBITS = 8;  // with EX_DROP: the forward stores the keep masks as bits (Extra::dbits)
 struct Extra {
   const float* kbias = nullptr;
   int hdiv = 1;
@@ -623,7 +624,40 @@ struct Extra {
   int64_t ild = 0;
   // optional device int64 [seed, step] mixed into `seed` on the GPU (graph-replayable dropout)
   const int64_t* rng = nullptr;
+  // EX_DROP keep masks stored by the forward, one bit per (query, key) (S % 64 == 0): dbits
+  // [bh][q][S/32] (bit = key % 32; read by the dQ kernel) and dbitsT [bh][k][S/32] (bit = query
+  // % 32; read by the dK/dV kernel), so the backward reads 2 words per lane and tile instead of
+  // re-hashing every (query, key) pair in both of its kernels.  Null: the backward hashes.
+  uint32_t* dbits = nullptr;
+  uint32_t* dbitsT = nullptr;
 };
+
+// Forward side of the stored masks: this lane's keep bits kw[t] of the tile's two 32-key blocks
+// (bit 8g + 4h + e of block t is key j0 + 32t + 8g + 4h + e of query myq).  The two wave halves
+// hold complementary bits, so one permlane32 swap gives every lane its query's full words; the
+// key-major words are the transpose of the wave's 32 x 32 bit matrix of a block, formed by five
+// xor-shuffle butterfly stages (half 0 transposes block 0, half 1 block 1).
+__device__ __forceinline__ void store_drop_bits(const Extra& ex, int64_t bh, int S, int myq, int q32, int j0,
+                                                uint32_t kw0, uint32_t kw1, int lane) {
+  const int h = lane >> 5, c32 = lane & 31;
+  const int nw = S >> 5;
+  const auto a = __builtin_amdgcn_permlane32_swap(kw0, kw0, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(kw1, kw1, false, false);
+  const uint32_t full0 = a[0] | a[1], full1 = b[0] | b[1];
+  if (h == 0 && myq < S)
+    *reinterpret_cast<uint2*>(ex.dbits + (bh * S + myq) * (int64_t)nw + (j0 >> 5)) = make_uint2(full0, full1);
+  uint32_t x = h ? full1 : full0;  // row c32 (query q32 + c32) of this half's block
+#pragma unroll
+  for (int j = 16; j >= 1; j >>= 1) {
+    const uint32_t lo = j == 16 ? 0x0000FFFFu : j == 8 ? 0x00FF00FFu : j == 4 ? 0x0F0F0F0Fu : j == 2 ? 0x33333333u
+                                                                                             : 0x55555555u;
+    const uint32_t y = (uint32_t)__shfl_xor((int)x, j, 64);
+    x = (c32 & j) ? ((x & ~lo) | ((y & ~lo) >> j)) : ((x & lo) | ((y & lo) << j));
+  }
+  // now bit i of x = keep of (query q32 + i, key j0 + 32h + c32)
+  const int key = j0 + 32 * h + c32;
+  if (key < S && q32 < S) ex.dbitsT[(bh * S + key) * (int64_t)nw + (q32 >> 5)] = x;
+}
 // compile-time layout switch: the head-major kernels keep constant row strides (immediate load
 // offsets); only EX_QKV instantiations pay for the runtime stride
 template <int D, int EX>
@@ -810,13 +844,18 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 2 : 3)) fwd_v2_kernel(const u
     ps = xhalf_sum(ps);
     l += ps;
     if constexpr (DROP) {  // values 2i, 2i+1 of a lane are keys 2j, 2j+1 of its query row
+      uint32_t kw0 = 0u, kw1 = 0u;  // keep bits of the two 32-key blocks (stored masks)
 #pragma unroll
       for (int i = 0; i < 32; i += 2) {
         const int key = j0 + 32 * (i >> 4) + 8 * ((i & 15) >> 2) + 4 * h + (i & 3);
         const uint32_t x = drop_pair(hb, myq, S >> 1, key >> 1);
-        if ((x & 0xffffu) < ex.thresh) sv[i] = 0.f;
-        if ((x >> 16) < ex.thresh) sv[i + 1] = 0.f;
+        const bool k0 = (x & 0xffffu) >= ex.thresh, k1 = (x >> 16) >= ex.thresh;
+        if (!k0) sv[i] = 0.f;
+        if (!k1) sv[i + 1] = 0.f;
+        const uint32_t bits = ((uint32_t)k0 | ((uint32_t)k1 << 1)) << (8 * ((i & 15) >> 2) + 4 * h + (i & 3));
+        if (i < 16) kw0 |= bits; else kw1 |= bits;
       }
+      if constexpr ((EX & EX_DBITS) != 0) store_drop_bits(ex, bh, S, myq, qb + 32 * w, j0, kw0, kw1, lane);
     }
     // O^T += V^T P^T over the 64 keys (4 steps of 16)
 #pragma unroll
@@ -1229,6 +1268,16 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
         }
       }
       if constexpr (DROP) {  // dV from the dropped P; dP = dP_dropped * Z / (1 - p)
+       if constexpr ((EX & EX_DBITS) != 0) {  // the forward's key-major keep bits: this key's word over 32 queries
+        const uint32_t word = mykey < S ? ex.dbitsT[(bh * S + mykey) * (int64_t)(S >> 5) + ((i0 + 32 * t) >> 5)] : 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+          const float zr = ((word >> (8 * (r >> 2) + 4 * h + (r & 3))) & 1u) ? ex.rscale : 0.f;
+          dsv[r] = pv[r] * fmaf(pacc[r], zr, -del_s[qi]);
+          pv[r] *= zr;
+        }
+       } else {
         // lanes l and l^1 hold keys 2j and 2j+1 of the same 16 queries and need the same 16
         // pair draws: each computes 8 and takes the other 8 from its neighbour (DPP quad_perm)
         uint32_t own[8], nbr[8];
@@ -1248,6 +1297,7 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
           dsv[r] = pv[r] * fmaf(pacc[r], zr, -del_s[qi]);
           pv[r] *= zr;
         }
+       }
       } else if constexpr (INIT) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dsv[r] = pv[r] * pacc[r];
@@ -1484,14 +1534,23 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
         }
       }
       if constexpr (DROP) {  // values r, r+1 are keys 2j, 2j+1 of this lane's query
+        if constexpr ((EX & EX_DBITS) != 0) {  // the forward's query-major keep bits of this 32-key block
+          const uint32_t word = myq < S ? ex.dbits[(bh * S + myq) * (int64_t)(S >> 5) + ((j0 + 32 * t) >> 5)] : 0u;
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-          const uint32_t x = drop_pair(hb, myq, S >> 1, key >> 1);
-          const float z0 = (x & 0xffffu) < ex.thresh ? 0.f : ex.rscale;
-          const float z1 = (x >> 16) < ex.thresh ? 0.f : ex.rscale;
-          dsv[r] = dsv[r] * fmaf(pacc[r], z0, -dl);
-          dsv[r + 1] = dsv[r + 1] * fmaf(pacc[r + 1], z1, -dl);
+          for (int r = 0; r < 16; ++r) {
+            const float z = ((word >> (8 * (r >> 2) + 4 * h + (r & 3))) & 1u) ? ex.rscale : 0.f;
+            dsv[r] = dsv[r] * fmaf(pacc[r], z, -dl);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+            const uint32_t x = drop_pair(hb, myq, S >> 1, key >> 1);
+            const float z0 = (x & 0xffffu) < ex.thresh ? 0.f : ex.rscale;
+            const float z1 = (x >> 16) < ex.thresh ? 0.f : ex.rscale;
+            dsv[r] = dsv[r] * fmaf(pacc[r], z0, -dl);
+            dsv[r + 1] = dsv[r + 1] * fmaf(pacc[r + 1], z1, -dl);
+          }
         }
       } else {
 #pragma unroll
@@ -2447,6 +2506,12 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     };                                                                                               \
     auto _q = [&](auto tt, auto dd, auto ee) {                                                       \
       constexpr int E0 = decltype(ee)::value;                                                        \
+      if constexpr ((E0 & fa::EX_DROP) != 0) {                                                       \
+        if (inh > 0 && ex.dbits) {                                                                   \
+          _go(tt, dd, std::integral_constant<int, E0 | fa::EX_QKV | fa::EX_DBITS>{});                 \
+          return;                                                                                    \
+        }                                                                                            \
+      }                                                                                              \
       if (inh > 0) _go(tt, dd, std::integral_constant<int, E0 | fa::EX_QKV>{});                      \
       else _go(tt, dd, ee);                                                                          \
     };                                                                                               \
@@ -2464,8 +2529,13 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
   } while (0)
 
 static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t seed, int inh = 0,
-                            int64_t ild = 0, const int64_t* rng = nullptr) {
+                            int64_t ild = 0, const int64_t* rng = nullptr, uint32_t* dbits = nullptr,
+                            int64_t nbits = 0) {
   fa::Extra ex;
+  if (dbits && pdrop > 0.f) {
+    ex.dbits = dbits;
+    ex.dbitsT = dbits + nbits;
+  }
   ex.rng = rng;
   ex.inh = inh;
   ex.ild = ild;
@@ -2477,10 +2547,13 @@ static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t 
   return ex;
 }
 
+bool flash_drop_bits_ok(int S) { return S % 64 == 0; }
+
 void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh, int64_t ild, const int64_t* rng) {
-  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng);
+                         int onh, int inh, int64_t ild, const int64_t* rng, uint32_t* dbits) {
+  if (dbits && !flash_drop_bits_ok(S)) throw std::runtime_error("flash fwd: stored dropout masks need S % 64 == 0");
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng, dbits, (int64_t)BH * S * (S / 32));
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
   const int kb_lds = kbias ? 4 * S : 0;  // the LDS-staged key-bias row
   if (kb_lds && fa::fwd_v2_lds<128>() + kb_lds > 160 * 1024)
@@ -2496,8 +2569,9 @@ void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, f
 void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const void* v, const void* o,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh, int64_t ild, const int64_t* rng) {
-  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng);
+                         int onh, int inh, int64_t ild, const int64_t* rng, uint32_t* dbits) {
+  if (dbits && !flash_drop_bits_ok(S)) throw std::runtime_error("flash bwd: stored dropout masks need S % 64 == 0");
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng, dbits, (int64_t)BH * S * (S / 32));
   const int64_t rows = (int64_t)BH * S;
   const int kb_lds = kbias ? 4 * S : 0;  // the dQ kernel's LDS-staged key-bias row
   if (kb_lds && fa::fwd_v2_lds<128>() + kb_lds > 160 * 1024)

@@ -642,17 +642,18 @@ class _FlashAttnQkvFn(torch.autograd.Function):
         B, S, _, H, D = qkv5.shape
         _macs(2 * B * H * S * S * D)
         o_out = _slab(slabs and slabs[0], qkv5[:, :, 0])
-        o, lse = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed, rng, o_out)
-        ctx.save_for_backward(qkv5, o, lse, kbias)
+        o, lse, bits = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed, rng, o_out)
+        ctx.save_for_backward(qkv5, o, lse, kbias, bits)
         ctx.scale, ctx.p, ctx.seed, ctx.rng = scale, p, seed, rng
         ctx.dqkv_slab = slabs and slabs[1]
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv5, o, lse, kbias = ctx.saved_tensors
+        qkv5, o, lse, kbias, bits = ctx.saved_tensors
         dqkv = hip_ops().flash_attn_qkv_bwd(do.contiguous(), qkv5, o, lse, kbias, ctx.scale, ctx.p, ctx.seed,
-                                            ctx.rng, _slab(ctx.dqkv_slab, qkv5, backward=True))
+                                            ctx.rng, _slab(ctx.dqkv_slab, qkv5, backward=True),
+                                            bits if bits.numel() else None)
         return dqkv, None, None, None, None, None, None
 
 
