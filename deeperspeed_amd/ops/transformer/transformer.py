@@ -377,6 +377,8 @@ def make_graphed_encoder(layers, sample_hidden, sample_mask=None, seed: int = 12
         object.__setattr__(layer, "_dsa_graphed", True)
         object.__setattr__(layer, "_dsa_next_norm", None)
         layer.enable_device_rng(seed + 7919 * i)
+        for p in layer.parameters():  # the graphs hold these addresses: never rebound later
+            p._dsa_graph_captured = True
         if persistent_grads:
             # the backward graphs accumulate weight / bias / LayerNorm gradients straight into these
             # buffers (ops/linear.py, native LayerNorm): no static gradient outputs to copy into .grad

@@ -120,7 +120,8 @@ def bind_grad_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> in
     Returns the number of parameters bound."""
     groups: Dict[tuple, list] = {}
     for p in params:
-        if p.requires_grad and p.is_cuda and (p.dim() == 1 or (p.dim() == 2 and p.numel() >= min_numel)):
+        if (p.requires_grad and p.is_cuda and (p.dim() == 1 or (p.dim() == 2 and p.numel() >= min_numel))
+                and not _captured(p)):
             groups.setdefault((tuple(p.shape), p.dtype, p.device), []).append(p)
     n = 0
     for (shape, dtype, dev), ps in groups.items():
@@ -128,11 +129,20 @@ def bind_grad_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> in
             continue
         buf = torch.zeros((len(ps),) + shape, dtype=dtype, device=dev)
         for i, p in enumerate(ps):
+            if p.grad is not None:  # keep what was accumulated before binding
+                buf[i].copy_(p.grad)
             p.grad = buf[i]
             p._dsa_persistent_grad = True
         state.stacks.append(_Slab(buf))
         n += len(ps)
     return n
+
+
+def _captured(p) -> bool:
+    """A parameter whose storage or .grad address a HIP graph holds (make_graphed_encoder), or whose
+    .grad is already a persistent buffer someone else bound: rebinding it would leave the graph
+    writing into freed memory."""
+    return getattr(p, "_dsa_graph_captured", False) or getattr(p, "_dsa_persistent_grad", False)
 
 
 def zero_stacks(grads):
@@ -158,7 +168,8 @@ def bind_weight_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> 
     the parameters' addresses (the optimizer's pointer tables are built at its first step)."""
     groups: Dict[tuple, list] = {}
     for p in params:
-        if p.dim() == 2 and p.numel() >= min_numel and p.is_cuda and p.dtype in (torch.bfloat16, torch.float16):
+        if (p.dim() == 2 and p.numel() >= min_numel and p.is_cuda and p.dtype in (torch.bfloat16, torch.float16)
+                and not _captured(p)):
             groups.setdefault((tuple(p.shape), p.dtype, p.device), []).append(p)
     n = 0
     for (shape, dtype, dev), ps in groups.items():

@@ -143,3 +143,24 @@ def test_bert_training_with_batched_wgrads(monkeypatch):
         assert abs(a - b) <= 2e-2 * abs(a)
     for a, b in zip(w0, w1):
         assert (a - b).abs().max().item() <= 1e-2 * max(1.0, a.abs().max().item())
+
+
+def test_graph_captured_params_are_not_rebound():
+    """Parameters whose addresses a HIP graph holds (make_graphed_encoder) keep their .grad and
+    storage: rebinding them to stacks would leave the graph writing into freed memory."""
+    from deeperspeed_amd.ops import wgrad_batch as wb
+    ps = [torch.nn.Parameter(torch.zeros(256, device="cuda", dtype=torch.bfloat16)) for _ in range(4)]
+    grads = [torch.ones_like(p) for p in ps]
+    for p, g in zip(ps, grads):
+        p.grad = g
+        p._dsa_graph_captured = True
+    n0 = len(wb.state.stacks)
+    assert wb.bind_grad_stacks(ps, min_numel=1) == 0 and len(wb.state.stacks) == n0
+    assert all(p.grad is g for p, g in zip(ps, grads))
+    free = [torch.nn.Parameter(torch.zeros(256, device="cuda", dtype=torch.bfloat16)) for _ in range(4)]
+    free[0].grad = torch.full_like(free[0], 3.0)
+    try:
+        assert wb.bind_grad_stacks(free, min_numel=1) == 4
+        assert torch.all(free[0].grad == 3.0) and free[1].grad.data_ptr() - free[0].grad.data_ptr() == 512
+    finally:
+        del wb.state.stacks[n0:]
