@@ -91,9 +91,12 @@ struct Gemm {
   hipDataType bias_type;
   void* aux;
   int64_t ld_aux;
+  // strided batch: `batch` problems, operand / output i at A + i*sa, B + i*sb, D (and C) + i*sd
+  int batch = 1;
+  int64_t sa = 0, sb = 0, sd = 0;
 };
 
-using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int, int, bool>;
+using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int, int, bool, int>;
 
 struct Algo {
   hipblasLtMatmulAlgo_t algo;
@@ -109,8 +112,8 @@ std::map<Key, Algo>& algo_cache() {
   return c;
 }
 
-// (ta, tb, m, n, k, epi, has_C, ab_type, d_type) -> solution indices from the offline sweep
-using RegKey = std::tuple<int, int, int64_t, int64_t, int64_t, int, bool, int, int>;
+// (ta, tb, m, n, k, epi, has_C, ab_type, d_type, batch) -> solution names from the offline sweep
+using RegKey = std::tuple<int, int, int64_t, int64_t, int64_t, int, bool, int, int, int>;
 std::map<RegKey, std::vector<std::string>>& registry() {
   static std::map<RegKey, std::vector<std::string>> r;
   return r;
@@ -150,6 +153,15 @@ std::mutex& cache_mu() {
   return mu;
 }
 
+void set_batch(hipblasLtMatrixLayout_t la, hipblasLtMatrixLayout_t lb, hipblasLtMatrixLayout_t ld, int batch,
+               int64_t sa, int64_t sb, int64_t sd) {
+  const int32_t bc = batch;
+  for (auto [l, st] : {std::make_pair(la, sa), std::make_pair(lb, sb), std::make_pair(ld, sd)}) {
+    LT_CHECK(hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc)));
+    LT_CHECK(hipblasLtMatrixLayoutSetAttribute(l, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &st, sizeof(st)));
+  }
+}
+
 void run(const Gemm& g, int device, hipStream_t stream) {
   Ctx& c = ctx_for(device);
   hipblasLtMatmulDesc_t op;
@@ -174,8 +186,10 @@ void run(const Gemm& g, int device, hipStream_t stream) {
   LT_CHECK(hipblasLtMatrixLayoutCreate(&la, g.ab_type, ar, ac, g.lda));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&lb, g.ab_type, br, bc, g.ldb));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&ld, g.d_type, g.m, g.n, g.ldd));
+  if (g.batch > 1) set_batch(la, lb, ld, g.batch, g.sa, g.sb, g.sd);
   const float alpha = 1.f, beta = g.C ? 1.f : 0.f;
-  const Key key{device, (int)g.epi, g.m, g.n, g.k, (int)g.ta, (int)g.tb, (int)g.ab_type, (int)g.d_type, g.C != nullptr};
+  const Key key{device, (int)g.epi, g.m, g.n, g.k, (int)g.ta, (int)g.tb, (int)g.ab_type, (int)g.d_type, g.C != nullptr,
+                g.batch};
   std::lock_guard<std::mutex> lock(cache_mu());
   auto& cache = algo_cache();
   auto it = cache.find(key);
@@ -190,7 +204,8 @@ void run(const Gemm& g, int device, hipStream_t stream) {
     hipblasLtMatmulPreferenceDestroy(pref);
     std::vector<hipblasLtMatmulHeuristicResult_t> res(hres, hres + nh);
     std::vector<char> from_table(res.size(), 0);
-    const RegKey rk{(int)g.ta, (int)g.tb, g.m, g.n, g.k, (int)g.epi, g.C != nullptr, (int)g.ab_type, (int)g.d_type};
+    const RegKey rk{(int)g.ta, (int)g.tb, g.m, g.n, g.k, (int)g.epi, g.C != nullptr, (int)g.ab_type, (int)g.d_type,
+                    g.batch};
     auto reg = registry().find(rk);
     if (reg != registry().end() && !reg->second.empty()) {
       // registered solutions are identified by NAME: hipBLASLt's solution indices depend on the
@@ -231,7 +246,7 @@ void run(const Gemm& g, int device, hipStream_t stream) {
       // the caller's output; otherwise D is overwritten by the final launch anyway
       at::Tensor scratch;
       if (g.C)
-        scratch = at::empty({g.m * g.n * (g.d_type == HIP_R_32F ? 4 : 2)},
+        scratch = at::empty({((g.batch > 1 ? g.sd * (g.batch - 1) : 0) + g.ldd * g.n) * (g.d_type == HIP_R_32F ? 4 : 2)},
                             at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device));
       void* sd = g.C ? scratch.data_ptr() : g.D;
       const void* sc = g.C ? sd : nullptr;
@@ -386,6 +401,31 @@ at::Tensor gemm_lt(at::Tensor a, at::Tensor b, bool trans_a, bool trans_b, c10::
   return c;
 }
 
+// Strided-batched row-major GEMM C[l] = op(A[l]) op(B[l]) (+ C[l] when accumulate) over 3-D
+// contiguous [L, ., .] operands -- the layer-batched weight gradients of ops/wgrad_batch.py, where
+// it replaces torch.baddbmm_ so the solution is timed (and table-registered) per shape instead of
+// taken from hipBLASLt's first heuristic answer.
+at::Tensor gemm_lt_batched(at::Tensor a, at::Tensor b, bool trans_a, bool trans_b, at::Tensor out, bool accumulate) {
+  for (auto* t : {&a, &b, &out})
+    TORCH_CHECK(t->is_cuda() && t->dim() == 3 && t->is_contiguous(), "gemm_lt_batched: contiguous 3-D device tensors");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf),
+              "gemm_lt_batched: bf16/fp16 operands of one dtype");
+  TORCH_CHECK(out.scalar_type() == a.scalar_type() || out.scalar_type() == at::kFloat,
+              "gemm_lt_batched: out of the operand dtype or fp32");
+  const int64_t L = a.size(0);
+  const int64_t M = trans_a ? a.size(2) : a.size(1), K = trans_a ? a.size(1) : a.size(2);
+  const int64_t N = trans_b ? b.size(1) : b.size(2);
+  TORCH_CHECK(b.size(0) == L && out.size(0) == L && (trans_b ? b.size(2) : b.size(1)) == K && out.size(1) == M &&
+                  out.size(2) == N, "gemm_lt_batched: shape mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  Gemm g{trans_b ? HIPBLAS_OP_T : HIPBLAS_OP_N, trans_a ? HIPBLAS_OP_T : HIPBLAS_OP_N, N, M, K,
+         trans_b ? K : N, trans_a ? M : K, N, dtype_of(a), dtype_of(out), HIPBLASLT_EPILOGUE_DEFAULT,
+         b.data_ptr(), a.data_ptr(), accumulate ? out.data_ptr() : nullptr, out.data_ptr(), nullptr, dtype_of(a),
+         nullptr, 0, (int)L, b.size(1) * b.size(2), a.size(1) * a.size(2), M * N};
+  run(g, a.get_device(), c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
+  return out;
+}
+
 // Number of heuristic algorithms hipBLASLt offers for a bf16 TN GEMM [m,n,k] with epilogue
 // code `epi` (diagnostics: epilogue availability differs between hipBLASLt builds).
 int64_t lt_algo_count(int64_t m, int64_t n, int64_t k, int64_t epi, bool with_aux) {
@@ -428,10 +468,10 @@ int64_t lt_algo_count(int64_t m, int64_t n, int64_t k, int64_t epi, bool with_au
 // Candidate solutions (by hipBLASLt solution name) for one column-major problem (bf16 operands;
 // d_bf16 false -> fp32 D).
 void lt_register(bool ta, bool tb, int64_t m, int64_t n, int64_t k, int64_t epi, bool beta, bool d_bf16,
-                 std::vector<std::string> names) {
+                 std::vector<std::string> names, int64_t batch) {
   std::lock_guard<std::mutex> lock(cache_mu());
   const RegKey rk{(int)(ta ? HIPBLAS_OP_T : HIPBLAS_OP_N), (int)(tb ? HIPBLAS_OP_T : HIPBLAS_OP_N), m, n, k, (int)epi,
-                  beta, (int)HIP_R_16BF, (int)(d_bf16 ? HIP_R_16BF : HIP_R_32F)};
+                  beta, (int)HIP_R_16BF, (int)(d_bf16 ? HIP_R_16BF : HIP_R_32F), (int)batch};
   auto& v = registry()[rk];
   for (auto& nm : names)
     if (std::find(v.begin(), v.end(), nm) == v.end()) v.push_back(nm);
@@ -460,7 +500,7 @@ std::vector<pybind11::tuple> lt_choices() {
 // operands; macro tiles under 128 skipped when both output dims are >= 2048) and returns
 // (heuristic first choice ms, [(ms, solution name, kernel name), ...] fastest first).
 // kind: 0 fwd (TN), 1 dgrad (NN), 2 wgrad (NT, beta 1), 3 wgradT (TN, beta 1); row-major M, N, K.
-pybind11::tuple lt_sweep(int64_t kind, int64_t M, int64_t N, int64_t K, bool bias, int64_t top) {
+pybind11::tuple lt_sweep(int64_t kind, int64_t M, int64_t N, int64_t K, bool bias, int64_t top, int64_t batch) {
   const int device = at::cuda::current_device();
   Ctx& c = ctx_for(device);
   hipblasOperation_t ta, tb;
@@ -479,8 +519,8 @@ pybind11::tuple lt_sweep(int64_t kind, int64_t M, int64_t N, int64_t K, bool bia
   }
   TORCH_CHECK(!bias || kind == 0, "lt_sweep: bias only for the forward");
   auto opts = at::TensorOptions().dtype(at::kBFloat16).device(at::kCUDA, device);
-  at::Tensor A = at::rand({ar * ac}, opts).mul_(2).sub_(1), B = at::rand({br * bc}, opts).mul_(2).sub_(1);
-  at::Tensor D = at::rand({m * n}, opts), bv = at::rand({m}, opts);
+  at::Tensor A = at::rand({batch * ar * ac}, opts).mul_(2).sub_(1), B = at::rand({batch * br * bc}, opts).mul_(2).sub_(1);
+  at::Tensor D = at::rand({batch * m * n}, opts), bv = at::rand({m}, opts);
   hipStream_t stream = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
   hipblasLtMatmulDesc_t op;
   LT_CHECK(hipblasLtMatmulDescCreate(&op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
@@ -498,6 +538,7 @@ pybind11::tuple lt_sweep(int64_t kind, int64_t M, int64_t N, int64_t K, bool bia
   LT_CHECK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, ar, ac, lda));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, br, bc, ldb));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&ld, HIP_R_16BF, m, n, ldd));
+  if (batch > 1) set_batch(la, lb, ld, (int)batch, ar * ac, br * bc, m * n);
   const float alpha = 1.f;
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -583,8 +624,12 @@ std::string lt_library() {
 
 void register_gemm_lt(pybind11::module& m) {
   m.def("lt_library", &lt_library);
-  m.def("lt_sweep", &lt_sweep);
-  m.def("lt_register", &lt_register);
+  m.def("lt_sweep", &lt_sweep, pybind11::arg("kind"), pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"),
+        pybind11::arg("bias"), pybind11::arg("top"), pybind11::arg("batch") = 1);
+  m.def("lt_register", &lt_register, pybind11::arg("ta"), pybind11::arg("tb"), pybind11::arg("m"), pybind11::arg("n"),
+        pybind11::arg("k"), pybind11::arg("epi"), pybind11::arg("beta"), pybind11::arg("d_bf16"),
+        pybind11::arg("names"), pybind11::arg("batch") = 1);
+  m.def("gemm_lt_batched", &gemm_lt_batched);
   m.def("lt_choices", &lt_choices);
   m.def("lt_algo_count", &lt_algo_count);
   m.def("linear_lt", &linear_lt);

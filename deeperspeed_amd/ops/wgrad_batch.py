@@ -44,6 +44,20 @@ STACK_WEIGHTS = os.environ.get("DSA_STACK_WEIGHTS", "0") == "1"
 # DSA_WGRAD_EARLY=k: as soon as k layers' records of one linear are in, their batched GEMM starts on
 # a low-priority stream of its own hardware queue, beside the rest of the backward (0: all at the end)
 EARLY = int(os.environ.get("DSA_WGRAD_EARLY", "0"))
+# the batched GEMMs through the extension's strided-batched hipBLASLt call, whose solution is timed
+# per shape on first use (gemm_lt_batched), instead of torch.baddbmm_'s first heuristic answer
+LT_BATCHED = os.environ.get("DSA_WGRAD_LT_BATCHED", "1") != "0"
+
+
+def _batched_gemm(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor) -> None:
+    """dw[l] += dy[l]^T x[l] over contiguous [L, M, N] / [L, M, K] / [L, N, K] slab views."""
+    if LT_BATCHED and dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float16) and x.dtype == dy.dtype \
+            and dw.dtype in (dy.dtype, torch.float32) and dy.is_contiguous() and x.is_contiguous() \
+            and dw.is_contiguous():
+        from . import native
+        native.hip_ops().gemm_lt_batched(dy, x, True, False, dw, True)
+    else:
+        dw.baddbmm_(dy.transpose(1, 2), x)
 
 
 class _Slab:
@@ -338,7 +352,7 @@ def flush():
             v = _batch(items)
             if v is not None:
                 dy, x, dw = v
-                dw.baddbmm_(dy.transpose(1, 2), x)
+                _batched_gemm(dy, x, dw)
                 state.batched += 1
                 continue
         from .linear import wgrad_into

@@ -139,7 +139,7 @@ def main():
             f.write("\n\nsmall copy / fill / memset call sites (python frames)\n")
             for e in prof.key_averages(group_by_stack_n=8):
                 if any(k in e.key for k in ("copy_", "fill_", "zero_", "aten::zeros", "aten::cat", "contiguous",
-                                            "aten::to", "_foreach", "aten::empty_like")) and e.count:
+                                            "aten::to", "_foreach", "aten::empty_like", "aten::add")) and e.count:
                     f.write(f"{e.key} count={e.count} device_us={e.device_time_total:.0f} "
                             f"cpu_us={e.cpu_time_total:.0f}\n")
                     for fr in e.stack:
