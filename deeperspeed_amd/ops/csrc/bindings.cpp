@@ -384,6 +384,24 @@ Tensor transpose2d(Tensor x, OptT colsum_out, bool accum, OptT out) {
   return y;
 }
 
+// [L, R, C] -> [L, C, R] for a contiguous 16-bit stack (R % 128 == 0, C % 64 == 0) in one launch:
+// the per-step W^T of every weight of a stack (ops/wgrad_batch.py stacked_wt)
+Tensor transpose_batched(Tensor x, Tensor out) {
+  check_dev(x, "x");
+  check_dev(out, "out");
+  TORCH_CHECK(x.dim() == 3 && x.is_contiguous() && aligned16(x.data_ptr()), "transpose_batched: contiguous [L, R, C] x");
+  const int dt = dcode(x);
+  TORCH_CHECK(dt != dsa::kCodeF32, "transpose_batched: 16-bit dtypes only");
+  const int64_t L = x.size(0), R = x.size(1), C = x.size(2);
+  TORCH_CHECK(dsa::transpose_supported(R, C), "transpose_batched: rows must be a multiple of 128 and cols of 64");
+  TORCH_CHECK(out.dim() == 3 && out.size(0) == L && out.size(1) == C && out.size(2) == R && out.is_contiguous() &&
+                  out.scalar_type() == x.scalar_type() && aligned16(out.data_ptr()),
+              "transpose_batched: out must be a contiguous [L, C, R] tensor of x's dtype");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  if (L > 0) dsa::launch_transpose_batched(x.data_ptr(), out.data_ptr(), (int)L, R, (int)C, C, dt, cur_stream());
+  return out;
+}
+
 // gelu(x + b)^T for x [R, C] contiguous 16-bit (R % 128 == 0, C % 64 == 0): the activation
 // recompute's fc1 output handed straight to fc2's weight gradient in the layout it wants.
 Tensor bias_gelu_fwd_t(Tensor x, OptT b, bool approx) {
@@ -1352,6 +1370,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("heads_split", &heads_split);
   m.def("heads_merge", &heads_merge);
   m.def("swap12", &swap12);
+  m.def("transpose_batched", &transpose_batched);
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("colsum_out") = py::none(), py::arg("accum") = false,
         py::arg("out") = py::none());
 }

@@ -85,6 +85,8 @@ void launch_profile_marker(int tag, hipStream_t s);
 // `partial` ([R/128, C] fp32 scratch) the column sums of x are also (accumulated) into colsum_out[C].
 bool transpose_supported(int64_t R, int64_t C);
 int64_t transpose_partial_rows(int64_t R);
+// [L][R][C] (row stride ldx) -> [L][C][R], one launch (plain copy, no column sums)
+void launch_transpose_batched(const void* x, void* y, int L, int64_t R, int C, int64_t ldx, int dt, hipStream_t s);
 void launch_transpose(const void* x, void* y, float* partial, void* colsum_out, int colsum_accum, int64_t R, int C,
                       int64_t ldx, int dt, hipStream_t s);
 // yt[C][R] = gelu(x[R][C] + b)^T (same shape rules, x contiguous)

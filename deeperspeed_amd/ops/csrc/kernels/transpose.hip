@@ -82,6 +82,10 @@ __global__ void __launch_bounds__(256) transpose_kernel(const uint16_t* __restri
                                                         uint16_t* __restrict__ yr, int approx) {
   __shared__ __attribute__((aligned(16))) uint16_t tile[TR * TC];
   const int t = threadIdx.x;
+  if (gridDim.z > 1) {  // batched plain copy (launch_transpose_batched): slot z of [L][R][ldx] -> [L][C][R]
+    x += (int64_t)blockIdx.z * R * ldx;
+    y += (int64_t)blockIdx.z * R * C;
+  }
   const int64_t r0 = (int64_t)blockIdx.y * TR;
   const int c0 = blockIdx.x * TC;
   uint4 v[4];
@@ -165,6 +169,13 @@ __global__ void __launch_bounds__(256) transpose_kernel(const uint16_t* __restri
 bool transpose_supported(int64_t R, int64_t C) { return R > 0 && C > 0 && R % TR == 0 && C % TC == 0; }
 
 int64_t transpose_partial_rows(int64_t R) { return R / TR; }
+
+void launch_transpose_batched(const void* x, void* y, int L, int64_t R, int C, int64_t ldx, int dt, hipStream_t s) {
+  const dim3 grid(C / TC, (unsigned)(R / TR), (unsigned)L);
+  DSA_DISPATCH_16(dt, T,
+    hipLaunchKernelGGL((transpose_kernel<T, false, kCopy>), grid, dim3(256), 0, s, (const uint16_t*)x, (uint16_t*)y,
+                       nullptr, R, C, ldx, nullptr, nullptr, nullptr, 0));
+}
 
 void launch_transpose(const void* x, void* y, float* partial, void* colsum_out, int colsum_accum, int64_t R, int C,
                       int64_t ldx, int dt, hipStream_t s) {

@@ -39,7 +39,9 @@ MIN_TOKENS = 1024
 # instead of one transpose per weight per backward.  Opt-in: BERT-Large measured 2,528-2,580 vs
 # 2,570-2,576 samples/s at seq 128 and 576 vs 587 at seq 512 (same box,
 # profiles/r5f_bert_stacked_weights_ab.jsonl): the input-gradient GEMMs reading W^T at the stack's
-# row stride and the one large transpose on the critical path cost what the 96 small ones did.
+# row stride and the one large transpose on the critical path cost what the 96 small ones did.  With
+# the W^T made per slot by one batched transpose (same leading dimension as a per-weight one):
+# 2,560 vs 2,551 and 585 vs 586, losses identical (profiles/r5h_bert_stacked_weights_batched_t_ab.jsonl).
 STACK_WEIGHTS = os.environ.get("DSA_STACK_WEIGHTS", "0") == "1"
 # DSA_WGRAD_EARLY=k: as soon as k layers' records of one linear are in, their batched GEMM starts on
 # a low-priority stream of its own hardware queue, beside the rest of the backward (0: all at the end)
@@ -200,8 +202,9 @@ def bind_weight_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> 
 
 
 def stacked_wt(weight: torch.Tensor, epoch: int) -> Optional[torch.Tensor]:
-    """W^T [in, out] of a stacked weight: a column block of the whole stack's transpose
-    [in, n * out], made by one HIP transpose the first time a weight of the stack asks after an
+    """W^T [in, out] of a stacked weight: slot i of the stack's batched transpose [n, in, out]
+    (contiguous per slot, so the input-gradient GEMM reads it at the same leading dimension as a
+    per-weight transpose), made by ONE HIP launch the first time a weight of the stack asks after an
     optimizer step (`epoch`) or after an in-place write to that weight (its version counter, checked
     per weight when it asks).  Not inside a HIP graph capture: a replay would not refresh the shared
     buffer for the other layers' graphs."""
@@ -215,13 +218,13 @@ def stacked_wt(weight: torch.Tensor, epoch: int) -> Optional[torch.Tensor]:
         L, N, K = slab.buf.shape
         if ws["epoch"] != epoch or ws["vers"][i] != weight._version:
             from . import native
-            if not native.transpose_supported(slab.buf.view(L * N, K)):
+            if not native.transpose_supported(slab.buf[0]):
                 return None
             if ws["wt"] is None:
-                ws["wt"] = torch.empty(K, L * N, dtype=slab.buf.dtype, device=slab.buf.device)
-            native.transpose2d(slab.buf.view(L * N, K), out=ws["wt"])
+                ws["wt"] = torch.empty(L, K, N, dtype=slab.buf.dtype, device=slab.buf.device)
+            native.hip_ops().transpose_batched(slab.buf, ws["wt"])
             ws["epoch"], ws["vers"] = epoch, [p._version for p in ws["params"]]
-        return ws["wt"][:, i * N:(i + 1) * N]
+        return ws["wt"][i]
     return None
 
 
