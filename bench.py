@@ -44,6 +44,19 @@ def emit_result(out):
     os.write(_RESULT_FD, (json.dumps(out) + "\n").encode())
 
 REF_TOKENS_PER_GPU = 410.0  # BASELINE.md "North-star planning targets (derived)"
+# 1-bit Adam / LAMB (BASELINE config 4).  Their update has no bias correction (reference
+# deepspeed/runtime/fp16/onebit/adam.py:197-265, mirrored in runtime/fp16/onebit/adam.py), so the
+# variance frozen at freeze_step is (1 - beta2^k) E[g^2]: after the old 2 warm-up steps at
+# beta2 = 0.999 that is 2e-3 E[g^2], and the compressed momentum then moves every element by
+# ~20x lr per step -- the PP rehearsals ended at loss 115-1,548 from 11.6.  The reference advises
+# freeze_step 400-23,000 at beta2 0.999 (docs/_tutorials/onebit-adam.md:87,187); a benchmark
+# cannot afford that many untimed steps, so it runs GPT-NeoX's beta2 = 0.95 (its 20B config) and
+# freezes after 16 steps, when the variance estimate holds 1 - 0.95^16 = 56 % of E[g^2].
+ONEBIT_FREEZE = 16
+ONEBIT_BETAS = [0.9, 0.95]
+# a run whose final loss is non-finite or above this multiple of its first warmup loss is marked
+# "diverged": true in the result line
+DIVERGED_RATIO = 1.2
 
 
 def parse():
@@ -74,7 +87,10 @@ def parse():
                    help="pipeline stages (BASELINE config 4: --model gpt3-6.7b --pipe 4 on 8 GPUs = PP4 x DP2)")
     p.add_argument("--optimizer", type=str, default="adam", choices=["adam", "onebitadam", "onebitlamb", "lamb"],
                    help="1-bit optimizers run without ZeRO (reference restriction)")
-    p.add_argument("--freeze-step", type=int, default=2, help="1-bit optimizers: full-precision warm-up steps")
+    p.add_argument("--freeze-step", type=int, default=None,
+                   help="1-bit optimizers: full-precision warm-up steps before compression (default "
+                        f"{ONEBIT_FREEZE}; the untimed warmup is extended past it so every timed step is a "
+                        "compressed one)")
     p.add_argument("--force-sharded", action="store_true",
                    help="ZeRO-3 on one GPU: run the gather / reduce-scatter unit path over a world-1 RCCL "
                         "communicator instead of binding parameters to their shards")
@@ -94,6 +110,11 @@ def parse():
                         "-> NVMe file (--nvme-path).  auto: HBM headroom, then the host budget "
                         "(DSA_HOST_MOMENTS_GIB, default min(available - 24 GiB, 215 GiB)), then the free disk; "
                         "host: everything in pinned host memory")
+    p.add_argument("--emulate-world", type=int, default=0,
+                   help="one process runs rank 0 of an N-rank ZeRO job at full depth: shards, buckets, "
+                        "micro-batch, recompute and memory fit planned for N ranks, collectives replaced by "
+                        "local stand-ins that write the same bytes (utils/comm.py).  Reports EMULATED per-rank "
+                        "tokens/s, the collective bytes per step and the xGMI rate full overlap needs")
     p.add_argument("--fp32-reduce", type=str, default="off", choices=["on", "off"],
                    help="reduce bf16 gradients in fp32 (DeeperSpeed's bf16 default fp32_allreduce; "
                         "tests/test_zero_reduce_precision.py measures what bf16 reduction costs)")
@@ -329,7 +350,14 @@ def main():
     if launched == 0 and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     world = launched or 1
-    if world != args.gpus:
+    emulated = args.emulate_world if args.emulate_world > 1 else 0
+    if emulated:
+        if world != 1:
+            raise SystemExit("[bench] --emulate-world runs as ONE process (no launcher, --gpus 1)")
+        if args.pipe != 1 or args.zero != 3:
+            raise SystemExit("[bench] --emulate-world emulates the ZeRO-3 data-parallel bench only")
+        world = emulated  # every plan below is the N-rank job's; the process group stays world 1
+    elif world != args.gpus:
         log(f"--gpus {args.gpus} differs from the launcher's WORLD_SIZE={world}; using {world}")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
@@ -345,7 +373,7 @@ def main():
 
     on_gpu = torch.cuda.is_available()
     hb = Heartbeat(int(os.environ["RANK"]))
-    if world > 1 and int(os.environ["RANK"]) == 0 and on_gpu:
+    if world > 1 and not emulated and int(os.environ["RANK"]) == 0 and on_gpu:
         # rank 0 logs RCCL's version, topology, channel and ring setup once (stdout of the C
         # library is redirected to stderr above), so a multi-GPU record shows how it was wired
         os.environ.setdefault("NCCL_DEBUG", "INFO")
@@ -354,7 +382,12 @@ def main():
     ds.init_distributed(dist_backend=args.dist_backend if on_gpu else "gloo", timeout=timedelta(seconds=PG_TIMEOUT_S))
     rank = dist.get_rank()
     hb.beat("process group up", backend=dist.get_backend(), world=world)
-    if rank == 0 and world > 1:
+    if emulated:
+        from deeperspeed_amd.utils import comm as _comm
+        _comm.set_emulated_world(emulated)
+        log(f"EMULATED world {emulated}: this process is rank 0 of a {emulated}-rank job; collectives are "
+            f"local stand-ins (values meaningless, memory / kernels / collective sequence are the rank's)")
+    if rank == 0 and world > 1 and not emulated:
         try:
             rccl = ".".join(map(str, torch.cuda.nccl.version())) if on_gpu else None
         except Exception:  # noqa: BLE001 - informational only
@@ -457,7 +490,7 @@ def main():
     # gloo rehearsal of an N-GPU job on one GPU: gloo's asynchronous collectives on device tensors
     # stalled for ~50 s when several ZeRO reductions were in flight (profiles/r5a_notes.md), so the
     # rehearsal waits for each collective as it is issued (RCCL runs keep the overlap)
-    gloo_gpu = on_gpu and args.dist_backend == "gloo"
+    gloo_gpu = on_gpu and args.dist_backend == "gloo" and not emulated
     zcfg = {"stage": args.zero, "overlap_comm": not gloo_gpu, "reduce_scatter": True, "reduce_bucket_size": int(2e8),
             "stage3_prefetch_bucket_size": int(5e8), "stage3_param_persistence_threshold": int(1e6),
             "stage3_unit_max_numel": int(2e8), "stage3_max_live_parameters": live,
@@ -707,6 +740,7 @@ def main():
         return True
 
     i, extra = 0, 0
+    first_loss = None
     while i < args.warmup + extra:
         if os.environ.get("DSA_BENCH_STOP_RANK") == str(rank) and i == 1:
             # watchdog test hook (tests/test_bench_contract.py): this rank freezes mid-run
@@ -714,6 +748,8 @@ def main():
             os.kill(os.getpid(), signal.SIGSTOP)
         ts = time.time()
         loss, ph = timed_step()
+        if i == 0:
+            first_loss = float(loss.detach())
         log(f"warmup {i} loss={float(loss.detach()):.4f} {time.time() - ts:.2f}s "
             + " ".join(f"{k}={v:.2f}s" for k, v in ph.items())
             + (f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB"
@@ -737,6 +773,8 @@ def main():
     sync()
     if on_gpu:  # trace markers around the timed steps (scripts/prof_summary.py --timed)
         native.hip_ops().profile_marker(1)
+    from deeperspeed_amd.utils import comm as _comm
+    _comm.reset_bytes()
     t_start = time.time()
     for i in range(args.steps):
         loss = train_step()
@@ -803,6 +841,7 @@ def main():
         "vs_baseline": round(tps / (REF_TOKENS_PER_GPU * world), 3) if full_model and args.zero == 3 else None,
         "dtype": "bf16",
         "data": "synthetic random tokens, random-init weights",
+        "diverged": None if emulated else diverged(first_loss, float(loss.detach())),
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq,
                    "parallelism": f"zero{args.zero}-dp{world}", "micro_batch": mb, "grad_accum": ga,
                    "offload": offload, "activation_checkpointing": ckpt == "on", "sparse_attention": args.sparse,
@@ -810,6 +849,7 @@ def main():
                    "params_per_gpu": round(P / world / 1e9, 3),
                    "model_tflops_per_gpu": round(tps * flops_tok / world / 1e12, 1),
                    "final_loss": round(float(loss.detach()), 4),
+                   "first_warmup_loss": round(first_loss, 4) if first_loss is not None else None,
                    "peak_hbm_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None,
                    "planned_hbm_gib": round(planned / 2**30, 1),
                    "stashed_attention_layers": stashed,
@@ -831,10 +871,65 @@ def main():
                                     "(reference's best published ZeRO-3 49 TFLOPS/GPU on V100 at 6N FLOPs/token); "
                                     "BASELINE.json publishes no number for this metric"},
     }
+    if emulated:
+        out = emulated_record(out, args, emulated, mb, ga, ms_step, _comm.bytes_by_kind(), flops_tok)
     if rank == 0:
         emit_result(out)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def emulated_record(out, args, n, mb, ga, ms_step, nbytes, flops_tok):
+    """Result of --emulate-world N: the measured step of ONE rank of the N-rank job (collectives
+    replaced by local stand-ins), the collective bytes that rank moves per step, and the xGMI
+    rate those bytes need to hide under the step.  Ring model (runtime/comm/bucket_sizing.py): a
+    ring all-gather / reduce-scatter of B bytes sends (N-1)/N * B per rank; RCCL over the 7 xGMI
+    links of an MI355X is ASSUMED to sustain 300 GB/s per rank (bucket_sizing.DEFAULT_BETA_BPS,
+    not measured here: one GPU cannot run a multi-rank RCCL job).  The projection is labelled as
+    such: per-rank step time if the collectives overlap fully, else the modelled comm time."""
+    from deeperspeed_amd.runtime.comm import bucket_sizing
+    steps = max(1, args.steps)
+    per = {k: v / steps for k, v in nbytes.items()}
+    ag, rs = per.get("all_gather", 0.0), per.get("reduce_scatter", 0.0)
+    t_step = ms_step / 1000.0
+    beta = bucket_sizing.DEFAULT_BETA_BPS
+    sent = (n - 1) / n * (ag + rs)
+    # the reduce-scatter input doubles with --fp32-reduce on (fp32 staging of bf16 gradients)
+    rs_fp32 = rs if args.fp32_reduce == "on" else 2 * rs
+    sent_fp32 = (n - 1) / n * (ag + rs_fp32)
+    tokens_rank = mb * ga * args.seq
+    proj_step = max(t_step, sent / beta)
+    proj_step_fp32 = max(t_step, sent_fp32 / beta)
+    out = dict(out)
+    out["metric"] = (f"EMULATED per-rank tokens/sec: rank 0 of an N={n} GPT-NeoX-20B ZeRO-3 job on one GPU "
+                     f"(collectives replaced by local stand-ins; not a node measurement)")
+    out["value"] = round(tokens_rank / t_step, 2)
+    out["n_gpus"] = 1
+    out["vs_baseline"] = None
+    out["emulated_world"] = n
+    cfg = dict(out["config"])
+    cfg["parallelism"] = f"zero3-dp{n} (emulated rank 0)"
+    cfg["model_tflops_per_gpu"] = round(tokens_rank / t_step * flops_tok / 1e12, 1)
+    cfg["final_loss_note"] = "stand-in collectives: the loss is not meaningful"
+    out["config"] = cfg
+    gib = 2**30
+    out["comm_per_rank_per_step"] = {
+        "all_gather_gib": round(ag / gib, 2), "reduce_scatter_gib": round(rs / gib, 2),
+        "all_reduce_mib": round(per.get("all_reduce", 0.0) / 2**20, 3),
+        "ring_bytes_sent_gib": round(sent / gib, 2),
+        "xgmi_gbps_needed_for_full_overlap": round(sent / t_step / 1e9, 1),
+        "ring_bytes_sent_gib_fp32_reduce": round(sent_fp32 / gib, 2),
+        "xgmi_gbps_needed_fp32_reduce": round(sent_fp32 / t_step / 1e9, 1),
+        "assumed_xgmi_gbps_per_rank": beta / 1e9,
+        "modelled_comm_s": round(sent / beta, 3), "modelled_comm_s_fp32_reduce": round(sent_fp32 / beta, 3),
+    }
+    out["projection"] = {
+        "label": "PROJECTION, not a measurement: node tok/s = N x per-rank tokens / max(measured step, "
+                 "modelled ring time at the assumed xGMI rate)",
+        "node_tokens_per_s": round(n * tokens_rank / proj_step, 1),
+        "node_tokens_per_s_fp32_reduce": round(n * tokens_rank / proj_step_fp32, 1),
+    }
+    return out
 
 
 def _peak_rss():
@@ -863,7 +958,14 @@ def _optimizer_block(args):
     if args.optimizer == "lamb":
         return {"type": "Lamb", "params": {"lr": 1e-3, "weight_decay": 0.01}}
     name = {"onebitadam": "OneBitAdam", "onebitlamb": "OneBitLamb"}[args.optimizer]
-    return {"type": name, "params": {"lr": 1e-4, "freeze_step": args.freeze_step, "comm_backend_name": "nccl"}}
+    freeze = ONEBIT_FREEZE if args.freeze_step is None else args.freeze_step
+    return {"type": name, "params": {"lr": 1e-4, "betas": list(ONEBIT_BETAS), "freeze_step": freeze,
+                                     "comm_backend_name": "nccl"}}
+
+
+def diverged(first, last):
+    import math
+    return not math.isfinite(last) or (first is not None and math.isfinite(first) and last > DIVERGED_RATIO * first)
 
 
 def run_pipeline(args, cfg, mb, ga, world, rank, dev, hb):
@@ -905,24 +1007,35 @@ def run_pipeline(args, cfg, mb, ga, world, rank, dev, hb):
             torch.cuda.synchronize()
 
     hb.beat("pipeline engine ready")
-    for i in range(args.warmup):
+    # a 1-bit run times compressed steps only: the untimed warmup runs past the freeze step
+    freeze = _optimizer_block(args)["params"]["freeze_step"] if onebit else 0
+    warmup = max(args.warmup, freeze + 1) if onebit else args.warmup
+    if warmup != args.warmup:
+        log(f"1-bit: {warmup} untimed warmup steps (freeze_step {freeze}), so the timed steps are compressed")
+    first = None
+    for i in range(warmup):
         ts = time.time()
         loss = train_step()
         sync()
+        if first is None:
+            first = float(loss)
         log(f"warmup {i} loss={float(loss):.4f} {time.time() - ts:.2f}s"
             + (f" peak={torch.cuda.max_memory_allocated() / 2**30:.1f} GiB" if on_gpu else ""))
         hb.beat(f"warmup {i} done", peak_gib=round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else 0.0)
     dist.barrier()
     sync()
+    timed_losses = []
     t_start = time.time()
     for i in range(args.steps):
         loss = train_step()
+        timed_losses.append(loss.detach() if isinstance(loss, torch.Tensor) else loss)
         hb.beat(f"timed step {i} done")
     sync()
     dist.barrier()
     t = torch.tensor([time.time() - t_start], device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    timed_losses = [round(float(l), 4) for l in timed_losses]
     global_batch = mb * ga * dp
     tps = global_batch * args.seq * args.steps / elapsed
     out = {
@@ -930,9 +1043,13 @@ def run_pipeline(args, cfg, mb, ga, world, rank, dev, hb):
         "value": round(tps, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1000.0, 2), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic random tokens, random-init weights",
+        "diverged": diverged(first, timed_losses[-1]),
         "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq,
                    "parallelism": f"pp{args.pipe}-dp{dp}" + ("" if onebit else "-zero1"), "micro_batch": mb,
                    "grad_accum": ga, "optimizer": args.optimizer,
+                   "optimizer_params": _optimizer_block(args)["params"], "warmup_steps_run": warmup,
+                   "first_warmup_loss": round(first, 4) if first is not None else None,
+                   "timed_losses": timed_losses,
                    "model_tflops_per_gpu": round(tps * cfg.flops_per_token(args.seq) / world / 1e12, 1),
                    "final_loss": round(float(loss.detach()), 4),
                    "dist_backend": dist.get_backend(),

@@ -10,9 +10,13 @@ batched GEMM runs at ~3 TF/s, so the operands must sit at a constant stride:
 
 * slabs -- the producers of every X and dY of these linears (LayerNorm, bias-GeLU, encoder flash
   attention forward and backward, the fused dropout + LayerNorm backward) write into per-layer
-  slots of persistent [layers, ...] buffers (`view`); a slot is lent once per backward pass and
-  reclaimed when that backward ends (`release`), so a second forward before a backward, or an
-  activation-checkpoint recompute, simply gets ordinary memory;
+  slots of persistent [layers, ...] buffers (`view`), at most one buffer per kind (a new shape
+  replaces an idle buffer; a kind whose shape keeps changing -- progressive layer drop, varying
+  batch shapes -- stops using slabs).  A slot belongs to the pass that took it: an engine forward
+  (`begin_forward` / `end_forward` tag its slots and hook its output's autograd node) or the
+  backward that runs (its own slots and recomputes).  The end of a backward frees only its own
+  slots and those of the forwards whose graph it ran through, so with two forwards in flight the
+  other one's saved activations are never lent again; a taken slot simply gets ordinary memory;
 * gradient stacks -- the parameters of equal shape get their .grad bound to slots of one
   [layers, out, in] buffer (`bind_grad_stacks`, persistent gradients zeroed in place by the
   optimizer);
@@ -43,9 +47,9 @@ MIN_TOKENS = 1024
 # the W^T made per slot by one batched transpose (same leading dimension as a per-weight one):
 # 2,560 vs 2,551 and 585 vs 586, losses identical (profiles/r5h_bert_stacked_weights_batched_t_ab.jsonl).
 STACK_WEIGHTS = os.environ.get("DSA_STACK_WEIGHTS", "0") == "1"
-# DSA_WGRAD_EARLY=k: as soon as k layers' records of one linear are in, their batched GEMM starts on
-# a low-priority stream of its own hardware queue, beside the rest of the backward (0: all at the end)
-EARLY = int(os.environ.get("DSA_WGRAD_EARLY", "0"))
+# a kind whose slab shape changed this many times (progressive layer drop, varying batch shapes)
+# stops using slabs: each change would allocate a fresh [count, ...] buffer
+MAX_RESHAPES = 3
 # the batched GEMMs through the extension's strided-batched hipBLASLt call, whose solution is timed
 # per shape on first use (gemm_lt_batched), instead of torch.baddbmm_'s first heuristic answer
 LT_BATCHED = os.environ.get("DSA_WGRAD_LT_BATCHED", "1") != "0"
@@ -63,9 +67,10 @@ def _batched_gemm(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor) -> None:
 
 
 class _Slab:
-    def __init__(self, buf: torch.Tensor):
+    def __init__(self, buf: torch.Tensor, key=None):
         self.buf = buf
-        self.busy = [False] * buf.shape[0]
+        self.key = key
+        self.busy = [None] * buf.shape[0]  # owner tag of each lent slot (None = free)
         self.slot_bytes = buf[0].numel() * buf.element_size()
         self.base = buf.data_ptr()
 
@@ -81,7 +86,13 @@ class _Slab:
 class _State:
     def __init__(self):
         self.slabs_on = False  # set by an engine whose backward may defer (no gradient hooks)
-        self.slabs: Dict[tuple, _Slab] = {}
+        self.slabs: Dict[str, _Slab] = {}  # one per kind
+        self.reshapes: Dict[str, int] = {}
+        self.off_kinds = set()  # kinds whose shape kept changing
+        self.fwd = None  # tag of the engine forward running (begin_forward)
+        self.next_tag = 1
+        self.bwd = None  # tag of the deferred backward running
+        self.seen = set()  # forward tags whose graph the running backward reached
         self.stacks: List[_Slab] = []  # persistent gradient stacks
         self.wstacks: List[dict] = []  # stacked weights and their shared transposes
         self.defer = False
@@ -90,9 +101,6 @@ class _State:
         self.single = 0  # records run one by one
         self.recorded = 0
         self.last_miss = None  # why the last group could not be batched (diagnostics)
-        self.side = None  # stream of the early batched GEMMs
-        self.side_pending = False
-        self.early = 0  # early batched GEMMs launched (tests / diagnostics)
 
 
 state = _State()
@@ -104,28 +112,74 @@ def enable(on: bool = True):
 
 
 def view(kind: str, index: int, count: int, like: torch.Tensor, backward: bool = False) -> Optional[torch.Tensor]:
-    """Slot `index` of the [count, *like.shape] slab `kind`, or None (slabs off, or the slot already
-    lent in this pass).  Callers ask only for tensors of a forward that records a graph (inside an
-    autograd Function grad mode is off, so the caller decides that before entering it)."""
-    if not (state.slabs_on and like.is_cuda and 0 <= index < count) or count < 2:
+    """Slot `index` of the [count, *like.shape] slab `kind`, or None (slabs off, the kind's shape
+    unstable, the slot taken by a pass still in flight).  Callers ask only for tensors of a forward
+    that records a graph (inside an autograd Function grad mode is off, so the caller decides that
+    before entering it).  The slot is tagged with its owner: the running deferred backward (its
+    recomputes and input gradients), else the running engine forward, else an anonymous pass that
+    the next backward end frees."""
+    if not (state.slabs_on and like.is_cuda and 0 <= index < count) or count < 2 or kind in state.off_kinds:
         return None
     if torch.cuda.is_current_stream_capturing():
         return None
-    key = (kind, count, tuple(like.shape), like.dtype, like.device)
-    slab = state.slabs.get(key)
+    key = (count, tuple(like.shape), like.dtype, like.device)
+    slab = state.slabs.get(kind)
+    if slab is not None and slab.key != key:
+        if any(t is not None for t in slab.busy):
+            return None  # the old buffer is still read by a pass in flight
+        n = state.reshapes[kind] = state.reshapes.get(kind, 0) + 1
+        del state.slabs[kind]
+        slab = None
+        if n >= MAX_RESHAPES:
+            state.off_kinds.add(kind)
+            return None
     if slab is None:
-        slab = state.slabs[key] = _Slab(torch.empty((count,) + tuple(like.shape), dtype=like.dtype,
-                                                    device=like.device))
-    if slab.busy[index]:
+        slab = state.slabs[kind] = _Slab(torch.empty((count,) + tuple(like.shape), dtype=like.dtype,
+                                                     device=like.device), key)
+    if slab.busy[index] is not None:
         return None
-    slab.busy[index] = True
+    slab.busy[index] = ("b", state.bwd) if state.bwd is not None else (("f", state.fwd) if state.fwd is not None
+                                                                       else ("a", 0))
     return slab.buf[index]
 
 
-def release():
-    """End of a backward: every lent slot may be written again by the next forward."""
+def begin_forward():
+    """An engine forward starts: the slots it takes are its own until a backward reaches its graph."""
+    if not state.slabs_on:
+        return None
+    state.fwd = state.next_tag
+    state.next_tag += 1
+    return state.fwd
+
+
+def end_forward(tag, outputs):
+    """Hook the autograd nodes of the forward's outputs, so the backward that runs through this
+    forward's graph (even from a loss derived from them) frees its slots; a forward without a graph
+    frees them now."""
+    state.fwd = None
+    if tag is None:
+        return
+    ts = [outputs] if isinstance(outputs, torch.Tensor) else (
+        list(outputs.values()) if isinstance(outputs, dict) else list(outputs) if isinstance(outputs, (tuple, list))
+        else [])
+    nodes = [t.grad_fn for t in ts if isinstance(t, torch.Tensor) and t.grad_fn is not None]
+    if not nodes:
+        _free(lambda o: o == ("f", tag))
+        return
+    for node in nodes:
+        node.register_prehook(lambda grad_out, _t=tag: state.seen.add(_t))
+
+
+def _free(pred):
     for slab in state.slabs.values():
-        slab.busy = [False] * len(slab.busy)
+        slab.busy = [None if (o is not None and pred(o)) else o for o in slab.busy]
+
+
+def release(tag=None):
+    """End of a backward: its own slots, the slots of the forwards whose graph it ran through and
+    anonymous slots may be written again."""
+    seen, state.seen = state.seen, set()
+    _free(lambda o: o == ("b", tag) or o[0] == "a" or (o[0] == "f" and o[1] in seen))
 
 
 def bind_grad_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> int:
@@ -238,18 +292,22 @@ class deferred:
         self.owner = self.enabled and not state.defer
         if self.owner:
             state.defer = True
+            state.bwd = self.tag = state.next_tag
+            state.next_tag += 1
+            state.seen = set()
         return self
 
     def __exit__(self, exc_type, exc, tb):
         if not self.owner:
             return False
         state.defer = False
+        state.bwd = None
         if exc_type is not None:
             state.pending.clear()
-            release()
+            release(self.tag)
             return False
         flush()
-        release()
+        release(self.tag)
         return False
 
 
@@ -273,38 +331,10 @@ def record(g2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor):
                            f"{None if gw._base is None else tuple(gw._base.shape)}")
     state.pending.append((g2, x2, gw))
     state.recorded += 1
-    if EARLY > 1:
-        key = _key(g2, x2)
-        group = [it for it in state.pending if _key(it[0], it[1]) == key]
-        if len(group) >= EARLY:
-            _flush_early(key, group)
 
 
 def _key(g2, x2):
     return (tuple(g2.shape), tuple(x2.shape), g2.dtype, g2.device)
-
-
-@torch.no_grad()
-def _flush_early(key, group):
-    if len({gw.data_ptr() for _, _, gw in group}) != len(group):
-        return
-    v = _batch(group)
-    if v is None:
-        return
-    dev = group[0][0].device
-    if state.side is None:
-        from ..runtime.overlap_step import priority_stream
-        state.side = priority_stream(dev, 1 << 20)
-    main = torch.cuda.current_stream(dev)
-    state.side.wait_stream(main)  # the records' dY / X are complete
-    with torch.cuda.stream(state.side):
-        dy, x, dw = v
-        dw.baddbmm_(dy.transpose(1, 2), x)
-    state.side_pending = True
-    state.early += 1
-    state.batched += 1
-    ids = {id(it) for it in group}
-    state.pending = [it for it in state.pending if id(it) not in ids]
 
 
 def _owner(t: torch.Tensor, pools) -> Optional[Tuple[_Slab, int]]:
@@ -362,6 +392,3 @@ def flush():
         for g2, x2, gw in items:  # a weight used twice accumulates in order, by the per-layer path
             wgrad_into(g2, x2, gw)
             state.single += 1
-    if state.side_pending:  # everything after the backward sees the early batches' gradients
-        torch.cuda.current_stream(state.side.device).wait_stream(state.side)
-        state.side_pending = False

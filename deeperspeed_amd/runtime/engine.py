@@ -641,7 +641,7 @@ class DeepSpeedEngine(Module):
     def _resolve_bucket_sizes(self, zc):
         """'auto' ZeRO bucket sizes from the data-parallel world (runtime/comm/bucket_sizing.py)."""
         from .comm import bucket_sizing
-        world = dist.get_world_size(self.data_parallel_group) if dist.is_initialized() else 1
+        world = comm.world_size(self.data_parallel_group)
         esize = 2 if (self.fp16_enabled() or self.bfloat16_enabled()) else 4
         for key, scale in (("reduce_bucket_size", 1.0), ("allgather_bucket_size", 1.0),
                            ("stage3_prefetch_bucket_size", 1.0)):
@@ -751,11 +751,21 @@ class DeepSpeedEngine(Module):
             self.timers("forward").start()
         if self.training_dataloader is None:
             self.tput_timer.start()
-        if self.amp is not None:
-            with self.amp.autocast():
+        # slots of the layer-stacked activation buffers taken by this forward stay its own until a
+        # backward runs through its graph (ops/wgrad_batch.py)
+        wtag = _wgrad_batch.begin_forward() if self._defer_wgrad else None
+        try:
+            if self.amp is not None:
+                with self.amp.autocast():
+                    loss = self.module(*inputs, **kwargs)
+            else:
                 loss = self.module(*inputs, **kwargs)
-        else:
-            loss = self.module(*inputs, **kwargs)
+        except BaseException:
+            if wtag is not None:
+                _wgrad_batch.end_forward(wtag, None)
+            raise
+        if wtag is not None:
+            _wgrad_batch.end_forward(wtag, loss)
         if self.wall_clock_breakdown():
             self.timers("forward").stop()
             self.timers("forward_microstep").stop()

@@ -150,8 +150,10 @@ class ShardedOptimizerBase:
         self.gradient_accumulation_steps = int(gradient_accumulation_steps)
         self.timers = timers
         self.verbose = verbose
-        self.dp_world = dist.get_world_size(dp_process_group) if _dist_ready() else 1
-        self.dp_rank = dist.get_rank(dp_process_group) if _dist_ready() else 0
+        # comm.world_size / rank: the real group's, or the N of an emulated world (bench.py
+        # --emulate-world: shards, buckets and units of one rank of an N-rank job)
+        self.dp_world = comm.world_size(dp_process_group)
+        self.dp_rank = comm.rank(dp_process_group)
         self.mp_world = mpu.get_model_parallel_world_size() if mpu is not None else 1
         self.mp_rank = mpu.get_model_parallel_rank() if mpu is not None else 0
         if dynamic_loss_scale:

@@ -19,7 +19,7 @@ from __future__ import annotations
 import contextlib
 import hashlib
 import os
-from typing import List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -34,6 +34,72 @@ _seq = 0
 # hung collective, different counts at a rank that took another path (order divergence)
 _issued = 0
 _last: Tuple[str, int, str] = ("none", 0, "")
+# bytes per collective kind (all_gather: the gathered output, reduce_scatter / all_reduce: the
+# input), always counted: the emulated-world bench turns them into the xGMI rate a real job needs
+_bytes: Dict[str, int] = {}
+# opt-in full (tag, numel, dtype) trace, independent of DEBUG's per-step log (tests compare the
+# sequence an emulated rank issues with a real world-N rank's)
+_trace: Optional[List[Tuple[str, int, str]]] = None
+
+# Emulated world (bench.py --emulate-world N): one process runs rank 0 of an N-rank data-parallel
+# job -- the ZeRO optimizers size shards, buckets and units for N ranks (`world_size` / `rank`
+# below) -- and every framework collective is replaced by a local stand-in that writes the bytes
+# the real collective would: all-gather = N copies of the local chunk, reduce-scatter = the sum of
+# the N slices of the input (the local HBM traffic of RCCL's reduce kernel), all-reduce = nothing.
+# Values are meaningless (the loss too); memory, kernels and the issued collective sequence are the
+# real rank's.  Reference counterpart: none.
+_emulated = 0
+
+
+class _Done:
+    """Work handle of a stand-in collective: already complete on the issuing stream."""
+
+    def wait(self, timeout=None):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+def set_emulated_world(n: int):
+    global _emulated
+    _emulated = int(n) if n and int(n) > 1 else 0
+
+
+def emulated_world() -> int:
+    return _emulated
+
+
+def world_size(group=None) -> int:
+    """Data-parallel world size the ZeRO layout is built for (the emulated N when set)."""
+    if _emulated:
+        return _emulated
+    return dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+
+
+def rank(group=None) -> int:
+    if _emulated:
+        return 0
+    return dist.get_rank(group) if (dist.is_available() and dist.is_initialized()) else 0
+
+
+def bytes_by_kind() -> Dict[str, int]:
+    return dict(_bytes)
+
+
+def reset_bytes():
+    _bytes.clear()
+
+
+def start_trace():
+    global _trace
+    _trace = []
+
+
+def stop_trace() -> List[Tuple[str, int, str]]:
+    global _trace
+    out, _trace = _trace or [], None
+    return out
 
 
 def set_debug(enabled: bool):
@@ -53,30 +119,41 @@ def trace_range(name: str):
         yield
 
 
-def _record(op: str, t: torch.Tensor):
+def _record(op: str, t: torch.Tensor, kind: str):
     global _seq, _issued, _last
     _issued += 1
     _last = (op, int(t.numel()), str(t.dtype))
+    _bytes[kind] = _bytes.get(kind, 0) + t.numel() * t.element_size()
+    if _trace is not None:
+        _trace.append(_last)
     if DEBUG:
         _log.append((_seq, op, int(t.numel()), str(t.dtype)))
         _seq += 1
 
 
 def all_gather_into_tensor(out, inp, group=None, async_op=False, tag="all_gather"):
-    _record(tag, out)
+    _record(tag, out, "all_gather")
     with trace_range(f"rccl.{tag}[{out.numel()}]"):
+        if _emulated:
+            out.view(_emulated, -1).copy_(inp.reshape(1, -1).expand(_emulated, -1))
+            return _Done() if async_op else None
         return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 
 def reduce_scatter_tensor(out, inp, group=None, async_op=False, tag="reduce_scatter"):
-    _record(tag, inp)
+    _record(tag, inp, "reduce_scatter")
     with trace_range(f"rccl.{tag}[{inp.numel()}]"):
+        if _emulated:
+            torch.sum(inp.view(_emulated, -1), 0, out=out.view(-1))
+            return _Done() if async_op else None
         return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
 
 
 def all_reduce(t, op=dist.ReduceOp.SUM, group=None, async_op=False, tag="all_reduce"):
-    _record(tag, t)
+    _record(tag, t, "all_reduce")
     with trace_range(f"rccl.{tag}[{t.numel()}]"):
+        if _emulated:
+            return _Done() if async_op else None
         return dist.all_reduce(t, op=op, group=group, async_op=async_op)
 
 

@@ -120,3 +120,35 @@ def test_watchdog_prints_collective_progress():
     from deeperspeed_amd.utils import comm
     line = comm.progress()
     assert line.startswith("collectives issued=")
+
+
+@pytest.mark.slow
+def test_bench_config4_onebit_trains_after_freeze():
+    """BASELINE config 4 (PP4 x DP2, 1-bit Adam) diverged in every rehearsal (loss
+    11.6 -> 115-1,548) with freeze_step 2 at beta2 0.999.  With the bench's own optimizer block
+    (bench.ONEBIT_*: beta2 0.95, freeze after 16 steps, warmup extended past the freeze) the
+    compressed timed steps must train: finite, at most +5 % over the first compressed step, below
+    the first warmup loss, and not flagged "diverged"."""
+    r = _run(["--gpus", "8", "--model", "gpt-neox-125m", "--layers", "4", "--seq", "64", "--micro-batch", "1",
+              "--grad-accum", "4", "--steps", "6", "--warmup", "2", "--pipe", "4", "--optimizer", "onebitadam"],
+             timeout=900)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    out = json.loads(r.stdout.decode().strip())
+    c = out["config"]
+    assert c["optimizer_params"]["freeze_step"] == 16 and c["optimizer_params"]["betas"] == [0.9, 0.95]
+    assert c["warmup_steps_run"] == 17  # every timed step is a compressed one
+    losses = c["timed_losses"]
+    assert all(l == l and abs(l) < 1e4 for l in losses), losses
+    assert losses[-1] <= 1.05 * losses[0], losses
+    assert losses[-1] < c["first_warmup_loss"], (c["first_warmup_loss"], losses)
+    assert out["diverged"] is False
+
+
+def test_diverged_flag():
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    # bench.py redirects fd 1 at import; evaluate only the pure helper
+    ns = {}
+    start = src.index("def diverged(")
+    exec(src[start:src.index("\n\n\n", start)], {"DIVERGED_RATIO": 1.2}, ns)
+    assert ns["diverged"](11.6, 115.0) and ns["diverged"](11.6, float("nan"))
+    assert not ns["diverged"](11.6, 10.9) and not ns["diverged"](11.6, 13.0)

@@ -110,7 +110,7 @@ def _train(batch, monkeypatch, steps=3):
         losses.append(float(loss.detach()))
     torch.cuda.synchronize()
     out = losses, [p.detach().float().clone() for p in engine.module.parameters()], wb.state.batched - b0
-    print("last batching miss:", wb.state.last_miss, "slabs:", [(k[0], k[1], k[2]) for k in wb.state.slabs],
+    print("last batching miss:", wb.state.last_miss, "slabs:", {k: v.key[:2] for k, v in wb.state.slabs.items()},
           "recorded:", wb.state.recorded, "single:", wb.state.single)
     wb.enable(False)
     return out
@@ -138,7 +138,7 @@ def test_stacked_weight_transposes():
 def test_bert_training_with_batched_wgrads(monkeypatch):
     l0, w0, n0 = _train(False, monkeypatch)
     l1, w1, n1 = _train(True, monkeypatch)
-    # qkv / attn-out / fc1 / fc2 every step (more with DSA_WGRAD_EARLY: several batches per linear)
+    # qkv / attn-out / fc1 / fc2 every step
     assert n0 == 0 and n1 >= 4 * 3, (n0, n1)
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 2e-2 * abs(a)
@@ -165,3 +165,80 @@ def test_graph_captured_params_are_not_rebound():
         assert torch.all(free[0].grad == 3.0) and free[1].grad.data_ptr() - free[0].grad.data_ptr() == 512
     finally:
         del wb.state.stacks[n0:]
+
+
+def _bert_engine(batch, monkeypatch, dropout=0.0, pld=False):
+    _env()
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.bert import BertForPreTraining, get_config
+    from deeperspeed_amd.ops import wgrad_batch as wb
+    monkeypatch.setattr(wb, "ENABLED", batch)
+    wb.state.slabs.clear()
+    wb.state.off_kinds.clear()
+    wb.state.reshapes.clear()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = get_config("bert-large", num_layers=4, vocab_size=4096, max_position=256, hidden_dropout=dropout,
+                     attn_dropout=dropout)
+    model = BertForPreTraining(cfg, device=dev, dtype=torch.bfloat16).train()
+    conf = {"train_micro_batch_size_per_gpu": 8, "optimizer": {"type": "Lamb", "params": {"lr": 2e-3}},
+            "fp16": {"enabled": True, "type": "bfloat16"}, "gradient_clipping": 1.0}
+    if pld:
+        conf["progressive_layer_drop"] = {"enabled": True, "theta": 0.5, "gamma": 0.01}
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    assert engine._defer_wgrad == batch
+    return engine, cfg, dev
+
+
+def _bert_batch(cfg, dev, seed, B=8, S=128):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    ids = torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)
+    am = torch.ones(B, S, device=dev, dtype=torch.long)
+    pos = torch.stack([torch.randperm(S - 8, device=dev, generator=g)[:20].sort().values for _ in range(B)])
+    lab = torch.randint(0, cfg.vocab_size, (B, 20), device=dev, generator=g)
+    nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
+    return ids, None, am, pos, lab, nsp
+
+
+def test_interleaved_forwards_keep_their_slots(monkeypatch):
+    """fwd A (takes the slots), fwd B (ordinary memory), bwd B, fwd C, bwd A.  The end of
+    bwd B must not free A's slots, or fwd C overwrites the activations bwd A reads (silently: the
+    kernels write slots through raw out= pointers).  Gradients must equal the unbatched engine's."""
+    from deeperspeed_amd.ops import wgrad_batch as wb
+    grads = {}
+    for batch in (False, True):
+        engine, cfg, dev = _bert_engine(batch, monkeypatch)
+        a, b, c = (_bert_batch(cfg, dev, s) for s in (1, 2, 3))
+        la = engine(*a)
+        lb = engine(*b)
+        engine.backward(lb)
+        lc = engine(*c)  # noqa: F841 - its graph is never backpropagated
+        engine.backward(la)
+        torch.cuda.synchronize()
+        grads[batch] = [p.grad.float().clone() for p in engine.module.parameters() if p.grad is not None]
+        if batch:
+            assert wb.state.recorded > 0
+        wb.enable(False)
+    assert len(grads[False]) == len(grads[True])
+    for x, y in zip(grads[False], grads[True]):
+        assert (x - y).abs().max().item() <= 2e-2 * max(1e-3, x.abs().max().item())
+
+
+def test_slab_memory_flat_under_pld_and_shape_changes(monkeypatch):
+    """slabs are keyed per kind -- progressive layer drop (a different kept-layer count
+    every step) and a seq-128 / seq-256 switch must not allocate a fresh set of slabs per shape."""
+    from deeperspeed_amd.ops import wgrad_batch as wb
+    engine, cfg, dev = _bert_engine(True, monkeypatch, pld=True)
+    peaks = []
+    for step in range(10):
+        S = 128 if step % 2 == 0 else 256
+        loss = engine(*_bert_batch(cfg, dev, step, S=S))
+        engine.backward(loss)
+        engine.step()
+        torch.cuda.synchronize()
+        peaks.append(torch.cuda.memory_allocated())
+    kinds = len(wb.state.slabs)
+    wb.enable(False)
+    # after the first few steps the unstable kinds are off and nothing more is allocated
+    assert max(peaks[4:]) <= peaks[3] + (64 << 20), [p >> 20 for p in peaks]
+    assert kinds <= 16
