@@ -57,6 +57,14 @@ ONEBIT_BETAS = [0.9, 0.95]
 # a run whose final loss is non-finite or above this multiple of its first warmup loss is marked
 # "diverged": true in the result line
 DIVERGED_RATIO = 1.2
+# memory margins (GiB): below the device for the measured fit / stash (allocator variance on another
+# box), on each moment tier, and the headroom the first fit grant keeps back
+MEM_FLOOR_GIB = 3.0
+STASH_MARGIN_GIB = 2.0
+STASH_FLOOR_GIB = 1.5
+TIER_MARGIN_GIB = 6.0
+FIT_MARGIN_GIB = 1.0
+HOST_MOMENTS_GIB = [0.0]  # set from --host-moments-gib
 
 
 def parse():
@@ -108,8 +116,19 @@ def parse():
     p.add_argument("--moments-tiers", type=str, default="auto",
                    help="--offload moments: where the Adam moments live, per layer, in the order HBM -> pinned host "
                         "-> NVMe file (--nvme-path).  auto: HBM headroom, then the host budget "
-                        "(DSA_HOST_MOMENTS_GIB, default min(available - 24 GiB, 215 GiB)), then the free disk; "
+                        "(--host-moments-gib, default min(available - 24 GiB, 215 GiB)), then the free disk; "
                         "host: everything in pinned host memory")
+    p.add_argument("--stash", type=str, default="auto", choices=["auto", "attn", "off"],
+                   help="selective recompute from measured headroom (one-GPU recompute runs): auto = attention "
+                        "outputs, then fc1 outputs with what is left; attn = attention only; off = full recompute")
+    p.add_argument("--stash-offload", action="store_true",
+                   help="park the attention stash of the layers HBM cannot hold in pinned host memory "
+                        "(measured slower on MI355X: profiles/aux/host_stash_ab.log)")
+    p.add_argument("--host-moments-gib", type=float, default=0.0,
+                   help="--offload moments: pinned-host budget of the moment tiers (0: min(available - 24, 215) GiB)")
+    p.add_argument("--overlap-step", type=str, default="on", choices=["on", "off"],
+                   help="bound single-rank ZeRO-3: the fused Adam step overlaps the next forward (side stream)")
+    p.add_argument("--memtrace", action="store_true", help="log HBM after every warmup phase and per layer")
     p.add_argument("--emulate-world", type=int, default=0,
                    help="one process runs rank 0 of an N-rank ZeRO job at full depth: shards, buckets, "
                         "micro-batch, recompute and memory fit planned for N ranks, collectives replaced by "
@@ -128,7 +147,7 @@ def plan_memory(cfg, mb, seq, world, offload, ckpt, ga=1):
     master 4 B (2 B int16 residual with compact_master, 0 B when offloaded).  The gradient
     shard is bf16 (2 B) on one rank (gradients accumulate in place into the bound shard) and
     fp32 (4 B) for N >= 2 with gradient accumulation (reduce-scattered micro-batch gradients
-    are summed in fp32).  Measured on MI355X (DSA_MEMTRACE=1, profiles/aux/memtrace_*.log):
+    are summed in fp32).  Measured on MI355X (--memtrace, profiles/aux/memtrace_*.log):
     20B, N=1, compact, recompute on -> planned 279 GiB, peak 274.7 GiB; activations of one
     GPT-NeoX layer without recompute = 32.0 * s * b * h bytes (budgeted as 34), one s*b*h
     layer input with it.  Transients: two gathered ZeRO-3 units, the logits (bf16 + grad,
@@ -151,16 +170,16 @@ def plan_moment_tiers(model, P, hbm_free, nvme_path):
     runtime/memory_fit.split_moment_tiers assigns the model's blocks to them in order."""
     import shutil
     from deeperspeed_amd.runtime import memory_fit
-    margin = float(os.environ.get("DSA_TIER_HBM_MARGIN_GIB", "6")) * 2**30
+    margin = TIER_MARGIN_GIB * 2**30
     hbm = max(0.0, hbm_free - margin)
     try:
         import psutil
         avail = psutil.virtual_memory().available
     except Exception:  # noqa: BLE001
         avail = 1 << 50
-    host = float(os.environ.get("DSA_HOST_MOMENTS_GIB", "0")) * 2**30 or min(avail - 24 * 2**30, 215 * 2**30)
+    host = HOST_MOMENTS_GIB[0] * 2**30 or min(avail - 24 * 2**30, 215 * 2**30)
     os.makedirs(nvme_path, exist_ok=True)
-    disk = max(0.0, shutil.disk_usage(nvme_path).free - float(os.environ.get("DSA_DISK_MARGIN_GIB", "6")) * 2**30)
+    disk = max(0.0, shutil.disk_usage(nvme_path).free - TIER_MARGIN_GIB * 2**30)
     blocks = [[model.embed_in]] + [[l] for l in model.layers] + [[model.final_layer_norm, model.embed_out]]
     blocks = [[p for m in mods for p in m.parameters()] for mods in blocks]
     try:
@@ -346,6 +365,7 @@ def spawn_ranks(n):
 
 def main():
     args = parse()
+    HOST_MOMENTS_GIB[0] = args.host_moments_gib
     launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
     if launched == 0 and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
@@ -475,7 +495,7 @@ def main():
     # They are sized from MEASUREMENT (runtime/memory_fit.py): the first warmup step runs lean
     # (none of either), its measured peak decides what the rest of HBM is granted to, and every
     # later warmup step gives back retention, then resident gradients, then halves the
-    # micro-batch if the peak comes within DSA_MEM_FLOOR_GIB of the device.
+    # micro-batch if the peak comes within MEM_FLOOR_GIB of the device.
     sharded = world > 1 or args.force_sharded
     fit = None
     if args.zero == 3 and sharded and ckpt == "off" and on_gpu and args.pipe == 1:
@@ -485,7 +505,7 @@ def main():
     resident = args.resident_grads == "on"
     if fit is not None:
         fit.live, fit.resident = live, resident
-    floor = float(os.environ.get("DSA_MEM_FLOOR_GIB", "3")) * 2**30
+    floor = MEM_FLOOR_GIB * 2**30
     limit = hbm / share - floor
     # gloo rehearsal of an N-GPU job on one GPU: gloo's asynchronous collectives on device tensors
     # stalled for ~50 s when several ZeRO reductions were in flight (profiles/r5a_notes.md), so the
@@ -502,9 +522,9 @@ def main():
     if resident:
         zcfg["resident_grads"] = True
     # bound single-rank ZeRO-3: the fused Adam step overlaps the next forward (side stream,
-    # per-bucket events); DSA_OVERLAP_STEP=0 keeps the serial step
+    # per-bucket events); --overlap-step off keeps the serial step
     if (world == 1 and not args.force_sharded and offload in ("compact", "none") and on_gpu
-            and os.environ.get("DSA_OVERLAP_STEP", "1") != "0"):
+            and args.overlap_step == "on"):
         zcfg["overlap_step"] = True
     if offload == "compact":
         zcfg["compact_master"] = True
@@ -546,12 +566,12 @@ def main():
     # gradient (early in the last micro-batch's backward) and their next read (late in the next
     # forward): their Adam moments live in pinned host memory and stream through HBM on the copy
     # engines during the overlapped step, and the 8 B/param freed goes to the attention stash.
-    hm = os.environ.get("DSA_BENCH_HOST_MOMENTS", args.host_moments_layers)
-    # (only where the freed HBM buys attention stash: with DSA_STASH=0 host moments only add the PCIe
+    hm = args.host_moments_layers
+    # (only where the freed HBM buys attention stash: with --stash off host moments only add the PCIe
     # phase to the step)
     k_host = (1 if (world == 1 and args.zero == 3 and offload == "compact" and ckpt == "on" and big and on_gpu
                     and not args.force_sharded and args.pipe == 1
-                    and os.environ.get("DSA_STASH", "1") != "0") else 0) if hm == "auto" else \
+                    and args.stash != "off") else 0) if hm == "auto" else \
         (0.5 if hm == "head" else int(hm))  # "head": the LM head only
     params = model.parameters()
     host_numel = 0
@@ -614,8 +634,8 @@ def main():
                         f"(peak {torch.cuda.max_memory_allocated() / 2**30:.2f})")
         return loss, ph
 
-    memtrace = os.environ.get("DSA_MEMTRACE", "0") == "1" and on_gpu
-    verbose_hb = world > 1 or os.environ.get("DSA_BENCH_VERBOSE_HB", "0") == "1"
+    memtrace = args.memtrace and on_gpu
+    verbose_hb = world > 1
     if memtrace:  # per-layer activation footprint of the first forward (planner calibration)
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         marks = []
@@ -639,11 +659,11 @@ def main():
         HBM left above the allocator's reserved peak (minus a margin) keeps the attention
         q, k, v, output and LSE of as many layers as fit (NeoXAttention.stash_outputs), so their
         recompute skips the QKV GEMM, rotary split and flash forward."""
-        if not cfg.checkpoint_activations or not on_gpu or os.environ.get("DSA_STASH", "1") == "0":
+        if not cfg.checkpoint_activations or not on_gpu or args.stash == "off":
             return 0
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
-        margin = float(os.environ.get("DSA_STASH_MARGIN_GIB", "2")) * 2**30
+        margin = STASH_MARGIN_GIB * 2**30
         free = hbm / share - reserved_peak() - margin
         n = int(max(0, min(len(layers), free // per_layer)))
         for m in layers[-n:] if n else []:
@@ -652,7 +672,7 @@ def main():
         # GEMM of their recompute; about the same GEMM time per GiB as the attention stash)
         per_mlp = mb * args.seq * cfg.intermediate_size * 2
         n_mlp = 0
-        if n == len(layers) and os.environ.get("DSA_MLP_STASH", "1") != "0":
+        if n == len(layers) and args.stash == "auto":
             n_mlp = int(max(0, min(len(layers), (free - n * per_layer) // per_mlp)))
             for m in layers[-n_mlp:] if n_mlp else []:
                 m.mlp.stash_outputs = True
@@ -661,11 +681,11 @@ def main():
         log(f"selective recompute: {n}/{len(layers)} layers keep attention outputs, {n_mlp} keep the fc1 output "
             f"({(n * per_layer + n_mlp * per_mlp) / 2**30:.1f} GiB; reserved peak {reserved_peak() / 2**30:.1f} GiB)")
         # the remaining layers park their stash in pinned host memory (copy engines over PCIe,
-        # prefetched back by the recompute of the layers above): opt-in, DSA_STASH_OFFLOAD=1 -- on the
+        # prefetched back by the recompute of the layers above): opt-in, --stash-offload -- on the
         # measured box the PCIe copies throttled the forward (profiles/aux/host_stash_ab.log)
-        if os.environ.get("DSA_STASH_OFFLOAD", "0") == "1" and n < len(layers):
+        if args.stash_offload and n < len(layers):
             from deeperspeed_amd.runtime.activation_checkpointing import host_stash as hs
-            hs.host_stash().max_backlog = int(os.environ.get("DSA_STASH_OFFLOAD_BACKLOG", "6"))
+            hs.host_stash().max_backlog = 6
             for m in layers[: len(layers) - n]:
                 m.attention.stash_outputs = True
                 m.attention.stash_offload = True
@@ -676,7 +696,7 @@ def main():
 
     def check_stash(n):
         """Safety check after the first step WITH the stash: if the allocator's reserved peak
-        came within DSA_STASH_FLOOR_GIB (default 1.5) of the HBM budget, give stashed layers
+        came within STASH_FLOOR_GIB of the HBM budget, give stashed layers
         back (first-stashed first) until the measured overshoot is covered, so allocator
         variance on another box cannot push a timed step into an out-of-memory error."""
         if n <= 0:
@@ -684,7 +704,7 @@ def main():
         nonlocal stashed_mlp
         layers = [m for m in engine.module.modules() if type(m).__name__ == "NeoXTransformerLayer"]
         per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
-        sfloor = float(os.environ.get("DSA_STASH_FLOOR_GIB", "1.5")) * 2**30
+        sfloor = STASH_FLOOR_GIB * 2**30
         over = reserved_peak() - (hbm / share - sfloor)
         if over <= 0:
             return n
@@ -723,7 +743,7 @@ def main():
         dist.all_reduce(h, op=dist.ReduceOp.MIN)
         head = float(h.item())
         if i == 0:
-            grow_margin = float(os.environ.get("DSA_FIT_MARGIN_GIB", "1")) * 2**30
+            grow_margin = FIT_MARGIN_GIB * 2**30
             acts = memory_fit.grow(fit, head - grow_margin)
         else:
             acts = memory_fit.shrink(fit, -head) if head < 0 else []
@@ -791,7 +811,7 @@ def main():
 
     if args.profile_steps > 0:
         from torch.profiler import ProfilerActivity, profile
-        stacks = os.environ.get("DSA_PROFILE_STACK", "0") == "1"
+        stacks = True
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
                      with_stack=stacks) as prof:
             for _ in range(args.profile_steps):
@@ -949,7 +969,7 @@ def _lt_summary():
     except Exception as e:  # diagnostics only
         return {"error": repr(e)}
     return {"enabled": True, "problems": len(ch), "table_wins": sum(1 for c in ch if c[10]),
-            "routes": {"fwd": lt_tune.FWD, "dgrad": lt_tune.DGRAD, "wgrad": lt_tune.WGRAD}}
+            "routes": {"fwd": lt_tune.FWD}}
 
 
 def _optimizer_block(args):

@@ -15,7 +15,6 @@ pipeline engine (`to_pipeline()` builds a PipelineModule of LayerSpecs).
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field, asdict
 from typing import Optional
 
@@ -24,7 +23,6 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import native
-from ..ops import lt_tune
 from ..ops.linear import Linear, grad_only_linear, linear, nt_wgrad_planned, zero_placeholder
 from ..ops.attention import attention, rotary_split
 from ..runtime.activation_checkpointing import checkpointing as ds_ckpt
@@ -134,11 +132,8 @@ class LinearBiasGeLU(nn.Linear):
             u = linear(x, self.weight)
             if self.keep_u:
                 self.kept_u = u
-        if (self.colmajor_in_recompute and _SKIP_OUTPUTS and torch.is_grad_enabled() and COLMAJOR_GELU
-                and native.bias_gelu_t_supported(u)
-                # fc2's weight gradient reads its input token-major when the measured NT GEMM wins
-                and not lt_tune.wgrad_nt(u.numel() // self.out_features, self.in_features, self.out_features,
-                                         u.element_size())):
+        if (self.colmajor_in_recompute and _SKIP_OUTPUTS and torch.is_grad_enabled()
+                and native.bias_gelu_t_supported(u)):
             return native.bias_gelu_colmajor(u, self.bias, self.approximate)
         # the backward also writes du^T when this layer's own weight gradient will read it
         offer = u.is_cuda and nt_wgrad_planned(u.numel() // self.out_features, self.out_features, self.in_features,
@@ -146,8 +141,6 @@ class LinearBiasGeLU(nn.Linear):
         return native.bias_gelu(u, self.bias, self.approximate, offer_t=offer)
 
 
-# DSA_COLMAJOR_GELU=0: the recompute writes the GeLU output row-major (fc2's wgrad transposes it)
-COLMAJOR_GELU = os.environ.get("DSA_COLMAJOR_GELU", "1") != "0"
 
 
 _SKIP_OUTPUTS = 0

@@ -13,7 +13,6 @@ CPU tensors use PyTorch reference math (unit tests on CPU CI).
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional
 
 import torch
@@ -155,9 +154,9 @@ def attention(q, k, v, causal: bool = True, mask=None, softmax_scale: float = 1.
     """q,k,v [B,NH,S,HD] -> [B,NH,S,HD] (out_layout "bhsd") or [B,S,NH,HD] ("bshd", which the
     flash kernel writes directly so `.reshape(B, S, NH*HD)` is free).  q is expected
     pre-scaled when softmax_scale == 1.  The fused kernel is used for self-attention without
-    mask/dropout unless `use_flash` is False or DSA_FLASH_ATTN=0."""
+    mask/dropout unless `use_flash` is False."""
     if use_flash is None:
-        use_flash = os.environ.get("DSA_FLASH_ATTN", "1") != "0"
+        use_flash = True
     if (use_flash and q.is_cuda and dropout_p == 0.0 and mask is None and q.shape == k.shape == v.shape
             and native.has_flash_attention(q)):
         return native.flash_attention(q, k, v, causal, softmax_scale, out_layout=out_layout)

@@ -1004,26 +1004,16 @@ std::vector<Tensor> flash_attn_qkv_fwd(Tensor qkv, c10::optional<Tensor> kbias, 
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   Tensor o = out_or_new(o_out, {B, S, H, D}, qkv.options(), "flash_attn_qkv_fwd");
   Tensor lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
-  // opt-in (DSA_FA_DROP_BITS=1): the attention-dropout keep masks stored as bits for the backward
-  // (query- and key-major). Same keep decisions as the hash; measured 1-3% slower on BERT-Large
-  // (the forward's bit transpose costs more than the backward saves), so the hash stays the default.
-  // Read per call so a test can exercise both paths in one process.
-  const char* bits_env = getenv("DSA_FA_DROP_BITS");
-  const bool store_bits = bits_env && bits_env[0] == '1';
-  Tensor bits = (store_bits && p_drop > 0.0 && dsa::flash_drop_bits_ok((int)S))
-                    ? at::empty({2 * B * H * S * (S / 32)}, qkv.options().dtype(at::kInt))
-                    : at::empty({0}, qkv.options().dtype(at::kInt));
   const char* base = static_cast<const char*>(qkv.data_ptr());
   const int64_t hd = H * D * qkv.element_size();
   dsa::launch_flash_fwd_ex(base, base + hd, base + 2 * hd, o.data_ptr(), lse.data_ptr<float>(), (int)(B * H), (int)S,
                            (int)D, (float)scale, kbias ? kbias->data_ptr<float>() : nullptr, (int)H, (float)p_drop,
-                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D, rng_ptr(rng, qkv),
-                           bits.numel() ? reinterpret_cast<uint32_t*>(bits.data_ptr<int>()) : nullptr);
-  return {o, lse, bits};
+                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D, rng_ptr(rng, qkv));
+  return {o, lse};
 }
 
 Tensor flash_attn_qkv_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, c10::optional<Tensor> kbias, double scale,
-                          double p_drop, int64_t seed, OptT rng, OptT dqkv_out, OptT bits) {
+                          double p_drop, int64_t seed, OptT rng, OptT dqkv_out) {
   check_qkv(qkv, "flash_attn_qkv_bwd");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(3), D = qkv.size(4);
   for (auto* t : {&dout, &o}) {
@@ -1047,9 +1037,7 @@ Tensor flash_attn_qkv_bwd(Tensor dout, Tensor qkv, Tensor o, Tensor lse, c10::op
   dsa::launch_flash_bwd_ex(dout.data_ptr(), base, base + hd, base + 2 * hd, o.data_ptr(), lse.data_ptr<float>(),
                            delta.data_ptr<float>(), dbase, dbase + hd, dbase + 2 * hd, (int)(B * H), (int)S, (int)D,
                            (float)scale, kbias ? kbias->data_ptr<float>() : nullptr, (int)H, (float)p_drop,
-                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D, rng_ptr(rng, qkv),
-                           (bits.has_value() && bits->numel() == 2 * B * H * S * (S / 32))
-                               ? reinterpret_cast<uint32_t*>(bits->data_ptr<int>()) : nullptr);
+                           (uint64_t)seed, dcode(qkv), cur_stream(), (int)H, (int)H, 3 * H * D, rng_ptr(rng, qkv));
   return dqkv;
 }
 
@@ -1311,7 +1299,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed"), py::arg("rng") = py::none(), py::arg("o_out") = py::none());
   m.def("flash_attn_qkv_bwd", &flash_attn_qkv_bwd, py::arg("dout"), py::arg("qkv"), py::arg("o"), py::arg("lse"),
         py::arg("kbias"), py::arg("scale"), py::arg("p_drop"), py::arg("seed"), py::arg("rng") = py::none(),
-        py::arg("dqkv_out") = py::none(), py::arg("bits") = py::none());
+        py::arg("dqkv_out") = py::none());
   m.def("sparse_flash_bwd", &sparse_flash_bwd);
   m.def("onebit_worker_compress", &onebit_worker_compress);
   m.def("onebit_server_compress", &onebit_server_compress);

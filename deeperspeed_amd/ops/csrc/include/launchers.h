@@ -172,18 +172,13 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
                       int dt, hipStream_t s, int onh = 0);
 // block-sparse flash attention (S % 64 == 0): LUTs per layout head (Hl = 1 or H), shift =
 // min(6, log2(layout block))
-// dbits: optional [2, BH * S * S/32] uint32 of stored attention-dropout keep masks (S % 64 == 0):
-// written by the forward, read by the backward instead of re-hashing
-bool flash_drop_bits_ok(int S);
 void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh = 0, int64_t ild = 0, const int64_t* rng = nullptr,
-                         uint32_t* dbits = nullptr);
+                         int onh, int inh = 0, int64_t ild = 0, const int64_t* rng = nullptr);
 void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const void* v, const void* o,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh = 0, int64_t ild = 0, const int64_t* rng = nullptr,
-                         uint32_t* dbits = nullptr);
+                         int onh, int inh = 0, int64_t ild = 0, const int64_t* rng = nullptr);
 void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
                              const int* cols, const uint32_t* masks, int BH, int H, int Hl, int S, int D, bool causal,
                              float scale, int shift, int dt, hipStream_t s, int onh = 0,

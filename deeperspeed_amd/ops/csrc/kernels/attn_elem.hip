@@ -572,11 +572,6 @@ static inline bool softmax_rows_shape(int C, int& G, int& NV) {
     default: { constexpr int NV = 16; __VA_ARGS__; } break;          \
   }
 
-static int os_env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
-
 static int elem_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   if (g > 16384) g = 16384;
@@ -587,15 +582,10 @@ void launch_rotary_split_fwd(const void* qkv, void* q, void* k, void* v, const f
                              int HD, int ROT, float qscale, int dt, hipStream_t s) {
   const int rows = B * S * NH;
   const int grid = (rows * 3 + 255) / 256;
-  const int tiled_mode = os_env_int("DSA_ROTARY_TILED", 1);
-  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0 && tiled_mode != 0;
+  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0;
 #define DSA_ROT_TILED_FWD(hd, rot)                                                                             \
   if (tiled && HD == hd && ROT == rot) {                                                                       \
     DSA_DISPATCH_16(dt, T,                                                                                     \
-      if (tiled_mode == 2)  /* DSA_ROTARY_TILED=2: unpadded LDS rows (A/B) */                              \
-        hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, false, false>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
-                           dim3(256), 0, s, (const T*)qkv, nullptr, nullptr, nullptr, nullptr, (T*)q, (T*)k, (T*)v, (const float2*)cs, S, NH, qscale);                                                     \
-      else                                                                                                     \
         hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, false>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
                            dim3(256), 0, s, (const T*)qkv, nullptr, nullptr, nullptr, nullptr, (T*)q, (T*)k, (T*)v, (const float2*)cs, S, NH, qscale));                                                    \
     return;                                                                                                    \
@@ -621,15 +611,10 @@ void launch_rotary_split_bwd(const void* dq, const void* dk, const void* dv, voi
                              int S, int NH, int HD, int ROT, float qscale, int dt, hipStream_t s) {
   const int rows = B * S * NH;
   const int grid = (rows * 3 + 255) / 256;
-  const int tiled_mode = os_env_int("DSA_ROTARY_TILED", 1);
-  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0 && tiled_mode != 0;
+  const bool tiled = S % ROT_SB == 0 && NH % ROT_HB == 0;
 #define DSA_ROT_TILED_BWD(hd, rot)                                                                             \
   if (tiled && HD == hd && ROT == rot) {                                                                       \
     DSA_DISPATCH_16(dt, T,                                                                                     \
-      if (tiled_mode == 2)  /* DSA_ROTARY_TILED=2: unpadded LDS rows (A/B) */                              \
-        hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, true, false>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
-                           dim3(256), 0, s, nullptr, (T*)dqkv, (const T*)dq, (const T*)dk, (const T*)dv, nullptr, nullptr, nullptr, (const float2*)cs, S, NH, qscale);                                                     \
-      else                                                                                                     \
         hipLaunchKernelGGL((rotary_split_tiled_kernel<T, hd, rot, true>), dim3(B * (S / ROT_SB) * (NH / ROT_HB)), \
                            dim3(256), 0, s, nullptr, (T*)dqkv, (const T*)dq, (const T*)dk, (const T*)dv, nullptr, nullptr, nullptr, (const float2*)cs, S, NH, qscale));                                                    \
     return;                                                                                                    \

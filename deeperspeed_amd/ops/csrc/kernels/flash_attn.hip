@@ -5,16 +5,12 @@
 // its S<8192 limit: scores never leave the CU.  Layout: q,k,v,o [B*H, S, D] row-major,
 // lse [B*H, S] fp32 (natural log of the scaled row sum), D in {64, 96, 128}.
 //
-// MFMA mapping (v_mfma_f32_16x16x32_bf16, wave64): lane l, g = l>>4, i = l&15
-//   A fragment: A[row i][k 8g..8g+7]      B fragment: B[k 8g..8g+7][col i]
-//   C/D:        C[row 4g+r][col i], r = 0..3
-// Every operand tile is staged in LDS in its natural [row][D] layout (rows padded by 16 B
-// so 16-lane row reads are conflict-free).  Operands needed "down a column" are read with
-// ds_read_b64_tr_b16 (hardware transpose, two 4-row blocks per 8-deep fragment), and the
-// softmax/dS tiles produced in C layout are re-laid out through a per-wave LDS scratch to
-// become A operands.  Workgroup = 4 waves = 64 rows (queries for fwd/dQ, keys for dK/dV).
-// Backward is FA2-style without atomics: one kernel owns dK/dV per key block, one owns dQ
-// per query block (both recompute P from the saved LSE).
+// Every kernel here runs v_mfma_f32_32x32x16 (bf16 / fp16) on wave64 with 4-wave workgroups of
+// 128 rows (BM2: queries for the forward and dQ, keys for dK/dV), K / V (or Q / dO) tiles of 64
+// rows (BN2) double-buffered in LDS and read "down a column" with ds_read_b64_tr_b16 (hardware
+// transpose), softmax in registers in the C layout (see "forward v2" below).  Backward is
+// FA2-style without atomics: dQ (+ Delta) first, then dK/dV per key block, both recomputing P
+// from the saved LSE.  Block-sparse variants walk a LUT of active 64 x 64 tiles (bottom).
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
@@ -33,9 +29,6 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-constexpr int BM = 64;  // rows per workgroup (16 per wave)
-constexpr int BN = 64;  // columns (keys or queries) per inner iteration
-
 // LDS row stride (elements) of the [rows][D] Q / K / V / dO tiles.  D + 8 keeps the ds_read_b128 row
 // reads conflict-free for every D; the 32x32x16 transposed reads (ds_read_b64_tr_b16, 4 rows x 4
 // lanes x 2 column halves per 32-lane half) are 2-way at D = 64 / 96 with +8 but 4-way at D = 128
@@ -44,169 +37,12 @@ constexpr int BN = 64;  // columns (keys or queries) per inner iteration
 // vs 1.2 at D = 96 before, profiles/r4z_notes.md).
 template <int D> constexpr int LDP = D + (D == 128 ? 24 : 8);
 
-template <typename T> struct Mfma;
-template <> struct Mfma<bf16_t> {
-  __device__ __forceinline__ static f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                   0, 0, 0);
-  }
-};
-template <> struct Mfma<f16_t> {
-  __device__ __forceinline__ static f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
-                                                  0, 0);
-  }
-};
-
 template <typename T> __device__ __forceinline__ uint16_t to16(float f);
 template <> __device__ __forceinline__ uint16_t to16<bf16_t>(float f) { return f32_to_bf16(f); }
 template <> __device__ __forceinline__ uint16_t to16<f16_t>(float f) { return f32_to_f16(f); }
 
 // 8 consecutive 16-bit elements of an LDS row (A fragment / B-from-transposed-storage)
 __device__ __forceinline__ s16x8 lds_row8(const uint16_t* p) { return *reinterpret_cast<const s16x8*>(p); }
-
-// B fragment read "down a column": rows r0+8g..r0+8g+7, column c0+i of a [rows][stride] tile.
-__device__ __forceinline__ s16x8 lds_col8(const uint16_t* base, int stride, int r0, int c0, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const uint16_t* a0 = base + (r0 + 8 * g + q) * stride + c0 + 4 * p;
-  const uint16_t* a1 = a0 + 4 * stride;
-  s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-  s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
-  return s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-}
-
-// Cooperative stage of `rows` rows of a [S, D] tensor (row base r0) into an LDS tile with
-// row stride D+8; out-of-range rows are zero-filled (keeps EXEC full for tr reads).
-template <int D>
-__device__ __forceinline__ void stage_rows(uint16_t* lds, const uint16_t* __restrict__ g, int r0, int S) {
-  constexpr int CH = D / 8;  // 16-byte chunks per row
-  for (int c = threadIdx.x; c < BN * CH; c += blockDim.x) {
-    const int r = c / CH, ch = c - r * CH;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + r < S) v = *reinterpret_cast<const uint4*>(g + (int64_t)(r0 + r) * D + ch * 8);
-    *reinterpret_cast<uint4*>(lds + r * LDP<D> + ch * 8) = v;
-  }
-}
-
-__device__ __forceinline__ float rowgroup_max(float v) {  // across the 16 lanes sharing g
-  v = fmaxf(v, __shfl_xor(v, 1, 64));
-  v = fmaxf(v, __shfl_xor(v, 2, 64));
-  v = fmaxf(v, __shfl_xor(v, 4, 64));
-  v = fmaxf(v, __shfl_xor(v, 8, 64));
-  return v;
-}
-__device__ __forceinline__ float rowgroup_sum(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
-  return v;
-}
-
-// ======================================================================== forward
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) fwd_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
-                                                  const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
-                                                  float* __restrict__ LSE, int S, float scale) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Ks = smem;                       // [BN][D+8]
-  uint16_t* Vs = Ks + BN * LDP<D>;          // [BN][D+8]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint16_t* Ps = Vs + BN * LDP<D> + w * 16 * (BN + 8);  // per wave [16][BN+8]
-  const int g = lane >> 4, i = lane & 15;
-  const int64_t bh = blockIdx.y;
-  const int qb = blockIdx.x * BM;
-  const int qrow0 = qb + 16 * w;
-  const uint16_t* Qb = Q + bh * (int64_t)S * D;
-  const uint16_t* Kb = K + bh * (int64_t)S * D;
-  const uint16_t* Vb = V + bh * (int64_t)S * D;
-
-  s16x8 qf[D / 32];
-#pragma unroll
-  for (int kk = 0; kk < D / 32; ++kk) {
-    const int row = qrow0 + i;
-    qf[kk] = row < S ? *reinterpret_cast<const s16x8*>(Qb + (int64_t)row * D + 32 * kk + 8 * g) : s16x8{};
-  }
-  f32x4 o[D / 16];
-#pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[4], l[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) { m[r] = -INFINITY; l[r] = 0.f; }
-  const float sl2 = scale * 1.4426950408889634f;  // exp(x) = exp2(x * log2 e)
-
-  const int kend = CAUSAL ? min(S, qb + BM) : S;
-  for (int j0 = 0; j0 < kend; j0 += BN) {
-    __syncthreads();
-    stage_rows<D>(Ks, Kb, j0, S);
-    stage_rows<D>(Vs, Vb, j0, S);
-    __syncthreads();
-    f32x4 s[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < D / 32; ++kk)
-        s[t] = Mfma<T>::run(qf[kk], lds_row8(Ks + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), s[t]);
-    }
-    // mask + online softmax (rows 4g+r of this wave, keys j0+16t+i)
-    float mx[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qrow = qrow0 + 4 * g + r;
-      float v = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int key = j0 + 16 * t + i;
-        float x = s[t][r] * sl2;
-        if (key >= S || (CAUSAL && key > qrow)) x = -INFINITY;
-        s[t][r] = x;
-        v = fmaxf(v, x);
-      }
-      mx[r] = rowgroup_max(v);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float mn = fmaxf(m[r], mx[r]);
-      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[r] - mn);
-      float ps = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float p = (mn == -INFINITY) ? 0.f : exp2f(s[t][r] - mn);
-        s[t][r] = p;
-        ps += p;
-      }
-      l[r] = l[r] * alpha + rowgroup_sum(ps);
-      m[r] = mn;
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) o[dt][r] *= alpha;
-    }
-    // P (C layout) -> per-wave LDS [16][BN+8] -> A fragments
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Ps[(4 * g + r) * (BN + 8) + 16 * t + i] = to16<T>(s[t][r]);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < BN / 32; ++c) {
-      const s16x8 pa = lds_row8(Ps + i * (BN + 8) + 32 * c + 8 * g);
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) o[dt] = Mfma<T>::run(pa, lds_col8(Vs, D + 8, 32 * c, 16 * dt, lane), o[dt]);
-    }
-  }
-  // epilogue
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qrow = qrow0 + 4 * g + r;
-    const float inv = l[r] > 0.f ? 1.f / l[r] : 0.f;
-    if (qrow < S) {
-      uint16_t* orow = O + (bh * (int64_t)S + qrow) * D;
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) orow[16 * dt + i] = to16<T>(o[dt][r] * inv);
-      if (i == 0) LSE[bh * (int64_t)S + qrow] = (m[r] == -INFINITY) ? -INFINITY : (m[r] + log2f(l[r])) * 0.6931471805599453f;
-    }
-  }
-}
 
 // O / dO addressing: onh == 0 -> [B*H, S, D] (head-major, like q/k/v); onh == H -> [B, S, H, D]
 // (token-major: the attention output is consumed as [B, S, H*D] by the output projection with
@@ -241,189 +77,6 @@ __global__ void __launch_bounds__(256) delta_kernel(const uint16_t* __restrict__
   acc += __shfl_xor(acc, 2, 64);
   acc += __shfl_xor(acc, 4, 64);
   if (row < rows && sub == 0) delta[row] = acc;
-}
-
-// ======================================================================== backward: dK, dV
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) bwd_dkdv_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
-                                                       const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
-                                                       const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                                                       uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S,
-                                                       float scale) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Qs = smem;                   // [BN queries][D+8]
-  uint16_t* dOs = Qs + BN * LDP<D>;     // [BN][D+8]
-  float* lse_s = reinterpret_cast<float*>(dOs + BN * LDP<D>);  // [BN]
-  float* del_s = lse_s + BN;                                     // [BN]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint16_t* Pt = reinterpret_cast<uint16_t*>(del_s + BN) + w * 2 * 16 * (BN + 8);  // per wave P^T [16][BN+8]
-  uint16_t* dSt = Pt + 16 * (BN + 8);                                             // per wave dS^T [16][BN+8]
-  const int g = lane >> 4, i = lane & 15;
-  const int64_t bh = blockIdx.y;
-  const int kb = blockIdx.x * BM;
-  const int krow0 = kb + 16 * w;
-  const int64_t base = bh * (int64_t)S * D;
-  const float sl2 = scale * 1.4426950408889634f;
-
-  s16x8 kf[D / 32], vf[D / 32];
-#pragma unroll
-  for (int kk = 0; kk < D / 32; ++kk) {
-    const int row = krow0 + i;
-    kf[kk] = row < S ? *reinterpret_cast<const s16x8*>(K + base + (int64_t)row * D + 32 * kk + 8 * g) : s16x8{};
-    vf[kk] = row < S ? *reinterpret_cast<const s16x8*>(V + base + (int64_t)row * D + 32 * kk + 8 * g) : s16x8{};
-  }
-  f32x4 dk[D / 16], dv[D / 16];
-#pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = dk[dt]; }
-
-  const int qstart = CAUSAL ? kb : 0;
-  for (int i0 = qstart; i0 < S; i0 += BN) {
-    __syncthreads();
-    stage_rows<D>(Qs, Q + base, i0, S);
-    stage_rows<D>(dOs, dO + base, i0, S);
-    if (threadIdx.x < BN) {
-      const int q = i0 + threadIdx.x;
-      lse_s[threadIdx.x] = q < S ? LSE[bh * (int64_t)S + q] : 0.f;
-      del_s[threadIdx.x] = q < S ? DELTA[bh * (int64_t)S + q] : 0.f;
-    }
-    __syncthreads();
-    // S^T = K Q^T, dP^T = V dO^T  (rows: keys 4g+r of this wave; cols: queries 16t+i)
-    f32x4 s[4], dp[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[t] = s[t];
-#pragma unroll
-      for (int kk = 0; kk < D / 32; ++kk) {
-        s[t] = Mfma<T>::run(kf[kk], lds_row8(Qs + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), s[t]);
-        dp[t] = Mfma<T>::run(vf[kk], lds_row8(dOs + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), dp[t]);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int qc = 16 * t + i;
-      const int q = i0 + qc;
-      const float lse2 = lse_s[qc] * 1.4426950408889634f;
-      const float dl = del_s[qc];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = krow0 + 4 * g + r;
-        float p = exp2f(s[t][r] * sl2 - lse2);
-        if (q >= S || key >= S || (CAUSAL && key > q)) p = 0.f;
-        const float ds = p * (dp[t][r] - dl);
-        Pt[(4 * g + r) * (BN + 8) + qc] = to16<T>(p);
-        dSt[(4 * g + r) * (BN + 8) + qc] = to16<T>(ds);
-      }
-    }
-    __syncthreads();
-    // dV += P^T dO ; dK += dS^T Q   (contraction over the BN queries)
-#pragma unroll
-    for (int c = 0; c < BN / 32; ++c) {
-      const s16x8 pa = lds_row8(Pt + i * (BN + 8) + 32 * c + 8 * g);
-      const s16x8 sa = lds_row8(dSt + i * (BN + 8) + 32 * c + 8 * g);
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) {
-        dv[dt] = Mfma<T>::run(pa, lds_col8(dOs, D + 8, 32 * c, 16 * dt, lane), dv[dt]);
-        dk[dt] = Mfma<T>::run(sa, lds_col8(Qs, D + 8, 32 * c, 16 * dt, lane), dk[dt]);
-      }
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int key = krow0 + 4 * g + r;
-    if (key < S) {
-      uint16_t* dkr = dK + base + (int64_t)key * D;
-      uint16_t* dvr = dV + base + (int64_t)key * D;
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) {
-        dkr[16 * dt + i] = to16<T>(dk[dt][r] * scale);
-        dvr[16 * dt + i] = to16<T>(dv[dt][r]);
-      }
-    }
-  }
-}
-
-// ======================================================================== backward: dQ
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256) bwd_dq_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
-                                                     const uint16_t* __restrict__ V, const uint16_t* __restrict__ dO,
-                                                     const float* __restrict__ LSE, const float* __restrict__ DELTA,
-                                                     uint16_t* __restrict__ dQ, int S, float scale) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Ks = smem;                 // [BN keys][D+8]
-  uint16_t* Vs = Ks + BN * LDP<D>;    // [BN][D+8]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint16_t* dSs = Vs + BN * LDP<D> + w * 16 * (BN + 8);  // per wave dS [16][BN+8]
-  const int g = lane >> 4, i = lane & 15;
-  const int64_t bh = blockIdx.y;
-  const int qb = blockIdx.x * BM;
-  const int qrow0 = qb + 16 * w;
-  const int64_t base = bh * (int64_t)S * D;
-  const float sl2 = scale * 1.4426950408889634f;
-
-  s16x8 qf[D / 32], of[D / 32];
-#pragma unroll
-  for (int kk = 0; kk < D / 32; ++kk) {
-    const int row = qrow0 + i;
-    qf[kk] = row < S ? *reinterpret_cast<const s16x8*>(Q + base + (int64_t)row * D + 32 * kk + 8 * g) : s16x8{};
-    of[kk] = row < S ? *reinterpret_cast<const s16x8*>(dO + base + (int64_t)row * D + 32 * kk + 8 * g) : s16x8{};
-  }
-  float lse2[4], dl[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = qrow0 + 4 * g + r;
-    lse2[r] = q < S ? LSE[bh * (int64_t)S + q] * 1.4426950408889634f : 0.f;
-    dl[r] = q < S ? DELTA[bh * (int64_t)S + q] : 0.f;
-  }
-  f32x4 dq[D / 16];
-#pragma unroll
-  for (int dt = 0; dt < D / 16; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int kend = CAUSAL ? min(S, qb + BM) : S;
-  for (int j0 = 0; j0 < kend; j0 += BN) {
-    __syncthreads();
-    stage_rows<D>(Ks, K + base, j0, S);
-    stage_rows<D>(Vs, V + base, j0, S);
-    __syncthreads();
-    f32x4 s[4], dp[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[t] = s[t];
-#pragma unroll
-      for (int kk = 0; kk < D / 32; ++kk) {
-        s[t] = Mfma<T>::run(qf[kk], lds_row8(Ks + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), s[t]);
-        dp[t] = Mfma<T>::run(of[kk], lds_row8(Vs + (16 * t + i) * LDP<D> + 32 * kk + 8 * g), dp[t]);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int key = j0 + 16 * t + i;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = qrow0 + 4 * g + r;
-        float p = exp2f(s[t][r] * sl2 - lse2[r]);
-        if (q >= S || key >= S || (CAUSAL && key > q)) p = 0.f;
-        dSs[(4 * g + r) * (BN + 8) + 16 * t + i] = to16<T>(p * (dp[t][r] - dl[r]));
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < BN / 32; ++c) {
-      const s16x8 sa = lds_row8(dSs + i * (BN + 8) + 32 * c + 8 * g);
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) dq[dt] = Mfma<T>::run(sa, lds_col8(Ks, D + 8, 32 * c, 16 * dt, lane), dq[dt]);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int q = qrow0 + 4 * g + r;
-    if (q < S) {
-      uint16_t* dqr = dQ + base + (int64_t)q * D;
-#pragma unroll
-      for (int dt = 0; dt < D / 16; ++dt) dqr[16 * dt + i] = to16<T>(dq[dt][r] * scale);
-    }
-  }
 }
 
 // ======================================================================== forward v2
@@ -610,7 +263,6 @@ constexpr float LAZY_TH = 8.0f;
 //            one 32-bit hash yields the 16-bit draws of keys 2j and 2j+1 of a query row.
 //            The normaliser l / LSE stays the undropped one; O = (P * Z) V / (1 - p).
 constexpr int EX_BIAS = 1, EX_DROP = 2, EX_QKV = 4;  // EX_QKV: token-major q/k/v (Extra::inh/ild)
-constexpr int EX_DBITS = 8;  // with EX_DROP: the forward stores the keep masks as bits (Extra::dbits)
 struct Extra {
   const float* kbias = nullptr;
   int hdiv = 1;
@@ -624,40 +276,8 @@ struct Extra {
   int64_t ild = 0;
   // optional device int64 [seed, step] mixed into `seed` on the GPU (graph-replayable dropout)
   const int64_t* rng = nullptr;
-  // EX_DROP keep masks stored by the forward, one bit per (query, key) (S % 64 == 0): dbits
-  // [bh][q][S/32] (bit = key % 32; read by the dQ kernel) and dbitsT [bh][k][S/32] (bit = query
-  // % 32; read by the dK/dV kernel), so the backward reads 2 words per lane and tile instead of
-  // re-hashing every (query, key) pair in both of its kernels.  Null: the backward hashes.
-  uint32_t* dbits = nullptr;
-  uint32_t* dbitsT = nullptr;
 };
 
-// Forward side of the stored masks: this lane's keep bits kw[t] of the tile's two 32-key blocks
-// (bit 8g + 4h + e of block t is key j0 + 32t + 8g + 4h + e of query myq).  The two wave halves
-// hold complementary bits, so one permlane32 swap gives every lane its query's full words; the
-// key-major words are the transpose of the wave's 32 x 32 bit matrix of a block, formed by five
-// xor-shuffle butterfly stages (half 0 transposes block 0, half 1 block 1).
-__device__ __forceinline__ void store_drop_bits(const Extra& ex, int64_t bh, int S, int myq, int q32, int j0,
-                                                uint32_t kw0, uint32_t kw1, int lane) {
-  const int h = lane >> 5, c32 = lane & 31;
-  const int nw = S >> 5;
-  const auto a = __builtin_amdgcn_permlane32_swap(kw0, kw0, false, false);
-  const auto b = __builtin_amdgcn_permlane32_swap(kw1, kw1, false, false);
-  const uint32_t full0 = a[0] | a[1], full1 = b[0] | b[1];
-  if (h == 0 && myq < S)
-    *reinterpret_cast<uint2*>(ex.dbits + (bh * S + myq) * (int64_t)nw + (j0 >> 5)) = make_uint2(full0, full1);
-  uint32_t x = h ? full1 : full0;  // row c32 (query q32 + c32) of this half's block
-#pragma unroll
-  for (int j = 16; j >= 1; j >>= 1) {
-    const uint32_t lo = j == 16 ? 0x0000FFFFu : j == 8 ? 0x00FF00FFu : j == 4 ? 0x0F0F0F0Fu : j == 2 ? 0x33333333u
-                                                                                             : 0x55555555u;
-    const uint32_t y = (uint32_t)__shfl_xor((int)x, j, 64);
-    x = (c32 & j) ? ((x & ~lo) | ((y & ~lo) >> j)) : ((x & lo) | ((y & lo) << j));
-  }
-  // now bit i of x = keep of (query q32 + i, key j0 + 32h + c32)
-  const int key = j0 + 32 * h + c32;
-  if (key < S && q32 < S) ex.dbitsT[(bh * S + key) * (int64_t)nw + (q32 >> 5)] = x;
-}
 // compile-time layout switch: the head-major kernels keep constant row strides (immediate load
 // offsets); only EX_QKV instantiations pay for the runtime stride
 template <int D, int EX>
@@ -844,7 +464,6 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 2 : 3)) fwd_v2_kernel(const u
     ps = xhalf_sum(ps);
     l += ps;
     if constexpr (DROP) {  // values 2i, 2i+1 of a lane are keys 2j, 2j+1 of its query row
-      uint32_t kw0 = 0u, kw1 = 0u;  // keep bits of the two 32-key blocks (stored masks)
 #pragma unroll
       for (int i = 0; i < 32; i += 2) {
         const int key = j0 + 32 * (i >> 4) + 8 * ((i & 15) >> 2) + 4 * h + (i & 3);
@@ -852,10 +471,7 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 2 : 3)) fwd_v2_kernel(const u
         const bool k0 = (x & 0xffffu) >= ex.thresh, k1 = (x >> 16) >= ex.thresh;
         if (!k0) sv[i] = 0.f;
         if (!k1) sv[i + 1] = 0.f;
-        const uint32_t bits = ((uint32_t)k0 | ((uint32_t)k1 << 1)) << (8 * ((i & 15) >> 2) + 4 * h + (i & 3));
-        if (i < 16) kw0 |= bits; else kw1 |= bits;
       }
-      if constexpr ((EX & EX_DBITS) != 0) store_drop_bits(ex, bh, S, myq, qb + 32 * w, j0, kw0, kw1, lane);
     }
     // O^T += V^T P^T over the 64 keys (4 steps of 16)
 #pragma unroll
@@ -893,177 +509,6 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 2 : 3)) fwd_v2_kernel(const u
       }
     if (h == 0)
       // a row with every key masked out stores +inf so the backward recomputes P = 0 for it
-      LSE[bh * (int64_t)S + myq] = (m == -INFINITY) ? INFINITY : (m + log2f(l)) * 0.6931471805599453f;
-  }
-}
-
-// ======================================================================== forward v3
-// (opt-in, DSA_FA_FWD=3; measured no faster than v2, which keeps 3 waves per SIMD at D=96)
-// v2's tile math with the key loop software-pipelined inside each wave: the S^T = K Q^T MFMAs of
-// tile j+1 are issued before the softmax and the O^T += V^T P^T MFMAs of tile j, so the matrix
-// pipe works on the next tile while the VALU forms this tile's probabilities (one wave per SIMD
-// no longer idles its matrix pipe through its own softmax; v2 relied on a second wave for that).
-// The K tiles run one stage ahead of the V tiles in LDS: during iteration j the waves read
-// K(j+1) and V(j) and write K(j+2) and V(j+1) into the slots nobody reads in iteration j.
-template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(256, 2) fwd_v3_kernel(const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K,
-                                                        const uint16_t* __restrict__ V, uint16_t* __restrict__ O,
-                                                        float* __restrict__ LSE, int S, float scale, int onh) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int TS = BN2 * LDP<D>;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int h = lane >> 5, c32 = lane & 31;
-  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
-  const int nqb = (S + BM2 - 1) / BM2;
-  const int task = xcd_task(blockIdx.x, gridDim.x);
-  const int64_t bh = task / nqb;
-  const int qb = (CAUSAL ? nqb - 1 - (task - (int)bh * nqb) : task - (int)bh * nqb) * BM2;
-  const int myq = qb + 32 * w + c32;
-  const int64_t ib = bh * (int64_t)S * D;
-  const uint16_t* Qb = Q + ib;
-  auto Kslot = [&](int i) { return smem + i * TS; };
-  auto Vslot = [&](int i) { return smem + (2 + i) * TS; };
-
-  s16x8 qf[D / 16];
-#pragma unroll
-  for (int ks = 0; ks < D / 16; ++ks)
-    qf[ks] = myq < S ? *reinterpret_cast<const s16x8*>(Qb + (int64_t)myq * D + 16 * ks + 8 * h) : s16x8{};
-  f32x16 o[D / 32];
-#pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  const float sl2 = scale * 1.4426950408889634f;
-
-  const int kend = CAUSAL ? min(S, qb + BM2) : S;
-  const int ntiles = (kend + BN2 - 1) / BN2;
-  uint4 kr[D / 32], vr[D / 32];
-  const __amdgpu_buffer_rsrc_t k_rs = head_rsrc(K + ib, S, D), v_rs = head_rsrc(V + ib, S, D);
-  tile_load_buf<D>(kr, k_rs, 0, D);
-  tile_load_buf<D>(vr, v_rs, 0, D);
-  tile_store<D>(Kslot(0), kr);
-  tile_store<D>(Vslot(0), vr);
-  if (ntiles > 1) {
-    tile_load_buf<D>(kr, k_rs, BN2, D);
-    tile_store<D>(Kslot(1), kr);
-  }
-  __syncthreads();
-
-  f32x16 sa[2];
-  // S^T of one tile: the two 32-key halves' MFMA chains interleaved (independent accumulators)
-  auto qk_mfma = [&](const uint16_t* Ks, f32x16 (&acc)[2], int k) {
-    const int t = k & 1, ks = k >> 1;
-    acc[t] = Mfma32<T>::run(lds_row8(Ks + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), qf[ks], acc[t]);
-  };
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sa[t][r] = 0.f;
-#pragma unroll
-  for (int k = 0; k < D / 8; ++k) qk_mfma(Kslot(0), sa, k);
-  __syncthreads();  // every wave has read K(0) before iteration 0 overwrites its slot with K(2)
-
-  // one key tile; NEXT: issue the next tile's S^T MFMAs between this tile's softmax instructions
-  auto tile = [&](int it, auto next_tag) {
-    constexpr bool NEXT = decltype(next_tag)::value;
-    const int j0 = it * BN2;
-    const bool has_next2 = it + 2 < ntiles;
-    if (NEXT) tile_load_buf<D>(vr, v_rs, j0 + BN2, D);
-    if (has_next2) tile_load_buf<D>(kr, k_rs, j0 + 2 * BN2, D);
-    const uint16_t* Vs = Vslot(it & 1);
-    const uint16_t* Kn = Kslot((it + 1) & 1);
-    if ((j0 + BN2 > S) || (CAUSAL && j0 + BN2 - 1 > qb + 32 * w)) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-          if (key >= S || (CAUSAL && key > myq)) sa[t][r] = -INFINITY;
-        }
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sa[t][r]);
-    mx = xhalf_max(mx);
-    const float mt = mx * sl2;
-    if (__any(mt > m + LAZY_TH)) {  // wave-uniform lazy rescale (v2's LAZY)
-      const float mn = fmaxf(m, mt);
-      const float alpha = fast_exp2(m - ((mn == -INFINITY) ? 0.f : mn));
-      l *= alpha;
-      m = mn;
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-    }
-    const float mu = (m == -INFINITY) ? 0.f : m;
-    f32x16 sn[2];
-    if constexpr (NEXT) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sn[t][r] = 0.f;
-    }
-    float pv[32];
-    float ps = 0.f, ps1 = 0.f;
-    // 16 element pairs of exp2 / sums; the next tile's D/8 MFMAs are spread over them
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      if constexpr (NEXT) {
-        if (e < D / 8) qk_mfma(Kn, sn, e);
-      }
-      const int t = e >> 3, r = 2 * (e & 7);
-      pv[16 * t + r] = fast_exp2(fmaf(sa[t][r], sl2, -mu));
-      pv[16 * t + r + 1] = fast_exp2(fmaf(sa[t][r + 1], sl2, -mu));
-      ps += pv[16 * t + r];
-      ps1 += pv[16 * t + r + 1];
-    }
-    if constexpr (NEXT) {
-#pragma unroll
-      for (int k = 16; k < D / 8; ++k) qk_mfma(Kn, sn, k);
-    }
-    ps = xhalf_sum(ps + ps1);
-    l += ps;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const s16x8 pf = __is_same(T, bf16_t) ? pack8(pv, 8 * ks) : pack8_h(pv, 8 * ks);
-      const int row1 = 16 * ks + 4 * (g16 >> 1) + qd;
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) {
-        const uint16_t* a0 = Vs + row1 * LDP<D> + 32 * dt + 16 * (g16 & 1) + 4 * pc;
-        const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 8 * LDP<D>));
-        o[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, pf, o[dt]);
-      }
-    }
-    if (NEXT) tile_store<D>(Vslot((it + 1) & 1), vr);
-    if (has_next2) tile_store<D>(Kslot(it & 1), kr);
-    __syncthreads();
-    if constexpr (NEXT) {
-      sa[0] = sn[0];
-      sa[1] = sn[1];
-    }
-  };
-  for (int it = 0; it + 1 < ntiles; ++it) tile(it, std::true_type{});
-  if (ntiles > 0) tile(ntiles - 1, std::false_type{});
-  if (myq < S) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh);
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        ushort4 v4;
-        v4.x = to16<T>(o[dt][4 * rb + 0] * inv);
-        v4.y = to16<T>(o[dt][4 * rb + 1] * inv);
-        v4.z = to16<T>(o[dt][4 * rb + 2] * inv);
-        v4.w = to16<T>(o[dt][4 * rb + 3] * inv);
-        *reinterpret_cast<ushort4*>(orow + 32 * dt + 8 * rb + 4 * h) = v4;
-      }
-    if (h == 0)
       LSE[bh * (int64_t)S + myq] = (m == -INFINITY) ? INFINITY : (m + log2f(l)) * 0.6931471805599453f;
   }
 }
@@ -1268,16 +713,6 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
         }
       }
       if constexpr (DROP) {  // dV from the dropped P; dP = dP_dropped * Z / (1 - p)
-       if constexpr ((EX & EX_DBITS) != 0) {  // the forward's key-major keep bits: this key's word over 32 queries
-        const uint32_t word = mykey < S ? ex.dbitsT[(bh * S + mykey) * (int64_t)(S >> 5) + ((i0 + 32 * t) >> 5)] : 0u;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qi = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
-          const float zr = ((word >> (8 * (r >> 2) + 4 * h + (r & 3))) & 1u) ? ex.rscale : 0.f;
-          dsv[r] = pv[r] * fmaf(pacc[r], zr, -del_s[qi]);
-          pv[r] *= zr;
-        }
-       } else {
         // lanes l and l^1 hold keys 2j and 2j+1 of the same 16 queries and need the same 16
         // pair draws: each computes 8 and takes the other 8 from its neighbour (DPP quad_perm)
         uint32_t own[8], nbr[8];
@@ -1297,7 +732,6 @@ __device__ __forceinline__ void dkdv_v2_body(int vblock, int nblock, const uint1
           dsv[r] = pv[r] * fmaf(pacc[r], zr, -del_s[qi]);
           pv[r] *= zr;
         }
-       }
       } else if constexpr (INIT) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dsv[r] = pv[r] * pacc[r];
@@ -1534,14 +968,6 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
         }
       }
       if constexpr (DROP) {  // values r, r+1 are keys 2j, 2j+1 of this lane's query
-        if constexpr ((EX & EX_DBITS) != 0) {  // the forward's query-major keep bits of this 32-key block
-          const uint32_t word = myq < S ? ex.dbits[(bh * S + myq) * (int64_t)(S >> 5) + ((j0 + 32 * t) >> 5)] : 0u;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float z = ((word >> (8 * (r >> 2) + 4 * h + (r & 3))) & 1u) ? ex.rscale : 0.f;
-            dsv[r] = dsv[r] * fmaf(pacc[r], z, -dl);
-          }
-        } else {
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const int key = j0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
@@ -1551,7 +977,6 @@ __device__ __forceinline__ void dq_v2_body(int vblock, int nblock, const uint16_
             dsv[r] = dsv[r] * fmaf(pacc[r], z0, -dl);
             dsv[r + 1] = dsv[r + 1] * fmaf(pacc[r + 1], z1, -dl);
           }
-        }
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dsv[r] = dsv[r] * (pacc[r] - dl);
@@ -1635,19 +1060,6 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v2_kernel(
   dq_v2_body<T, D, CAUSAL, EX, BUF>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh, ex);
 }
 
-template <typename T, int D, bool CAUSAL, int EX = 0>
-__global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_both_v2_kernel(
-    int ndkdv, const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
-    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    uint16_t* __restrict__ dQ, uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh,
-    Extra ex = Extra()) {
-  if ((int)blockIdx.x < ndkdv)
-    dkdv_v2_body<T, D, CAUSAL, EX>(blockIdx.x, ndkdv, Q, K, V, dO, LSE, DELTA, dK, dV, S, scale, onh, ex);
-  else
-    dq_v2_body<T, D, CAUSAL, EX>(blockIdx.x - ndkdv, gridDim.x - ndkdv, Q, K, V, dO, LSE, DELTA, dQ, S, scale, onh,
-                                 ex);
-}
-
 template <int D> constexpr int dkdv_v2_lds() { return 2 * 2 * BN2 * LDP<D> * 2 + 2 * 2 * BN2 * 4; }
 // + K [BM2][D+8] and one tile's dS [BN2][BM2+8] for the fused short-sequence backward
 template <int D> constexpr int bwd_short_lds() { return dkdv_v2_lds<D>() + BM2 * LDP<D> * 2 + BN2 * (BM2 + 8) * 2 + BM2 * 4; }
@@ -1666,9 +1078,6 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 1 : 2)) bwd_short_kernel(
 
 template <int D> constexpr int fwd_v2_lds() { return 2 * 2 * BN2 * LDP<D> * 2; }
 
-template <int D> constexpr int fwd_lds() { return (2 * BN * LDP<D> + 4 * 16 * (BN + 8)) * 2; }
-template <int D> constexpr int dkdv_lds() { return (2 * BN * LDP<D>) * 2 + 2 * BN * 4 + 4 * 2 * 16 * (BN + 8) * 2; }
-template <int D> constexpr int dq_lds() { return (2 * BN * LDP<D> + 4 * 16 * (BN + 8)) * 2; }
 
 // ======================================================================== block-sparse (LUT-driven)
 // Flash attention restricted to the active blocks of a block-sparse layout (reference:
@@ -2362,135 +1771,44 @@ bool flash_supported(int D) { return D == 64 || D == 96 || D == 128; }
 
 void launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                       bool causal, float scale, int dt, hipStream_t s, int onh) {
-  static const bool v1 = getenv("DSA_FLASH_FWD_V1") != nullptr;
-  static const bool eager = getenv("DSA_FLASH_EAGER_RESCALE") != nullptr;
-  static const bool bufload = !(getenv("DSA_FA_BUFLOAD") && getenv("DSA_FA_BUFLOAD")[0] == '0');
   // K / V tiles are addressed per head with 32-bit buffer offsets
   if ((int64_t)S * D * 2 >= (1LL << 31))
     throw std::runtime_error("flash fwd: S * head dim too large for 32-bit buffer offsets");
-  // DSA_FA_FWD=3: the software-pipelined v3 forward (opt-in: 0.357 vs 0.339 ms at B4 H64 S2048 D96
-  // causal, equal at D=64/128 -- it needs 2 waves/SIMD where v2 runs 3, profiles/r5c_notes.md)
-  static const int fwdv = getenv("DSA_FA_FWD") ? atoi(getenv("DSA_FA_FWD")) : 2;
-  // DSA_FA_LAYOUT=0: padded V rows in the forward and the padded K image in dQ (round 4), for A/B
-  // against the transposed-read layouts (unpadded V at D = 96, swizzled dual-use K image)
-  static const bool old_layout = getenv("DSA_FA_LAYOUT") && getenv("DSA_FA_LAYOUT")[0] == '0';
-  if (!v1 || onh) {
-    dim3 grid2((S + fa::BM2 - 1) / fa::BM2, BH);
-    FA_DISPATCH(dt, D, causal,
-      if (fwdv == 3 && !eager && bufload)
-        hipLaunchKernelGGL((fa::fwd_v3_kernel<T, DD, CC>), dim3(grid2.x * grid2.y), dim3(256),
-                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                           (uint16_t*)o, lse, S, scale, onh);
-      else if (eager)
-        hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, false>), dim3(grid2.x * grid2.y), dim3(256),
-                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                           (uint16_t*)o, lse, S, scale, onh);
-      else if (bufload && !old_layout)
-        hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true>), dim3(grid2.x * grid2.y), dim3(256),
-                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                           (uint16_t*)o, lse, S, scale, onh);
-      else if (bufload)  // DSA_FA_LAYOUT=0: the round-4 LDS layout (A/B)
-        hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true, 0, true, false>), dim3(grid2.x * grid2.y), dim3(256),
-                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                           (uint16_t*)o, lse, S, scale, onh);
-      else  // DSA_FA_BUFLOAD=0: pointer-form K / V tile loads (A/B only)
-        hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true, 0, false>), dim3(grid2.x * grid2.y), dim3(256),
-                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                           (uint16_t*)o, lse, S, scale, onh));
-    return;
-  }
-  dim3 grid((S + fa::BM - 1) / fa::BM, BH);
+  // v2: lazy rescale, buffer-resource tile loads, transposed-read V layout.  Measured and removed
+  // (round 6): a software-pipelined v3 (0.357 vs 0.339 ms at B4 H64 S2048 D96 causal: it needs 2
+  // waves/SIMD where v2 runs 3, profiles/r5c_notes.md), the round-1 64-row kernel, eager rescale,
+  // pointer-form loads and the round-4 padded layouts.
+  const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
   FA_DISPATCH(dt, D, causal,
-    hipLaunchKernelGGL((fa::fwd_kernel<T, DD, CC>), grid, dim3(256), fa::fwd_lds<DD>(), s, (const uint16_t*)q,
-                       (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale));
+    hipLaunchKernelGGL((fa::fwd_v2_kernel<T, DD, CC, true>), dim3(grid), dim3(256), fa::fwd_v2_lds<DD>(), s,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, S, scale, onh));
 }
 
+// dQ (+ Delta) first, then dK/dV reading that Delta: two launches, no separate Delta pass.  The
+// row constants enter the MFMAs as initial accumulators (v3).  Measured and removed (round 6):
+// the round-1 kernels, one merged dK/dV + dQ launch (neutral, r2v) and the v2 bodies behind a
+// Delta pass (slower, r4-r5).
 void launch_flash_bwd(const void* dout, const void* q, const void* k, const void* v, const void* o, const float* lse,
                       float* delta, void* dq, void* dk, void* dv, int BH, int S, int D, bool causal, float scale,
                       int dt, hipStream_t s, int onh) {
-  const int64_t rows = (int64_t)BH * S;
-  static const bool v1_env = getenv("DSA_FLASH_BWD_V1") != nullptr;
-  // DSA_FLASH_BWD_MERGE=1: dK/dV and dQ workgroups in one launch (measured neutral, r2v)
-  static const bool merge = getenv("DSA_FLASH_BWD_MERGE") && getenv("DSA_FLASH_BWD_MERGE")[0] == '1';
-  const bool v1 = v1_env && onh == 0;  // the v1 kernels read dO head-major only
-  static const bool bufload = !(getenv("DSA_FA_BUFLOAD") && getenv("DSA_FA_BUFLOAD")[0] == '0');
-  static const int dkdv = getenv("DSA_FA_DKDV") ? atoi(getenv("DSA_FA_DKDV")) : 3;
   // the buffer resources of the dK/dV tile loads address one head's rows with 32-bit offsets
   if ((int64_t)S * (onh ? onh * D : D) * 2 >= (1LL << 31))
     throw std::runtime_error("flash bwd: S * row stride too large for 32-bit buffer offsets");
-  static const bool fdelta = !(getenv("DSA_FA_FUSED_DELTA") && getenv("DSA_FA_FUSED_DELTA")[0] == '0');
-  if (!v1 && !merge && bufload && fdelta && (dkdv == 3 || dkdv == 31)) {
-    // dQ (+ Delta) first, then dK/dV reading that Delta: two launches, no Delta pass
-    const unsigned g = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
-    static const bool old_layout = getenv("DSA_FA_LAYOUT") && getenv("DSA_FA_LAYOUT")[0] == '0';
-    FA_DISPATCH(dt, D, causal,
-      if (old_layout)
-        hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC, false>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
-                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
-                           (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
-      else
-        hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
-                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
-                           (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
-      // D = 128 at two waves per SIMD spills ~160 VGPRs to scratch (hipcc resource usage): one
-      // wave per SIMD keeps the whole working set in VGPR + AGPR (4.7x -> see profiles/r4b_*)
-      if (dkdv == 3 && DD < 128)
-        hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 2>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
-                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
-                           delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh);
-      else
-        hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 1>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
-                           (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
-                           delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh));
-    return;
-  }
+  const unsigned g = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
   FA_DISPATCH(dt, D, causal,
-    hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
-                       (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
-    if (!v1 && merge) {
-      const int g = (S + fa::BM2 - 1) / fa::BM2 * BH;
-      hipLaunchKernelGGL((fa::bwd_both_v2_kernel<T, DD, CC>), dim3(2 * g), dim3(256), fa::dkdv_v2_lds<DD>(), s, g,
+    hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
+                       (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
+                       (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
+    // D = 128 at two waves per SIMD spills ~160 VGPRs to scratch (hipcc resource usage): one
+    // wave per SIMD keeps the whole working set in VGPR + AGPR (4.7x -> see profiles/r4b_*)
+    if constexpr (DD < 128)
+      hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 2>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
-                         delta, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, fa::Extra());
-    } else if (!v1) {
-      // DSA_FA_DKDV: 3 (default) initial-accumulator row constants, 31 the same at one wave per
-      // SIMD, 2 the v2 body; DSA_FA_BUFLOAD=0: pointer-form Q / dO tile loads (A/B only)
-      if (dkdv == 3 && bufload && DD < 128)
-        hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 2>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
-                           dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
-                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
-                           scale, onh);
-      else if ((dkdv == 31 || dkdv == 3) && bufload)
-        hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 1>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
-                           dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
-                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
-                           scale, onh);
-      else if (bufload)
-        hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC, 0, true>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
-                           dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
-                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
-                           scale, onh);
-      else
-        hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, CC, 0, false>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
-                           dim3(256), fa::dkdv_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
-                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S,
-                           scale, onh);
-      if (bufload)
-        hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH), dim3(256),
-                           fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                           (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale, onh);
-      else
-        hipLaunchKernelGGL((fa::bwd_dq_v2_kernel<T, DD, CC, 0, false>), dim3((S + fa::BM2 - 1) / fa::BM2 * BH),
-                           dim3(256), fa::fwd_v2_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k,
-                           (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale, onh);
-    } else {
-      hipLaunchKernelGGL((fa::bwd_dkdv_kernel<T, DD, CC>), dim3((S + fa::BM - 1) / fa::BM, BH), dim3(256),
-                         fa::dkdv_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                         (const uint16_t*)dout, lse, delta, (uint16_t*)dk, (uint16_t*)dv, S, scale);
-      hipLaunchKernelGGL((fa::bwd_dq_kernel<T, DD, CC>), dim3((S + fa::BM - 1) / fa::BM, BH), dim3(256),
-                         fa::dq_lds<DD>(), s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v,
-                         (const uint16_t*)dout, lse, delta, (uint16_t*)dq, S, scale);
-    });
+                         delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh);
+    else
+      hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 1>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
+                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
+                         delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh));
 }
 
 // Encoder attention (non-causal) with a per-key additive bias and/or in-kernel dropout.
@@ -2506,12 +1824,6 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     };                                                                                               \
     auto _q = [&](auto tt, auto dd, auto ee) {                                                       \
       constexpr int E0 = decltype(ee)::value;                                                        \
-      if constexpr ((E0 & fa::EX_DROP) != 0) {                                                       \
-        if (inh > 0 && ex.dbits) {                                                                   \
-          _go(tt, dd, std::integral_constant<int, E0 | fa::EX_QKV | fa::EX_DBITS>{});                 \
-          return;                                                                                    \
-        }                                                                                            \
-      }                                                                                              \
       if (inh > 0) _go(tt, dd, std::integral_constant<int, E0 | fa::EX_QKV>{});                      \
       else _go(tt, dd, ee);                                                                          \
     };                                                                                               \
@@ -2529,13 +1841,8 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
   } while (0)
 
 static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t seed, int inh = 0,
-                            int64_t ild = 0, const int64_t* rng = nullptr, uint32_t* dbits = nullptr,
-                            int64_t nbits = 0) {
+                            int64_t ild = 0, const int64_t* rng = nullptr) {
   fa::Extra ex;
-  if (dbits && pdrop > 0.f) {
-    ex.dbits = dbits;
-    ex.dbitsT = dbits + nbits;
-  }
   ex.rng = rng;
   ex.inh = inh;
   ex.ild = ild;
@@ -2547,13 +1854,10 @@ static fa::Extra make_extra(const float* kbias, int hdiv, float pdrop, uint64_t 
   return ex;
 }
 
-bool flash_drop_bits_ok(int S) { return S % 64 == 0; }
-
 void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, float* lse, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh, int64_t ild, const int64_t* rng, uint32_t* dbits) {
-  if (dbits && !flash_drop_bits_ok(S)) throw std::runtime_error("flash fwd: stored dropout masks need S % 64 == 0");
-  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng, dbits, (int64_t)BH * S * (S / 32));
+                         int onh, int inh, int64_t ild, const int64_t* rng) {
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng);
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
   const int kb_lds = kbias ? 4 * S : 0;  // the LDS-staged key-bias row
   if (kb_lds && fa::fwd_v2_lds<128>() + kb_lds > 160 * 1024)
@@ -2569,41 +1873,27 @@ void launch_flash_fwd_ex(const void* q, const void* k, const void* v, void* o, f
 void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const void* v, const void* o,
                          const float* lse, float* delta, void* dq, void* dk, void* dv, int BH, int S, int D,
                          float scale, const float* kbias, int hdiv, float pdrop, uint64_t seed, int dt, hipStream_t s,
-                         int onh, int inh, int64_t ild, const int64_t* rng, uint32_t* dbits) {
-  if (dbits && !flash_drop_bits_ok(S)) throw std::runtime_error("flash bwd: stored dropout masks need S % 64 == 0");
-  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng, dbits, (int64_t)BH * S * (S / 32));
+                         int onh, int inh, int64_t ild, const int64_t* rng) {
+  const fa::Extra ex = make_extra(kbias, hdiv, pdrop, seed, inh, ild, rng);
   const int64_t rows = (int64_t)BH * S;
   const int kb_lds = kbias ? 4 * S : 0;  // the dQ kernel's LDS-staged key-bias row
   if (kb_lds && fa::fwd_v2_lds<128>() + kb_lds > 160 * 1024)
     throw std::runtime_error("flash bwd: key-bias row too long for LDS staging");
   const unsigned grid = (unsigned)((S + fa::BM2 - 1) / fa::BM2 * BH);
-  // DSA_FLASH_BWD_MERGE=1: dK/dV and dQ workgroups in one launch (measured neutral, r2v)
-  static const bool merge = getenv("DSA_FLASH_BWD_MERGE") && getenv("DSA_FLASH_BWD_MERGE")[0] == '1';
-  // S <= 128: one workgroup per head does dK, dV and dQ (DSA_FLASH_BWD_SHORT=0: two kernels)
-  static const bool short_ok = !(getenv("DSA_FLASH_BWD_SHORT") && getenv("DSA_FLASH_BWD_SHORT")[0] == '0');
-  const bool use_short = short_ok && S <= fa::BM2;
+  // S <= 128: one workgroup per head does dK, dV and dQ
+  const bool use_short = S <= fa::BM2;
   // the buffer resources of the dK/dV tile loads address one head's rows with 32-bit offsets
   if ((int64_t)S * std::max<int64_t>(ild > 0 ? ild : D, onh ? (int64_t)onh * D : D) * 2 >= (1LL << 31))
     throw std::runtime_error("flash bwd: S * row stride too large for 32-bit buffer offsets");
-  // DSA_FA_SHORT_DELTA=1: the short backward forms Delta itself instead of reading a separate pass
-  // (opt-in: BERT-Large seq 128 measured 2,530 vs 2,551 samples/s with the separate pass, same box,
-  // profiles/r5f_bert_short_delta_ab2.jsonl -- the per-workgroup prologue serialises what the
-  // Delta kernel spreads over the whole chip)
-  static const bool short_delta = getenv("DSA_FA_SHORT_DELTA") && getenv("DSA_FA_SHORT_DELTA")[0] == '1';
+  // Delta from its own pass: the short backward forming it per workgroup measured slower (BERT-Large
+  // seq 128: 2,530 vs 2,551 samples/s, profiles/r5f_bert_short_delta_ab2.jsonl), removed in round 6
   FA_EX_DISPATCH(dt, D, kbias, pdrop,
-    if (!(use_short && short_delta))
-      hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
-                         (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
+    hipLaunchKernelGGL((fa::delta_kernel<T, DD>), dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s,
+                       (const uint16_t*)dout, (const uint16_t*)o, delta, rows, S, onh);
     if (use_short)
       hipLaunchKernelGGL((fa::bwd_short_kernel<T, DD, EE>), dim3(grid), dim3(256), fa::bwd_short_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex,
-                         short_delta ? (const uint16_t*)o : nullptr);
-    else if (merge)
-      hipLaunchKernelGGL((fa::bwd_both_v2_kernel<T, DD, false, EE>), dim3(2 * grid), dim3(256),
-                         std::max(fa::dkdv_v2_lds<DD>(), fa::fwd_v2_lds<DD>() + kb_lds), s, (int)grid, (const uint16_t*)q, (const uint16_t*)k,
-                         (const uint16_t*)v, (const uint16_t*)dout, lse, delta, (uint16_t*)dq, (uint16_t*)dk,
-                         (uint16_t*)dv, S, scale, onh, ex);
+                         (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh, ex);
     else {
       hipLaunchKernelGGL((fa::bwd_dkdv_v2_kernel<T, DD, false, EE>), dim3(grid), dim3(256), fa::dkdv_v2_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
@@ -2614,13 +1904,8 @@ void launch_flash_bwd_ex(const void* dout, const void* q, const void* k, const v
     });
 }
 
-// default: register prefetch + double-buffered LDS (2 workgroups / CU, measured faster);
-// DSA_SPARSE_FLASH_RP=0: one LDS stage, 3 workgroups / CU (the short per-row tile lists of
-// block-sparse layouts leave little to pipeline inside one workgroup)
-static bool sparse_rp() {
-  static const bool rp = !(getenv("DSA_SPARSE_FLASH_RP") && getenv("DSA_SPARSE_FLASH_RP")[0] == '0');
-  return rp;
-}
+// (sparse kernels: register prefetch + double-buffered LDS, 2 workgroups / CU -- measured faster
+// than one LDS stage at 3 workgroups / CU, which was removed in round 6)
 
 // kbias / ebias (SExtra): null when absent; either one selects the SX = 1 kernels
 void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, const int* rowptr,
@@ -2629,7 +1914,6 @@ void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* 
                              const void* ebias, int64_t ez, int64_t eh, int64_t er) {
   const int4* cols = reinterpret_cast<const int4*>(cols_);
   const unsigned grid = (unsigned)(BH * (S / fa::STILE));
-  const bool rp = sparse_rp();
   fa::SExtra sx;
   sx.kbias = kbias;
   sx.ebias = (const uint16_t*)ebias;
@@ -2643,12 +1927,8 @@ void launch_sparse_flash_fwd(const void* q, const void* k, const void* v, void* 
       hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, true, 1>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
                          masks, S, scale, onh, H, Hl, shift, sx);
-    else if (rp)
-      hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
-                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
-                         masks, S, scale, onh, H, Hl, shift, fa::SExtra());
     else
-      hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, false>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(false), s,
+      hipLaunchKernelGGL((fa::sfwd_kernel<T, DD, CC, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, rowptr, cols,
                          masks, S, scale, onh, H, Hl, shift, fa::SExtra()));
 }
@@ -2667,7 +1947,6 @@ void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, con
   const int4* kgroups = reinterpret_cast<const int4*>(kgroups_);
   const unsigned grid = (unsigned)(BH * (S / fa::STILE));
   const unsigned tgrid = (unsigned)(BH * ntask);
-  const bool rp = sparse_rp();
   const int4* tk = reinterpret_cast<const int4*>(tasks);
   fa::SExtra sx;
   sx.kbias = kbias;
@@ -2690,21 +1969,12 @@ void launch_sparse_flash_bwd(const void* dout, const void* q, const void* k, con
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                          (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, kgroups, ws, nslot, S, scale, onh, H, Hl,
                          shift, sx);
-    } else if (rp) {
+    } else {
       hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, true, 0, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(true), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                          (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, fa::SExtra(),
                          (const uint16_t*)o);
       hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, true>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(true), s,
-                         (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
-                         (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, kgroups, ws, nslot, S, scale, onh, H, Hl,
-                         shift, fa::SExtra());
-    } else {
-      hipLaunchKernelGGL((fa::sdq_kernel<T, DD, CC, false, 0, true>), dim3(grid), dim3(128), fa::sfwd_lds<DD>(false),
-                         s, (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
-                         delta, (uint16_t*)dq, rowptr, cols, masks, S, scale, onh, H, Hl, shift, fa::SExtra(),
-                         (const uint16_t*)o);
-      hipLaunchKernelGGL((fa::sdkdv_kernel<T, DD, CC, false>), dim3(tgrid), dim3(128), fa::sdkdv_lds<DD>(false), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse, delta,
                          (uint16_t*)dk, (uint16_t*)dv, rows, masks_t, tk, ntask, kgroups, ws, nslot, S, scale, onh, H, Hl,
                          shift, fa::SExtra());

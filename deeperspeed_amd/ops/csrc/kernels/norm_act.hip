@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(LN_THREADS) ln_bwd_kernel(const T* __restrict_
   };
   if ((int64_t)blockIdx.x < rows) fetch(blockIdx.x);
   for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
-    if (!pf && row != blockIdx.x) fetch(row);  // DSA_LN_BWD_PREFETCH=0: load the row just in time (A/B)
+    if (!pf && row != blockIdx.x) fetch(row);  // pf = 0: load the row just in time (A/B)
     const float mu = nmu, rs = nrs;
     float xh[NV][VN], g[NV][VN], rr[NV][VN];
 #pragma unroll
@@ -563,11 +563,8 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict_
 int ln_max_hidden(int dt) { return LN_THREADS * LN_MAXV * (dt == kF32 ? 4 : 8); }
 
 // rows of at most 64 lanes x 2 vectors (H <= 1024 for 16-bit, 512 for fp32) take the
-// wave-per-row kernels; DSA_LN_WAVE=0 keeps the block-per-row ones
-static bool ln_wave(int H, int dt) {
-  static const bool on = !(getenv("DSA_LN_WAVE") && getenv("DSA_LN_WAVE")[0] == '0');
-  return on && H <= 64 * 2 * (dt == kF32 ? 4 : 8);
-}
+// wave-per-row kernels, wider rows the block-per-row ones
+static bool ln_wave(int H, int dt) { return H <= 64 * 2 * (dt == kF32 ? 4 : 8); }
 
 void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_out, const void* gamma,
                    const void* beta, void* y, float* mean, float* rstd, int64_t rows, int H, float eps, int dt,
@@ -589,14 +586,6 @@ void launch_ln_fwd(const void* x, const void* res, const void* bias, void* sum_o
 
 int ln_bwd_grid(int64_t rows) { return (int)(rows < 512 ? rows : 512); }
 
-// Row prefetch in the block-per-row backward: +5-9 % at hidden 2048 (one vector per thread), but
-// -15 % at 6144 (three vectors per thread: the doubled row registers cost more than the latency
-// they hide), so only the one-vector instances take it (profiles/r4g_notes.md)
-static int ln_bwd_prefetch() {
-  const char* v = getenv("DSA_LN_BWD_PREFETCH");
-  return (v && v[0] == '0') ? 0 : 1;
-}
-
 // partial workspace: 2 * ln_bwd_grid(rows) * H floats
 void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float* mean, const float* rstd,
                    const void* dres, void* dx, void* dgamma, void* dbeta, float* partial, int64_t rows, int H,
@@ -614,7 +603,10 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
     else
       DSA_DISPATCH_NV(nv, NV, hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(grid), dim3(LN_THREADS), 0, s,
                          (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx,
-                         partial, rows, H, (NV == 1) ? ln_bwd_prefetch() : 0));
+                         // row prefetch: +5-9 % at hidden 2048 (one vector per thread), -15 % at 6144
+                         // (three: the doubled row registers cost more than the latency they hide),
+                         // profiles/r4g_notes.md
+                         partial, rows, H, (NV == 1) ? 1 : 0));
     hipLaunchKernelGGL((colsum_kernel<T>), dim3((H + 15) / 16, dbeta ? 2 : 1), dim3(256), 0, s, partial, grid, H,
                        (T*)dgamma, accum, (int64_t)grid * H, (T*)dbeta));
 }
@@ -635,23 +627,15 @@ void launch_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, i
   const int64_t n = rows * C;
   if (n <= 0) return;
   const int vn = dt == kF32 ? 4 : 8;
-  // vectors per thread and pass (DSA_GELU_FWD_U=1|2|4); the GeLU math is cheap enough since the
-  // sigmoid form that the kernel is bound by HBM, where more loads in flight pay
-  static const int U = [] {
-    const char* e = getenv("DSA_GELU_FWD_U");
-    const int u = e ? atoi(e) : 2;
-    return u == 1 || u == 4 ? u : 2;
-  }();
+  // two vectors per thread and pass: the GeLU math is cheap enough since the sigmoid form that
+  // the kernel is bound by HBM, where more loads in flight pay (1 and 4 measured slower, r5h)
+  constexpr int U = 2;
   int64_t g = (n / vn + 256 * U - 1) / (256 * U);
   if (g > 16384) g = 16384;
   if (g < 1) g = 1;
   DSA_DISPATCH_T(dt, T,
-    if (U == 1) hipLaunchKernelGGL((bias_gelu_fwd_kernel<T, 1>), dim3((unsigned)g), dim3(256), 0, s,
-                                   (const T*)x, (const T*)b, (T*)y, n, C, approx);
-    else if (U == 2) hipLaunchKernelGGL((bias_gelu_fwd_kernel<T, 2>), dim3((unsigned)g), dim3(256), 0, s,
-                                        (const T*)x, (const T*)b, (T*)y, n, C, approx);
-    else hipLaunchKernelGGL((bias_gelu_fwd_kernel<T, 4>), dim3((unsigned)g), dim3(256), 0, s,
-                            (const T*)x, (const T*)b, (T*)y, n, C, approx));
+    hipLaunchKernelGGL((bias_gelu_fwd_kernel<T, U>), dim3((unsigned)g), dim3(256), 0, s,
+                       (const T*)x, (const T*)b, (T*)y, n, C, approx));
 }
 
 int bias_gelu_row_chunks(int64_t rows, int C, int dt) {

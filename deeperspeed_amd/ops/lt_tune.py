@@ -11,18 +11,17 @@ At run time (`ops/csrc/gemm_lt.cpp`):
 - the table's solutions (by hipBLASLt solution name; indices differ between processes) join the
   heuristic candidates that the wrapper times on the first call of each problem (a stale name is
   checked with matmulIsAlgoSupported and can only lose the timing);
-- `ops/linear.py` routes a linear's forward, input gradient and weight gradient through the
-  wrapper for the problems the table covers, and picks per shape between the untransposed
-  weight gradient (NT) and the transposed-operand one (TN + two HIP transposes) from the measured
-  rates plus the transposes' HBM traffic.
+- `ops/linear.py` routes a linear's forward through the wrapper for the problems where the
+  table's best solution beats the heuristic's by MIN_GAIN.  The table's input- and weight-gradient
+  records (untransposed NN / NT, transposed TN) were measured too; routing them lost in the step
+  (20B N=1 -0.8 %, 1.3B ZeRO-2 -0.2 %, profiles/r4u_notes.md, r4m_notes.md), so those GEMMs keep
+  torch's hipBLASLt call on transposed operands (ops/linear.py).
 
 Reference counterpart: the reference calls cuBLAS with the default heuristic
 (`csrc/includes/cublas_wrappers.h`, `cublasGemmEx(..., CUBLAS_GEMM_DEFAULT_TENSOR_OP)`); the
 per-shape algorithm choice is an MI355X addition.
 
-DSA_LT=0 disables every route; DSA_LT_FWD=0 the forward route (on by default), DSA_LT_WGRAD=1 /
-DSA_LT_NN=1 / DSA_LT_NT=1 enable the weight-gradient / untransposed routes (off: they measured
-slower in the step); DSA_LT_TABLE names another table file.
+DSA_LT=0 disables the route; DSA_LT_TABLE names another table file.
 """
 
 from __future__ import annotations
@@ -33,20 +32,10 @@ import threading
 from typing import Dict, Optional, Tuple
 
 ENABLED = os.environ.get("DSA_LT", "1") != "0"
-# forward GEMMs with a measured solution >= MIN_GAIN over the heuristic: on by default (BERT-Large
-# QKV projection +22 %, the seq-128 step +1.2 %, profiles/r4u_notes.md)
-FWD = ENABLED and os.environ.get("DSA_LT_FWD", "1") != "0"
-DGRAD = ENABLED and os.environ.get("DSA_LT_DGRAD", "1") != "0"
-# weight gradients through the measured TN solutions: opt-in -- isolated gains of 5-50 % did not
-# survive in the step (20B N=1 -0.8 %, 1.3B ZeRO-2 -0.2 %, same boxes, profiles/r4u_notes.md)
-WGRAD = ENABLED and os.environ.get("DSA_LT_WGRAD", "0") == "1"
-# the untransposed layouts (NN input gradient, NT weight gradient): opt-in, slower on torch's build
-NN = os.environ.get("DSA_LT_NN", "0") == "1"
-NT = os.environ.get("DSA_LT_NT", "0") == "1"
+# forward GEMMs with a measured solution >= MIN_GAIN over the heuristic (BERT-Large QKV projection
+# +22 %, the seq-128 step +1.2 %, profiles/r4u_notes.md)
+FWD = ENABLED
 TABLE_PATH = os.environ.get("DSA_LT_TABLE", os.path.join(os.path.dirname(__file__), "lt_table.json"))
-# effective HBM rate of the HIP transpose kernel (read + write), bytes/s: profiles/aux transposes
-# stream at 4-4.5 TB/s on MI355X
-TRANSPOSE_BPS = 4.2e12
 
 EPI_DEFAULT, EPI_BIAS = 1, 4
 
@@ -116,7 +105,7 @@ def entry(kind: str, M: int, N: int, K: int, bias: bool = False) -> Optional[dic
 
 # a measured solution is routed only when it beats the heuristic's first choice by this factor
 # (the sweep times each solution over few launches; smaller gains are within its noise)
-MIN_GAIN = float(os.environ.get("DSA_LT_MIN_GAIN", "1.05"))
+MIN_GAIN = 1.05
 
 
 def gain(kind: str, M: int, N: int, K: int, bias: bool = False) -> float:
@@ -129,43 +118,3 @@ def gain(kind: str, M: int, N: int, K: int, bias: bool = False) -> float:
 
 def use_fwd(M: int, N: int, K: int, bias: bool) -> bool:
     return FWD and gain("fwd", M, N, K, bias) >= MIN_GAIN
-
-
-def use_dgrad(M: int, N: int, K: int) -> bool:
-    """Untransposed (NN) input gradient instead of W^T + TN: only on request (DSA_LT_NN=1) -- on
-    torch's hipBLASLt the NN solutions are slower than the transposed formulation at every
-    GPT-NeoX shape measured (profiles/r4m_notes.md)."""
-    return DGRAD and NN and entry("dgrad", M, N, K) is not None
-
-
-def use_wgrad_t(M: int, N: int, K: int) -> bool:
-    """Transposed-operand weight gradient (TN) through the wrapper's measured solution."""
-    return WGRAD and gain("wgradT", M, N, K) >= MIN_GAIN
-
-
-_nt_cache: Dict[Tuple[int, int, int, int], bool] = {}
-
-
-def wgrad_nt(M: int, N: int, K: int, elem_size: int = 2) -> bool:
-    """True when the weight gradient of an [N, K] linear over M tokens is cheaper as one NT GEMM
-    on the token-major operands than as transposes of both operands plus the TN GEMM, by the
-    table's measured rates."""
-    if not (WGRAD and NT):
-        return False
-    ck = (M, N, K, elem_size)
-    r = _nt_cache.get(ck)
-    if r is None:
-        nt, tn = entry("wgrad", M, N, K), entry("wgradT", M, N, K)
-        if nt is None:
-            r = False
-        else:
-            flops = 2.0 * M * N * K
-            cost_nt = flops / (nt["tflops"] * 1e12)
-            if tn is None:
-                r = True  # no TN record: the NT kernel was measured, the transposes were not needed
-            else:
-                t_bytes = 2.0 * elem_size * M * (N + K)  # read + write of dY and X
-                cost_tn = flops / (tn["tflops"] * 1e12) + t_bytes / TRANSPOSE_BPS
-                r = cost_nt < cost_tn
-        _nt_cache[ck] = r
-    return r

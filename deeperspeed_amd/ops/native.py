@@ -9,7 +9,6 @@ implementation of the same math; that path is never taken for tensors on the MI3
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -261,8 +260,8 @@ def _gelu_bwd(dy, x, bias, approx, offer_t, dx_out=None, db_acc=None):
     return hip_ops().bias_gelu_bwd(dy, x, bias, approx, dx_out, db_acc)
 
 
-# DSA_DUAL_GELU_BWD=0: the bias+GeLU backward writes only dx (the linear transposes it itself)
-DUAL_GELU_BWD = os.environ.get("DSA_DUAL_GELU_BWD", "1") != "0"
+# the bias+GeLU backward also writes dx^T for the linear's weight gradient (False: dx only)
+DUAL_GELU_BWD = True
 
 
 class _BiasGeluFn(torch.autograd.Function):
@@ -642,18 +641,17 @@ class _FlashAttnQkvFn(torch.autograd.Function):
         B, S, _, H, D = qkv5.shape
         _macs(2 * B * H * S * S * D)
         o_out = _slab(slabs and slabs[0], qkv5[:, :, 0])
-        o, lse, bits = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed, rng, o_out)
-        ctx.save_for_backward(qkv5, o, lse, kbias, bits)
+        o, lse = hip_ops().flash_attn_qkv_fwd(qkv5, kbias, scale, p, seed, rng, o_out)
+        ctx.save_for_backward(qkv5, o, lse, kbias)
         ctx.scale, ctx.p, ctx.seed, ctx.rng = scale, p, seed, rng
         ctx.dqkv_slab = slabs and slabs[1]
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv5, o, lse, kbias, bits = ctx.saved_tensors
+        qkv5, o, lse, kbias = ctx.saved_tensors
         dqkv = hip_ops().flash_attn_qkv_bwd(do.contiguous(), qkv5, o, lse, kbias, ctx.scale, ctx.p, ctx.seed,
-                                            ctx.rng, _slab(ctx.dqkv_slab, qkv5, backward=True),
-                                            bits if bits.numel() else None)
+                                            ctx.rng, _slab(ctx.dqkv_slab, qkv5, backward=True))
         return dqkv, None, None, None, None, None, None
 
 
@@ -777,8 +775,8 @@ class _CrossEntropyFn(torch.autograd.Function):
         return dx.view(ctx.shape), None, None
 
 
-# DSA_XENT_INPLACE=0: the cross-entropy backward writes dlogits into a fresh buffer
-XENT_INPLACE = os.environ.get("DSA_XENT_INPLACE", "1") != "0"
+# the cross-entropy backward writes dlogits over the logits (False: into a fresh buffer)
+XENT_INPLACE = True
 
 
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor, inplace_grad: bool = False) -> torch.Tensor:
@@ -1039,8 +1037,8 @@ class _BiasDropoutResidualLNFn(torch.autograd.Function):
                 None if (acc is not None or not ctx.has_beta) else dbt, None, None, None, None, None)
 
 
-# DSA_BDR_LN=0: the residual sum and the LayerNorm stay two kernels (A/B)
-BDR_LN = os.environ.get("DSA_BDR_LN", "1") != "0"
+# bias + dropout + residual and the next LayerNorm in one kernel (False: two kernels, tests' A/B)
+BDR_LN = True
 
 
 def bdr_ln_supported(x: torch.Tensor, res: torch.Tensor, bias, gamma, beta) -> bool:

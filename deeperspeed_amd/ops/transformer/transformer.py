@@ -20,7 +20,6 @@ reference's fast path.
 
 import json
 import math
-import os
 
 import torch
 import torch.nn as nn
@@ -111,8 +110,8 @@ class _MergeHeads(torch.autograd.Function):
         return native.hip_ops().swap12(g.contiguous().view(B, S, ctx.nh, ctx.hd))
 
 
-# DSA_ENCODER_FLASH=0 keeps the materialised scores -> softmax -> dropout -> P V path
-_ENCODER_FLASH = os.environ.get("DSA_ENCODER_FLASH", "1") != "0"
+# flash attention for the encoder (False: the materialised scores -> softmax -> dropout -> P V path)
+_ENCODER_FLASH = True
 
 
 def _use_head_kernels(x, hd):

@@ -26,33 +26,24 @@ batched GEMM runs at ~3 TF/s, so the operands must sit at a constant stride:
   consecutive slots of their buffers (`flush`), else one GEMM per record.
 
 Bias gradients are still formed in place.  Same math as the per-layer path up to fp32 summation
-order.  DSA_BATCH_WGRAD=0 disables.  No reference counterpart: the reference computes each
+order.  No reference counterpart: the reference computes each
 layer's weight gradients inside its layer backward (csrc/transformer/ds_transformer_cuda.cpp:370-540).
 """
 
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
 
-ENABLED = os.environ.get("DSA_BATCH_WGRAD", "1") != "0"
+ENABLED = True
 MIN_TOKENS = 1024
-# DSA_STACK_WEIGHTS=1: equal-shape weights share a buffer and one W^T transpose per step (stacked_wt)
-# instead of one transpose per weight per backward.  Opt-in: BERT-Large measured 2,528-2,580 vs
-# 2,570-2,576 samples/s at seq 128 and 576 vs 587 at seq 512 (same box,
-# profiles/r5f_bert_stacked_weights_ab.jsonl): the input-gradient GEMMs reading W^T at the stack's
-# row stride and the one large transpose on the critical path cost what the 96 small ones did.  With
-# the W^T made per slot by one batched transpose (same leading dimension as a per-weight one):
-# 2,560 vs 2,551 and 585 vs 586, losses identical (profiles/r5h_bert_stacked_weights_batched_t_ab.jsonl).
-STACK_WEIGHTS = os.environ.get("DSA_STACK_WEIGHTS", "0") == "1"
 # a kind whose slab shape changed this many times (progressive layer drop, varying batch shapes)
 # stops using slabs: each change would allocate a fresh [count, ...] buffer
 MAX_RESHAPES = 3
 # the batched GEMMs through the extension's strided-batched hipBLASLt call, whose solution is timed
 # per shape on first use (gemm_lt_batched), instead of torch.baddbmm_'s first heuristic answer
-LT_BATCHED = os.environ.get("DSA_WGRAD_LT_BATCHED", "1") != "0"
+LT_BATCHED = True
 
 
 def _batched_gemm(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor) -> None:
@@ -94,7 +85,6 @@ class _State:
         self.bwd = None  # tag of the deferred backward running
         self.seen = set()  # forward tags whose graph the running backward reached
         self.stacks: List[_Slab] = []  # persistent gradient stacks
-        self.wstacks: List[dict] = []  # stacked weights and their shared transposes
         self.defer = False
         self.pending: List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
         self.batched = 0  # batched GEMMs launched (tests / diagnostics)
@@ -229,57 +219,6 @@ def zero_stacks(grads):
         if id(slab) in hit:
             slab.buf.zero_()
     return rest
-
-
-def bind_weight_stacks(params, min_count: int = 4, min_numel: int = 1 << 20) -> int:
-    """Move every group of >= min_count equal-shape 2-D weights into one [n, out, in] buffer (each
-    parameter's data becomes a slot view, values copied) so that the input-gradient GEMMs can take
-    all their W^T from ONE transpose per optimizer step (`stacked_wt`).  Call before anything caches
-    the parameters' addresses (the optimizer's pointer tables are built at its first step)."""
-    groups: Dict[tuple, list] = {}
-    for p in params:
-        if (p.dim() == 2 and p.numel() >= min_numel and p.is_cuda and p.dtype in (torch.bfloat16, torch.float16)
-                and not _captured(p)):
-            groups.setdefault((tuple(p.shape), p.dtype, p.device), []).append(p)
-    n = 0
-    for (shape, dtype, dev), ps in groups.items():
-        if len(ps) < min_count:
-            continue
-        buf = torch.empty((len(ps),) + shape, dtype=dtype, device=dev)
-        with torch.no_grad():
-            for i, p in enumerate(ps):
-                buf[i].copy_(p.data)
-                p.data = buf[i]
-        state.wstacks.append({"slab": _Slab(buf), "wt": None, "epoch": None, "params": list(ps), "vers": None})
-        n += len(ps)
-    return n
-
-
-def stacked_wt(weight: torch.Tensor, epoch: int) -> Optional[torch.Tensor]:
-    """W^T [in, out] of a stacked weight: slot i of the stack's batched transpose [n, in, out]
-    (contiguous per slot, so the input-gradient GEMM reads it at the same leading dimension as a
-    per-weight transpose), made by ONE HIP launch the first time a weight of the stack asks after an
-    optimizer step (`epoch`) or after an in-place write to that weight (its version counter, checked
-    per weight when it asks).  Not inside a HIP graph capture: a replay would not refresh the shared
-    buffer for the other layers' graphs."""
-    if torch.cuda.is_current_stream_capturing():
-        return None
-    for ws in state.wstacks:
-        slab = ws["slab"]
-        i = slab.slot_of(weight)
-        if i is None:
-            continue
-        L, N, K = slab.buf.shape
-        if ws["epoch"] != epoch or ws["vers"][i] != weight._version:
-            from . import native
-            if not native.transpose_supported(slab.buf[0]):
-                return None
-            if ws["wt"] is None:
-                ws["wt"] = torch.empty(L, K, N, dtype=slab.buf.dtype, device=slab.buf.device)
-            native.hip_ops().transpose_batched(slab.buf, ws["wt"])
-            ws["epoch"], ws["vers"] = epoch, [p._version for p in ws["params"]]
-        return ws["wt"][i]
-    return None
 
 
 class deferred:

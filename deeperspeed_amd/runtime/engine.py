@@ -128,11 +128,6 @@ class DeepSpeedEngine(Module):
             self._configure_optimizer(optimizer, model_parameters)
             self._configure_lr_scheduler(lr_scheduler)
             self._report_progress(0)
-        # whole weights stay resident below ZeRO-3: their input-gradient transposes are made once
-        # per optimizer step, beside the forward (ops/linear.py WeightTCache); ZeRO-3 gathers and
-        # releases weights per unit, and its HBM goes to retention instead
-        _linear_ops.weight_t_cache.enable(self.optimizer is not None and self.zero_optimization_stage() < 3
-                                          and self.device.type == "cuda")
         # weight gradients may wait for the end of backward only where no gradient hook reads them
         # during it: no ZeRO stage, no bucket hooks of a flat-arena optimizer, no overlapped step;
         # then equal layers' weight gradients run as batched GEMMs (ops/wgrad_batch.py) with their
@@ -144,8 +139,6 @@ class DeepSpeedEngine(Module):
         _wgrad_batch.enable(self._defer_wgrad)
         if self._defer_wgrad:
             _wgrad_batch.bind_grad_stacks(self.module.parameters())
-            if _wgrad_batch.STACK_WEIGHTS:  # one dgrad weight transpose per stack and step
-                _wgrad_batch.bind_weight_stacks(self.module.parameters())
 
         self.csr_tensor_module_names = set()
         if self.sparse_gradients_enabled():
@@ -892,7 +885,6 @@ class DeepSpeedEngine(Module):
             self.amp.step(self.optimizer)
         else:
             self.optimizer.step()
-        _linear_ops.weight_t_cache.bump()  # the weights changed under any cached transposes
         self.timers("_step_step").stop()
         self.timers("_step_zero_grad").start()
         if hasattr(self.optimizer, "groups"):
@@ -1233,7 +1225,6 @@ class DeepSpeedEngine(Module):
     def load_checkpoint(self, load_dir, tag=None, load_module_strict=True, load_optimizer_states=True,
                         load_lr_scheduler_states=True):
         self.synchronize()
-        _linear_ops.weight_t_cache.bump()  # weights are about to be overwritten
         if tag is None:
             latest_path = os.path.join(load_dir, "latest")
             if os.path.isfile(latest_path):

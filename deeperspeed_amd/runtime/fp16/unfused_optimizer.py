@@ -10,7 +10,6 @@ buffered_allreduce_fallback), exactly like the reference.
 """
 
 import math
-import os
 
 import torch
 import torch.distributed as dist
@@ -20,8 +19,8 @@ from ..utils import CheckOverflow, get_grad_norm, grad_norm_sq_tensor
 from .loss_scaler import DynamicLossScaler, LossScaler
 
 
-# bf16 / static-scale steps without a host read of the gradient norm (DSA_SYNC_FREE_STEP=0: off)
-SYNC_FREE_STEP = os.environ.get("DSA_SYNC_FREE_STEP", "1") != "0"
+# bf16 / static-scale steps without a host read of the gradient norm
+SYNC_FREE_STEP = True
 
 
 class FP16_UnfusedOptimizer:

@@ -19,21 +19,15 @@ Used by the per-tensor mixed-precision wrapper (runtime/fp16/unfused_optimizer.p
 from __future__ import annotations
 
 import contextlib
-import os
 from typing import Dict, List, Sequence
 
 import torch
 
-# DSA_OVERLAP_CUS=n: the side stream may only use n of the CUs (spread evenly over the
-# enumeration, so every XCD keeps most of its CUs for the compute stream); 0 = all CUs
-OVERLAP_CUS = int(os.environ.get("DSA_OVERLAP_CUS", "0"))
-
-
-# DSA_DEDICATED_STREAMS=1: side / copy streams on hardware queues of their own (dedicated_stream).
-# Off by default: on the 20B N=1 step the optimizer step then runs concurrently with the next
-# forward and costs more than the queue sharing it removes (8,720 vs 8,868 tok/s, same box,
-# profiles/r4s_notes.md)
-DEDICATED_STREAMS = os.environ.get("DSA_DEDICATED_STREAMS", "0") == "1"
+# Side / copy streams are torch pool streams.  Measured alternatives, removed: hardware queues of
+# their own for every side stream (20B N=1: 8,720 vs 8,868 tok/s, profiles/r4s_notes.md), HIP
+# low-priority streams (same step time, profiles/r5d_notes.md), a CU-masked step stream.  Only the
+# offloaded optimizer step -- which IS the critical path -- puts its copy streams on dedicated
+# hardware queues (ZeRO sharded_base._new_stream, profiles/r4ag_notes.md).
 
 
 def side_stream(device, num_cus: int = 0) -> torch.cuda.Stream:
@@ -62,12 +56,6 @@ def dedicated_stream(device) -> torch.cuda.Stream:
     return side_stream(device, 1 << 30)
 
 
-# DSA_STREAM_KIND: what new_stream() creates for the framework's side / copy streams
-#   torch - a stream from torch's pool;
-#   hip   - hipStreamCreateWithPriority(normal) through the extension;
-#   low   - the same at HIP's lowest priority (a queue pool of its own: never the compute
-#           stream's hardware queue, and the dispatcher favours the compute queue's waves).
-STREAM_KIND = os.environ.get("DSA_STREAM_KIND", "torch")
 _keep = []  # external streams live for the process (torch does not own them)
 
 
@@ -82,14 +70,8 @@ def priority_stream(device, priority: int) -> torch.cuda.Stream:
     return s
 
 
-def new_stream(device, kind: str = None) -> torch.cuda.Stream:
-    """The framework's side / copy streams: plain torch streams by default, dedicated_stream
-    with DSA_DEDICATED_STREAMS=1, HIP priority streams with DSA_STREAM_KIND=hip|low."""
-    kind = kind or STREAM_KIND
-    if DEDICATED_STREAMS and torch.cuda.is_available():
-        return dedicated_stream(device)
-    if kind in ("hip", "low") and torch.cuda.is_available():
-        return priority_stream(device, 0 if kind == "hip" else 1 << 20)
+def new_stream(device) -> torch.cuda.Stream:
+    """The framework's side / copy streams: streams from torch's pool."""
     return torch.cuda.Stream(device=device)
 
 
@@ -130,7 +112,7 @@ class OverlapStep:
 
     def __init__(self, module: torch.nn.Module, params: Sequence[torch.nn.Parameter], buckets: List[List[int]],
                  device):
-        self.stream = side_stream(device, OVERLAP_CUS)
+        self.stream = new_stream(device)
         owner = {id(params[i]): b for b, idxs in enumerate(buckets) for i in idxs}
         self._module_buckets: Dict[torch.nn.Module, list] = {}
         self._handles = []

@@ -124,7 +124,7 @@ def _dev():
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
 
-_SUMSQ_MULTI = os.environ.get("DSA_SUMSQ_MULTI", "1") != "0"  # 0: torch _foreach_norm
+_SUMSQ_MULTI = True  # False: torch _foreach_norm
 
 
 def grad_norm_sq_tensor(parameters, mpu=None) -> torch.Tensor:

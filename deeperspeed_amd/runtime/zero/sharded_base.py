@@ -40,35 +40,22 @@ from . import compact_master as cm
 from .layout import FlatGroup, layout_signature, params_to_shard, shards_to_params
 from .ref_layout import LAYOUT_VERSION, is_reference_layout, merge_reference_shards
 
-# Host-moments groups ("stream" mode): DSA_HOST_D2H_NOCU=1 writes m / v back with
-# hipMemcpyDeviceToDeviceNoCU -- measured to take the same blit-kernel path as torch copy_
-# (profiles/r4p_*), kept for the record
-HOST_D2H_NOCU = os.environ.get("DSA_HOST_D2H_NOCU", "0") == "1"
-# "stream" (default): the host-moments Adam on a stream of its own, copies on two copy streams,
-# beside the HBM groups; "side": Adam on the step stream after the HBM groups; "serial": copies and
-# Adam all on the step stream.  Measured on the 20B N=1 step (profiles/r4q_notes.md,
-# profiles/r4s_notes.md): stream 8,868-8,972, side 8,557-8,670, serial 8,540-8,559 tok/s.
-HOST_STEP_MODE = os.environ.get("DSA_HOST_STEP_MODE", "stream")
-
-# workgroups of the HBM -> pinned-host moment write-back kernel (copy_narrow_kernel); 0 (default):
-# torch copy_, a ROCclr blit kernel with a workgroup on every CU, which measured faster in the step
-# (8,787 vs 8,720 tok/s with dedicated queues, profiles/r4s_notes.md)
-HOST_D2H_WGS = int(os.environ.get("DSA_HOST_D2H_WGS", "0"))
-# DSA_NVME_PROGRESS=1: the NVMe moments tier logs its progress every 8 buckets (long steps)
-NVME_PROGRESS = os.environ.get("DSA_NVME_PROGRESS", "0") == "1"
-# optimizer offload (states all / master / moments, NVMe): copy streams on dedicated hardware queues
-OFFLOAD_DEDICATED_STREAMS = os.environ.get("DSA_OFFLOAD_DEDICATED_STREAMS", "1") != "0"
+# Host-moments groups: the Adam of the host-moments pieces runs on a stream of its own, the copies
+# on two copy streams, beside the HBM groups.  Measured on the 20B N=1 step (profiles/r4q_notes.md,
+# r4s_notes.md) against Adam after the HBM groups on the step stream (8,557-8,670 tok/s) and
+# everything serial on the step stream (8,540-8,559): 8,868-8,972 tok/s; the write-back of m / v is
+# torch's copy_ (a ROCclr blit kernel), which beat a 16-workgroup copy kernel (8,787 vs 8,720 tok/s,
+# r4s_notes.md) and a hipMemcpy NoCU variant (the same blit path, r4p).  Those variants are gone.
 
 OFFLOAD_SUBCHUNK = int(64 * 1024 * 1024)  # elements per staged piece (256 MB fp32)
 # device staging slots of the states="moments" step (each holds one piece of m and v)
-OFFLOAD_NBUF = int(os.environ.get("DSA_OFFLOAD_NBUF", "6"))  # 6 vs 3: +4 % at 30.3B (profiles/r4ag_notes.md)
+OFFLOAD_NBUF = 6  # 6 vs 3: +4 % at 30.3B (profiles/r4ag_notes.md)
 CPU_STEP_PIECE = int(16 * 1024 * 1024)  # elements per CPU-Adam piece of the pipelined offload step
 
 
 def _pipelined_offload() -> bool:
-    """DSA_OFFLOAD_PIPELINE=0 restores the serial D2H -> CPU Adam -> H2D offload step (A/B)."""
-    import os
-    return torch.cuda.is_available() and os.environ.get("DSA_OFFLOAD_PIPELINE", "1") != "0"
+    """The pipelined D2H -> CPU Adam -> H2D offload step (GPU); the serial one on CPU-only hosts."""
+    return torch.cuda.is_available()
 
 
 class HostGradStream:
@@ -536,14 +523,8 @@ class ShardedOptimizerBase:
                     self.optimizer.state[g.master]
                 st["step"] = st.get("step", 0) + 1
             host_groups = [g for g in self.groups if self._host_moment_group(g)]
-            pipe = None
-            if host_groups and HOST_STEP_MODE == "stream":  # copy pipeline + kernels beside the HBM groups
+            if host_groups:  # copy pipeline + kernels beside the HBM groups
                 self._host_moments_step(host_groups, grad_scale)
-            elif host_groups and HOST_STEP_MODE == "serial":  # after the HBM groups, on this stream only
-                pipe = self._host_moments_serial(host_groups, grad_scale)
-            elif host_groups:  # H2D of the first pieces starts now; their Adam follows the HBM groups
-                pipe = self._host_moments_pipeline(host_groups, grad_scale)
-                next(pipe)
             for g in self.groups:
                 if self._host_moment_group(g):
                     continue
@@ -555,10 +536,7 @@ class ShardedOptimizerBase:
                         self.optimizer.update_flat(grp, g.master, g.master, g.shard_grad, out=o,
                                                    grad_scale=grad_scale, lo=lo, hi=hi)
                     self._after_bucket_update(g, b)
-            if pipe is not None:
-                for _ in pipe:
-                    pass
-            elif host_groups:  # the step's end (and the gradient zeroing after it) follows their kernels
+            if host_groups:  # the step's end (and the gradient zeroing after it) follows their kernels
                 torch.cuda.current_stream().wait_stream(self._host_stream)
             return
         # generic torch optimizer over the fp32 master shards
@@ -637,156 +615,13 @@ class ShardedOptimizerBase:
                         ev_done.record(hs)
                     with torch.cuda.stream(d2h):
                         d2h.wait_event(ev_done)
-                        if HOST_D2H_NOCU:
-                            native.copy_nocu_(st["exp_avg"][lo:hi], m_dev)
-                            native.copy_nocu_(st["exp_avg_sq"][lo:hi], v_dev)
-                        elif HOST_D2H_WGS > 0:
-                            native.copy_narrow_(st["exp_avg"][lo:hi], m_dev, HOST_D2H_WGS)
-                            native.copy_narrow_(st["exp_avg_sq"][lo:hi], v_dev, HOST_D2H_WGS)
-                        else:
-                            st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
-                            st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
+                        st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
+                        st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
                         ev_free = torch.cuda.Event()
                         ev_free.record(d2h)
                     free_ev[i] = ev_free
                 self._after_host_bucket_update(g, b, hs)
         self._host_free_ev = free_ev
-        done = torch.cuda.Event()
-        done.record(d2h)
-        self._host_d2h_done = done
-
-    def _host_moments_serial(self, groups, grad_scale):
-        """Adam for the host-moments groups entirely on the CURRENT stream (the overlapped step's
-        side stream), after the HBM groups: per piece, H2D of m / v (DMA engine), the fused Adam,
-        D2H of m / v (copy_narrow_kernel on HOST_D2H_WGS workgroups).  One stream and no cross-stream
-        waits: HIP maps streams onto 4 hardware queues by default, and a copy stream that waits on
-        another stream's events blocks whatever shares its queue -- the compute stream's next
-        forward waited for the whole copy pipeline that way (profiles/r4q_notes.md).  The PCIe
-        phase is serial (~0.4 s for 1.2 B parameters) but runs beside the next forward, whose
-        modules wait only for their own buckets (the host groups hold the LAST layers)."""
-        cur = torch.cuda.current_stream()
-        piece = min(self.HOST_PIECE, max(b.chunk for g in groups for b in g.buckets))
-        if self._host_staging is None or self._host_staging[0][0].numel() < piece:
-            self._host_staging = [(torch.empty(piece, dtype=torch.float32, device=self.device),
-                                   torch.empty(piece, dtype=torch.float32, device=self.device)) for _ in range(3)]
-        m_buf, v_buf = self._host_staging[0]
-        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
-        yield
-        for g in groups:
-            grp = self._inner_group(g)
-            b1, b2 = grp["betas"]
-            st = self.optimizer.state_for(g.master) if isinstance(self.optimizer, FusedAdam) else \
-                self.optimizer.state[g.master]
-            for b in g.buckets:
-                out_full = self._bucket_out(g, b)
-                for s0 in range(0, b.chunk, piece):
-                    e0 = min(s0 + piece, b.chunk)
-                    lo, hi, n = b.shard_offset + s0, b.shard_offset + e0, e0 - s0
-                    m_dev, v_dev = m_buf[:n], v_buf[:n]
-                    m_dev.copy_(st["exp_avg"][lo:hi], non_blocking=True)
-                    v_dev.copy_(st["exp_avg_sq"][lo:hi], non_blocking=True)
-                    o = None if out_full is None else out_full[s0:e0]
-                    if self.compact_master:
-                        native.adam_compact_(o, g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, grp["lr"], b1,
-                                             b2, grp["eps"], grp["weight_decay"], st["step"],
-                                             grp.get("bias_correction", True), grad_scale, adamw)
-                    else:
-                        native.adam_flat_(g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, o, grp["lr"], b1, b2,
-                                          grp["eps"], grp["weight_decay"], st["step"],
-                                          grp.get("bias_correction", True), grad_scale, adamw)
-                    if HOST_D2H_WGS > 0:
-                        native.copy_narrow_(st["exp_avg"][lo:hi], m_dev, HOST_D2H_WGS)
-                        native.copy_narrow_(st["exp_avg_sq"][lo:hi], v_dev, HOST_D2H_WGS)
-                    else:
-                        st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
-                        st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
-                    yield
-                self._after_host_bucket_update(g, b, cur)
-        done = torch.cuda.Event()
-        done.record(cur)
-        self._host_d2h_done = done
-
-    def _host_moments_pipeline(self, groups, grad_scale):
-        """Adam for the host-moments groups on the CURRENT stream (the overlapped step's side
-        stream), after the HBM groups: a generator whose first next() issues the H2D of the first
-        pieces (copy stream, DMA engine) and whose remaining iterations issue, per piece, the fused
-        Adam on the current stream (waiting for that piece's H2D), the D2H of m / v on the second
-        copy stream (copy_narrow_kernel on HOST_D2H_WGS workgroups, not a blit kernel on every CU),
-        and the H2D of the piece three ahead into the slot it frees.  No extra compute stream: with
-        HIP's 4 hardware queues a fifth stream shares a queue with the compute stream, whose next
-        forward then waited for the whole copy pipeline (profiles/r4n_notes.md)."""
-        h2d, d2h = self._streams()
-        cur = torch.cuda.current_stream()
-        piece = min(self.HOST_PIECE, max(b.chunk for g in groups for b in g.buckets))
-        if self._host_staging is None or self._host_staging[0][0].numel() < piece:
-            self._host_staging = [(torch.empty(piece, dtype=torch.float32, device=self.device),
-                                   torch.empty(piece, dtype=torch.float32, device=self.device)) for _ in range(3)]
-        stages = self._host_staging
-        work = []  # (group, bucket, lo, hi, n, s, e, state, is_last_piece_of_bucket)
-        for g in groups:
-            st = self.optimizer.state_for(g.master) if isinstance(self.optimizer, FusedAdam) else \
-                self.optimizer.state[g.master]
-            for b in g.buckets:
-                starts = list(range(0, b.chunk, piece))
-                for j, s0 in enumerate(starts):
-                    e0 = min(s0 + piece, b.chunk)
-                    work.append((g, b, b.shard_offset + s0, b.shard_offset + e0, e0 - s0, s0, e0, st,
-                                 j == len(starts) - 1))
-        free_ev = [None] * 3
-        ev_in = [None] * len(work)
-        if self._host_d2h_done is not None:  # the previous step's moments are home
-            h2d.wait_event(self._host_d2h_done)
-
-        def issue_h2d(k):
-            g, b, lo, hi, n, _, _, st, _ = work[k]
-            i = k % 3
-            with torch.cuda.stream(h2d):
-                if free_ev[i] is not None:
-                    h2d.wait_event(free_ev[i])
-                stages[i][0][:n].copy_(st["exp_avg"][lo:hi], non_blocking=True)
-                stages[i][1][:n].copy_(st["exp_avg_sq"][lo:hi], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(h2d)
-            ev_in[k] = ev
-
-        for k in range(min(3, len(work))):
-            issue_h2d(k)
-        yield
-        adamw = bool(getattr(self.optimizer, "adam_w_mode", True))
-        for k, (g, b, lo, hi, n, s0, e0, st, last) in enumerate(work):
-            i = k % 3
-            m_dev, v_dev = stages[i][0][:n], stages[i][1][:n]
-            grp = self._inner_group(g)
-            b1, b2 = grp["betas"]
-            cur.wait_event(ev_in[k])
-            out_full = self._bucket_out(g, b)
-            o = None if out_full is None else out_full[s0:e0]
-            if self.compact_master:
-                native.adam_compact_(o, g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, grp["lr"], b1, b2,
-                                     grp["eps"], grp["weight_decay"], st["step"], grp.get("bias_correction", True),
-                                     grad_scale, adamw)
-            else:
-                native.adam_flat_(g.master[lo:hi], g.shard_grad[lo:hi], m_dev, v_dev, o, grp["lr"], b1, b2,
-                                  grp["eps"], grp["weight_decay"], st["step"], grp.get("bias_correction", True),
-                                  grad_scale, adamw)
-            ev_done = torch.cuda.Event()
-            ev_done.record(cur)
-            with torch.cuda.stream(d2h):
-                d2h.wait_event(ev_done)
-                if HOST_D2H_WGS > 0:
-                    native.copy_narrow_(st["exp_avg"][lo:hi], m_dev, HOST_D2H_WGS)
-                    native.copy_narrow_(st["exp_avg_sq"][lo:hi], v_dev, HOST_D2H_WGS)
-                else:
-                    st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
-                    st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
-                ev_free = torch.cuda.Event()
-                ev_free.record(d2h)
-            free_ev[i] = ev_free
-            if k + 3 < len(work):
-                issue_h2d(k + 3)
-            if last:
-                self._after_host_bucket_update(g, b, cur)
-            yield
         done = torch.cuda.Event()
         done.record(d2h)
         self._host_d2h_done = done
@@ -808,7 +643,7 @@ class ShardedOptimizerBase:
 
     def _new_stream(self):
         from ..overlap_step import dedicated_stream, new_stream
-        if self.offload is not None and OFFLOAD_DEDICATED_STREAMS:
+        if self.offload is not None:
             # an offloaded step IS the critical path (nothing computes beside it): its copy
             # streams get hardware queues of their own, or a copy stream's waits can stall the
             # compute stream's Adam kernels behind them in a shared queue (profiles/r4ag_notes.md)
@@ -953,12 +788,8 @@ class ShardedOptimizerBase:
                     ev_done.record(cur)
                     with torch.cuda.stream(d2h):
                         d2h.wait_event(ev_done)
-                        if HOST_D2H_NOCU:  # DMA engine, not a copy kernel on every CU
-                            native.copy_nocu_(st["exp_avg"][lo:hi], m_dev)
-                            native.copy_nocu_(st["exp_avg_sq"][lo:hi], v_dev)
-                        else:
-                            st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
-                            st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
+                        st["exp_avg"][lo:hi].copy_(m_dev, non_blocking=True)
+                        st["exp_avg_sq"][lo:hi].copy_(v_dev, non_blocking=True)
                         ev_free = torch.cuda.Event()
                         ev_free.record(d2h)
                     free_ev[i] = ev_free
@@ -996,8 +827,8 @@ class ShardedOptimizerBase:
             gi, bi = key
             g, b = self.groups[gi], self._mswap_keys[key]
             done_n[0] += 1
-            if NVME_PROGRESS and done_n[0] % 8 == 0:
-                logger.info(f"NVMe moments tier: {done_n[0]}/{len(keys)} buckets, {time.time() - t0:.1f}s, "
+            if done_n[0] % 64 == 0:
+                logger.debug(f"NVMe moments tier: {done_n[0]}/{len(keys)} buckets, {time.time() - t0:.1f}s, "
                             f"{self._mswap.bytes_read / 2**30:.1f} GiB read")
             grp = self._inner_group(g)
             out_full = self._bucket_out(g, b)

@@ -35,7 +35,7 @@ from ...utils import comm
 from .layout import ALIGN, FlatGroup, build_unit_buckets
 from .sharded_base import ShardedOptimizerBase, _dist_ready
 
-OVERLAP_TRACE = os.environ.get("DSA_OVERLAP_TRACE", "0") == "1"
+OVERLAP_TRACE = False  # log each overlapped-step bucket wait (diagnostics)
 
 
 class ZeroParamStatus:
@@ -517,9 +517,8 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self._bucket_events: Dict[tuple, torch.cuda.Event] = {}
         if not self._overlap_step:
             return
-        from ..overlap_step import OVERLAP_CUS, side_stream
-        # DSA_OVERLAP_CUS: CU-masked; otherwise a hardware queue of its own (overlap_step.new_stream)
-        self._step_stream = side_stream(self.device, OVERLAP_CUS)
+        from ..overlap_step import new_stream
+        self._step_stream = new_stream(self.device)
         self._bucket_key = {}
         owner = {}
         for gi, g in enumerate(self.groups):
@@ -546,7 +545,7 @@ class DeepSpeedZeroOptimizer_Stage3(ShardedOptimizerBase):
         self._handles.append(self.module.register_forward_pre_hook(self._root_wait_uncovered))
 
     def _trace_wait(self, what, key):
-        """DSA_OVERLAP_TRACE=1: log each bucket wait of the first forward after a step, with the
+        """OVERLAP_TRACE = True: log each bucket wait of the first forward after a step, with the
         position of that bucket's update in the step (how much of the step the forward waits for)."""
         if not OVERLAP_TRACE:
             return

@@ -119,7 +119,7 @@ def trace_range(name: str):
         yield
 
 
-def _record(op: str, t: torch.Tensor, kind: str):
+def _record(op: str, t: torch.Tensor, kind: str = "other"):
     global _seq, _issued, _last
     _issued += 1
     _last = (op, int(t.numel()), str(t.dtype))

@@ -53,14 +53,13 @@ def init_distributed(dist_backend="nccl", auto_mpi_discovery=True, distributed_p
             kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
             # RCCL on high-priority HIP streams: ZeRO's all-gathers / reduce-scatters are
             # scheduled ahead of the compute kernels they overlap with, so a prefetch does not
-            # queue behind a long GEMM (DSA_RCCL_HIGH_PRIORITY=0 turns it off)
-            if os.environ.get("DSA_RCCL_HIGH_PRIORITY", "1") != "0":
-                try:
-                    opts = dist.ProcessGroupNCCL.Options()
-                    opts.is_high_priority_stream = True
-                    kwargs["pg_options"] = opts
-                except (AttributeError, RuntimeError):
-                    pass
+            # queue behind a long GEMM
+            try:
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kwargs["pg_options"] = opts
+            except (AttributeError, RuntimeError):
+                pass
         try:
             dist.init_process_group(**kwargs)
         except TypeError:

@@ -116,25 +116,6 @@ def _train(batch, monkeypatch, steps=3):
     return out
 
 
-def test_stacked_weight_transposes():
-    from deeperspeed_amd.ops import wgrad_batch as wb
-    ps = [torch.nn.Parameter(torch.randn(256, 128, device="cuda", dtype=torch.bfloat16)) for _ in range(4)]
-    vals = [p.detach().clone() for p in ps]
-    n0 = len(wb.state.wstacks)
-    assert wb.bind_weight_stacks(ps, min_numel=1) == 4
-    try:
-        assert all(torch.equal(p, v) for p, v in zip(ps, vals))
-        assert ps[1].data_ptr() - ps[0].data_ptr() == 256 * 128 * 2
-        wt = wb.stacked_wt(ps[2], epoch=7)
-        assert torch.equal(wt, vals[2].t()) and wt.is_contiguous()
-        assert all(torch.equal(wb.stacked_wt(p, epoch=7), v.t()) for p, v in zip(ps, vals))
-        with torch.no_grad():
-            ps[2].mul_(2)  # in-place write: the stack's version moves, the transpose is redone
-        assert torch.equal(wb.stacked_wt(ps[2], epoch=7), (2 * vals[2]).t())
-    finally:
-        del wb.state.wstacks[n0:]
-
-
 def test_bert_training_with_batched_wgrads(monkeypatch):
     l0, w0, n0 = _train(False, monkeypatch)
     l1, w1, n1 = _train(True, monkeypatch)

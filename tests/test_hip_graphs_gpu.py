@@ -22,9 +22,6 @@ def _env():
 def _train(graphs, steps=4):
     _env()
     import deeperspeed_amd as ds
-    from deeperspeed_amd.ops import wgrad_batch
-    # stacked weights (opt-in) share one W^T per step outside graphs only; compare like with like
-    stack0, wgrad_batch.STACK_WEIGHTS = wgrad_batch.STACK_WEIGHTS, False
     from deeperspeed_amd.models.bert import BertForPreTraining, get_config
     from deeperspeed_amd.ops.transformer.transformer import make_graphed_encoder
     dev = torch.device("cuda", 0)
@@ -66,7 +63,6 @@ def _train(graphs, steps=4):
         engine.step()
         losses.append(float(loss))
     torch.cuda.synchronize()
-    wgrad_batch.STACK_WEIGHTS = stack0
     return losses, [p.detach().float().cpu() for p in engine.module.parameters()]
 
 

@@ -760,19 +760,11 @@ def test_sum_slices_and_colsum_accumulate(out_f32, accumulate):
     assert (got.float() - want).abs().max().item() <= 2e-2 * want.abs().max().item()
 
 
-@pytest.mark.parametrize("bits", [False, True])
 @pytest.mark.parametrize("S", [128, 256, 512])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_qkv_layout_flash_matches_head_major(p, S, bits, monkeypatch):
+def test_qkv_layout_flash_matches_head_major(p, S):
     """Encoder flash attention reading q, k, v straight from the fused QKV output (and writing
-    dqkv in that layout) equals the head-major path bit for bit (same kernels, same keep mask).
-    With dropout and ``bits`` (DSA_FA_DROP_BITS=1) the QKV path's backward reads the keep masks the
-    forward stored as bits (query- and key-major, EX_DBITS) while the head-major one re-hashes
-    them: equality pins the stored masks to the hash."""
-    if bits:
-        if p == 0.0:
-            pytest.skip("no dropout: no masks")
-        monkeypatch.setenv("DSA_FA_DROP_BITS", "1")
+    dqkv in that layout) equals the head-major path bit for bit (same kernels, same keep mask)."""
     from deeperspeed_amd.ops import native
     torch.manual_seed(2)
     dev = _dev()

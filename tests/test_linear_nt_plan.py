@@ -7,10 +7,7 @@ import torch
 from deeperspeed_amd.ops import linear as lin
 
 
-def test_nt_wgrad_planned_shapes(monkeypatch):
-    from deeperspeed_amd.ops import lt_tune
-    monkeypatch.setattr(lt_tune, "WGRAD", False)  # measured NT solutions off (see the next test)
-    lt_tune._nt_cache.clear()
+def test_nt_wgrad_planned_shapes():
     # GPT-NeoX-20B at 8192 / 16384 tokens: every projection takes the transposed path
     for M in (8192, 16384):
         for out, inp in ((18432, 6144), (6144, 6144), (24576, 6144), (6144, 24576)):
@@ -23,18 +20,6 @@ def test_nt_wgrad_planned_shapes(monkeypatch):
     # transient copies beyond the byte cap, unless the big operand is already transposed
     assert not lin.nt_wgrad_planned(16384, 32768, 8192)
     assert lin.nt_wgrad_planned(16384, 32768, 8192, g_ready=True)
-
-
-def test_measured_nt_solution_replaces_the_transposed_path(monkeypatch):
-    """With the shipped table, a projection whose NT solution beats transposes + TN (ops/lt_tune.py)
-    is not planned for the transposed path, so no producer offers a transpose for it."""
-    from deeperspeed_amd.ops import lt_tune
-    monkeypatch.setattr(lt_tune, "WGRAD", True)
-    monkeypatch.setattr(lt_tune, "ENABLED", True)
-    lt_tune._nt_cache.clear()
-    for out, inp in ((18432, 6144), (6144, 6144), (24576, 6144), (6144, 24576)):
-        assert lin.nt_wgrad_planned(8192, out, inp) == (not lt_tune.wgrad_nt(8192, out, inp))
-    lt_tune._nt_cache.clear()
 
 
 def test_transposed_registry_fifo_and_match():

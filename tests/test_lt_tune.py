@@ -42,28 +42,6 @@ def _table(tmp_path, rows):
     return str(p)
 
 
-def test_nt_choice_counts_transpose_traffic(tmp_path, monkeypatch):
-    M, N, K = 8192, 6144, 6144
-    # NT 10 % slower than TN: the GEMM costs 0.04 ms more, the two transposes ~0.048 ms -> NT
-    path = _table(tmp_path, [("wgrad", M, N, K, 1400.0), ("wgradT", M, N, K, 1540.0)])
-    monkeypatch.setattr(lt_tune, "_table", lt_tune.load_table(path))
-    monkeypatch.setattr(lt_tune, "WGRAD", True)
-    monkeypatch.setattr(lt_tune, "NT", True)
-    monkeypatch.setattr(lt_tune, "ENABLED", True)
-    lt_tune._nt_cache.clear()
-    assert lt_tune.wgrad_nt(M, N, K)
-    # NT 25 % slower: the transposes are cheaper -> TN
-    path = _table(tmp_path, [("wgrad", M, N, K, 1200.0), ("wgradT", M, N, K, 1600.0)])
-    monkeypatch.setattr(lt_tune, "_table", lt_tune.load_table(path))
-    lt_tune._nt_cache.clear()
-    assert not lt_tune.wgrad_nt(M, N, K)
-    # no NT record -> never NT; switch off -> never NT
-    monkeypatch.setattr(lt_tune, "_table", {})
-    lt_tune._nt_cache.clear()
-    assert not lt_tune.wgrad_nt(M, N, K)
-    lt_tune._nt_cache.clear()
-
-
 def test_shipped_table_parses():
     t = lt_tune.load_table(lt_tune.TABLE_PATH)
     assert t, "ops/lt_table.json missing or empty"
@@ -82,7 +60,5 @@ def test_routes_gated_by_measured_gain(tmp_path, monkeypatch):
     monkeypatch.setattr(lt_tune, "_table", lt_tune.load_table(str(p)))
     monkeypatch.setattr(lt_tune, "ENABLED", True)
     monkeypatch.setattr(lt_tune, "FWD", True)
-    monkeypatch.setattr(lt_tune, "WGRAD", True)
     assert lt_tune.use_fwd(8192, 3072, 1024, True)  # +22 %
-    assert not lt_tune.use_wgrad_t(8192, 3072, 1024)  # +1 %: noise
     assert not lt_tune.use_fwd(8192, 1024, 1024, True)  # no record
