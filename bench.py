@@ -124,6 +124,12 @@ def parse():
     p.add_argument("--stash-offload", action="store_true",
                    help="park the attention stash of the layers HBM cannot hold in pinned host memory "
                         "(measured slower on MI355X: profiles/aux/host_stash_ab.log)")
+    p.add_argument("--mlp-host-layers", type=int, default=0,
+                   help="one-GPU recompute runs: the first K layers without an HBM fc1 stash park their fc1 "
+                        "output in pinned host memory (copy engines) instead of recomputing the fc1 GEMM")
+    p.add_argument("--park-backlog", type=int, default=6,
+                   help="host-parked stashes whose device->host copy may be outstanding before the compute "
+                        "stream waits (bounds the HBM they pin)")
     p.add_argument("--host-moments-gib", type=float, default=0.0,
                    help="--offload moments: pinned-host budget of the moment tiers (0: min(available - 24, 215) GiB)")
     p.add_argument("--overlap-step", type=str, default="on", choices=["on", "off"],
@@ -653,6 +659,7 @@ def main():
 
     stashed = 0
     stashed_mlp = 0
+    parked_mlp = 0
 
     def plan_stash():
         """Selective recompute from MEASURED headroom: after a warmup step with full recompute,
@@ -665,21 +672,37 @@ def main():
         per_layer = 4 * mb * args.seq * cfg.hidden_size * 2 + mb * cfg.num_heads * args.seq * 4
         margin = STASH_MARGIN_GIB * 2**30
         free = hbm / share - reserved_peak() - margin
+        per_mlp = mb * args.seq * cfg.intermediate_size * 2
+        k_park = max(0, min(len(layers), args.mlp_host_layers))
+        if k_park:
+            # HBM the parked fc1 outputs pin: the device->host backlog and the backward's prefetch
+            from deeperspeed_amd.models.gpt_neox import STASH_PREFETCH_DEPTH
+            free -= (args.park_backlog + STASH_PREFETCH_DEPTH + 1) * per_mlp
         n = int(max(0, min(len(layers), free // per_layer)))
         for m in layers[-n:] if n else []:
             m.attention.stash_outputs = True
         # then the MLP: the fc1 output u [tokens, 4h] of as many layers as still fit (saves the fc1
         # GEMM of their recompute; about the same GEMM time per GiB as the attention stash)
-        per_mlp = mb * args.seq * cfg.intermediate_size * 2
         n_mlp = 0
         if n == len(layers) and args.stash == "auto":
             n_mlp = int(max(0, min(len(layers), (free - n * per_layer) // per_mlp)))
             for m in layers[-n_mlp:] if n_mlp else []:
                 m.mlp.stash_outputs = True
-        nonlocal stashed_mlp
+        nonlocal stashed_mlp, parked_mlp
         stashed_mlp = n_mlp
         log(f"selective recompute: {n}/{len(layers)} layers keep attention outputs, {n_mlp} keep the fc1 output "
             f"({(n * per_layer + n_mlp * per_mlp) / 2**30:.1f} GiB; reserved peak {reserved_peak() / 2**30:.1f} GiB)")
+        if k_park:
+            from deeperspeed_amd.runtime.activation_checkpointing import host_stash as hs
+            hs.host_stash().max_backlog = args.park_backlog
+            park = [m for m in layers[:k_park] if not m.mlp.stash_outputs]
+            for m in park:
+                m.mlp.stash_outputs = True
+                m.mlp.stash_offload = True
+            parked_mlp = len(park)
+            log(f"selective recompute: the first {len(park)} layers park their fc1 output in pinned host memory "
+                f"({len(park) * per_mlp / 2**30:.1f} GiB per micro-batch each way over PCIe, backlog "
+                f"{args.park_backlog})")
         # the remaining layers park their stash in pinned host memory (copy engines over PCIe,
         # prefetched back by the recompute of the layers above): opt-in, --stash-offload -- on the
         # measured box the PCIe copies throttled the forward (profiles/aux/host_stash_ab.log)
@@ -874,6 +897,7 @@ def main():
                    "planned_hbm_gib": round(planned / 2**30, 1),
                    "stashed_attention_layers": stashed,
                    "stashed_mlp_layers": stashed_mlp,
+                   "host_parked_mlp_layers": parked_mlp,
                    "host_stashed_attention_layers": sum(1 for m in engine.module.modules()
                                                         if getattr(m, "stash_offload", False)),
                    "zero3_path": zpath,

@@ -132,7 +132,7 @@ class LinearBiasGeLU(nn.Linear):
             u = linear(x, self.weight)
             if self.keep_u:
                 self.kept_u = u
-        if (self.colmajor_in_recompute and _SKIP_OUTPUTS and torch.is_grad_enabled()
+        if (self.colmajor_in_recompute and _SKIP_OUTPUTS and torch.is_grad_enabled() and COLMAJOR_GELU
                 and native.bias_gelu_t_supported(u)):
             return native.bias_gelu_colmajor(u, self.bias, self.approximate)
         # the backward also writes du^T when this layer's own weight gradient will read it
@@ -142,6 +142,10 @@ class LinearBiasGeLU(nn.Linear):
 
 
 
+
+# the recompute writes the GeLU output column-major for fc2's weight gradient (False: row-major,
+# fc2's wgrad transposes it; tests' A/B)
+COLMAJOR_GELU = True
 
 _SKIP_OUTPUTS = 0
 
@@ -380,16 +384,29 @@ class NeoXMLP(nn.Module):
         # Selective MLP recompute (set per layer by the trainer when HBM allows, after the
         # attention stash): the first forward of a checkpointed block keeps the fc1 GEMM output
         # u [tokens, 4h]; the recompute takes it instead of re-running the GEMM (the bias + GeLU
-        # and fc1's gradients run as usual).  Keyed like NeoXAttention's stash.
+        # and fc1's gradients run as usual).  Keyed like NeoXAttention's stash.  stash_offload:
+        # u is parked in pinned host memory between the forward and the recompute (the copy
+        # engines move it while the later layers compute; the recompute of the layers above
+        # prefetches it back) -- for the FIRST layers, whose u is written earliest in the forward
+        # and read latest in the backward.
         self.stash_outputs = False
+        self.stash_offload = False
         self._stash = {}
         self._stash_key = None
+        self.__dict__["_below"] = []  # MLP modules of the next layers in backward order
 
     def forward(self, x):
         key, fc1 = self._stash_key, self.dense_h_to_4h
         if self.stash_outputs and key is not None:
             if ds_ckpt.is_recomputing() and torch.is_grad_enabled():
                 u = self._stash.pop(key, None)
+                from ..runtime.activation_checkpointing.host_stash import StashEntry, host_stash
+                for below in self.__dict__["_below"]:  # start bringing the next layers' u back
+                    for e in below._stash.values():
+                        if isinstance(e, StashEntry):
+                            host_stash().prefetch(e)
+                if isinstance(u, StashEntry):
+                    u = host_stash().fetch(u)[0]
                 if u is not None:
                     fc1.stashed_u = u
             elif ds_ckpt.is_checkpoint_forward():
@@ -400,7 +417,11 @@ class NeoXMLP(nn.Module):
                     h = fc1(x)
                 finally:
                     fc1.keep_u = False
-                self._stash[key] = fc1.kept_u
+                if self.stash_offload:
+                    from ..runtime.activation_checkpointing.host_stash import host_stash
+                    self._stash[key] = host_stash().park(id(self), (fc1.kept_u,))
+                else:
+                    self._stash[key] = fc1.kept_u
                 fc1.kept_u = None
                 return self.dense_4h_to_h(h)
         return self.dense_4h_to_h(fc1(x))
@@ -409,11 +430,11 @@ class NeoXMLP(nn.Module):
 STASH_PREFETCH_DEPTH = 2  # layers whose host-parked stash a recompute starts bringing back
 
 
-def link_stash_prefetch(attentions):
-    """Each attention module learns the modules recomputed right after it in backward (the
-    layers below), whose host-parked stashes its own recompute prefetches."""
-    for i, a in enumerate(attentions):
-        a.__dict__["_below"] = [attentions[j] for j in range(i - 1, max(-1, i - 1 - STASH_PREFETCH_DEPTH), -1)]
+def link_stash_prefetch(mods):
+    """Each attention (or MLP) module learns the modules recomputed right after it in backward
+    (the layers below), whose host-parked stashes its own recompute prefetches."""
+    for i, a in enumerate(mods):
+        a.__dict__["_below"] = [mods[j] for j in range(i - 1, max(-1, i - 1 - STASH_PREFETCH_DEPTH), -1)]
 
 
 class NeoXTransformerLayer(nn.Module):
@@ -470,6 +491,7 @@ class GPTNeoX(nn.Module):
         self.embed_in = native.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
         self.layers = nn.ModuleList([NeoXTransformerLayer(cfg, i, device, dtype) for i in range(cfg.num_layers)])
         link_stash_prefetch([l.attention for l in self.layers])
+        link_stash_prefetch([l.mlp for l in self.layers])
         self.final_layer_norm = native.FusedLayerNorm(cfg.hidden_size, cfg.layernorm_eps, device=device, dtype=dtype)
         self.embed_out = Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
         self.reset_parameters()
