@@ -140,9 +140,12 @@ def parse():
                         "micro-batch, recompute and memory fit planned for N ranks, collectives replaced by "
                         "local stand-ins that write the same bytes (utils/comm.py).  Reports EMULATED per-rank "
                         "tokens/s, the collective bytes per step and the xGMI rate full overlap needs")
-    p.add_argument("--fp32-reduce", type=str, default="off", choices=["on", "off"],
+    p.add_argument("--fp32-reduce", type=str, default="auto", choices=["auto", "on", "off"],
                    help="reduce bf16 gradients in fp32 (DeeperSpeed's bf16 default fp32_allreduce; "
-                        "tests/test_zero_reduce_precision.py measures what bf16 reduction costs)")
+                        "tests/test_zero_reduce_precision.py measures what bf16 reduction costs).  auto: on "
+                        "for N >= 2 -- the emulated N = 2 / 4 / 8 ranks measured -2.3 / -2.1 / +0.1 %% per-rank "
+                        "throughput and 33.5 vs 22.3 GB/s of xGMI at N = 8 (profiles/r6a_emulated_world_notes.md); "
+                        "one rank reduces nothing")
     return p.parse_args()
 
 
@@ -372,6 +375,9 @@ def spawn_ranks(n):
 def main():
     args = parse()
     HOST_MOMENTS_GIB[0] = args.host_moments_gib
+    if args.fp32_reduce == "auto":
+        n_ranks = args.emulate_world or int(os.environ.get("WORLD_SIZE", "0") or 0) or args.gpus
+        args.fp32_reduce = "on" if n_ranks > 1 else "off"
     launched = int(os.environ.get("WORLD_SIZE", "0") or 0)
     if launched == 0 and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
