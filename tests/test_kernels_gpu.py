@@ -879,4 +879,3 @@ def test_embedding_backward_int32_ids():
         emb(ids.to(dt)).backward(dy)
         grads.append(emb.weight.grad.clone())
     assert torch.equal(grads[0], grads[1])
-
