@@ -1041,15 +1041,257 @@ __global__ void __launch_bounds__(256, 2) bwd_dq_v3_kernel(
                                           O);
 }
 
-// dK/dV with the initial-accumulator row constants (V3); OCC = waves per SIMD the launch
-// bounds allow (1: the whole 512-register file per wave, no spills; 2: latency hiding)
-template <typename T, int D, bool CAUSAL, int OCC>
-__global__ void __launch_bounds__(256, OCC) bwd_dkdv_v3_kernel(
+// dK/dV with the initial-accumulator row constants (V3), two waves per SIMD (D <= 96)
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) bwd_dkdv_v3_kernel(
     const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
     const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh) {
   dkdv_v2_body<T, D, CAUSAL, 0, false, true, true>(blockIdx.x, gridDim.x, Q, K, V, dO, LSE, DELTA, dK, dV, S,
                                                    scale, onh, Extra());
+}
+
+// ======================================================================== backward: dK/dV, wave pairs
+// dkdv_v2_body keeps dK and dV (2 x D/2 accumulator registers), the K and V fragments (2 x D/4)
+// and the staging of both tiles in ONE wave; at D = 128 that fits only at one wave per SIMD,
+// which leaves nothing to hide the LDS latency (247 TF/s at B16 H16 S2048 causal vs 361 at
+// D = 96 with two).  Here each 32-key group is owned by a PAIR of waves of a 512-thread
+// workgroup, one per role, so every wave holds half that state and two run per SIMD:
+//   role 0 (waves 0-3): S = Q K^T -> P, dV^T += dO^T P   (K fragments, dV; stages Q + LSE)
+//   role 1 (waves 4-7): dP = dO V^T, dS = P (dP - Delta), dK^T += Q^T dS   (V, dK; dO + Delta)
+// P crosses from role 0 to role 1 through LDS as the packed 16-bit B fragments role 0 feeds its
+// own dV MFMAs: both sides hold the score tile in the same C layout (lane = key), so it is a
+// plain per-lane copy.  The exchange is software-pipelined so both roles issue 16 MFMAs between
+// the two barriers of a 64-query tile (half = 32 queries):
+//   A: role 0: dV += previous tile's half 1 (P1 in registers); S of half 0 -> P0 to LDS
+//      role 1: dK += previous tile's half 1 (P1 from LDS);     dP of half 0
+//   -- barrier --
+//   B: role 0: dV += half 0; S of half 1 -> P1 to LDS (and kept for the next A)
+//      role 1: dK += half 0 (P0 from LDS); dP of half 1 (kept for the next A)
+//      the next Q / dO tile goes into the other LDS buffer (its last readers ran in A)
+//   -- barrier --
+// The row constants enter as initial accumulators (S at -LSE/scale, dP at -Delta), as in V3.
+template <int D>
+__device__ __forceinline__ void tile_load_buf_t(uint4 (&r)[D / 32], __amdgpu_buffer_rsrc_t rs, int r0, int ld,
+                                                int tid) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int k = 0; k < D / 32; ++k) {
+    const int c = tid + 256 * k;
+    const int row = c / CH, ch = c - row * CH;
+    const fa_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ((r0 + row) * ld + ch * 8) * 2, 0, 0);
+    r[k] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+template <int D>
+__device__ __forceinline__ void tile_store_t(uint16_t* lds, const uint4 (&r)[D / 32], int tid) {
+  constexpr int CH = D / 8;
+#pragma unroll
+  for (int k = 0; k < D / 32; ++k) {
+    const int c = tid + 256 * k;
+    const int row = c / CH, ch = c - row * CH;
+    *reinterpret_cast<uint4*>(lds + row * LDP<D> + ch * 8) = r[k];
+  }
+}
+__device__ __forceinline__ void tohold(f32x16& hold, const s16x8 (&f)[2]) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const f32x4 v = __builtin_bit_cast(f32x4, f[kk]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hold[4 * kk + j] = v[j];
+  }
+}
+__device__ __forceinline__ void unhold(const f32x16& hold, s16x8 (&f)[2]) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) f[kk] = __builtin_bit_cast(s16x8, f32x4{hold[4 * kk], hold[4 * kk + 1], hold[4 * kk + 2], hold[4 * kk + 3]});
+}
+template <int D> constexpr int dkdv_pair_lds() { return 2 * 2 * BN2 * LDP<D> * 2 + 2 * 2 * BN2 * 4 + 2 * 4 * 2 * 64 * 16; }
+
+template <typename T, int D, bool CAUSAL>
+__global__ void __launch_bounds__(512, 2) bwd_dkdv_pair_kernel(
+    const uint16_t* __restrict__ Q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V,
+    const uint16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    uint16_t* __restrict__ dK, uint16_t* __restrict__ dV, int S, float scale, int onh) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int TS = BN2 * LDP<D>;
+  // [2 stages][Q | dO] tiles, [2 stages][-LSE/scale 64 | -Delta 64], P slots [2 halves][4 groups][2][64]
+  float* const stats = reinterpret_cast<float*>(smem + 4 * TS);
+  s16x8* const pslot = reinterpret_cast<s16x8*>(stats + 4 * BN2);
+  const int lane = threadIdx.x & 63, ltid = threadIdx.x & 255;
+  const int role = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8);
+  const int kg = __builtin_amdgcn_readfirstlane(((int)threadIdx.x >> 6) & 3);
+  const int h = lane >> 5, c32 = lane & 31;
+  const int g16 = lane >> 4, qd = (lane & 15) >> 2, pc = lane & 3;
+  const int nkb = (S + BM2 - 1) / BM2;
+  const int task = xcd_task(blockIdx.x, gridDim.x);
+  const int64_t bh = task / nkb;
+  const int kb = (task - (int)bh * nkb) * BM2;
+  const int mykey = kb + 32 * kg + c32;
+  const int64_t base = bh * (int64_t)S * D;
+  const float sl2 = scale * LOG2E;
+  // each role stages its own A-row tile (role 0: Q, role 1: dO) and reads the other one transposed
+  const int sld = role ? o_ld<D>(onh) : D;
+  const __amdgpu_buffer_rsrc_t rs = head_rsrc(role ? dO + o_base<D>(bh, S, onh) : Q + base, S, sld);
+  const float* const rowc = (role ? DELTA : LSE) + bh * (int64_t)S;
+  const float cmul = role ? -1.f : -1.f / scale;
+
+  s16x8 bfr[D / 16];  // B fragments of this lane's key: K (role 0) or V (role 1)
+  {
+    const uint16_t* brow = (role ? V : K) + base + (int64_t)mykey * D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks)
+      bfr[ks] = mykey < S ? *reinterpret_cast<const s16x8*>(brow + 16 * ks) : s16x8{};
+  }
+  f32x16 acc[D / 32];
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[dt][r] = 0.f;
+
+  const int qstart = CAUSAL ? kb : 0;
+  const int ntiles = (S - qstart + BN2 - 1) / BN2;
+  uint4 stg[D / 32];
+  float st = 0.f;
+  auto fetch = [&](int i0) {
+    tile_load_buf_t<D>(stg, rs, i0, sld, ltid);
+    if (ltid < BN2) {
+      const int q = i0 + ltid;
+      st = q < S ? rowc[q] * cmul : 0.f;
+    }
+  };
+  auto put = [&](int stage) {
+    tile_store_t<D>(smem + stage * 2 * TS + role * TS, stg, ltid);
+    if (ltid < BN2) stats[stage * 2 * BN2 + role * BN2 + ltid] = st;
+  };
+  // S (role 0) or dP (role 1) of one 32-query half, started at the row constants
+  auto scores = [&](const uint16_t* X, const float* cs, int t) {
+    f32x16 c;
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const float4 v4 = *reinterpret_cast<const float4*>(cs + 32 * t + 8 * rb + 4 * h);
+      c[4 * rb + 0] = v4.x; c[4 * rb + 1] = v4.y; c[4 * rb + 2] = v4.z; c[4 * rb + 3] = v4.w;
+    }
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks)
+      c = Mfma32<T>::run(lds_row8(X + (32 * t + c32) * LDP<D> + 16 * ks + 8 * h), bfr[ks], c);
+    return c;
+  };
+  // acc^T += Y^T F for one half: Y^T fragments by transposed reads of the other role's tile
+  auto accum = [&](const uint16_t* Y, int t, const s16x8 (&f)[2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int row1 = 16 * (2 * t + kk) + 4 * (g16 >> 1) + qd;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const int col = 32 * dt + 16 * (g16 & 1) + 4 * pc;
+        const s16x4 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Y + row1 * LDP<D> + col));
+        const s16x4 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Y + (row1 + 8) * LDP<D> + col));
+        acc[dt] = Mfma32<T>::run(s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]}, f[kk], acc[dt]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // bounds the tr-read hoisting
+    }
+  };
+  // role 0: P of one half (masked), packed as B fragments and published in slot t
+  auto probs = [&](const f32x16& s, int i0, int t, s16x8 (&pf)[2]) {
+    float pv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pv[r] = fast_exp2(s[r] * sl2);
+    if ((i0 + 32 * t + 32 > S) || (kb + 32 * kg + 32 > S) || (CAUSAL && kb + 32 * kg + 31 > i0 + 32 * t)) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = i0 + 32 * t + 8 * (r >> 2) + 4 * h + (r & 3);
+        if (q >= S || mykey >= S || (CAUSAL && mykey > q)) pv[r] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      pf[kk] = __is_same(T, bf16_t) ? pack8(pv, 8 * kk) : pack8_h(pv, 8 * kk);
+      pslot[((t * 4 + kg) * 2 + kk) * 64 + lane] = pf[kk];
+    }
+  };
+  // role 1: dS = P * (dP - Delta) of one half from the published P
+  auto dsfrag = [&](const f32x16& dp, int t, s16x8 (&sf)[2]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const s16x8 p = pslot[((t * 4 + kg) * 2 + kk) * 64 + lane];
+      float ds[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        ds[j] = (__is_same(T, bf16_t) ? bf16_to_f32((uint16_t)p[j]) : f16_to_f32((uint16_t)p[j])) * dp[8 * kk + j];
+      sf[kk] = __is_same(T, bf16_t) ? pack8(ds, 0) : pack8_h(ds, 0);
+    }
+  };
+
+  fetch(qstart);
+  put(0);
+  __syncthreads();
+  // the half pending across a barrier, in ONE register block for both roles (the compiler cannot
+  // tell the role branches apart, so separate variables would all be live at the barriers):
+  // role 0 keeps its P fragments there (bit-cast into the first 8 elements), role 1 its dP
+  f32x16 hold1;
+  for (int it = 0; it < ntiles; ++it) {
+    const int i0 = qstart + it * BN2;
+    const bool has_next = it + 1 < ntiles;
+    const int cur = it & 1;
+    const uint16_t* const X = smem + cur * 2 * TS + role * TS;        // own tile, row reads
+    const uint16_t* const Y = smem + cur * 2 * TS + (1 - role) * TS;  // other tile, transposed reads
+    const uint16_t* const Yp = smem + (cur ^ 1) * 2 * TS + (1 - role) * TS;
+    const float* const cs = stats + cur * 2 * BN2 + role * BN2;
+    if (has_next) fetch(i0 + BN2);
+    f32x16 hold0;
+    if (role == 0) {
+      if (it > 0) {
+        s16x8 f[2];
+        unhold(hold1, f);
+        accum(Yp, 1, f);
+      }
+      s16x8 f[2];
+      probs(scores(X, cs, 0), i0, 0, f);
+      tohold(hold0, f);
+    } else {
+      if (it > 0) {
+        s16x8 sf[2];
+        dsfrag(hold1, 1, sf);
+        accum(Yp, 1, sf);
+      }
+      hold0 = scores(X, cs, 0);
+    }
+    __syncthreads();
+    if (role == 0) {
+      s16x8 f[2];
+      unhold(hold0, f);
+      accum(Y, 0, f);
+      probs(scores(X, cs, 1), i0, 1, f);
+      tohold(hold1, f);
+    } else {
+      s16x8 sf[2];
+      dsfrag(hold0, 0, sf);
+      accum(Y, 0, sf);
+      hold1 = scores(X, cs, 1);
+    }
+    if (has_next) put(cur ^ 1);
+    __syncthreads();
+  }
+  {
+    const uint16_t* const Yl = smem + ((ntiles - 1) & 1) * 2 * TS + (1 - role) * TS;
+    s16x8 f[2];
+    if (role == 0) unhold(hold1, f);
+    else dsfrag(hold1, 1, f);
+    accum(Yl, 1, f);
+  }
+  if (mykey < S) {
+    uint16_t* const out = (role ? dK : dV) + base + (int64_t)mykey * D;
+    const float m = role ? scale : 1.f;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        ushort4 v4;
+        v4.x = to16<T>(acc[dt][4 * rb + 0] * m); v4.y = to16<T>(acc[dt][4 * rb + 1] * m);
+        v4.z = to16<T>(acc[dt][4 * rb + 2] * m); v4.w = to16<T>(acc[dt][4 * rb + 3] * m);
+        *reinterpret_cast<ushort4*>(out + 32 * dt + 8 * rb + 4 * h) = v4;
+      }
+  }
 }
 
 template <typename T, int D, bool CAUSAL, int EX = 0, bool BUF = true>
@@ -1799,14 +2041,16 @@ void launch_flash_bwd(const void* dout, const void* q, const void* k, const void
     hipLaunchKernelGGL((fa::bwd_dq_v3_kernel<T, DD, CC>), dim3(g), dim3(256), fa::fwd_v2_lds<DD>(), s,
                        (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout,
                        (const uint16_t*)o, lse, delta, (uint16_t*)dq, S, scale, onh);
-    // D = 128 at two waves per SIMD spills ~160 VGPRs to scratch (hipcc resource usage): one
-    // wave per SIMD keeps the whole working set in VGPR + AGPR (4.7x -> see profiles/r4b_*)
-    if constexpr (DD < 128)
-      hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 2>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
+    // D = 128: the wave-pair kernel (one wave per SIMD held the whole working set of the
+    // single-wave body and shuffled it through AGPRs: 1.50 -> 1.44 ms for the whole backward at
+    // B4 H64 S2048 causal, profiles/r6h_dkdv_pair.md); at D = 96 / 64 the single-wave body runs
+    // two waves per SIMD on its own and is faster (1.01 vs 1.15 ms at D = 96)
+    if constexpr (DD >= 128)
+      hipLaunchKernelGGL((fa::bwd_dkdv_pair_kernel<T, DD, CC>), dim3(g), dim3(512), fa::dkdv_pair_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
                          delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh);
     else
-      hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC, 1>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
+      hipLaunchKernelGGL((fa::bwd_dkdv_v3_kernel<T, DD, CC>), dim3(g), dim3(256), fa::dkdv_v2_lds<DD>(), s,
                          (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)dout, lse,
                          delta, (uint16_t*)dk, (uint16_t*)dv, S, scale, onh));
 }
