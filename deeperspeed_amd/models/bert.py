@@ -117,6 +117,15 @@ class BertForPreTraining(nn.Module):
         u = torch.rand(L, generator=self._pld_gen).tolist()
         return [u[i] < 1.0 - (i + 1) / L * (1.0 - theta) for i in range(L)]
 
+    def enable_device_rng(self, seed: int = 1234):
+        """Every dropout of the model draws from device [seed, step] counters that kernels inside
+        the forward advance (the embeddings' here, each encoder layer its own), so a HIP graph
+        captured around a whole training step gets fresh masks on every replay
+        (`scripts/bench_bert.py --hip-graphs step`).  The masks differ from host-seeded ones."""
+        self._emb_rng = torch.tensor([int(seed), 0], dtype=torch.int64, device=self.word_embeddings.weight.device)
+        for i, layer in enumerate(self.layers):
+            layer.enable_device_rng(seed + 7919 * (i + 1))
+
     def encode(self, input_ids, token_type_ids=None, attention_mask=None, progressive_layer_drop=False,
                pld_theta=1.0):
         B, S = input_ids.shape
@@ -125,7 +134,10 @@ class BertForPreTraining(nn.Module):
         if token_type_ids is not None:
             x = x + self.token_type_embeddings(token_type_ids)
         x = self.embeddings_ln(x)
-        x = native.dropout(x, self.cfg.hidden_dropout, self.training)
+        rng = getattr(self, "_emb_rng", None)
+        if rng is not None and self.training and torch.is_grad_enabled():
+            rng[1:].add_(1)
+        x = native.dropout(x, self.cfg.hidden_dropout, self.training, rng=rng)
         ext = None
         if attention_mask is not None:
             ext = ((1.0 - attention_mask.to(x.dtype)) * -10000.0)[:, None, None, :]

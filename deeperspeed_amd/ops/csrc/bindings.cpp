@@ -160,8 +160,12 @@ void lamb(Tensor w, Tensor g, Tensor m, Tensor v, Tensor upd, OptT out, double l
 void lamb_multi(Tensor meta, int64_t T, int64_t total_chunks, int64_t chunk, int64_t wt, int64_t gt, int64_t ot,
                 double lr, double beta1, double beta2, double eps, double wd, double bc1, double bc2,
                 double grad_scale, double max_coeff, double min_coeff, bool adamw, Tensor partial, Tensor coeff,
-                OptT scale) {
+                OptT scale, OptT lr_dev) {
   check_dev(meta, "meta"); check_dev(partial, "partial"); check_dev(coeff, "coeff");
+  if (lr_dev.has_value()) {
+    check_dev(*lr_dev, "lr_dev");
+    TORCH_CHECK(lr_dev->scalar_type() == at::kFloat && lr_dev->numel() == 1, "lamb_multi: lr_dev must be one fp32");
+  }
   if (scale.has_value()) {
     check_dev(*scale, "scale");
     TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1, "lamb_multi: scale must be one fp32");
@@ -172,7 +176,8 @@ void lamb_multi(Tensor meta, int64_t T, int64_t total_chunks, int64_t chunk, int
   c10::hip::HIPGuardMasqueradingAsCUDA guard(meta.device());
   dsa::LambArgs a{(float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2,
                   (float)grad_scale, (float)max_coeff, (float)min_coeff, adamw ? 1 : 0,
-                  scale.has_value() ? scale->data_ptr<float>() : nullptr};
+                  scale.has_value() ? scale->data_ptr<float>() : nullptr,
+                  lr_dev.has_value() ? lr_dev->data_ptr<float>() : nullptr};
   dsa::launch_lamb_multi(meta.data_ptr<int64_t>(), (int)T, total_chunks, chunk, (int)wt, (int)gt, (int)ot, a,
                          partial.data_ptr<float>(), coeff.data_ptr<float>(), cur_stream());
 }
@@ -1343,7 +1348,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lamb_multi", &lamb_multi, py::arg("meta"), py::arg("T"), py::arg("total_chunks"), py::arg("chunk"),
         py::arg("wt"), py::arg("gt"), py::arg("ot"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("eps"),
         py::arg("wd"), py::arg("bc1"), py::arg("bc2"), py::arg("grad_scale"), py::arg("max_coeff"), py::arg("min_coeff"),
-        py::arg("adamw"), py::arg("partial"), py::arg("coeff"), py::arg("scale") = py::none());
+        py::arg("adamw"), py::arg("partial"), py::arg("coeff"), py::arg("scale") = py::none(),
+        py::arg("lr_dev") = py::none());
   m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("res"),
         py::arg("bias"), py::arg("y_out") = py::none());
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),

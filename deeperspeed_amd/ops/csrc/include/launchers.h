@@ -23,6 +23,9 @@ struct LambArgs {
   // optional device-resident factor multiplied into grad_scale (unscale x clip computed on the
   // GPU after backward, no host round trip); a non-finite value skips the whole update
   const float* scale_ptr = nullptr;
+  // optional device-resident step size replacing lr (the bias correction of a step counter kept
+  // on the GPU, so a captured HIP graph of the whole training step advances it on every replay)
+  const float* lr_ptr = nullptr;
 };
 
 // optim.hip

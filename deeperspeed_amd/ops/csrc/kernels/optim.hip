@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(256) lamb_multi_apply_kernel(const int64_t* __
   const int64_t start = (c - pref[t]) * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
   if (a.scale_ptr && !isfinite(a.grad_scale * *a.scale_ptr)) return;  // skipped step
-  const float s = a.lr * coeff[t];
+  const float s = (a.lr_ptr ? *a.lr_ptr : a.lr) * coeff[t];
   auto step = [&](float wf, float mf, float vf) {
     const float denom = a.adamw ? sqrtf(vf) + a.eps : sqrtf(vf + a.eps);
     return wf - s * (mf / denom + a.weight_decay * wf);

@@ -34,6 +34,7 @@ class FusedLamb(torch.optim.Optimizer):
         self.requires_per_param_masters = True  # trust ratio is per tensor: never flatten
         self.multi_tensor = True  # GPU: one multi-tensor launch set per (dtype, step) bucket
         self._meta_cache = {}
+        self._dev_step = None  # param group -> device step counter (enable_device_step)
 
     supports_fused_lp_step = True  # FP16_UnfusedOptimizer passes low-precision grads/outputs
 
@@ -41,6 +42,29 @@ class FusedLamb(torch.optim.Optimizer):
     def supports_device_scale(self):
         """step(scale_tensor=...) is honoured (the multi-tensor GPU kernels read it)."""
         return self.multi_tensor
+
+    def enable_device_step(self):
+        """Keep each param group's step counter on the GPU and form the bias-corrected step size
+        lr * sqrt(1 - b2^t) / (1 - b1^t) there (a few scalar kernels per group and step), so a HIP
+        graph captured around a whole training step (`scripts/bench_bert.py --hip-graphs step`)
+        advances it on every replay.  The host-side state["step"] only advances on eager steps;
+        `device_step(gi)` holds the true count."""
+        if self._dev_step is None:
+            self._dev_step = {}
+
+    def device_step(self, gi=0):
+        return None if self._dev_step is None else self._dev_step.get(gi)
+
+    def _device_lr(self, gi, group, dev):
+        t = self._dev_step.get(gi)
+        if t is None:
+            steps = [self.state[p]["step"] for p in group["params"] if len(self.state[p])]
+            t = self._dev_step[gi] = torch.tensor(float(steps[0] if steps else 0), dtype=torch.float64, device=dev)
+        t.add_(1)
+        b1, b2 = group["betas"]
+        if not group["bias_correction"]:
+            return torch.full((1,), group["lr"], dtype=torch.float32, device=dev)
+        return (group["lr"] * torch.sqrt(1.0 - torch.pow(b2, t)) / (1.0 - torch.pow(b1, t))).float().reshape(1)
 
     @torch.no_grad()
     def step(self, closure=None, grads=None, output_params=None, scale=1.0, grad_norms=None, scale_tensor=None):
@@ -81,9 +105,12 @@ class FusedLamb(torch.optim.Optimizer):
                                  group["weight_decay"], st["step"], group["bias_correction"], 1.0 / scale,
                                  group["max_coeff"], group["min_coeff"], self.eps_mode == 1)
                 self.lamb_coeffs.append(c)
+            lr_dev = None
+            if buckets and self._dev_step is not None:
+                lr_dev = self._device_lr(gi, group, next(iter(buckets))[0])
             for (dev, pdt, gdt, odt, step), items in buckets.items():
                 self.lamb_coeffs.append(self._multi_step(dev, pdt, gdt, odt, step, items, group, 1.0 / scale,
-                                                         scale_tensor))
+                                                         scale_tensor, lr_dev))
         return loss
 
     @torch.no_grad()
@@ -112,7 +139,7 @@ class FusedLamb(torch.optim.Optimizer):
         return [self._multi_step(dev, pdt, gdt, odt, step, items, group, 1.0, scale_tensor)
                 for (dev, pdt, gdt, odt, step), items in buckets.items()]
 
-    def _multi_step(self, dev, pdt, gdt, odt, step, items, group, grad_scale, scale_tensor=None):
+    def _multi_step(self, dev, pdt, gdt, odt, step, items, group, grad_scale, scale_tensor=None, lr_dev=None):
         import math
         ws = [p.data for p, _, _ in items]
         gs = [g for _, g, _ in items]
@@ -121,6 +148,9 @@ class FusedLamb(torch.optim.Optimizer):
         outs = [o for _, _, o in items]
         key = tuple(t.data_ptr() for t in ws + gs) + tuple(o.data_ptr() if o is not None else 0 for o in outs)
         hit = self._meta_cache.get(key)
+        if hit is None and dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("FusedLamb: new parameter / gradient addresses while a HIP graph is being captured; "
+                               "give the parameters persistent gradients first (runtime/step_graph.persistent_grads)")
         if hit is None:
             numels = [t.numel() for t in ws]
             pref = [0]
@@ -130,13 +160,15 @@ class FusedLamb(torch.optim.Optimizer):
                     [t.data_ptr() for t in vs] + [(o.data_ptr() if o is not None else 0) for o in outs] + numels
                     + pref)
             # pinned staging + async copy: a pageable H2D copy would wait for the whole stream
-            # (the gradients are new tensors every step, so this runs every step)
-            meta = torch.tensor(rows, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
-            hit = (meta, len(ws), pref[-1], torch.empty(2 * pref[-1], dtype=torch.float32, device=dev))
+            # (the gradients are new tensors every step, so this runs every step).  The pinned
+            # table stays referenced: a graph that captured the copy re-reads it on every replay.
+            host = torch.tensor(rows, dtype=torch.int64).pin_memory()
+            meta = host.to(dev, non_blocking=True)
+            hit = (meta, len(ws), pref[-1], torch.empty(2 * pref[-1], dtype=torch.float32, device=dev), host)
             if len(self._meta_cache) > 64:
                 self._meta_cache.clear()
             self._meta_cache[key] = hit
-        meta, T, total, partial = hit
+        meta, T, total, partial, _ = hit
         b1, b2 = group["betas"]
         bc1 = 1.0 - b1 ** step if group["bias_correction"] else 1.0
         bc2 = 1.0 - b2 ** step if group["bias_correction"] else 1.0
@@ -145,7 +177,7 @@ class FusedLamb(torch.optim.Optimizer):
         native.hip_ops().lamb_multi(meta, T, total, _CHUNK, code[pdt], code[gdt], code[odt or pdt],
                                     group["lr"] * math.sqrt(bc2) / bc1, b1, b2, group["eps"], group["weight_decay"],
                                     bc1, bc2, grad_scale, group["max_coeff"], group["min_coeff"],
-                                    self.eps_mode == 1, partial, coeff, scale_tensor)
+                                    self.eps_mode == 1, partial, coeff, scale_tensor, lr_dev)
         return coeff
 
     def get_lamb_coeffs(self):

@@ -883,9 +883,9 @@ def _draw_seed(generator=None):
 
 class _DropoutFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, p, seed):
+    def forward(ctx, x, p, seed, rng=None):
         if x.is_cuda:
-            y, mask = hip_ops().dropout_fwd(x.contiguous(), p, seed, 0)
+            y, mask = hip_ops().dropout_fwd(x.contiguous(), p, seed, 0, rng)
         else:
             g = torch.Generator().manual_seed(seed)
             mask = (torch.rand(x.shape, generator=g) >= p).to(torch.uint8)
@@ -898,13 +898,18 @@ class _DropoutFn(torch.autograd.Function):
     def backward(ctx, dy):
         (mask,) = ctx.saved_tensors
         if dy.is_cuda:
-            return hip_ops().dropout_bwd(dy.contiguous(), mask, ctx.p), None, None
-        return (dy.float() * mask / (1 - ctx.p)).to(dy.dtype), None, None
+            return hip_ops().dropout_bwd(dy.contiguous(), mask, ctx.p), None, None, None
+        return (dy.float() * mask / (1 - ctx.p)).to(dy.dtype), None, None, None
 
 
-def dropout(x, p, training=True, generator=None):
+def dropout(x, p, training=True, generator=None, rng=None, site=0):
+    """rng: optional device int64 [seed, step] read by the kernel (graph-replayable masks, see
+    DeepSpeedTransformerLayer.enable_device_rng); the host part of the seed is then the
+    constant `site`, never a host draw, which a captured graph would freeze."""
     if not training or p <= 0:
         return x
+    if rng is not None and x.is_cuda:
+        return _DropoutFn.apply(x, float(p), int(site) << 20, rng)
     return _DropoutFn.apply(x, float(p), _draw_seed(generator))
 
 

@@ -91,9 +91,17 @@ class _State:
         self.single = 0  # records run one by one
         self.recorded = 0
         self.last_miss = None  # why the last group could not be batched (diagnostics)
+        # a whole training step is being captured as one HIP graph (runtime/step_graph): slots
+        # lent and the deferred weight gradients flushed inside that one graph stay valid, so
+        # slabs and deferral keep working (per-layer graphs share no slot state: off there)
+        self.whole_step_capture = False
 
 
 state = _State()
+
+
+def _capture_blocks() -> bool:
+    return torch.cuda.is_current_stream_capturing() and not state.whole_step_capture
 
 
 def enable(on: bool = True):
@@ -110,7 +118,7 @@ def view(kind: str, index: int, count: int, like: torch.Tensor, backward: bool =
     the next backward end frees."""
     if not (state.slabs_on and like.is_cuda and 0 <= index < count) or count < 2 or kind in state.off_kinds:
         return None
-    if torch.cuda.is_current_stream_capturing():
+    if _capture_blocks():
         return None
     key = (count, tuple(like.shape), like.dtype, like.device)
     slab = state.slabs.get(kind)
@@ -254,7 +262,7 @@ def deferrable(g2: torch.Tensor, x2: torch.Tensor, gw: torch.Tensor) -> bool:
     return (state.defer and g2.is_cuda and g2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == g2.dtype
             and gw.dtype == g2.dtype and g2.dim() == 2 and x2.dim() == 2 and g2.is_contiguous()
             and x2.is_contiguous() and gw.is_contiguous() and g2.size(0) >= MIN_TOKENS
-            and not torch.cuda.is_current_stream_capturing())
+            and not _capture_blocks())
 
 
 def in_slab(t: torch.Tensor) -> bool:

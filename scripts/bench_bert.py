@@ -11,6 +11,7 @@ deeperspeed_amd.initialize, bf16.  Synthetic token ids / random-init weights.
 """
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -37,9 +38,13 @@ def main():
     ap.add_argument("--host-sleep-ms", type=float, default=0.0,
                     help="diagnostic: sleep this long on the host after issuing each step (a GPU-bound "
                          "step absorbs it up to its host slack; a host-bound one slows by it)")
-    ap.add_argument("--hip-graphs", choices=["on", "off"], default="off",
-                    help="capture every encoder layer's forward / backward as HIP graphs "
-                         "(ops/transformer make_graphed_encoder; dropout from device RNG state)")
+    ap.add_argument("--hip-graphs", choices=["on", "off", "step", "step-eager"], default="off",
+                    help="on: capture every encoder layer's forward / backward as HIP graphs "
+                         "(ops/transformer make_graphed_encoder); step: capture the WHOLE training step "
+                         "(forward, backward, batched weight gradients, clipping, LAMB) as one graph "
+                         "replayed per step; both draw dropout from device RNG state; step-eager: the step "
+                         "mode's setup (device RNG / step counter, persistent gradients, side stream) without "
+                         "the capture, for A/B runs")
     ap.add_argument("--overlap-step", choices=["on", "off"], default="off",
                     help="run the LAMB step on a side stream overlapped with the next forward "
                          "(zero_optimization.overlap_step; identical math)")
@@ -49,7 +54,9 @@ def main():
                     help="PLD decay rate; the default reaches theta within the warmup steps, so the timed "
                          "steps measure the steady state (the reference's default 0.001 gets there after ~5k steps)")
     args = ap.parse_args()
-    if args.pld and (args.hip_graphs == "on" or args.overlap_step == "on"):
+    if args.hip_graphs.startswith("step") and args.overlap_step == "on":
+        raise SystemExit("--hip-graphs step captures the plain step (the overlapped step's hooks are host-driven)")
+    if args.pld and (args.hip_graphs != "off" or args.overlap_step == "on"):
         raise SystemExit("--pld runs the eager encoder (graphs / overlapped-step hooks assume every layer runs)")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29541")
@@ -109,7 +116,30 @@ def main():
             time.sleep(args.host_sleep_ms / 1e3)
         return loss
 
+    graph_stream = None
+    if args.hip_graphs.startswith("step"):
+        if dev.type != "cuda":
+            raise SystemExit("--hip-graphs step needs a GPU")
+        from deeperspeed_amd.runtime.step_graph import capture_step, persistent_grads
+        model.enable_device_rng(1234)
+        engine.basic_optimizer.enable_device_step()
+        persistent_grads(model.parameters())
+        # every step runs on one side stream from the first (runtime/step_graph.capture_step)
+        graph_stream = torch.cuda.Stream()
+        graph_stream.wait_stream(torch.cuda.current_stream())
+    stream_ctx = torch.cuda.stream(graph_stream) if graph_stream is not None else contextlib.nullcontext()
+    stream_ctx.__enter__()
     for _ in range(args.warmup):
+        loss = step()
+    if args.hip_graphs == "step":
+        replay, _ = capture_step(step, stream=graph_stream)
+
+        def step():
+            loss = replay()
+            if args.loss_trace:
+                trace.append(loss.detach().float())
+            kept.append(cfg.num_layers)
+            return loss
         loss = step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -124,6 +154,7 @@ def main():
     dt = (time.time() - t0) / args.steps
     if dev.type == "cuda":
         native.hip_ops().profile_marker(2)
+    stream_ctx.__exit__(None, None, None)
     if args.torch_profile:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
@@ -154,7 +185,7 @@ def main():
                       "unit": "samples/s", "ms_per_step": round(dt * 1e3, 2), "batch": B, "seq": S,
                       "masked_per_seq": npred, "model_tflops": round(tflops, 1), "dtype": "bf16",
                       "optimizer": "FusedLamb", "overlap_step": args.overlap_step == "on",
-                      "hip_graphs": args.hip_graphs == "on",
+                      "hip_graphs": args.hip_graphs,
                       "pld_theta": args.pld or None,
                       "mean_layers_run": round(run, 2),
                       "gradient_clipping": 1.0, "data": "synthetic", "final_loss": round(float(loss.detach()), 4),

@@ -93,3 +93,66 @@ def test_device_rng_masks_change_per_step():
     layer._rng[1] = 0
     c = layer(x)
     assert torch.equal(a, c)
+
+
+def _train_whole_step(graph, steps=6, warmup=3):
+    """BERT steps through the engine with device RNG and LAMB's device step counter:
+    eager for every step, or eager for `warmup` steps, one side-stream step, then replays of one
+    graph of the whole step (runtime/step_graph.capture_step)."""
+    _env()
+    import deeperspeed_amd as ds
+    from deeperspeed_amd.models.bert import BertForPreTraining, get_config
+    from deeperspeed_amd.runtime.step_graph import capture_step, persistent_grads
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = get_config("bert-large", num_layers=3, vocab_size=4096, max_position=128)  # dropout 0.1
+    model = BertForPreTraining(cfg, device=dev, dtype=torch.bfloat16).train()
+    conf = {"train_micro_batch_size_per_gpu": 8, "optimizer": {"type": "Lamb", "params": {"lr": 2e-3}},
+            "fp16": {"enabled": True, "type": "bfloat16"}, "gradient_clipping": 1.0}
+    engine, _, _, _ = ds.initialize(model=model, model_parameters=model.parameters(), config_params=conf)
+    model.enable_device_rng(55)
+    engine.basic_optimizer.enable_device_step()
+    persistent_grads(model.parameters())
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.Generator(device=dev).manual_seed(1)
+    B, S, npred = 8, 128, 20
+    ids = torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)
+    am = torch.ones(B, S, device=dev, dtype=torch.long)
+    am[:, 100:] = 0
+    pos = torch.stack([torch.randperm(100, device=dev, generator=g)[:npred].sort().values for _ in range(B)])
+    lab = torch.randint(0, cfg.vocab_size, (B, npred), device=dev, generator=g)
+    nsp = torch.randint(0, 2, (B,), device=dev, generator=g)
+
+    def step():
+        loss = engine(ids, None, am, pos, lab, nsp)
+        engine.backward(loss)
+        engine.step()
+        return loss
+
+    losses = []
+    with torch.cuda.stream(side):  # both runs on the same kind of stream from the first step
+        if not graph:
+            for _ in range(steps):
+                losses.append(float(step()))
+        else:
+            for _ in range(warmup):
+                losses.append(float(step()))
+            replay, warm = capture_step(step, stream=side)
+            losses.append(float(warm))
+            for _ in range(steps - warmup - 1):
+                losses.append(float(replay()))
+    torch.cuda.synchronize()
+    return losses, [p.detach().float().cpu() for p in engine.module.parameters()]
+
+
+def test_whole_step_graph_equals_eager():
+    """One graph of forward + backward + clipping + LAMB, replayed, trains exactly like the eager
+    steps: same losses and weights bit for bit (dropout masks and bias correction advance on
+    the device inside the graph)."""
+    eager_l, eager_w = _train_whole_step(False)
+    graph_l, graph_w = _train_whole_step(True)
+    assert graph_l == eager_l, (graph_l, eager_l)
+    for a, b in zip(eager_w, graph_w):
+        assert torch.equal(a, b)
+    assert len(set(eager_l)) == len(eager_l)
