@@ -496,16 +496,25 @@ __global__ void __launch_bounds__(256, (D >= 128 ? 2 : 3)) fwd_v2_kernel(const u
   if (myq < S) {
     const float inv = l > 0.f ? (DROP ? ex.rscale : 1.f) / l : 0.f;
     uint16_t* orow = O + o_base<D>(bh, S, onh) + (int64_t)myq * o_ld<D>(onh);
+    // widened store (cdna_hip_programming T21): lanes c32 and c32 + 32 hold the two 4-element
+    // halves of each 8-element group of the row; one v_permlane32_swap per dword pair hands
+    // the lower lane groups rb, rb+1 = elements 16j .. 16j+7 and the upper lane 16j+8 .. 16j+15
 #pragma unroll
     for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
-        ushort4 v4;
-        v4.x = to16<T>(o[dt][4 * rb + 0] * inv);
-        v4.y = to16<T>(o[dt][4 * rb + 1] * inv);
-        v4.z = to16<T>(o[dt][4 * rb + 2] * inv);
-        v4.w = to16<T>(o[dt][4 * rb + 3] * inv);
-        *reinterpret_cast<ushort4*>(orow + 32 * dt + 8 * rb + 4 * h) = v4;
+      for (int j = 0; j < 2; ++j) {
+        uint32_t a[2], b[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          a[e] = (uint32_t)to16<T>(o[dt][8 * j + 2 * e] * inv) |
+                 ((uint32_t)to16<T>(o[dt][8 * j + 2 * e + 1] * inv) << 16);
+          b[e] = (uint32_t)to16<T>(o[dt][8 * j + 4 + 2 * e] * inv) |
+                 ((uint32_t)to16<T>(o[dt][8 * j + 4 + 2 * e + 1] * inv) << 16);
+          const auto r = __builtin_amdgcn_permlane32_swap(a[e], b[e], false, false);
+          a[e] = r[0];
+          b[e] = r[1];
+        }
+        *reinterpret_cast<uint4*>(orow + 32 * dt + 16 * j + 8 * h) = make_uint4(a[0], a[1], b[0], b[1]);
       }
     if (h == 0)
       // a row with every key masked out stores +inf so the backward recomputes P = 0 for it
