@@ -1,5 +1,5 @@
 """Rotary split kernels (QKV projection output -> rotated, scaled q / k / v and back) at the
-GPT-NeoX-20B shape, per DSA_ROTARY_TILED mode, with the max difference between modes.
+GPT-NeoX-20B shape: time and HBM rate of each direction.
 
     python scripts/bench_rotary.py [--batch 4 --seq 2048 --heads 64 --hd 96 --rot 24]
 """
@@ -43,19 +43,12 @@ def main():
     qkv = torch.randn(B, S, NH * 3 * HD, device="cuda", dtype=torch.bfloat16)
     cs = rotary_table(S, R, 10000.0, qkv.device)
     dq, dk, dv = (torch.randn(B, NH, S, HD, device="cuda", dtype=torch.bfloat16) for _ in range(3))
-    outs = {}
-    nbytes = qkv.numel() * 2 * 2
-    for mode in ("1", "2"):
-        os.environ["DSA_ROTARY_TILED"] = mode
-        tf = timed(lambda: ops.rotary_split_fwd(qkv, cs, NH, HD, R, 0.5))
-        tb = timed(lambda: ops.rotary_split_bwd(dq, dk, dv, cs, R, 0.5))
-        outs[mode] = (ops.rotary_split_fwd(qkv, cs, NH, HD, R, 0.5), ops.rotary_split_bwd(dq, dk, dv, cs, R, 0.5))
-        print(json.dumps({"mode": mode, "B": B, "S": S, "NH": NH, "HD": HD, "rot": R, "fwd_us": round(tf * 1e3, 1),
-                          "fwd_TBps": round(nbytes / tf / 1e9, 2), "bwd_us": round(tb * 1e3, 1),
-                          "bwd_TBps": round(nbytes / tb / 1e9, 2)}), flush=True)
-    (f1, b1), (f3, b3) = outs["1"], outs["2"]
-    dmax = max((a.float() - b.float()).abs().max().item() for a, b in zip(list(f1) + [b1], list(f3) + [b3]))
-    print(json.dumps({"max_abs_diff_mode1_vs_2": dmax}))
+    nbytes = qkv.numel() * 2 * 2  # read + write of the QKV projection output
+    tf = timed(lambda: ops.rotary_split_fwd(qkv, cs, NH, HD, R, 0.5))
+    tb = timed(lambda: ops.rotary_split_bwd(dq, dk, dv, cs, R, 0.5))
+    print(json.dumps({"B": B, "S": S, "NH": NH, "HD": HD, "rot": R, "fwd_us": round(tf * 1e3, 1),
+                      "fwd_TBps": round(nbytes / tf / 1e9, 2), "bwd_us": round(tb * 1e3, 1),
+                      "bwd_TBps": round(nbytes / tb / 1e9, 2)}), flush=True)
 
 
 if __name__ == "__main__":
