@@ -221,7 +221,6 @@ __global__ void __launch_bounds__(256) rotary_split_tiled_kernel(const T* __rest
   // rows padded by 16 bytes: in the per-row rotation phase every lane walks its own row, and an
   // unpadded 256-byte row (HD 128) puts all 64 lanes' accesses on the same banks
   constexpr int HDP = PAD ? HD + 8 : HD;
-  constexpr int PER = (CHUNKS + 255) / 256;  // 16-byte chunks per thread, all loads issued first
   __shared__ __attribute__((aligned(16))) uint16_t tile[ROWS * HDP];  // [which][h][s][HD (+8)]
   const int tid = threadIdx.x;
   const int nsb = S / ROT_SB, nhb = NH / ROT_HB;
@@ -240,34 +239,21 @@ __global__ void __launch_bounds__(256) rotary_split_tiled_kernel(const T* __rest
     sl = r % ROT_SB; r /= ROT_SB;
     hl = r % ROT_HB; which = r / ROT_HB;
   };
-  {
-    uint4 v[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {  // every global load in flight before the first LDS store
-      const int c = tid + 256 * k;
-      if (c < CHUNKS) {
-        int which, hl, sl, ch;
-        if constexpr (!BWD) {
-          packed_chunk(c, which, hl, sl, ch);
-          v[k] = *reinterpret_cast<const uint4*>(qkv_in + ((((int64_t)b * S + s0 + sl) * NH + h0 + hl) * 3 + which) *
-                                                              HD + ch * 8);
-        } else {
-          split_chunk(c, which, hl, sl, ch);
-          const T* src = which == 0 ? q_in : (which == 1 ? k_in : v_in);
-          v[k] = *reinterpret_cast<const uint4*>(src + (((int64_t)b * NH + h0 + hl) * S + s0 + sl) * HD + ch * 8);
-        }
-      }
+  // one load and its LDS store per chunk: issuing all of a thread's loads before the first store
+  // (PER uint4 registers live at once) ran 28 % slower -- 188 vs 136 us on the 20B shape,
+  // profiles/r6l_rotary_load_loop_ab.log -- the loop lets more workgroups' loads overlap instead
+  for (int c = tid; c < CHUNKS; c += 256) {
+    int which, hl, sl, ch;
+    uint4 v;
+    if constexpr (!BWD) {
+      packed_chunk(c, which, hl, sl, ch);
+      v = *reinterpret_cast<const uint4*>(qkv_in + ((((int64_t)b * S + s0 + sl) * NH + h0 + hl) * 3 + which) * HD + ch * 8);
+    } else {
+      split_chunk(c, which, hl, sl, ch);
+      const T* src = which == 0 ? q_in : (which == 1 ? k_in : v_in);
+      v = *reinterpret_cast<const uint4*>(src + (((int64_t)b * NH + h0 + hl) * S + s0 + sl) * HD + ch * 8);
     }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int c = tid + 256 * k;
-      if (c < CHUNKS) {
-        int which, hl, sl, ch;
-        if constexpr (!BWD) packed_chunk(c, which, hl, sl, ch);
-        else split_chunk(c, which, hl, sl, ch);
-        *reinterpret_cast<uint4*>(tile + lds_off(which, hl, sl) + ch * 8) = v[k];
-      }
-    }
+    *reinterpret_cast<uint4*>(tile + lds_off(which, hl, sl) + ch * 8) = v;
   }
   __syncthreads();
   if (tid < ROWS) {
