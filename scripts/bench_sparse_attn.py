@@ -81,8 +81,7 @@ def main():
     t_dense_f, t_sparse_f = time_it(dense_fwd), time_it(sparse_fwd)
     res = [{"variant": "dense causal flash", "ms_fwd_bwd": round(t_dense, 3), "ms_fwd": round(t_dense_f, 3),
             "tflops": round(flops_dense / t_dense / 1e9, 1)},
-           {"variant": f"block-sparse flash ({a.mode}, block {a.block})" +
-            (" [single-stage LDS]" if os.environ.get("DSA_SPARSE_FLASH_RP") == "0" else ""), "ms_fwd_bwd": round(t_sparse, 3),
+           {"variant": f"block-sparse flash ({a.mode}, block {a.block})", "ms_fwd_bwd": round(t_sparse, 3),
             "ms_fwd": round(t_sparse_f, 3),
             "tile_density": round(lut.density, 4), "speedup_vs_dense": round(t_dense / t_sparse, 2),
             "effective_tflops": round(flops_dense * lut.density * 2 / t_sparse / 1e9, 1)}]
