@@ -22,3 +22,15 @@ ms = t(lambda: w.t().contiguous()); print(json.dumps({"op": "torch t().contiguou
 z = torch.empty(8192 * 18432 * 2, device="cuda", dtype=torch.bfloat16)
 ms = t(lambda: z.zero_()); print(json.dumps({"op": "zero_ 604MB", "ms": round(ms, 4), "TBps": round(z.numel() * 2 / ms / 1e9, 2)}))
 ms = t(lambda: x.sum()); print(json.dumps({"op": "sum read 302MB", "ms": round(ms, 4), "TBps": round(x.numel() * 2 / ms / 1e9, 2)}))
+
+# compact-master Adam over one 77M-parameter group (the 20B step's per-group call): bytes moved per
+# element: bf16 hi + int16 residual + bf16 grad + fp32 m, v read; hi, residual, m, v written
+n = 77_000_000
+hi = torch.randn(n, device="cuda").to(torch.bfloat16)
+res = torch.zeros(n, device="cuda", dtype=torch.int16)
+g = torch.randn(n, device="cuda").to(torch.bfloat16)
+m = torch.zeros(n, device="cuda")
+v = torch.zeros(n, device="cuda")
+ops = native.hip_ops()
+ms = t(lambda: ops.adam_compact(hi, res, g, m, v, 1e-4, 0.9, 0.95, 1e-8, 0.01, 0.1, 0.05, 1.0, True))
+print(json.dumps({"op": "adam_compact 77M", "ms": round(ms, 4), "TBps": round(26 * n / ms / 1e9, 2)}))
