@@ -592,12 +592,20 @@ void launch_ln_bwd(const void* dy, const void* x, const void* gamma, const float
                    int dt, hipStream_t s, int accum) {
   if (rows <= 0) return;
   const bool wave = ln_wave(H, dt);
+  // 16-bit rows of up to 64 lanes x 4 vectors (H <= 2048) also take the wave-per-row backward: at
+  // NeoX-1.3B's [32768, 2048] 110-115 vs 158-171 us for the block-per-row kernel, one wave per SIMD
+  // and all (profiles/r6r_layernorm_bwd_wave4_ab.log)
+  const bool wave4 = !wave && dt != kF32 && H <= 64 * 4 * 8;
   // partial rows: one per block (<= ln_bwd_grid(rows), the caller's workspace)
-  const int grid = wave ? (int)std::min<int64_t>(ln_bwd_grid(rows), (rows + 3) / 4) : ln_bwd_grid(rows);
+  const int grid = (wave || wave4) ? (int)std::min<int64_t>(ln_bwd_grid(rows), (rows + 3) / 4) : ln_bwd_grid(rows);
   const int nv = (H / (dt == kF32 ? 4 : 8) + LN_THREADS - 1) / LN_THREADS;
   DSA_DISPATCH_T(dt, T,
     if (wave)
       hipLaunchKernelGGL((ln_bwd_wave_kernel<T, 2>), dim3(grid), dim3(256), 8 * H * sizeof(float), s,
+                         (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx, partial,
+                         rows, H);
+    else if (wave4)
+      hipLaunchKernelGGL((ln_bwd_wave_kernel<T, 4>), dim3(grid), dim3(256), 8 * H * sizeof(float), s,
                          (const T*)dy, (const T*)x, (const T*)gamma, mean, rstd, (const T*)dres, (T*)dx, partial,
                          rows, H);
     else

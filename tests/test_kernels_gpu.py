@@ -41,7 +41,7 @@ def test_layernorm_fwd_bwd(dtype, H):
 
 
 @pytest.mark.parametrize("rows", [3, 4100, 8192])
-@pytest.mark.parametrize("H", [768, 1024])
+@pytest.mark.parametrize("H", [768, 1024, 2048])
 def test_layernorm_residual_wave_bwd(rows, H):
     """Wave-per-row LayerNorm backward with the fused residual-gradient add (pre-LN blocks):
     rows beyond one grid pass exercise the software-pipelined row loop and its tail."""
